@@ -1,0 +1,113 @@
+/*
+ * vaevar.h — C ABI of libvaevar.so, the MI355X-native (gfx950, HIP) VAE-Var 4D-Var inner loop.
+ *
+ * The reference (xiaoyi018/VAE-Var) has no FFI: its boundary is the PyTorch module + optimiser
+ * protocol. Each entry point below replaces one piece of that protocol:
+ *
+ *   vv_lgunet_param_count/_info   the state_dict key set of networks_old.transformer.LGUnet_all
+ *                                 (networks_old/transformer.py:716-745, swinblock.py:189-262)
+ *   vv_model_create/load_weights  LGUnet_all(**cfg) + load_state_dict (da_4dvar.py:590-603, 571-588)
+ *   vv_model_forward              LGUnet_all.forward (transformer.py:747-752) = VAE_lr.decoder (vae.py:83-85)
+ *   vv_model_backward             autograd of the above w.r.t. its input (input gradient only, quirk Q5)
+ *   vv_bind_problem               the closure state of one_step_DA 'vae4dvar' (da_4dvar.py:1179-1251)
+ *   vv_closure                    closure() -> loss(z); backward (da_4dvar.py:1183-1208, 1242-1246)
+ *   vv_decode                     the analysis xa = decoder_hr(z)*stdTr*std + xb (da_4dvar.py:1301-1306)
+ *   vv_dot/axpy/... , vv_adam     vector arithmetic of torch/optim/lbfgs.py:333-535 and adam.py
+ *
+ * Conventions: every function returns 0 on success, a non-zero status otherwise (HIP error code or
+ * VV_E_*), never throws; vv_last_error() describes the last failure of the calling thread.
+ * All float pointers passed to compute entry points are DEVICE pointers (fp32, 16-byte aligned)
+ * owned by the caller; `stream` is a hipStream_t (NULL = default stream). A context is bound to
+ * one device and is not thread-safe. All work is enqueued on the given stream; only functions
+ * that return host scalars (vv_closure, vv_dot, ...) synchronise it.
+ */
+#ifndef VAEVAR_H
+#define VAEVAR_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VV_E_ARG 1001     /* invalid argument / unsupported configuration */
+#define VV_E_STATE 1002   /* call out of order (e.g. closure before bind_problem) */
+#define VV_E_ALLOC 1003   /* device allocation failed */
+
+typedef struct vv_ctx vv_ctx;
+
+/* networks_old.transformer.LGUnet_all keyword arguments (nf_model/parameters0_old.yaml:49-96) */
+typedef struct vv_lgunet_config {
+  int img_size[2];
+  int patch_size[2];   /* must equal stride: (2,2) */
+  int stride[2];
+  int n_groups;        /* len(inchans_list) == len(outchans_list) */
+  int inchans[8];
+  int outchans[8];
+  int enc_dim;
+  int embed_dim;
+  int window_size;     /* 4 */
+  int n_enc_levels;    /* len(enc_depths) == 2 */
+  int enc_depths[4];
+  int enc_heads[4];
+  int n_lg_layers;
+  int lg_depths[8];
+  int lg_heads[8];
+} vv_lgunet_config;
+
+int vv_version(void);
+int vv_last_error(char* buf, int cap);
+
+/* parameter enumeration (no device needed) */
+int vv_lgunet_param_count(const vv_lgunet_config* cfg, int* count);
+int vv_lgunet_param_info(const vv_lgunet_config* cfg, int index, char* name, int name_cap, int64_t* shape,
+                         int* ndim);
+
+int vv_ctx_create(int device, vv_ctx** out);
+int vv_ctx_destroy(vv_ctx* ctx);
+
+/* a network instance: `batch` images per forward, `n_slots` independent saved-activation sets
+   (one per forecast step of the 4D-Var window) */
+int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_slots, int* model_id);
+/* ptrs[i] points to parameter i in vv_lgunet_param_info order (host or device memory, fp32) */
+int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n);
+/* out: (batch, sum(outchans), H, W); only channels < out_limit are written (0 = all) */
+int vv_model_forward(vv_ctx* ctx, int model_id, int slot, const float* in, float* out, int out_limit, void* stream);
+/* din = add + (d out / d in)^T dout, reading only dout channels < out_limit; add may be NULL */
+int vv_model_backward(vv_ctx* ctx, int model_id, int slot, const float* dout, float* din, const float* add,
+                      int out_limit, void* stream);
+int vv_model_workspace_bytes(vv_ctx* ctx, int model_id, int64_t* bytes);
+
+/* one_step_DA 'vae4dvar' problem: state (C,Hs,Ws), window of T times; flow_model_id < 0 when T == 1.
+   xb (C,Hs,Ws); yo, Hmask, R (T,C,Hs,Ws); mean, std, std_tr (C). Buffers stay owned by the caller. */
+int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int C, int Hs, int Ws,
+                    const float* xb, const float* yo, const float* Hmask, const float* R, const float* mean,
+                    const float* std_, const float* std_tr, float obs_coeff);
+/* J = J_b + obs_coeff * J_o at latent z (1,32,128,256); grad_z = dJ/dz. Synchronises `stream`. */
+int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream);
+/* same, leaving {J_b, J_o} in device memory d_J[2]; no synchronisation */
+int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, void* stream);
+/* analysis state xa (C,Hs,Ws) */
+int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
+/* trajectory x_t (T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
+int vv_state_ptr(vv_ctx* ctx, const float** x);
+
+/* vector primitives (n floats). Host-returning ones synchronise `stream`. */
+int vv_dot(vv_ctx* ctx, const float* a, const float* b, int64_t n, double* out, void* stream);
+int vv_abssum(vv_ctx* ctx, const float* a, int64_t n, double* out, void* stream);
+int vv_absmax(vv_ctx* ctx, const float* a, int64_t n, float* out, void* stream);
+int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream);
+int vv_axpby(vv_ctx* ctx, float* out, const float* x, float a, const float* y, float b, int64_t n, void* stream);
+int vv_scale(vv_ctx* ctx, float* y, float alpha, int64_t n, void* stream);
+int vv_copy(vv_ctx* ctx, float* dst, const float* src, int64_t n, void* stream);
+/* torch.optim.Adam step (no weight decay / amsgrad): step is the 1-based step count */
+int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+            float beta2, float eps, int step, void* stream);
+
+/* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), epi as vv::Epi */
+int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
+            int tile, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAEVAR_H */

@@ -1,0 +1,230 @@
+"""ORACLE (survey container only) — generate golden fixtures from the REAL
+reference (`/root/reference`, imported through oracle/ref_harness.py) and pin
+the oracle's restatement against it.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python -B oracle/make_golden.py [--full]
+
+Writes small .npz fixtures to tests/golden/ (inputs are regenerated from the
+counter-hash RNG in vae-var_amd/vaevar/synth.py; only outputs and small inputs
+are stored):
+
+  g1_tiny_decoder.npz   G1: tiny networks_old.LGUnet_all: z, cotangent, out, d<out,cot>/dz
+  g2_swin_block.npz     G2: single SwinTransformerBlock (shift 0 / 2): x, out, grad, attn_mask
+  g4_nearest_maps.npz   G4: nearest index maps of F.interpolate 721<->128, 1440<->256
+  g5_tiny_lbfgs.npz     G5: restated vae4dvar loop on the tiny decoder (Nit=2): J per outer pass, xa
+  g5b_tiny_4dvar.npz    tiny decoder + tiny flow, T=2: J terms and dJ/dz of one closure
+  g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
+                        and one config-2 closure (J_b, J_o, sampled dJ/dz)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "vae-var_amd"))
+
+from oracle import ref_harness  # noqa: E402
+from oracle.lgunet_ref import lgunet_forward, param_shapes, synth_params, swin_block, shift_mask  # noqa: E402
+from oracle.da_ref import RefProblem, oracle_problem, one_step_da_ref  # noqa: E402
+from vaevar import config as C  # noqa: E402
+from vaevar.problem import make_problem  # noqa: E402
+from vaevar.synth import smooth_field, uniform_sym, param_value  # noqa: E402
+
+GOLD = os.path.join(REPO, "tests", "golden")
+
+
+def build_ref(tr, cfg, prefix=""):
+    torch.manual_seed(0)
+    m = tr.LGUnet_all(rank=0, **cfg)
+    p = synth_params(cfg)
+    sd = m.state_dict()
+    missing = [k for k in sd if k not in p]
+    assert all(k.endswith("relative_position_index") or k.endswith("attn_mask") for k in missing), missing[:5]
+    extra = [k for k in p if k not in sd]
+    assert not extra, extra[:5]
+    for k, v in p.items():
+        assert tuple(sd[k].shape) == tuple(v.shape), (k, sd[k].shape, v.shape)
+    m.load_state_dict(p, strict=False)
+    m.eval()
+    return m, p
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+def g1(tr):
+    cfg = C.TINY
+    m, p = build_ref(tr, cfg)
+    z = torch.from_numpy(0.5 * smooth_field(101, (1, 4, 32, 64), sigma=2.0)).requires_grad_(True)
+    cot = torch.from_numpy(uniform_sym(102, (1, 4, 32, 64), 1.0))
+    out = m(z)
+    (out * cot).sum().backward()
+    # the oracle restatement on the same inputs
+    z2 = z.detach().clone().requires_grad_(True)
+    out2 = lgunet_forward(p, cfg, z2)
+    (out2 * cot).sum().backward()
+    e_out, e_g = rel(out2.detach(), out.detach()), rel(z2.grad, z.grad)
+    print(f"G1 tiny decoder: restatement vs reference rel out {e_out:.2e} grad {e_g:.2e}")
+    assert e_out < 1e-5 and e_g < 1e-5
+    np.savez(os.path.join(GOLD, "g1_tiny_decoder.npz"), z=z.detach().numpy(), cot=cot.numpy(),
+             out=out.detach().numpy(), grad=z.grad.numpy())
+
+
+def g2(sb):
+    out = {}
+    for shift in (0, 2):
+        torch.manual_seed(0)
+        blk = sb.SwinTransformerBlock(dim=32, input_resolution=(16, 32), num_heads=2, window_size=4,
+                                      shift_size=shift)
+        pre = f"g2.s{shift}"
+        sd = blk.state_dict()
+        p = {}
+        for k, v in sd.items():
+            if k.endswith("relative_position_index") or k.endswith("attn_mask"):
+                continue
+            p[f"{pre}.{k}"] = torch.from_numpy(param_value(f"{pre}.{k}", tuple(v.shape)))
+        blk.load_state_dict({k[len(pre) + 1:]: v for k, v in p.items()}, strict=False)
+        x = torch.from_numpy(uniform_sym(200 + shift, (1, 16, 32, 32), 1.0)).requires_grad_(True)
+        cot = torch.from_numpy(uniform_sym(210 + shift, (1, 16, 32, 32), 1.0))
+        y = blk(x)
+        (y * cot).sum().backward()
+        x2 = x.detach().clone().requires_grad_(True)
+        y2 = swin_block(x2, p, pre, 2, 4, shift)
+        (y2 * cot).sum().backward()
+        print(f"G2 shift {shift}: rel out {rel(y2.detach(), y.detach()):.2e} grad {rel(x2.grad, x.grad):.2e}")
+        assert rel(y2.detach(), y.detach()) < 1e-5 and rel(x2.grad, x.grad) < 1e-5
+        out[f"x_s{shift}"] = x.detach().numpy()
+        out[f"cot_s{shift}"] = cot.numpy()
+        out[f"out_s{shift}"] = y.detach().numpy()
+        out[f"grad_s{shift}"] = x.grad.numpy()
+        if shift:
+            ref_mask = blk.attn_mask.numpy()
+            assert np.array_equal(ref_mask, shift_mask(16, 32, 4, shift).numpy())
+            out["attn_mask_s2"] = ref_mask
+            out["rel_index"] = blk.attn.relative_position_index.numpy()
+    np.savez(os.path.join(GOLD, "g2_swin_block.npz"), **out)
+
+
+def g4():
+    import torch.nn.functional as F
+
+    out = {}
+    for (a, b), key in (((721, 128), "lat_721_to_128"), ((128, 721), "lat_128_to_721"),
+                        ((1440, 256), "lon_1440_to_256"), ((256, 1440), "lon_256_to_1440")):
+        ramp = torch.arange(a, dtype=torch.float32).view(1, 1, a, 1)
+        m = F.interpolate(ramp, (b, 1)).view(-1).to(torch.int64).numpy()
+        out[key] = m.astype(np.int32)
+    np.savez(os.path.join(GOLD, "g4_nearest_maps.npz"), **out)
+    print("G4 nearest maps written")
+
+
+def tiny_problem(T=1):
+    return make_problem(nch=4, Hs=32, Ws=64, T=T, seed=777, obs_frac=0.1)
+
+
+def g5(tr):
+    cfg = C.TINY
+    m, p = build_ref(tr, cfg)
+    prob = tiny_problem()
+    rp = RefProblem(prob, m, cfg["img_size"])
+    t0 = time.time()
+    xa, z, js, nev, nit = one_step_da_ref(rp, 2, (4, 32, 64))
+    print(f"G5 reference-module L-BFGS: J {js}  evals {nev} iters {nit} ({time.time() - t0:.1f}s)")
+    ro = oracle_problem(prob, p, cfg)
+    xa2, z2, js2, nev2, nit2 = one_step_da_ref(ro, 2, (4, 32, 64))
+    print(f"G5 oracle restatement:     J {js2}  evals {nev2} iters {nit2}; xa rel {rel(xa2, xa):.2e}")
+    np.savez(os.path.join(GOLD, "g5_tiny_lbfgs.npz"), J=np.array(js, np.float64), n_eval=nev, n_iter=nit,
+             xa=xa.numpy(), z=z.numpy())
+
+
+def g5b(tr):
+    cfg, fcfg = C.TINY, C.TINY_FLOW
+    m, p = build_ref(tr, cfg)
+    fm, fp = build_ref(tr, fcfg)
+    prob = tiny_problem(T=2)
+    z = torch.from_numpy(0.3 * smooth_field(303, (1, 4, 32, 64), sigma=2.0)).requires_grad_(True)
+    rp = RefProblem(prob, m, cfg["img_size"], fm)
+    r, o = rp.loss_terms(z)
+    (r + o).backward()
+    ro = oracle_problem(prob, p, cfg, fp, fcfg)
+    z2 = z.detach().clone().requires_grad_(True)
+    r2, o2 = ro.loss_terms(z2)
+    (r2 + o2).backward()
+    print(f"G5b tiny 4D-Var T=2: J_b {float(r):.6e} J_o {float(o):.6e}; oracle rel J_o "
+          f"{abs(float(o2) - float(o)) / abs(float(o)):.2e} grad {rel(z2.grad, z.grad):.2e}")
+    np.savez(os.path.join(GOLD, "g5b_tiny_4dvar.npz"), z=z.detach().numpy(), J_b=float(r), J_o=float(o),
+             grad=z.grad.numpy())
+
+
+def sample_idx(n, k=4096, seed=909):
+    rng = np.random.default_rng(seed)
+    return np.sort(rng.choice(n, size=k, replace=False)).astype(np.int64)
+
+
+def g3(tr):
+    cfg = C.DECODER
+    t0 = time.time()
+    m, p = build_ref(tr, cfg)
+    print(f"G3 built full decoder in {time.time() - t0:.1f}s")
+    z = torch.from_numpy(0.5 * smooth_field(401, (1, 32, 128, 256))).requires_grad_(True)
+    cot = torch.from_numpy(uniform_sym(402, (1, 69, 128, 256), 1.0))
+    t0 = time.time()
+    out = m(z)
+    (out * cot).sum().backward()
+    print(f"G3 reference fwd+bwd {time.time() - t0:.1f}s")
+    z2 = z.detach().clone().requires_grad_(True)
+    out2 = lgunet_forward(p, cfg, z2)
+    (out2 * cot).sum().backward()
+    print(f"G3 restatement rel out {rel(out2.detach(), out.detach()):.2e} grad {rel(z2.grad, z.grad):.2e}")
+    io = sample_idx(out.numel())
+    ig = sample_idx(z.numel(), seed=910)
+    o = out.detach().numpy().reshape(-1).astype(np.float64)
+    g = z.grad.numpy().reshape(-1).astype(np.float64)
+    res = dict(idx_out=io, out_sample=o[io].astype(np.float32), out_sum=o.sum(), out_sumsq=(o * o).sum(),
+               out_abssum=np.abs(o).sum(), idx_grad=ig, grad_sample=g[ig].astype(np.float32), grad_sum=g.sum(),
+               grad_sumsq=(g * g).sum(), grad_abssum=np.abs(g).sum())
+    # one config-2 closure (T=1, 128x256 state) at a non-zero latent
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620)
+    rp = RefProblem(prob, m, cfg["img_size"])
+    zc = torch.from_numpy(0.3 * smooth_field(403, (1, 32, 128, 256))).requires_grad_(True)
+    rr, oo = rp.loss_terms(zc)
+    (rr + oo).backward()
+    gc = zc.grad.numpy().reshape(-1).astype(np.float64)
+    res.update(J_b=float(rr), J_o=float(oo), cgrad_sample=gc[ig].astype(np.float32), cgrad_sumsq=(gc * gc).sum(),
+               cgrad_sum=gc.sum())
+    print(f"G3 closure J_b {float(rr):.6e} J_o {float(oo):.6e} |g| {np.sqrt((gc * gc).sum()):.6e}")
+    np.savez(os.path.join(GOLD, "g3_full_decoder.npz"), **res)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--full", action="store_true", help="also generate G3 (full decoder, ~1 min)")
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    os.makedirs(GOLD, exist_ok=True)
+    torch.set_num_threads(8)
+    cwd = os.getcwd()
+    tr, sb = ref_harness.import_reference()
+    os.chdir(cwd)
+    steps = {"g1": lambda: g1(tr), "g2": lambda: g2(sb), "g4": g4, "g5": lambda: g5(tr), "g5b": lambda: g5b(tr)}
+    if a.full:
+        steps["g3"] = lambda: g3(tr)
+    for k, f in steps.items():
+        if a.only and k not in a.only.split(","):
+            continue
+        f()
+
+
+if __name__ == "__main__":
+    main()

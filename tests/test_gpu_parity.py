@@ -1,0 +1,204 @@
+"""Parity of the HIP path (through the C-ABI) with the reference, via the golden fixtures generated
+from /root/reference (oracle/make_golden.py) and the oracle restatement run here on the same inputs.
+
+Tolerances: single evaluation J and gradient rel <= 1e-5 (tiny) / 1e-4 (full);
+after N L-BFGS iterations J_final rel <= 1e-3 and xa rel-L2 <= 1e-3. "rel" = max|a-b| / max|b|.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLD
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    from vaevar import config as C
+    from vaevar.engine import LGUnet
+
+    return LGUnet(C.TINY, 1, 1).load_synthetic()
+
+
+def test_tiny_decoder_g1(tiny):
+    g = gold("g1_tiny_decoder.npz")
+    z = torch.from_numpy(g["z"]).cuda()
+    out = tiny.forward_raw(z)
+    dz = torch.empty_like(z)
+    tiny.backward_raw(torch.from_numpy(g["cot"]).cuda(), dz)
+    e_out, e_g = rel(out.cpu(), g["out"]), rel(dz.cpu(), g["grad"])
+    print(f"G1 tiny decoder: out rel {e_out:.2e}  grad rel {e_g:.2e}")
+    assert e_out < 1e-5 and e_g < 1e-5
+
+
+def test_tiny_autograd_fn(tiny):
+    g = gold("g1_tiny_decoder.npz")
+    z = torch.from_numpy(g["z"]).cuda().requires_grad_(True)
+    out = tiny(z)
+    (out * torch.from_numpy(g["cot"]).cuda()).sum().backward()
+    assert rel(z.grad.cpu(), g["grad"]) < 1e-5
+
+
+def test_batch2_matches_batch1():
+    """B=2 images in one launch == two B=1 launches (window maps / masks per image)."""
+    from vaevar import config as C
+    from vaevar.engine import LGUnet
+
+    g = gold("g1_tiny_decoder.npz")
+    n2 = LGUnet(C.TINY, 2, 1).load_synthetic()
+    z = torch.from_numpy(g["z"]).cuda()
+    z2 = torch.cat([z, 0.5 * z], 0).contiguous()
+    out = n2.forward_raw(z2)
+    assert rel(out[0:1].cpu(), g["out"]) < 1e-5
+    n1 = LGUnet(C.TINY, 1, 1).load_synthetic()
+    o1 = n1.forward_raw((0.5 * z).contiguous())
+    assert rel(out[1:2].cpu(), o1.cpu()) < 1e-6
+
+
+@pytest.fixture(scope="module")
+def full_dec():
+    from vaevar import config as C
+    from vaevar.engine import LGUnet
+
+    return LGUnet(C.DECODER, 1, 1).load_synthetic()
+
+
+def test_full_decoder_g3(full_dec):
+    from vaevar.synth import smooth_field, uniform_sym
+
+    g = gold("g3_full_decoder.npz")
+    z = torch.from_numpy(0.5 * smooth_field(401, (1, 32, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(402, (1, 69, 128, 256), 1.0)).cuda()
+    out = full_dec.forward_raw(z)
+    dz = torch.empty_like(z)
+    full_dec.backward_raw(cot, dz)
+    o = out.cpu().numpy().reshape(-1).astype(np.float64)
+    gr = dz.cpu().numpy().reshape(-1).astype(np.float64)
+    e_o = rel(o[g["idx_out"]], g["out_sample"])
+    e_g = rel(gr[g["idx_grad"]], g["grad_sample"])
+    e_ss = abs((o * o).sum() - g["out_sumsq"]) / g["out_sumsq"]
+    e_gs = abs((gr * gr).sum() - g["grad_sumsq"]) / g["grad_sumsq"]
+    print(f"G3 full decoder: out rel {e_o:.2e} (sumsq {e_ss:.1e})  grad rel {e_g:.2e} (sumsq {e_gs:.1e})")
+    assert e_o < 1e-4 and e_g < 1e-4 and e_ss < 1e-4 and e_gs < 1e-4
+
+
+def test_full_closure_g3(full_dec):
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    g = gold("g3_full_decoder.npz")
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    z = torch.from_numpy(0.3 * smooth_field(403, (1, 32, 128, 256))).cuda()
+    grad = torch.empty_like(z)
+    jb, jo = prob.closure(z, grad)
+    gr = grad.cpu().numpy().reshape(-1).astype(np.float64)
+    e_b = abs(jb - g["J_b"]) / g["J_b"]
+    e_o = abs(jo - g["J_o"]) / g["J_o"]
+    e_g = rel(gr[g["idx_grad"]], g["cgrad_sample"])
+    print(f"G3 closure: J_b rel {e_b:.2e} J_o rel {e_o:.2e} grad rel {e_g:.2e}")
+    assert e_b < 1e-5 and e_o < 1e-4 and e_g < 1e-4
+
+
+def _tiny_problem(T):
+    from vaevar.problem import make_problem
+
+    return make_problem(nch=4, Hs=32, Ws=64, T=T, seed=777, obs_frac=0.1)
+
+
+def test_tiny_4dvar_closure_g5b():
+    from vaevar import config as C
+    from vaevar.engine import DAProblem, LGUnet
+
+    g = gold("g5b_tiny_4dvar.npz")
+    dec = LGUnet(C.TINY, 1, 1).load_synthetic()
+    flow = LGUnet(C.TINY_FLOW, 1, 1).load_synthetic()
+    prob = DAProblem(dec, _tiny_problem(2), flow=flow)
+    z = torch.from_numpy(g["z"]).cuda()
+    grad = torch.empty_like(z)
+    jb, jo = prob.closure(z, grad)
+    e = (abs(jb - g["J_b"]) / g["J_b"], abs(jo - g["J_o"]) / g["J_o"], rel(grad.cpu(), g["grad"]))
+    print(f"G5b tiny 4D-Var T=2: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
+    assert e[0] < 1e-5 and e[1] < 1e-5 and e[2] < 1e-5
+
+
+def test_tiny_lbfgs_trajectory_g5():
+    from vaevar import config as C
+    from vaevar.da import one_step_da
+    from vaevar.engine import DAProblem, LGUnet
+
+    g = gold("g5_tiny_lbfgs.npz")
+    dec = LGUnet(C.TINY, 1, 1).load_synthetic()
+    prob = DAProblem(dec, _tiny_problem(1))
+    res = one_step_da(prob, nit=2)
+    J = np.array([a + b for a, b in res["J"]])
+    Jr = g["J"].sum(1)
+    print("G5 J per outer pass", J, "reference", Jr, "evals", res["n_eval"], g["n_eval"])
+    assert abs(J[-1] - Jr[-1]) / Jr[-1] < 1e-3
+    xa = res["xa"].cpu().numpy()
+    assert np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]) < 1e-3
+
+
+def test_torch_lbfgs_dropin():
+    """torch.optim.LBFGS drives the HIP closure unchanged through the autograd wrapper."""
+    from vaevar import config as C
+    from vaevar.engine import DAProblem, LGUnet, loss
+
+    g = gold("g5_tiny_lbfgs.npz")
+    dec = LGUnet(C.TINY, 1, 1).load_synthetic()
+    prob = DAProblem(dec, _tiny_problem(1))
+    z = torch.zeros(1, 4, 32, 64, device="cuda", requires_grad=True)
+    lb = torch.optim.LBFGS([z], history_size=10, max_iter=10, line_search_fn="strong_wolfe")
+
+    def closure():
+        lb.zero_grad()
+        obj = loss(prob, z)
+        obj.backward()
+        return obj
+
+    for _ in range(2):
+        lb.step(closure)
+    jb, jo = prob.closure(z.detach(), None)
+    Jr = g["J"].sum(1)[-1]
+    assert abs(jb + jo - Jr) / Jr < 1e-3
+
+
+def test_oracle_on_box_tiny_adam():
+    """BASELINE config 1: 3D-Var on the tiny decoder with 20 Adam iterations (lr 0.1, build choice)
+    against the oracle restatement + torch.optim.Adam on CPU."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.da import one_step_da
+    from vaevar.engine import DAProblem, LGUnet
+
+    p = _tiny_problem(1)
+    dec = LGUnet(C.TINY, 1, 1).load_synthetic()
+    prob = DAProblem(dec, p)
+    res = one_step_da(prob, nit=20, optimizer="adam", lr=0.1, log_terms=False)
+    ro = oracle_problem(p, synth_params(C.TINY), C.TINY)
+    z = torch.zeros(1, 4, 32, 64, requires_grad=True)
+    opt = torch.optim.Adam([z], lr=0.1)
+    for _ in range(20):
+        opt.zero_grad()
+        ro.loss(z).backward()
+        opt.step()
+    with torch.no_grad():
+        xa_ref = ro.analysis(z).numpy()
+    xa = res["xa"].cpu().numpy()
+    e = np.linalg.norm(xa - xa_ref) / np.linalg.norm(xa_ref)
+    print(f"config 1 (Adam x20): xa rel-L2 {e:.2e}")
+    assert e < 1e-4

@@ -1,0 +1,1343 @@
+// libvaevar engine: the Swin-U-Net (networks_old.transformer.LGUnet_all) forward and input-gradient
+// backward as a fixed schedule of HIP kernels over a library-owned weight/activation arena, and the
+// vae4dvar closure (da_4dvar.py:1183-1246) on top of it. C-ABI: include/vaevar.h.
+//
+// Data layout (HBM): tokens NHWC [B][H][W][C] fp32; encoder/decoder towers (Enc_net.enc_list,
+// Dec_net.dec_list, transformer.py:538-594) are stored group-major [G][B*H*W][C] and every kernel
+// runs all G towers in one launch (blockIdx.z / .y = tower). Linear weights are kept as given
+// ([N][K], forward operand) plus a transposed copy ([K][N], backward operand).
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/vaevar.h"
+#include "vv_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define VV_HIP(expr)                                                                           \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return fail((int)e_, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,     \
+                                      hipGetErrorString(e_));                                  \
+  } while (0)
+
+using namespace vv;
+
+// ----------------------------------------------------------------------------
+// configuration
+// ----------------------------------------------------------------------------
+struct Cfg {
+  vv_lgunet_config raw;
+  int G, C0, C1, E, ws;
+  int Himg, Wimg, H0, W0, H1, W1;
+  int d0, d1, h0, h1;
+  int Cin, Cout;
+  std::vector<int> lg_depth, lg_heads;
+};
+
+int parse_cfg(const vv_lgunet_config* c, Cfg& o) {
+  if (!c) return fail(VV_E_ARG, "null config");
+  o.raw = *c;
+  if (c->n_groups < 1 || c->n_groups > kMaxGroups) return fail(VV_E_ARG, "n_groups %d out of range", c->n_groups);
+  if (c->patch_size[0] != 2 || c->patch_size[1] != 2 || c->stride[0] != 2 || c->stride[1] != 2)
+    return fail(VV_E_ARG, "only patch_size = stride = (2,2) is supported");
+  if (c->n_enc_levels != 2) return fail(VV_E_ARG, "only 2 encoder levels (enc_depths of length 2) supported");
+  if (c->window_size != 4) return fail(VV_E_ARG, "only window_size 4 supported");
+  if (c->n_lg_layers < 0 || c->n_lg_layers > 8) return fail(VV_E_ARG, "n_lg_layers out of range");
+  o.G = c->n_groups;
+  o.C0 = c->enc_dim;
+  o.C1 = 2 * c->enc_dim;
+  o.E = c->embed_dim;
+  o.ws = c->window_size;
+  o.Himg = c->img_size[0];
+  o.Wimg = c->img_size[1];
+  o.H0 = o.Himg / 2;
+  o.W0 = o.Wimg / 2;
+  o.H1 = o.H0 / 2;
+  o.W1 = o.W0 / 2;
+  if (o.H1 % o.ws || o.W1 % o.ws || o.Himg % 4 || o.Wimg % 4) return fail(VV_E_ARG, "image size not window-aligned");
+  o.d0 = c->enc_depths[0];
+  o.d1 = c->enc_depths[1];
+  o.h0 = c->enc_heads[0];
+  o.h1 = c->enc_heads[1];
+  if (o.C0 % o.h0 || o.C1 % o.h1) return fail(VV_E_ARG, "dims not divisible by heads");
+  if (o.C0 % 32 || o.E % 32) return fail(VV_E_ARG, "enc_dim and embed_dim must be multiples of 32");
+  o.Cin = o.Cout = 0;
+  for (int g = 0; g < o.G; ++g) {
+    o.Cin += c->inchans[g];
+    o.Cout += c->outchans[g];
+  }
+  o.lg_depth.assign(c->lg_depths, c->lg_depths + c->n_lg_layers);
+  o.lg_heads.assign(c->lg_heads, c->lg_heads + c->n_lg_layers);
+  for (int l = 0; l < c->n_lg_layers; ++l)
+    if (o.E % o.lg_heads[l]) return fail(VV_E_ARG, "embed_dim not divisible by lg heads");
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// parameter enumeration: the exact state_dict keys of LGUnet_all (buffers excluded)
+// ----------------------------------------------------------------------------
+struct PInfo {
+  std::string name;
+  std::vector<int64_t> shape;
+};
+
+void add_block(std::vector<PInfo>& v, const std::string& pre, int C, int nh, int ws) {
+  const int64_t T = (int64_t)(2 * ws - 1) * (2 * ws - 1);
+  v.push_back({pre + ".norm1.weight", {C}});
+  v.push_back({pre + ".norm1.bias", {C}});
+  v.push_back({pre + ".attn.relative_position_bias_table", {T, nh}});
+  v.push_back({pre + ".attn.qkv.weight", {3 * C, C}});
+  v.push_back({pre + ".attn.qkv.bias", {3 * C}});
+  v.push_back({pre + ".attn.proj.weight", {C, C}});
+  v.push_back({pre + ".attn.proj.bias", {C}});
+  v.push_back({pre + ".norm2.weight", {C}});
+  v.push_back({pre + ".norm2.bias", {C}});
+  v.push_back({pre + ".mlp.fc1.weight", {4 * C, C}});
+  v.push_back({pre + ".mlp.fc1.bias", {4 * C}});
+  v.push_back({pre + ".mlp.fc2.weight", {C, 4 * C}});
+  v.push_back({pre + ".mlp.fc2.bias", {C}});
+}
+
+std::vector<PInfo> enumerate_params(const Cfg& c) {
+  std::vector<PInfo> v;
+  const int C0 = c.C0, C1 = c.C1, E = c.E, ws = c.ws;
+  for (int g = 0; g < c.G; ++g) {
+    const std::string e = "enc.enc_list." + std::to_string(g);
+    v.push_back({e + ".absolute_pos_embed", {1, (int64_t)c.H0 * c.W0, C0}});
+    v.push_back({e + ".patch_embed.proj.weight", {C0, c.raw.inchans[g], 2, 2}});
+    v.push_back({e + ".patch_embed.proj.bias", {C0}});
+    for (int b = 0; b < c.d0; ++b) add_block(v, e + ".layers.0.blocks." + std::to_string(b), C0, c.h0, ws);
+    v.push_back({e + ".layers.1.downsample.reduction.weight", {C1, 4 * C0}});
+    v.push_back({e + ".layers.1.downsample.norm.weight", {4 * C0}});
+    v.push_back({e + ".layers.1.downsample.norm.bias", {4 * C0}});
+    for (int b = 0; b < c.d1; ++b) add_block(v, e + ".layers.1.blocks." + std::to_string(b), C1, c.h1, ws);
+    v.push_back({e + ".norm.weight", {C1}});
+    v.push_back({e + ".norm.bias", {C1}});
+  }
+  v.push_back({"enc.proj.weight", {E, (int64_t)C1 * c.G}});
+  v.push_back({"enc.proj.bias", {E}});
+  v.push_back({"net.pos_embed", {1, (int64_t)c.H1 * c.W1, E}});
+  for (size_t l = 0; l < c.lg_depth.size(); ++l)
+    for (int b = 0; b < c.lg_depth[l]; ++b)
+      add_block(v, "net.layers." + std::to_string(l) + ".blocks." + std::to_string(b), E, c.lg_heads[l], ws);
+  for (int g = 0; g < c.G; ++g) {
+    const std::string d = "dec.dec_list." + std::to_string(g);
+    for (int b = 0; b < c.d1; ++b) add_block(v, d + ".layers_up.0.blocks." + std::to_string(b), C1, c.h1, ws);
+    v.push_back({d + ".layers_up.0.upsample.expand.weight", {2 * C1, C1}});
+    v.push_back({d + ".layers_up.0.upsample.norm.weight", {C1 / 2}});
+    v.push_back({d + ".layers_up.0.upsample.norm.bias", {C1 / 2}});
+    for (int b = 0; b < c.d0; ++b) add_block(v, d + ".layers_up.1.blocks." + std::to_string(b), C0, c.h0, ws);
+    v.push_back({d + ".concat_back_dim.0.weight", {C1, 2 * C1}});
+    v.push_back({d + ".concat_back_dim.0.bias", {C1}});
+    v.push_back({d + ".concat_back_dim.1.weight", {C0, 2 * C0}});
+    v.push_back({d + ".concat_back_dim.1.bias", {C0}});
+    v.push_back({d + ".norm_up.weight", {C0}});
+    v.push_back({d + ".norm_up.bias", {C0}});
+  }
+  for (int g = 0; g < c.G; ++g) {
+    const std::string f = "dec.final_proj_list." + std::to_string(g);
+    v.push_back({f + ".weight", {C0, c.raw.outchans[g], 2, 2}});
+    v.push_back({f + ".bias", {c.raw.outchans[g]}});
+  }
+  v.push_back({"dec.proj.weight", {(int64_t)C1 * c.G, E}});
+  v.push_back({"dec.proj.bias", {(int64_t)C1 * c.G}});
+  return v;
+}
+
+int64_t numel(const std::vector<int64_t>& s) {
+  int64_t n = 1;
+  for (auto x : s) n *= x;
+  return n;
+}
+
+// ----------------------------------------------------------------------------
+// device arena
+// ----------------------------------------------------------------------------
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+  ~Arena() {
+    if (base) (void)hipFree(base);
+  }
+  static size_t up(size_t x) { return (x + 255) & ~size_t(255); }
+};
+
+struct Planner {  // two-pass: first count bytes, then hand out pointers
+  size_t bytes = 0;
+  char* base = nullptr;
+  float* f(size_t n) {
+    char* p = base ? base + bytes : nullptr;
+    bytes += Arena::up(n * sizeof(float));
+    return reinterpret_cast<float*>(p);
+  }
+};
+
+// ----------------------------------------------------------------------------
+// model
+// ----------------------------------------------------------------------------
+struct BlockW {
+  const float *n1g, *n1b, *table, *qkvW, *qkvWT, *qkvb, *projW, *projWT, *projb, *n2g, *n2b, *fc1W, *fc1WT, *fc1b,
+      *fc2W, *fc2WT, *fc2b;
+};
+
+struct Stage {
+  int G, H, W, C, heads, depth, M, nWh, nWw;
+  std::vector<std::array<BlockW, kMaxGroups>> w;  // [depth][G]
+  const int* idx[2];                              // window maps, shift 0 / ws/2
+};
+
+struct StageSave {
+  std::vector<float*> x, st1, qkv, P, x1, st2, h1;  // x has depth+1 entries
+};
+
+struct Scratch {
+  float *t1, *t2, *h, *dqkv;
+};
+
+struct Save {
+  StageSave enc0, enc1, dec1, dec0;
+  std::vector<StageSave> lg;
+  float *st_m, *st_en, *ex, *st_ex, *st_nu;
+};
+
+struct Model {
+  Cfg cfg;
+  int B = 1, nslots = 1;
+  std::vector<PInfo> params;
+  std::vector<float*> pptr;  // device pointer per param
+  std::unordered_map<std::string, const float*> W;   // name -> weights ; name + "^T" -> transposed
+  std::unique_ptr<Arena> warena, aarena;
+  Stage enc0, enc1, dec1, dec0;
+  std::vector<Stage> lg;
+  std::vector<Save> saves;
+  Scratch sc;
+  // model-level scratch / gradient buffers
+  float *xm, *cat, *dp, *xe, *yn, *gy, *gd0, *gxe, *gsk0, *gex, *gd1, *gdp, *gsk1, *glg, *gcat, *gxm, *gtok;
+  std::vector<int*> maps_owned;
+  bool loaded = false;
+  int64_t workspace = 0;
+};
+
+struct Problem {
+  bool bound = false;
+  int dec = -1, flow = -1, T = 1, C = 0, Hs = 0, Ws = 0;
+  const float *xb, *yo, *Hm, *R, *mean, *std_, *std_tr;
+  float obs_coeff = 1.f;
+  std::unique_ptr<Arena> arena;
+  float *X, *dec_out, *gdec, *prod, *FI, *FO, *GFO, *GFI, *carry;
+  double *partial, *dJ;
+  int nblk = 1024;
+};
+
+}  // namespace
+
+struct vv_ctx {
+  int device = 0;
+  std::vector<std::unique_ptr<Model>> models;
+  Problem prob;
+  double* red = nullptr;   // reduction scratch
+  float* redf = nullptr;
+  double* dout = nullptr;  // device scalar
+  float* doutf = nullptr;
+};
+
+namespace {
+
+constexpr int kRedBlocks = 1024;
+
+int set_dev(vv_ctx* ctx) {
+  VV_HIP(hipSetDevice(ctx->device));
+  return 0;
+}
+
+std::vector<int> window_map(int B, int H, int W, int ws, int shift) {
+  std::vector<int> m((size_t)B * H * W);
+  const int nWh = H / ws, nWw = W / ws;
+  size_t p = 0;
+  for (int b = 0; b < B; ++b)
+    for (int wr = 0; wr < nWh; ++wr)
+      for (int wc = 0; wc < nWw; ++wc)
+        for (int i = 0; i < ws; ++i)
+          for (int j = 0; j < ws; ++j) {
+            const int r = (wr * ws + i + shift) % H, c = (wc * ws + j + shift) % W;
+            m[p++] = (b * H + r) * W + c;
+          }
+  return m;
+}
+
+int upload_map(Model& m, const std::vector<int>& h, const int** out) {
+  int* d = nullptr;
+  VV_HIP(hipMalloc(&d, h.size() * sizeof(int)));
+  VV_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+  m.maps_owned.push_back(d);
+  *out = d;
+  return 0;
+}
+
+int init_stage(Model& m, Stage& s, int G, int H, int W, int C, int heads, int depth) {
+  s.G = G;
+  s.H = H;
+  s.W = W;
+  s.C = C;
+  s.heads = heads;
+  s.depth = depth;
+  s.M = m.B * H * W;
+  s.nWh = H / m.cfg.ws;
+  s.nWw = W / m.cfg.ws;
+  s.w.assign(depth, {});
+  int rc;
+  if ((rc = upload_map(m, window_map(m.B, H, W, m.cfg.ws, 0), &s.idx[0]))) return rc;
+  if ((rc = upload_map(m, window_map(m.B, H, W, m.cfg.ws, m.cfg.ws / 2), &s.idx[1]))) return rc;
+  return 0;
+}
+
+void plan_stage_save(Planner& P, const Stage& s, StageSave& sv, float* x0_external) {
+  const size_t GMC = (size_t)s.G * s.M * s.C;
+  sv.x.assign(s.depth + 1, nullptr);
+  sv.st1.assign(s.depth, nullptr);
+  sv.qkv = sv.P = sv.x1 = sv.st2 = sv.h1 = sv.st1;
+  sv.x[0] = x0_external ? x0_external : P.f(GMC);
+  const size_t nwin = (size_t)s.M / 16;
+  for (int b = 0; b < s.depth; ++b) {
+    sv.st1[b] = P.f((size_t)s.G * s.M * 2);
+    sv.qkv[b] = P.f(GMC * 3);
+    sv.P[b] = P.f((size_t)s.G * nwin * s.heads * 256);
+    sv.x1[b] = P.f(GMC);
+    sv.st2[b] = P.f((size_t)s.G * s.M * 2);
+    sv.h1[b] = P.f(GMC * 4);
+    sv.x[b + 1] = P.f(GMC);
+  }
+}
+
+int bind_weights(Model& m) {
+  const Cfg& c = m.cfg;
+  auto w = [&](const std::string& n) -> const float* {
+    auto it = m.W.find(n);
+    return it == m.W.end() ? nullptr : it->second;
+  };
+  auto blk = [&](const std::string& pre) {
+    BlockW b;
+    b.n1g = w(pre + ".norm1.weight");
+    b.n1b = w(pre + ".norm1.bias");
+    b.table = w(pre + ".attn.relative_position_bias_table");
+    b.qkvW = w(pre + ".attn.qkv.weight");
+    b.qkvWT = w(pre + ".attn.qkv.weight^T");
+    b.qkvb = w(pre + ".attn.qkv.bias");
+    b.projW = w(pre + ".attn.proj.weight");
+    b.projWT = w(pre + ".attn.proj.weight^T");
+    b.projb = w(pre + ".attn.proj.bias");
+    b.n2g = w(pre + ".norm2.weight");
+    b.n2b = w(pre + ".norm2.bias");
+    b.fc1W = w(pre + ".mlp.fc1.weight");
+    b.fc1WT = w(pre + ".mlp.fc1.weight^T");
+    b.fc1b = w(pre + ".mlp.fc1.bias");
+    b.fc2W = w(pre + ".mlp.fc2.weight");
+    b.fc2WT = w(pre + ".mlp.fc2.weight^T");
+    b.fc2b = w(pre + ".mlp.fc2.bias");
+    return b;
+  };
+  for (int g = 0; g < c.G; ++g) {
+    const std::string e = "enc.enc_list." + std::to_string(g), d = "dec.dec_list." + std::to_string(g);
+    for (int b = 0; b < c.d0; ++b) {
+      m.enc0.w[b][g] = blk(e + ".layers.0.blocks." + std::to_string(b));
+      m.dec0.w[b][g] = blk(d + ".layers_up.1.blocks." + std::to_string(b));
+    }
+    for (int b = 0; b < c.d1; ++b) {
+      m.enc1.w[b][g] = blk(e + ".layers.1.blocks." + std::to_string(b));
+      m.dec1.w[b][g] = blk(d + ".layers_up.0.blocks." + std::to_string(b));
+    }
+  }
+  for (size_t l = 0; l < m.lg.size(); ++l)
+    for (int b = 0; b < m.lg[l].depth; ++b)
+      m.lg[l].w[b][0] = blk("net.layers." + std::to_string(l) + ".blocks." + std::to_string(b));
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// forward / backward of one Swin stage (BasicLayer / BasicLayer_up / Layer: blocks only)
+// ----------------------------------------------------------------------------
+GemmArgs gemm_base(int M, int N, int K, int G, int epi) {
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.ksplit = K;
+  a.lda = K;
+  a.lda2 = 0;
+  a.ldc = N;
+  a.ldr = N;
+  a.ldaux = N;
+  a.epi = epi;
+  a.ngroups = G;
+  return a;
+}
+
+LnArgs ln_base(int rows, int C, int G, float eps) {
+  LnArgs a;
+  memset(&a, 0, sizeof(a));
+  a.rows = rows;
+  a.C = C;
+  a.ldx = a.ldy = a.lddy = a.ldres = C;
+  a.mode = LN_ROWMAP;
+  a.eps = eps;
+  a.ngroups = G;
+  return a;
+}
+
+#define CK(expr)                                                                                   \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) return fail((int)e_, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,         \
+                                      hipGetErrorString(e_));                                      \
+  } while (0)
+
+int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st) {
+  const int G = S.G, M = S.M, C = S.C;
+  const size_t MC = (size_t)M * C;
+  const int nwin = M / 16;
+  for (int b = 0; b < S.depth; ++b) {
+    const int shift = (b % 2 == 0) ? 0 : ws / 2;
+    const int* idx = S.idx[shift ? 1 : 0];
+    // LN1 -> window order
+    LnArgs ln = ln_base(M, C, G, 1e-5f);
+    ln.map = idx;
+    for (int g = 0; g < G; ++g)
+      ln.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, sc.t1 + g * MC, sv.st1[b] + (size_t)g * M * 2,
+                 nullptr, nullptr};
+    CK(layernorm_fwd(ln, st));
+    // qkv
+    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE);
+    for (int g = 0; g < G; ++g)
+      q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
+    CK(gemm_nt(q, st));
+    // window attention
+    AttnArgs at;
+    memset(&at, 0, sizeof(at));
+    at.nwin = nwin;
+    at.nWh = S.nWh;
+    at.nWw = S.nWw;
+    at.ws = ws;
+    at.shift = shift;
+    at.H = S.H;
+    at.C = C;
+    at.heads = S.heads;
+    at.scale = (float)std::pow((double)(C / S.heads), -0.5);
+    at.ngroups = G;
+    for (int g = 0; g < G; ++g)
+      at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, sc.t2 + g * MC,
+                 sv.P[b] + (size_t)g * nwin * S.heads * 256, nullptr, nullptr};
+    CK(attn_fwd(at, st));
+    // proj + window reverse + residual
+    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID);
+    p.crow = idx;
+    for (int g = 0; g < G; ++g)
+      p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
+                nullptr};
+    CK(gemm_nt(p, st));
+    // LN2
+    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
+    for (int g = 0; g < G; ++g)
+      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, sc.t1 + g * MC, sv.st2[b] + (size_t)g * M * 2,
+                  nullptr, nullptr};
+    CK(layernorm_fwd(ln2, st));
+    // fc1 + GELU
+    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU);
+    for (int g = 0; g < G; ++g)
+      f1.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, sc.h + g * MC * 4, nullptr,
+                 sv.h1[b] + g * MC * 4};
+    CK(gemm_nt(f1, st));
+    // fc2 + residual
+    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID);
+    for (int g = 0; g < G; ++g)
+      f2.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, sv.x[b + 1] + g * MC, sv.x1[b] + g * MC,
+                 nullptr};
+    CK(gemm_nt(f2, st));
+  }
+  return 0;
+}
+
+// gx: [G][M][C] gradient w.r.t. the stage output, overwritten in place with the input gradient
+int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, float* gx, hipStream_t st) {
+  const int G = S.G, M = S.M, C = S.C;
+  const size_t MC = (size_t)M * C;
+  const int nwin = M / 16;
+  for (int b = S.depth - 1; b >= 0; --b) {
+    const int shift = (b % 2 == 0) ? 0 : ws / 2;
+    const int* idx = S.idx[shift ? 1 : 0];
+    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU);
+    for (int g = 0; g < G; ++g)
+      f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
+    CK(gemm_nt(f2, st));
+    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE);
+    for (int g = 0; g < G; ++g)
+      f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
+    CK(gemm_nt(f1, st));
+    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
+    for (int g = 0; g < G; ++g)
+      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
+                  sc.t1 + g * MC, gx + g * MC};
+    CK(layernorm_bwd(ln2, st));
+    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE);
+    p.arow = idx;
+    for (int g = 0; g < G; ++g)
+      p.g[g] = {gx + g * MC, nullptr, S.w[b][g].projWT, nullptr, sc.t2 + g * MC, nullptr, nullptr};
+    CK(gemm_nt(p, st));
+    AttnArgs at;
+    memset(&at, 0, sizeof(at));
+    at.nwin = nwin;
+    at.nWh = S.nWh;
+    at.nWw = S.nWw;
+    at.ws = ws;
+    at.shift = shift;
+    at.H = S.H;
+    at.C = C;
+    at.heads = S.heads;
+    at.scale = (float)std::pow((double)(C / S.heads), -0.5);
+    at.ngroups = G;
+    for (int g = 0; g < G; ++g)
+      at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, nullptr, sv.P[b] + (size_t)g * nwin * S.heads * 256,
+                 sc.t2 + g * MC, sc.dqkv + g * MC * 3};
+    CK(attn_bwd(at, st));
+    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE);
+    for (int g = 0; g < G; ++g)
+      q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
+    CK(gemm_nt(q, st));
+    LnArgs ln1 = ln_base(M, C, G, 1e-5f);
+    ln1.map = idx;
+    for (int g = 0; g < G; ++g)
+      ln1.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, nullptr, gx + g * MC, sv.st1[b] + (size_t)g * M * 2,
+                  sc.t1 + g * MC, gx + g * MC};
+    CK(layernorm_bwd(ln1, st));
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// model construction
+// ----------------------------------------------------------------------------
+int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int* id) {
+  auto m = std::make_unique<Model>();
+  int r;
+  if ((r = parse_cfg(rc, m->cfg))) return r;
+  if (B < 1 || nslots < 1) return fail(VV_E_ARG, "batch and n_slots must be >= 1");
+  m->B = B;
+  m->nslots = nslots;
+  const Cfg& c = m->cfg;
+  m->params = enumerate_params(c);
+  // weights arena: params + transposed copies of 2-D weights
+  size_t wbytes = 0;
+  for (auto& p : m->params) {
+    wbytes += Arena::up(numel(p.shape) * 4);
+    if (p.shape.size() == 2 && p.name.size() > 7 && p.name.compare(p.name.size() - 7, 7, ".weight") == 0)
+      wbytes += Arena::up(numel(p.shape) * 4);
+  }
+  m->warena = std::make_unique<Arena>();
+  if (hipMalloc(&m->warena->base, wbytes) != hipSuccess) return fail(VV_E_ALLOC, "weights: %zu bytes", wbytes);
+  m->warena->cap = wbytes;
+  size_t off = 0;
+  for (auto& p : m->params) {
+    float* d = reinterpret_cast<float*>(m->warena->base + off);
+    off += Arena::up(numel(p.shape) * 4);
+    m->pptr.push_back(d);
+    m->W[p.name] = d;
+    if (p.shape.size() == 2 && p.name.size() > 7 && p.name.compare(p.name.size() - 7, 7, ".weight") == 0) {
+      float* t = reinterpret_cast<float*>(m->warena->base + off);
+      off += Arena::up(numel(p.shape) * 4);
+      m->W[p.name + "^T"] = t;
+    }
+  }
+  // stages
+  if ((r = init_stage(*m, m->enc0, c.G, c.H0, c.W0, c.C0, c.h0, c.d0))) return r;
+  if ((r = init_stage(*m, m->enc1, c.G, c.H1, c.W1, c.C1, c.h1, c.d1))) return r;
+  if ((r = init_stage(*m, m->dec1, c.G, c.H1, c.W1, c.C1, c.h1, c.d1))) return r;
+  if ((r = init_stage(*m, m->dec0, c.G, c.H0, c.W0, c.C0, c.h0, c.d0))) return r;
+  m->lg.resize(c.lg_depth.size());
+  for (size_t l = 0; l < m->lg.size(); ++l)
+    if ((r = init_stage(*m, m->lg[l], 1, c.H1, c.W1, c.E, c.lg_heads[l], c.lg_depth[l]))) return r;
+  bind_weights(*m);
+  // activation arena (two passes: size, then carve)
+  const size_t M0 = (size_t)B * c.H0 * c.W0, M1 = (size_t)B * c.H1 * c.W1;
+  const size_t G = c.G;
+  for (int pass = 0; pass < 2; ++pass) {
+    Planner P;
+    if (pass == 1) P.base = m->aarena->base;
+    // scratch sized for the largest stage
+    size_t mx = 0;
+    auto upd = [&](const Stage& s) { mx = std::max(mx, (size_t)s.G * s.M * s.C); };
+    upd(m->enc0);
+    upd(m->enc1);
+    for (auto& s : m->lg) upd(s);
+    m->sc.t1 = P.f(mx);
+    m->sc.t2 = P.f(mx);
+    m->sc.h = P.f(mx * 4);
+    m->sc.dqkv = P.f(mx * 3);
+    m->xm = P.f(G * M1 * 4 * c.C0);
+    m->cat = P.f(M1 * G * c.C1);
+    m->dp = P.f(M1 * G * c.C1);
+    m->xe = P.f(G * M0 * c.C0);
+    m->yn = P.f(G * M0 * c.C0);
+    m->gy = P.f(G * M0 * c.C0);
+    m->gd0 = P.f(G * M0 * c.C0);
+    m->gxe = P.f(G * M0 * c.C0);
+    m->gsk0 = P.f(G * M0 * c.C0);
+    m->gex = P.f(G * M1 * 2 * c.C1);
+    m->gd1 = P.f(G * M1 * c.C1);
+    m->gdp = P.f(M1 * G * c.C1);
+    m->gsk1 = P.f(G * M1 * c.C1);
+    m->glg = P.f(M1 * c.E);
+    m->gcat = P.f(M1 * G * c.C1);
+    m->gxm = P.f(G * M1 * 4 * c.C0);
+    m->saves.assign(nslots, Save{});
+    for (int s = 0; s < nslots; ++s) {
+      Save& sv = m->saves[s];
+      plan_stage_save(P, m->enc0, sv.enc0, nullptr);
+      sv.st_m = P.f(G * M1 * 2);
+      plan_stage_save(P, m->enc1, sv.enc1, nullptr);
+      sv.st_en = P.f(G * M1 * 2);
+      sv.lg.resize(m->lg.size());
+      for (size_t l = 0; l < m->lg.size(); ++l)
+        plan_stage_save(P, m->lg[l], sv.lg[l], l == 0 ? nullptr : sv.lg[l - 1].x.back());
+      plan_stage_save(P, m->dec1, sv.dec1, nullptr);
+      sv.ex = P.f(G * M1 * 2 * c.C1);
+      sv.st_ex = P.f(G * M0 * 2);
+      plan_stage_save(P, m->dec0, sv.dec0, nullptr);
+      sv.st_nu = P.f(G * M0 * 2);
+    }
+    if (pass == 0) {
+      m->aarena = std::make_unique<Arena>();
+      if (hipMalloc(&m->aarena->base, P.bytes) != hipSuccess)
+        return fail(VV_E_ALLOC, "activations: %zu bytes", P.bytes);
+      m->aarena->cap = P.bytes;
+      m->workspace = (int64_t)(P.bytes + wbytes);
+    }
+  }
+  *id = (int)ctx->models.size();
+  ctx->models.push_back(std::move(m));
+  return 0;
+}
+
+Model* get_model(vv_ctx* ctx, int id) {
+  if (!ctx || id < 0 || id >= (int)ctx->models.size()) return nullptr;
+  return ctx->models[id].get();
+}
+
+// ----------------------------------------------------------------------------
+// whole-network forward / backward   (LGUnet_all.forward, transformer.py:747-752)
+// ----------------------------------------------------------------------------
+int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipStream_t st) {
+  const Cfg& c = m.cfg;
+  Save& sv = m.saves[slot];
+  const int G = c.G, B = m.B, C0 = c.C0, C1 = c.C1, E = c.E;
+  const int M0 = B * c.H0 * c.W0, M1 = B * c.H1 * c.W1;
+  const size_t M0C0 = (size_t)M0 * C0, M1C1 = (size_t)M1 * C1;
+  auto w = [&](const std::string& n) { return m.W.at(n); };
+  auto eg = [&](int g) { return "enc.enc_list." + std::to_string(g); };
+  auto dg = [&](int g) { return "dec.dec_list." + std::to_string(g); };
+
+  // ---- Enc_net: PatchEmbed + absolute_pos_embed (transformer.py:392-394)
+  PatchArgs pa;
+  memset(&pa, 0, sizeof(pa));
+  pa.B = B;
+  pa.Himg = c.Himg;
+  pa.Wimg = c.Wimg;
+  pa.Cimg = c.Cin;
+  pa.Ctok = C0;
+  pa.img = in;
+  pa.ngroups = G;
+  for (int g = 0, off = 0; g < G; off += c.raw.inchans[g], ++g) {
+    pa.g[g].w = w(eg(g) + ".patch_embed.proj.weight");
+    pa.g[g].bias = w(eg(g) + ".patch_embed.proj.bias");
+    pa.g[g].pos = w(eg(g) + ".absolute_pos_embed");
+    pa.g[g].tok = sv.enc0.x[0] + g * M0C0;
+    pa.g[g].cin_off = off;
+    pa.g[g].cin = c.raw.inchans[g];
+  }
+  CK(patch_embed_fwd(pa, st));
+  int r;
+  if ((r = stage_fwd(m.enc0, sv.enc0, m.sc, c.ws, st))) return r;
+  float* skip0 = sv.enc0.x.back();
+  // PatchMerging: gather + LN(4C0, eps 1e-6) + reduction (transformer.py:76-96)
+  LnArgs lm = ln_base(M1, 4 * C0, G, 1e-6f);
+  lm.mode = LN_MERGE;
+  lm.Hin = c.H0;
+  lm.Win = c.W0;
+  lm.ldx = C0;
+  for (int g = 0; g < G; ++g)
+    lm.g[g] = {skip0 + g * M0C0, w(eg(g) + ".layers.1.downsample.norm.weight"),
+               w(eg(g) + ".layers.1.downsample.norm.bias"), m.xm + (size_t)g * M1 * 4 * C0,
+               sv.st_m + (size_t)g * M1 * 2, nullptr, nullptr};
+  CK(layernorm_fwd(lm, st));
+  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE);
+  for (int g = 0; g < G; ++g)
+    red.g[g] = {m.xm + (size_t)g * M1 * 4 * C0, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight"), nullptr,
+                sv.enc1.x[0] + g * M1C1, nullptr, nullptr};
+  CK(gemm_nt(red, st));
+  if ((r = stage_fwd(m.enc1, sv.enc1, m.sc, c.ws, st))) return r;
+  float* skip1 = sv.enc1.x.back();
+  // encoder norm -> concat (transformer.py:402, 567)
+  LnArgs le = ln_base(M1, C1, G, 1e-6f);
+  le.ldy = G * C1;
+  for (int g = 0; g < G; ++g)
+    le.g[g] = {skip1 + g * M1C1, w(eg(g) + ".norm.weight"), w(eg(g) + ".norm.bias"), m.cat + g * C1,
+               sv.st_en + (size_t)g * M1 * 2, nullptr, nullptr};
+  CK(layernorm_fwd(le, st));
+  // Enc_net.proj (+ LG_net.pos_embed, transformer.py:704)
+  float* lg_in = m.lg.empty() ? sv.dec1.x[0] : sv.lg[0].x[0];
+  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID);
+  ep.rmod = c.H1 * c.W1;
+  ep.ldr = E;
+  ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
+  CK(gemm_nt(ep, st));
+  // ---- LG_net layers
+  for (size_t l = 0; l < m.lg.size(); ++l)
+    if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st))) return r;
+  const float* lg_out = m.lg.empty() ? lg_in : sv.lg.back().x.back();
+  // ---- Dec_net.proj (transformer.py:600)
+  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE);
+  dp.g[0] = {lg_out, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m.dp, nullptr, nullptr};
+  CK(gemm_nt(dp, st));
+  // concat_back_dim[0]: cat(x, skip1) (transformer.py:468-469)
+  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE);
+  c0.lda = G * C1;
+  c0.ksplit = C1;
+  c0.lda2 = C1;
+  for (int g = 0; g < G; ++g)
+    c0.g[g] = {m.dp + g * C1, skip1 + g * M1C1, w(dg(g) + ".concat_back_dim.0.weight"),
+               w(dg(g) + ".concat_back_dim.0.bias"), sv.dec1.x[0] + g * M1C1, nullptr, nullptr};
+  CK(gemm_nt(c0, st));
+  if ((r = stage_fwd(m.dec1, sv.dec1, m.sc, c.ws, st))) return r;
+  // PatchExpand: expand (no bias) + rearrange + LN(C0, eps 1e-6) (transformer.py:106-118)
+  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE);
+  for (int g = 0; g < G; ++g)
+    ex.g[g] = {sv.dec1.x.back() + g * M1C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight"), nullptr,
+               sv.ex + (size_t)g * M1 * 2 * C1, nullptr, nullptr};
+  CK(gemm_nt(ex, st));
+  LnArgs lx = ln_base(M0, C0, G, 1e-6f);
+  lx.mode = LN_EXPAND;
+  lx.Hin = c.H1;
+  lx.Win = c.W1;
+  lx.ldx = 2 * C1;
+  for (int g = 0; g < G; ++g)
+    lx.g[g] = {sv.ex + (size_t)g * M1 * 2 * C1, w(dg(g) + ".layers_up.0.upsample.norm.weight"),
+               w(dg(g) + ".layers_up.0.upsample.norm.bias"), m.xe + g * M0C0, sv.st_ex + (size_t)g * M0 * 2, nullptr,
+               nullptr};
+  CK(layernorm_fwd(lx, st));
+  // concat_back_dim[1]: cat(x, skip0)
+  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE);
+  c1.lda = C0;
+  c1.ksplit = C0;
+  c1.lda2 = C0;
+  for (int g = 0; g < G; ++g)
+    c1.g[g] = {m.xe + g * M0C0, skip0 + g * M0C0, w(dg(g) + ".concat_back_dim.1.weight"),
+               w(dg(g) + ".concat_back_dim.1.bias"), sv.dec0.x[0] + g * M0C0, nullptr, nullptr};
+  CK(gemm_nt(c1, st));
+  if ((r = stage_fwd(m.dec0, sv.dec0, m.sc, c.ws, st))) return r;
+  // norm_up (transformer.py:472)
+  LnArgs lu = ln_base(M0, C0, G, 1e-6f);
+  for (int g = 0; g < G; ++g)
+    lu.g[g] = {sv.dec0.x.back() + g * M0C0, w(dg(g) + ".norm_up.weight"), w(dg(g) + ".norm_up.bias"),
+               m.yn + g * M0C0, sv.st_nu + (size_t)g * M0 * 2, nullptr, nullptr};
+  CK(layernorm_fwd(lu, st));
+  // ConvTranspose2d + mean/std reorder (transformer.py:605-623, quirk Q2)
+  PatchArgs pu;
+  memset(&pu, 0, sizeof(pu));
+  pu.B = B;
+  pu.Himg = c.Himg;
+  pu.Wimg = c.Wimg;
+  pu.Cimg = c.Cout;
+  pu.Ctok = C0;
+  pu.climit = climit > 0 ? std::min(climit, c.Cout) : c.Cout;
+  pu.img_out = out;
+  pu.ngroups = G;
+  int moff = 0, soff = 0;
+  for (int g = 0; g < G; ++g) soff += c.raw.outchans[g] / 2;
+  for (int g = 0; g < G; ++g) {
+    const std::string f = "dec.final_proj_list." + std::to_string(g);
+    pu.g[g].w = w(f + ".weight");
+    pu.g[g].bias = w(f + ".bias");
+    pu.g[g].tok = m.yn + g * M0C0;
+    pu.g[g].cout = c.raw.outchans[g];
+    pu.g[g].mean_off = moff;
+    pu.g[g].std_off = soff;
+    moff += c.raw.outchans[g] / 2;
+    soff += c.raw.outchans[g] - c.raw.outchans[g] / 2;
+  }
+  CK(patch_unembed_fwd(pu, st));
+  return 0;
+}
+
+int model_bwd(Model& m, int slot, const float* dout, float* din, const float* add, int climit, hipStream_t st) {
+  const Cfg& c = m.cfg;
+  Save& sv = m.saves[slot];
+  const int G = c.G, B = m.B, C0 = c.C0, C1 = c.C1, E = c.E;
+  const int M0 = B * c.H0 * c.W0, M1 = B * c.H1 * c.W1;
+  const size_t M0C0 = (size_t)M0 * C0, M1C1 = (size_t)M1 * C1;
+  auto w = [&](const std::string& n) { return m.W.at(n); };
+  auto eg = [&](int g) { return "enc.enc_list." + std::to_string(g); };
+  auto dg = [&](int g) { return "dec.dec_list." + std::to_string(g); };
+  int r;
+  // ConvTranspose2d backward
+  PatchArgs pu;
+  memset(&pu, 0, sizeof(pu));
+  pu.B = B;
+  pu.Himg = c.Himg;
+  pu.Wimg = c.Wimg;
+  pu.Cimg = c.Cout;
+  pu.Ctok = C0;
+  pu.climit = climit > 0 ? std::min(climit, c.Cout) : c.Cout;
+  pu.img = dout;
+  pu.ngroups = G;
+  int moff = 0, soff = 0;
+  for (int g = 0; g < G; ++g) soff += c.raw.outchans[g] / 2;
+  for (int g = 0; g < G; ++g) {
+    pu.g[g].w = w("dec.final_proj_list." + std::to_string(g) + ".weight");
+    pu.g[g].tok = m.gy + g * M0C0;
+    pu.g[g].cout = c.raw.outchans[g];
+    pu.g[g].mean_off = moff;
+    pu.g[g].std_off = soff;
+    moff += c.raw.outchans[g] / 2;
+    soff += c.raw.outchans[g] - c.raw.outchans[g] / 2;
+  }
+  CK(patch_unembed_bwd(pu, st));
+  // norm_up backward
+  LnArgs lu = ln_base(M0, C0, G, 1e-6f);
+  for (int g = 0; g < G; ++g)
+    lu.g[g] = {sv.dec0.x.back() + g * M0C0, w(dg(g) + ".norm_up.weight"), nullptr, m.gd0 + g * M0C0,
+               sv.st_nu + (size_t)g * M0 * 2, m.gy + g * M0C0, nullptr};
+  CK(layernorm_bwd(lu, st));
+  if ((r = stage_bwd(m.dec0, sv.dec0, m.sc, c.ws, m.gd0, st))) return r;
+  // concat_back_dim[1] backward: left -> PatchExpand output, right -> skip0
+  for (int half = 0; half < 2; ++half) {
+    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE);
+    for (int g = 0; g < G; ++g)
+      cb.g[g] = {m.gd0 + g * M0C0, nullptr, w(dg(g) + ".concat_back_dim.1.weight^T") + (size_t)half * C0 * C0,
+                 nullptr, (half ? m.gsk0 : m.gxe) + g * M0C0, nullptr, nullptr};
+    CK(gemm_nt(cb, st));
+  }
+  // PatchExpand backward: LN (expand mode) then expand^T
+  LnArgs lx = ln_base(M0, C0, G, 1e-6f);
+  lx.mode = LN_EXPAND;
+  lx.Hin = c.H1;
+  lx.Win = c.W1;
+  lx.ldx = lx.ldy = 2 * C1;
+  for (int g = 0; g < G; ++g)
+    lx.g[g] = {sv.ex + (size_t)g * M1 * 2 * C1, w(dg(g) + ".layers_up.0.upsample.norm.weight"), nullptr,
+               m.gex + (size_t)g * M1 * 2 * C1, sv.st_ex + (size_t)g * M0 * 2, m.gxe + g * M0C0, nullptr};
+  CK(layernorm_bwd(lx, st));
+  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE);
+  for (int g = 0; g < G; ++g)
+    ex.g[g] = {m.gex + (size_t)g * M1 * 2 * C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight^T"), nullptr,
+               m.gd1 + g * M1C1, nullptr, nullptr};
+  CK(gemm_nt(ex, st));
+  if ((r = stage_bwd(m.dec1, sv.dec1, m.sc, c.ws, m.gd1, st))) return r;
+  // concat_back_dim[0] backward: left -> Dec_net.proj output slice g, right -> skip1
+  for (int half = 0; half < 2; ++half) {
+    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE);
+    if (!half) cb.ldc = G * C1;
+    for (int g = 0; g < G; ++g)
+      cb.g[g] = {m.gd1 + g * M1C1, nullptr, w(dg(g) + ".concat_back_dim.0.weight^T") + (size_t)half * C1 * C1,
+                 nullptr, half ? m.gsk1 + g * M1C1 : m.gdp + g * C1, nullptr, nullptr};
+    CK(gemm_nt(cb, st));
+  }
+  // Dec_net.proj backward
+  float* glg = m.glg;
+  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE);
+  dp.g[0] = {m.gdp, nullptr, w("dec.proj.weight^T"), nullptr, glg, nullptr, nullptr};
+  CK(gemm_nt(dp, st));
+  for (int l = (int)m.lg.size() - 1; l >= 0; --l)
+    if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st))) return r;
+  // pos_embed: identity ; Enc_net.proj backward
+  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE);
+  ep.g[0] = {glg, nullptr, w("enc.proj.weight^T"), nullptr, m.gcat, nullptr, nullptr};
+  CK(gemm_nt(ep, st));
+  // encoder norm backward (+ skip1 gradient), in place on gsk1
+  float* skip1 = sv.enc1.x.back();
+  LnArgs le = ln_base(M1, C1, G, 1e-6f);
+  le.lddy = G * C1;
+  for (int g = 0; g < G; ++g)
+    le.g[g] = {skip1 + g * M1C1, w(eg(g) + ".norm.weight"), nullptr, m.gsk1 + g * M1C1, sv.st_en + (size_t)g * M1 * 2,
+               m.gcat + g * C1, m.gsk1 + g * M1C1};
+  CK(layernorm_bwd(le, st));
+  if ((r = stage_bwd(m.enc1, sv.enc1, m.sc, c.ws, m.gsk1, st))) return r;
+  // PatchMerging backward: reduction^T, then LN (merge mode) scattered onto level-0 tokens (+ skip0 grad)
+  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE);
+  for (int g = 0; g < G; ++g)
+    red.g[g] = {m.gsk1 + g * M1C1, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight^T"), nullptr,
+                m.gxm + (size_t)g * M1 * 4 * C0, nullptr, nullptr};
+  CK(gemm_nt(red, st));
+  float* skip0 = sv.enc0.x.back();
+  LnArgs lm = ln_base(M1, 4 * C0, G, 1e-6f);
+  lm.mode = LN_MERGE;
+  lm.Hin = c.H0;
+  lm.Win = c.W0;
+  lm.ldx = lm.ldy = lm.ldres = C0;
+  for (int g = 0; g < G; ++g)
+    lm.g[g] = {skip0 + g * M0C0, w(eg(g) + ".layers.1.downsample.norm.weight"), nullptr, m.gsk0 + g * M0C0,
+               sv.st_m + (size_t)g * M1 * 2, m.gxm + (size_t)g * M1 * 4 * C0, m.gsk0 + g * M0C0};
+  CK(layernorm_bwd(lm, st));
+  if ((r = stage_bwd(m.enc0, sv.enc0, m.sc, c.ws, m.gsk0, st))) return r;
+  // PatchEmbed backward (+ add)
+  PatchArgs pa;
+  memset(&pa, 0, sizeof(pa));
+  pa.B = B;
+  pa.Himg = c.Himg;
+  pa.Wimg = c.Wimg;
+  pa.Cimg = c.Cin;
+  pa.Ctok = C0;
+  pa.img_out = din;
+  pa.add_img = add;
+  pa.ngroups = G;
+  for (int g = 0, off = 0; g < G; off += c.raw.inchans[g], ++g) {
+    pa.g[g].w = w(eg(g) + ".patch_embed.proj.weight");
+    pa.g[g].dtok = m.gsk0 + g * M0C0;
+    pa.g[g].cin_off = off;
+    pa.g[g].cin = c.raw.inchans[g];
+  }
+  CK(patch_embed_bwd(pa, st));
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// closure  (da_4dvar.py:1183-1208 loss(z) + backward)
+// ----------------------------------------------------------------------------
+int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
+  Problem& P = ctx->prob;
+  if (!P.bound) return fail(VV_E_STATE, "vv_bind_problem first");
+  Model& D = *ctx->models[P.dec];
+  Model* F = P.flow >= 0 ? ctx->models[P.flow].get() : nullptr;
+  const int C = P.C, HW = P.Hs * P.Ws;
+  const size_t CHW = (size_t)C * HW;
+  int r;
+  // forward: x_0 = decoder(z)*stdTr*std + xb
+  if ((r = model_fwd(D, 0, z, P.dec_out, C, st))) return r;
+  MisfitArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  ma.C = C;
+  ma.Hs = ma.Hl = P.Hs;
+  ma.Ws = ma.Wl = P.Ws;
+  ma.net = P.dec_out;
+  ma.scale = P.std_tr;
+  ma.scale2 = P.std_;
+  ma.xb = P.xb;
+  ma.yo = P.yo;
+  ma.Hm = P.Hm;
+  ma.R = P.R;
+  ma.x_out = P.X;
+  ma.flow_in = P.T > 1 ? P.FI : nullptr;
+  ma.mean = P.mean;
+  ma.std_ = P.std_;
+  ma.partial = P.partial;
+  ma.nblk = P.nblk;
+  CK(misfit_fwd(ma, st));
+  for (int t = 1; t < P.T; ++t) {
+    // x_t = integrate(x_{t-1}) = flow((x - mean)/std)[:C]*std + mean   (da_4dvar.py:666-681)
+    if ((r = model_fwd(*F, t - 1, P.FI + (t - 1) * CHW, P.FO + (size_t)(t - 1) * F->cfg.Cout * HW, C, st))) return r;
+    MisfitArgs mt = ma;
+    mt.net = P.FO + (size_t)(t - 1) * F->cfg.Cout * HW;
+    mt.scale = P.std_;
+    mt.scale2 = nullptr;
+    mt.xb = nullptr;
+    mt.offset = P.mean;
+    mt.yo = P.yo + t * CHW;
+    mt.Hm = P.Hm + t * CHW;
+    mt.R = P.R + t * CHW;
+    mt.x_out = P.X + t * CHW;
+    mt.flow_in = t < P.T - 1 ? P.FI + t * CHW : nullptr;
+    mt.partial = P.partial + (size_t)t * P.nblk;
+    CK(misfit_fwd(mt, st));
+  }
+  CK(reduce_final(P.partial, P.nblk * P.T, P.dJ + 1, st));
+  CK(reduce_sumsq(z, (int64_t)D.B * D.cfg.Cin * D.cfg.Himg * D.cfg.Wimg, P.partial + (size_t)P.T * P.nblk, P.nblk, st));
+  CK(reduce_final(P.partial + (size_t)P.T * P.nblk, P.nblk, P.dJ, st));
+  if (!grad) return 0;
+  // backward
+  const float* carry = nullptr;
+  for (int t = P.T - 1; t >= 1; --t) {
+    MisfitBwdArgs mb;
+    memset(&mb, 0, sizeof(mb));
+    mb.C = C;
+    mb.Hs = mb.Hl = P.Hs;
+    mb.Ws = mb.Wl = P.Ws;
+    mb.x = P.X + t * CHW;
+    mb.yo = P.yo + t * CHW;
+    mb.Hm = P.Hm + t * CHW;
+    mb.R = P.R + t * CHW;
+    mb.g_carry = carry;
+    mb.coeff = P.obs_coeff;
+    mb.scale = P.std_;
+    mb.g_net = P.GFO;
+    mb.net_cstride = F->cfg.Cout;
+    CK(misfit_bwd(mb, st));
+    if ((r = model_bwd(*F, t - 1, P.GFO, P.GFI, nullptr, C, st))) return r;
+    CK(scale_channels(P.GFI, P.carry, P.std_, C, HW, nullptr, st));
+    carry = P.carry;
+  }
+  MisfitBwdArgs mb;
+  memset(&mb, 0, sizeof(mb));
+  mb.C = C;
+  mb.Hs = mb.Hl = P.Hs;
+  mb.Ws = mb.Wl = P.Ws;
+  mb.x = P.X;
+  mb.yo = P.yo;
+  mb.Hm = P.Hm;
+  mb.R = P.R;
+  mb.g_carry = carry;
+  mb.coeff = P.obs_coeff;
+  mb.scale = P.prod;
+  mb.g_net = P.gdec;
+  mb.net_cstride = D.cfg.Cout;
+  CK(misfit_bwd(mb, st));
+  // grad_z = z + decoder^T(g)   (d/dz of sum(z^2)/2 is z)
+  if ((r = model_bwd(D, 0, P.gdec, grad, z, C, st))) return r;
+  return 0;
+}
+
+__global__ void k_prod(const float* a, const float* b, float* o, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = a[i] * b[i];
+}
+__global__ void k_half(double* d) {
+  if (threadIdx.x == 0) {
+    d[0] *= 0.5;
+    d[1] *= 0.5;
+  }
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int vv_version(void) { return 100; }
+
+int vv_last_error(char* buf, int cap) {
+  if (!buf || cap <= 0) return VV_E_ARG;
+  snprintf(buf, cap, "%s", g_err.c_str());
+  return 0;
+}
+
+int vv_lgunet_param_count(const vv_lgunet_config* cfg, int* count) {
+  Cfg c;
+  int r = parse_cfg(cfg, c);
+  if (r) return r;
+  *count = (int)enumerate_params(c).size();
+  return 0;
+}
+
+int vv_lgunet_param_info(const vv_lgunet_config* cfg, int index, char* name, int name_cap, int64_t* shape,
+                         int* ndim) {
+  Cfg c;
+  int r = parse_cfg(cfg, c);
+  if (r) return r;
+  auto v = enumerate_params(c);
+  if (index < 0 || index >= (int)v.size()) return fail(VV_E_ARG, "param index %d out of range", index);
+  if (name) snprintf(name, name_cap, "%s", v[index].name.c_str());
+  if (ndim) *ndim = (int)v[index].shape.size();
+  if (shape)
+    for (size_t i = 0; i < v[index].shape.size(); ++i) shape[i] = v[index].shape[i];
+  return 0;
+}
+
+int vv_ctx_create(int device, vv_ctx** out) {
+  if (!out) return fail(VV_E_ARG, "null out");
+  int n = 0;
+  VV_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(VV_E_ARG, "device %d of %d", device, n);
+  auto* c = new vv_ctx();
+  c->device = device;
+  VV_HIP(hipSetDevice(device));
+  VV_HIP(hipMalloc(&c->red, kRedBlocks * sizeof(double)));
+  VV_HIP(hipMalloc(&c->redf, kRedBlocks * sizeof(float)));
+  VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
+  VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
+  *out = c;
+  return 0;
+}
+
+int vv_ctx_destroy(vv_ctx* ctx) {
+  if (!ctx) return 0;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  for (auto& m : ctx->models)
+    for (int* p : m->maps_owned) (void)hipFree(p);
+  (void)hipFree(ctx->red);
+  (void)hipFree(ctx->redf);
+  (void)hipFree(ctx->dout);
+  (void)hipFree(ctx->doutf);
+  delete ctx;
+  return 0;
+}
+
+int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_slots, int* model_id) {
+  if (!ctx || !model_id) return fail(VV_E_ARG, "null argument");
+  int r = set_dev(ctx);
+  if (r) return r;
+  return create_model(ctx, cfg, batch, n_slots, model_id);
+}
+
+int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
+  Model* m = get_model(ctx, model_id);
+  if (!m || !ptrs) return fail(VV_E_ARG, "bad model or ptrs");
+  if (n != (int)m->params.size()) return fail(VV_E_ARG, "expected %zu params, got %d", m->params.size(), n);
+  int r = set_dev(ctx);
+  if (r) return r;
+  for (int i = 0; i < n; ++i) {
+    if (!ptrs[i]) return fail(VV_E_ARG, "null pointer for param %s", m->params[i].name.c_str());
+    VV_HIP(hipMemcpy(m->pptr[i], ptrs[i], numel(m->params[i].shape) * 4, hipMemcpyDefault));
+  }
+  for (auto& p : m->params) {
+    auto it = m->W.find(p.name + "^T");
+    if (it == m->W.end()) continue;
+    VV_HIP(vv::transpose2d(m->W[p.name], const_cast<float*>(it->second), (int)p.shape[0], (int)p.shape[1], 0));
+  }
+  VV_HIP(hipDeviceSynchronize());
+  m->loaded = true;
+  return 0;
+}
+
+int vv_model_workspace_bytes(vv_ctx* ctx, int model_id, int64_t* bytes) {
+  Model* m = get_model(ctx, model_id);
+  if (!m || !bytes) return fail(VV_E_ARG, "bad model");
+  *bytes = m->workspace;
+  return 0;
+}
+
+int vv_model_forward(vv_ctx* ctx, int model_id, int slot, const float* in, float* out, int out_limit, void* stream) {
+  Model* m = get_model(ctx, model_id);
+  if (!m || !in || !out) return fail(VV_E_ARG, "bad model or pointers");
+  if (!m->loaded) return fail(VV_E_STATE, "weights not loaded");
+  if (slot < 0 || slot >= m->nslots) return fail(VV_E_ARG, "slot %d out of range", slot);
+  int r = set_dev(ctx);
+  if (r) return r;
+  return model_fwd(*m, slot, in, out, out_limit, (hipStream_t)stream);
+}
+
+int vv_model_backward(vv_ctx* ctx, int model_id, int slot, const float* dout, float* din, const float* add,
+                      int out_limit, void* stream) {
+  Model* m = get_model(ctx, model_id);
+  if (!m || !dout || !din) return fail(VV_E_ARG, "bad model or pointers");
+  if (!m->loaded) return fail(VV_E_STATE, "weights not loaded");
+  if (slot < 0 || slot >= m->nslots) return fail(VV_E_ARG, "slot %d out of range", slot);
+  int r = set_dev(ctx);
+  if (r) return r;
+  return model_bwd(*m, slot, dout, din, add, out_limit, (hipStream_t)stream);
+}
+
+int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int C, int Hs, int Ws, const float* xb,
+                    const float* yo, const float* Hmask, const float* R, const float* mean, const float* std_,
+                    const float* std_tr, float obs_coeff) {
+  Model* D = get_model(ctx, dec_model_id);
+  if (!D) return fail(VV_E_ARG, "bad decoder model");
+  if (T < 1 || C < 1) return fail(VV_E_ARG, "bad T/C");
+  if (D->B != 1) return fail(VV_E_ARG, "closure needs a batch-1 decoder");
+  if (D->cfg.Cout < C) return fail(VV_E_ARG, "decoder produces %d channels < C=%d", D->cfg.Cout, C);
+  if (Hs != D->cfg.Himg || Ws != D->cfg.Wimg)
+    return fail(VV_E_ARG, "state grid %dx%d != network grid %dx%d (nearest-interpolated grids not yet supported)", Hs,
+                Ws, D->cfg.Himg, D->cfg.Wimg);
+  Model* F = nullptr;
+  if (T > 1) {
+    F = get_model(ctx, flow_model_id);
+    if (!F) return fail(VV_E_ARG, "T > 1 needs a flow model");
+    if (F->cfg.Cin != C || F->cfg.Cout < C || F->nslots < T - 1 || F->B != 1)
+      return fail(VV_E_ARG, "flow model shape/slots incompatible (Cin %d Cout %d slots %d)", F->cfg.Cin, F->cfg.Cout,
+                  F->nslots);
+    if (F->cfg.Himg != Hs || F->cfg.Wimg != Ws) return fail(VV_E_ARG, "flow grid mismatch");
+  }
+  if (!xb || !yo || !Hmask || !R || !mean || !std_ || !std_tr) return fail(VV_E_ARG, "null problem buffer");
+  int r = set_dev(ctx);
+  if (r) return r;
+  Problem& P = ctx->prob;
+  P = Problem();
+  P.dec = dec_model_id;
+  P.flow = T > 1 ? flow_model_id : -1;
+  P.T = T;
+  P.C = C;
+  P.Hs = Hs;
+  P.Ws = Ws;
+  P.xb = xb;
+  P.yo = yo;
+  P.Hm = Hmask;
+  P.R = R;
+  P.mean = mean;
+  P.std_ = std_;
+  P.std_tr = std_tr;
+  P.obs_coeff = obs_coeff;
+  const size_t CHW = (size_t)C * Hs * Ws;
+  const size_t HW = (size_t)Hs * Ws;
+  const int fcout = F ? F->cfg.Cout : 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    Planner pl;
+    if (pass) pl.base = P.arena->base;
+    P.X = pl.f(CHW * T);
+    P.dec_out = pl.f((size_t)D->cfg.Cout * HW);
+    P.gdec = pl.f((size_t)D->cfg.Cout * HW);
+    P.prod = pl.f(C);
+    P.FI = pl.f(CHW * std::max(T - 1, 1));
+    P.FO = pl.f((size_t)fcout * HW * std::max(T - 1, 1) + 1);
+    P.GFO = pl.f((size_t)fcout * HW + 1);
+    P.GFI = pl.f(CHW);
+    P.carry = pl.f(CHW);
+    double* pd = reinterpret_cast<double*>(pl.f((size_t)2 * P.nblk * (T + 1) + 8));
+    if (pass) {
+      P.partial = pd;
+      P.dJ = pd + (size_t)P.nblk * (T + 1) + 2;
+    }
+    if (!pass) {
+      P.arena = std::make_unique<Arena>();
+      if (hipMalloc(&P.arena->base, pl.bytes) != hipSuccess) return fail(VV_E_ALLOC, "problem arena");
+      P.arena->cap = pl.bytes;
+    }
+  }
+  hipLaunchKernelGGL(k_prod, dim3((C + 255) / 256), dim3(256), 0, 0, std_tr, std_, P.prod, C);
+  VV_HIP(hipGetLastError());
+  VV_HIP(hipDeviceSynchronize());
+  P.bound = true;
+  return 0;
+}
+
+int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, void* stream) {
+  if (!ctx || !z) return fail(VV_E_ARG, "null argument");
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  if ((r = closure_impl(ctx, z, grad_z, st))) return r;
+  hipLaunchKernelGGL(k_half, dim3(1), dim3(64), 0, st, ctx->prob.dJ);
+  VV_HIP(hipGetLastError());
+  if (d_J) VV_HIP(hipMemcpyAsync(d_J, ctx->prob.dJ, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream) {
+  int r = vv_closure_async(ctx, z, grad_z, nullptr, stream);
+  if (r) return r;
+  double h[2];
+  hipStream_t st = (hipStream_t)stream;
+  VV_HIP(hipMemcpyAsync(h, ctx->prob.dJ, sizeof(h), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipStreamSynchronize(st));
+  if (J_b) *J_b = h[0];
+  if (J_o) *J_o = h[1];
+  return 0;
+}
+
+int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream) {
+  if (!ctx || !z || !xa) return fail(VV_E_ARG, "null argument");
+  Problem& P = ctx->prob;
+  if (!P.bound) return fail(VV_E_STATE, "vv_bind_problem first");
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  Model& D = *ctx->models[P.dec];
+  if ((r = model_fwd(D, 0, z, P.dec_out, P.C, st))) return r;
+  MisfitArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  ma.C = P.C;
+  ma.Hs = ma.Hl = P.Hs;
+  ma.Ws = ma.Wl = P.Ws;
+  ma.net = P.dec_out;
+  ma.scale = P.std_tr;
+  ma.scale2 = P.std_;
+  ma.xb = P.xb;
+  ma.yo = P.yo;
+  ma.Hm = P.Hm;
+  ma.R = P.R;
+  ma.x_out = xa;
+  ma.partial = P.partial;
+  ma.nblk = P.nblk;
+  CK(misfit_fwd(ma, st));
+  return 0;
+}
+
+int vv_state_ptr(vv_ctx* ctx, const float** x) {
+  if (!ctx || !x || !ctx->prob.bound) return fail(VV_E_STATE, "no problem bound");
+  *x = ctx->prob.X;
+  return 0;
+}
+
+int vv_dot(vv_ctx* ctx, const float* a, const float* b, int64_t n, double* out, void* stream) {
+  if (!ctx || !a || !b || !out) return fail(VV_E_ARG, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  VV_HIP(vv::vec_dot(a, b, n, ctx->red, kRedBlocks, ctx->dout, st));
+  VV_HIP(hipMemcpyAsync(out, ctx->dout, sizeof(double), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipStreamSynchronize(st));
+  return 0;
+}
+int vv_abssum(vv_ctx* ctx, const float* a, int64_t n, double* out, void* stream) {
+  if (!ctx || !a || !out) return fail(VV_E_ARG, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  VV_HIP(vv::vec_abssum(a, n, ctx->red, kRedBlocks, ctx->dout, st));
+  VV_HIP(hipMemcpyAsync(out, ctx->dout, sizeof(double), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipStreamSynchronize(st));
+  return 0;
+}
+int vv_absmax(vv_ctx* ctx, const float* a, int64_t n, float* out, void* stream) {
+  if (!ctx || !a || !out) return fail(VV_E_ARG, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  VV_HIP(vv::vec_absmax(a, n, ctx->redf, kRedBlocks, ctx->doutf, st));
+  VV_HIP(hipMemcpyAsync(out, ctx->doutf, sizeof(float), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipStreamSynchronize(st));
+  return 0;
+}
+int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream) {
+  if (!ctx || !y || !x) return fail(VV_E_ARG, "null argument");
+  VV_HIP(vv::vec_axpy(y, x, alpha, n, (hipStream_t)stream));
+  return 0;
+}
+int vv_axpby(vv_ctx* ctx, float* out, const float* x, float a, const float* y, float b, int64_t n, void* stream) {
+  if (!ctx || !out || !x) return fail(VV_E_ARG, "null argument");
+  VV_HIP(vv::vec_axpby(out, x, a, y, b, n, (hipStream_t)stream));
+  return 0;
+}
+int vv_scale(vv_ctx* ctx, float* y, float alpha, int64_t n, void* stream) {
+  if (!ctx || !y) return fail(VV_E_ARG, "null argument");
+  VV_HIP(vv::vec_scale(y, alpha, n, (hipStream_t)stream));
+  return 0;
+}
+int vv_copy(vv_ctx* ctx, float* dst, const float* src, int64_t n, void* stream) {
+  if (!ctx || !dst || !src) return fail(VV_E_ARG, "null argument");
+  VV_HIP(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+            float eps, int step, void* stream) {
+  if (!ctx || !p || !g || !m || !v || step < 1) return fail(VV_E_ARG, "bad argument");
+  const float bc1 = 1.0f - std::pow(beta1, (float)step);
+  const float bc2 = 1.0f - std::pow(beta2, (float)step);
+  VV_HIP(vv::adam_step(p, g, m, v, n, lr, beta1, beta2, eps, bc1, std::sqrt(bc2), (hipStream_t)stream));
+  return 0;
+}
+
+int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C, int tile,
+            void* stream) {
+  if (!ctx || !A || !B || !C) return fail(VV_E_ARG, "null argument");
+  GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE);
+  a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
+  VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile));
+  return 0;
+}
+
+}  // extern "C"

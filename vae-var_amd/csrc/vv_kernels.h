@@ -1,0 +1,196 @@
+// Internal kernel interface of libvaevar (not the public C-ABI; see include/vaevar.h).
+// All kernels are fp32, gfx950-only, launched on the caller's stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace vv {
+
+constexpr int kMaxGroups = 8;
+
+// ---------------------------------------------------------------------------
+// GEMM: C[o(r)][n] = epi( sum_k A(r,k) * B[n][k] )      (B is [N][K] = nn.Linear weight)
+//   A(r,k) = k <  ksplit : A [arow ? arow[r] : r][k]          (row stride lda)
+//            k >= ksplit : A2[r][k - ksplit]                  (row stride lda2) -- torch.cat on -1
+//   o(r)   = crow ? crow[r] : r
+// ---------------------------------------------------------------------------
+enum Epi : int {
+  EPI_STORE = 0,   // C = acc (+bias)
+  EPI_GELU = 1,    // aux = acc + bias ; C = gelu(aux)        (Mlp fc1 fwd, swinblock.py:23-29)
+  EPI_RESID = 2,   // C = R[o % rmod] + acc (+bias)            (residual adds)
+  EPI_DGELU = 3,   // C = acc * gelu'(aux[o])                  (fc1 backward)
+};
+
+struct GemmGroup {
+  const float* A;
+  const float* A2;
+  const float* B;
+  const float* bias;
+  float* C;
+  const float* R;
+  float* aux;
+};
+
+struct GemmArgs {
+  int M, N, K, ksplit;
+  int lda, lda2, ldc, ldr, ldaux;
+  int rmod;
+  const int* arow;
+  const int* crow;
+  int epi;
+  int ngroups;
+  GemmGroup g[kMaxGroups];
+};
+
+hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1);
+
+// ---------------------------------------------------------------------------
+// LayerNorm over the last dim, one wave per output row.
+// ---------------------------------------------------------------------------
+enum LnMode : int {
+  LN_ROWMAP = 0,   // in row = map ? map[r] : r
+  LN_MERGE = 1,    // PatchMerging gather (transformer.py:86-91): row (b,h,w) of the half grid,
+                   // feature q*Cs + c, q = dh + 2*dw, from token (b, 2h+dh, 2w+dw) of (Hin,Win)
+  LN_EXPAND = 2,   // PatchExpand rearrange (transformer.py:114): out (b,y,x) <- in row (b,y/2,x/2),
+                   // segment (y%2)*2 + x%2 of width C; (Hin,Win) = half grid
+};
+
+struct LnGroup {
+  const float* x;     // input
+  const float* gamma;
+  const float* beta;
+  float* y;           // output (fwd) / dx destination (bwd)
+  float* stats;       // [rows][2] mean, rstd
+  const float* dy;    // bwd: gradient wrt LN output
+  const float* res;   // bwd: added to dx (may alias y), may be null
+};
+
+struct LnArgs {
+  int rows, C;        // output rows and normalised width
+  int ldx, ldy, lddy, ldres;
+  int mode;
+  const int* map;
+  int Hin, Win;       // mode geometry (input grid for MERGE, half grid for EXPAND)
+  float eps;
+  int ngroups;
+  LnGroup g[kMaxGroups];
+};
+
+hipError_t layernorm_fwd(const LnArgs& a, hipStream_t s);
+hipError_t layernorm_bwd(const LnArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Window attention (swinblock.py:133-172) on qkv in window order.
+// ---------------------------------------------------------------------------
+struct AttnGroup {
+  const float* qkv;   // [nwin*N][3C]
+  const float* table; // relative_position_bias_table [(2ws-1)^2][nH]
+  float* o;           // fwd out [nwin*N][C]
+  float* P;           // saved softmax [nwin][nH][N][N]
+  const float* dO;    // bwd in
+  float* dqkv;        // bwd out [nwin*N][3C]
+};
+
+struct AttnArgs {
+  int nwin;           // windows over the whole batch
+  int nWh, nWw;       // windows per image per axis
+  int ws, shift, H;   // H: image rows (mask labels, quirk Q1)
+  int C, heads;
+  float scale;
+  int ngroups;
+  AttnGroup g[kMaxGroups];
+};
+
+hipError_t attn_fwd(const AttnArgs& a, hipStream_t s);
+hipError_t attn_bwd(const AttnArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// PatchEmbed conv (k = stride = 2) + absolute_pos_embed, and ConvTranspose2d (k = stride = 2)
+// ---------------------------------------------------------------------------
+struct PatchGroup {
+  const float* w;     // conv: [Cout][cin][2][2] ; convT: [Cin][cout][2][2]
+  const float* bias;
+  const float* pos;   // conv: absolute_pos_embed [Ho*Wo][Cout]
+  float* tok;         // tokens [B*Ho*Wo][Ctok]
+  const float* dtok;  // bwd
+  int cin_off, cin;   // conv: channel slice of the image ; convT: mean/std channel placement
+  int mean_off, std_off, cout;
+};
+
+struct PatchArgs {
+  int B, Himg, Wimg, Cimg;   // image tensor (B, Cimg, Himg, Wimg)
+  int Ctok;                  // token width (enc_dim)
+  int climit;                // convT: only channels < climit are produced / back-propagated
+  const float* img;          // conv fwd input / convT bwd input (dimg)
+  float* img_out;            // conv bwd output (dz) / convT fwd output
+  const float* add_img;      // conv bwd: added to dz (latent regulariser term z), may be null
+  int ngroups;
+  PatchGroup g[kMaxGroups];
+};
+
+hipError_t patch_embed_fwd(const PatchArgs& a, hipStream_t s);
+hipError_t patch_embed_bwd(const PatchArgs& a, hipStream_t s);   // img_out = add_img + d img
+hipError_t patch_unembed_fwd(const PatchArgs& a, hipStream_t s); // ConvTranspose2d
+hipError_t patch_unembed_bwd(const PatchArgs& a, hipStream_t s); // dtok <- d out
+
+// ---------------------------------------------------------------------------
+// DA misfit (da_4dvar.py:1183-1208) and vector primitives
+// ---------------------------------------------------------------------------
+struct MisfitArgs {
+  int C, Hs, Ws;          // state grid
+  int Hl, Wl;             // network grid (nearest maps when different)
+  const int* mi;          // [Hs] state row -> net row (nearest)  (null: identity)
+  const int* mj;          // [Ws]
+  const int* ri0;         // adjoint row ranges [Hl+1] (null: identity)
+  const int* rj0;         // [Wl+1]
+  const float* net;       // network output (C', Hl, Wl) first C channels used
+  int net_cstride;        // channels in net tensor
+  const float* scale;     // [C] first multiply (stdTr for the decoder, std for the flow)
+  const float* scale2;    // null or [C] second multiply (std for the decoder): (net*scale)*scale2
+  const float* offset;    // null or [C] per-channel additive (mean, flow step)
+  const float* xb;        // null or (C,Hs,Ws) additive field (background, decoder step)
+  const float* yo;
+  const float* Hm;
+  const float* R;
+  float* x_out;           // state x_t (C,Hs,Ws)
+  float* flow_in;         // null or (C,Hl,Wl) next-step normalised input (x - mean)/std
+  const float* mean;      // for flow_in
+  const float* std_;
+  double* partial;        // per-block partial sums of H(x-yo)^2/R
+  int nblk;
+};
+
+hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s);
+// g_state = coeff*H*(x-yo)/R + g_carry ; g_net(net grid) = adjoint(g_state) * scale
+struct MisfitBwdArgs {
+  int C, Hs, Ws, Hl, Wl;
+  const int* ri0; const int* rj0; const int* mi; const int* mj;
+  const float* x; const float* yo; const float* Hm; const float* R;
+  const float* g_carry;   // null or (C,Hs,Ws) gradient arriving from later times
+  float coeff;
+  const float* scale;     // [C]
+  float* g_net;           // (C', Hl, Wl) first C channels written, the rest zero-filled
+  int net_cstride;
+  float* g_state;         // scratch (C,Hs,Ws) (needed when maps are not identity)
+};
+hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s);
+// g_x(prev step) = g_flow_in / std (+ nothing else): flow input normalisation adjoint
+hipError_t scale_channels(const float* in, float* out, const float* inv_std, int C, int HW, const float* add,
+                          hipStream_t s);
+
+hipError_t reduce_sumsq(const float* x, int64_t n, double* partial, int nblk, hipStream_t s);
+hipError_t reduce_final(const double* partial, int n, double* out, hipStream_t s);
+
+// L-BFGS / Adam vector primitives (torch/optim/lbfgs.py, torch/optim/adam.py)
+hipError_t vec_dot(const float* a, const float* b, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
+hipError_t vec_axpy(float* y, const float* x, float alpha, int64_t n, hipStream_t s);       // y += alpha x
+hipError_t vec_axpby(float* out, const float* x, float a, const float* y, float b, int64_t n, hipStream_t s);
+hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s);
+hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float* out, hipStream_t s);
+hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
+hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                     float eps, float bc1, float bc2_sqrt, hipStream_t s);
+hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStream_t s);
+hipError_t fill(float* p, float v, int64_t n, hipStream_t s);
+
+}  // namespace vv

@@ -1,0 +1,634 @@
+// Non-GEMM kernels of the Swin-U-Net engine and the DA inner loop (fp32, gfx950).
+//   LayerNorm fwd/bwd with the window / PatchMerging / PatchExpand gathers folded into addressing
+//   window attention fwd/bwd (16-token windows, relative-position bias, quirk-Q1 shift mask)
+//   PatchEmbed conv + absolute_pos_embed, ConvTranspose2d with the quirk-Q2 channel reorder
+//   misfit J_o and its adjoint, vector primitives of L-BFGS / Adam
+#include "vv_kernels.h"
+
+namespace vv {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ============================================================================
+// LayerNorm  (nn.LayerNorm: biased variance, y = (x-mean)/sqrt(var+eps)*g + b)
+// ============================================================================
+struct LnAddr {
+  // element (r, c) of the *input* row for output row r, in a buffer with row stride ld
+  int mode, C, Hin, Win;
+  const int* map;
+  __device__ __forceinline__ size_t off(int r, int c, int ld) const {
+    if (mode == LN_ROWMAP) {
+      const int ir = map ? map[r] : r;
+      return (size_t)ir * ld + c;
+    } else if (mode == LN_MERGE) {
+      const int Hh = Hin >> 1, Wh = Win >> 1;
+      const int b = r / (Hh * Wh);
+      const int rem = r - b * Hh * Wh;
+      const int h = rem / Wh, w = rem - h * Wh;
+      const int Cs = C >> 2;
+      const int q = c / Cs, cc = c - q * Cs;
+      const int tok = (b * Hin + 2 * h + (q & 1)) * Win + 2 * w + (q >> 1);
+      return (size_t)tok * ld + cc;
+    } else {  // LN_EXPAND: output grid (2Hin, 2Win); input row (b, y/2, x/2), segment (y%2)*2 + x%2
+      const int Wo = Win * 2, Ho = Hin * 2;
+      const int b = r / (Ho * Wo);
+      const int rem = r - b * Ho * Wo;
+      const int y = rem / Wo, x = rem - y * Wo;
+      const int ir = (b * Hin + (y >> 1)) * Win + (x >> 1);
+      const int seg = (y & 1) * 2 + (x & 1);
+      return (size_t)ir * ld + seg * C + c;
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const LnGroup G = a.g[blockIdx.y];
+  const LnAddr ad{a.mode, a.C, a.Hin, a.Win, a.map};
+  const int C = a.C;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += G.x[ad.off(r, c, a.ldx)];
+  const float mean = wave_sum(s) / (float)C;
+  float v = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float d = G.x[ad.off(r, c, a.ldx)] - mean;
+    v += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)C + a.eps);
+  float* y = G.y + (size_t)r * a.ldy;
+  for (int c = lane; c < C; c += 64) {
+    const float xh = (G.x[ad.off(r, c, a.ldx)] - mean) * rstd;
+    y[c] = xh * G.gamma[c] + G.beta[c];
+  }
+  if (lane == 0 && G.stats) {
+    G.stats[2 * r] = mean;
+    G.stats[2 * r + 1] = rstd;
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) ; written back at the input position
+__global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const LnGroup G = a.g[blockIdx.y];
+  const LnAddr ad{a.mode, a.C, a.Hin, a.Win, a.map};
+  const int C = a.C;
+  const float mean = G.stats[2 * r], rstd = G.stats[2 * r + 1];
+  const float* dy = G.dy + (size_t)r * a.lddy;
+  float s1 = 0.f, s2 = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float gdy = G.gamma[c] * dy[c];
+    const float xh = (G.x[ad.off(r, c, a.ldx)] - mean) * rstd;
+    s1 += gdy;
+    s2 += gdy * xh;
+  }
+  const float m1 = wave_sum(s1) / (float)C;
+  const float m2 = wave_sum(s2) / (float)C;
+  for (int c = lane; c < C; c += 64) {
+    const float gdy = G.gamma[c] * dy[c];
+    const float xh = (G.x[ad.off(r, c, a.ldx)] - mean) * rstd;
+    float dx = rstd * (gdy - m1 - xh * m2);
+    if (G.res) dx += G.res[ad.off(r, c, a.ldres)];
+    G.y[ad.off(r, c, a.ldy)] = dx;
+  }
+}
+
+hipError_t layernorm_fwd(const LnArgs& a, hipStream_t s) {
+  if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ln_fwd, dim3((a.rows + 3) / 4, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t layernorm_bwd(const LnArgs& a, hipStream_t s) {
+  if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ln_bwd, dim3((a.rows + 3) / 4, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// Window attention, 4x4 windows (N = 16 tokens), one wave per (window, head)
+// ============================================================================
+constexpr int WN_ = 16;
+
+__device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* table, int win, int h, int i,
+                                                int j) {
+  const int ws = a.ws;
+  const int ri = i / ws, ci = i - ri * ws, rj = j / ws, cj = j - rj * ws;
+  float b = table[((ri - rj + ws - 1) * (2 * ws - 1) + (ci - cj + ws - 1)) * a.heads + h];
+  if (a.shift > 0) {
+    // quirk Q1 (swinblock.py:240-258): labels depend on the (shifted-frame) row only
+    const int wr = (win % (a.nWh * a.nWw)) / a.nWw;
+    const int yi = wr * ws + ri, yj = wr * ws + rj;
+    const int H = a.H;
+    const int li = yi < H - ws ? 0 : (yi < H - a.shift ? 1 : 2);
+    const int lj = yj < H - ws ? 0 : (yj < H - a.shift ? 1 : 2);
+    if (li != lj) b += -100.0f;
+  }
+  return b;
+}
+
+__global__ __launch_bounds__(64) void k_attn_fwd(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int win = blockIdx.x, h = blockIdx.y;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int lane = threadIdx.x;
+  const int C = a.C, hd = C / a.heads, ldq = 3 * C;
+  const int st = hd + 1;
+  float* q = sm;
+  float* k = q + WN_ * st;
+  float* v = k + WN_ * st;
+  float* p = v + WN_ * st;  // [16][17]
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * hd;
+  for (int idx = lane; idx < WN_ * hd; idx += 64) {
+    const int t = idx / hd, d = idx - t * hd;
+    const float* row = base + (size_t)t * ldq + d;
+    q[t * st + d] = row[0];
+    k[t * st + d] = row[C];
+    v[t * st + d] = row[2 * C];
+  }
+  __syncthreads();
+  const int i = lane >> 2, j0 = (lane & 3) * 4;
+  float sv[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int d = 0; d < hd; ++d) {
+    const float qd = q[i * st + d] * a.scale;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) sv[jj] += qd * k[(j0 + jj) * st + d];
+  }
+  // NOTE: the reference scales q before the product (q = q * scale; q @ k^T, swinblock.py:151-152)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    sv[jj] += attn_bias_mask(a, G.table, win, h, i, j0 + jj);
+    mx = fmaxf(mx, sv[jj]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 1));
+  mx = fmaxf(mx, __shfl_xor(mx, 2));
+  float sum = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    sv[jj] = expf(sv[jj] - mx);
+    sum += sv[jj];
+  }
+  sum += __shfl_xor(sum, 1);
+  sum += __shfl_xor(sum, 2);
+  const float inv = 1.0f / sum;
+  float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const float pv = sv[jj] * inv;
+    p[i * 17 + j0 + jj] = pv;
+    Pg[i * WN_ + j0 + jj] = pv;
+  }
+  __syncthreads();
+  float* ob = G.o + (size_t)win * WN_ * C + h * hd;
+  for (int idx = lane; idx < WN_ * hd; idx += 64) {
+    const int t = idx / hd, d = idx - t * hd;
+    float acc = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < WN_; ++jj) acc += p[t * 17 + jj] * v[jj * st + d];
+    ob[(size_t)t * C + d] = acc;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_attn_bwd(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int win = blockIdx.x, h = blockIdx.y;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int lane = threadIdx.x;
+  const int C = a.C, hd = C / a.heads, ldq = 3 * C;
+  const int st = hd + 1;
+  float* q = sm;
+  float* k = q + WN_ * st;
+  float* v = k + WN_ * st;
+  float* dO = v + WN_ * st;
+  float* p = dO + WN_ * st;  // [16][17]
+  float* ds = p + WN_ * 17;  // [16][17]
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * hd;
+  const float* dob = G.dO + (size_t)win * WN_ * C + h * hd;
+  for (int idx = lane; idx < WN_ * hd; idx += 64) {
+    const int t = idx / hd, d = idx - t * hd;
+    const float* row = base + (size_t)t * ldq + d;
+    q[t * st + d] = row[0];
+    k[t * st + d] = row[C];
+    v[t * st + d] = row[2 * C];
+    dO[t * st + d] = dob[(size_t)t * C + d];
+  }
+  const float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
+  for (int idx = lane; idx < WN_ * WN_; idx += 64) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
+  __syncthreads();
+  const int i = lane >> 2, j0 = (lane & 3) * 4;
+  float dp[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int d = 0; d < hd; ++d) {
+    const float od = dO[i * st + d];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) dp[jj] += od * v[(j0 + jj) * st + d];
+  }
+  float rd = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) rd += p[i * 17 + j0 + jj] * dp[jj];
+  rd += __shfl_xor(rd, 1);
+  rd += __shfl_xor(rd, 2);
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) ds[i * 17 + j0 + jj] = p[i * 17 + j0 + jj] * (dp[jj] - rd);
+  __syncthreads();
+  float* gb = G.dqkv + (size_t)win * WN_ * ldq + h * hd;
+  for (int idx = lane; idx < WN_ * hd; idx += 64) {
+    const int t = idx / hd, d = idx - t * hd;
+    float aq = 0.f, ak = 0.f, av = 0.f;
+#pragma unroll
+    for (int u = 0; u < WN_; ++u) {
+      aq += ds[t * 17 + u] * k[u * st + d];   // dQ[t] = sum_j dS[t][j] k[j]
+      ak += ds[u * 17 + t] * q[u * st + d];   // dK[t] = sum_i dS[i][t] q[i]
+      av += p[u * 17 + t] * dO[u * st + d];   // dV[t] = sum_i P[i][t] dO[i]
+    }
+    float* row = gb + (size_t)t * ldq + d;
+    row[0] = aq * a.scale;
+    row[C] = ak * a.scale;
+    row[2 * C] = av;
+  }
+}
+
+hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
+  if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  const int hd = a.C / a.heads;
+  const size_t lds = (3 * WN_ * (hd + 1) + WN_ * 17) * sizeof(float);
+  hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
+  if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  const int hd = a.C / a.heads;
+  const size_t lds = (4 * WN_ * (hd + 1) + 2 * WN_ * 17) * sizeof(float);
+  hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// PatchEmbed (Conv2d k=s=2) + absolute_pos_embed   (transformer.py:41-49, 392-394)
+// ============================================================================
+__global__ __launch_bounds__(256) void k_patch_fwd(PatchArgs a) {
+  const PatchGroup G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2;
+  const int total = a.B * Ho * Wo * a.Ctok;
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= total) return;
+  const int co = id % a.Ctok;
+  const int tok = id / a.Ctok;
+  const int b = tok / (Ho * Wo);
+  const int rem = tok - b * Ho * Wo;
+  const int ho = rem / Wo, wo = rem - ho * Wo;
+  float acc = 0.f;
+  for (int ci = 0; ci < G.cin; ++ci) {
+    const float* img = a.img + (((size_t)b * a.Cimg + G.cin_off + ci) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
+    const float* w = G.w + ((size_t)co * G.cin + ci) * 4;
+    acc += w[0] * img[0] + w[1] * img[1] + w[2] * img[a.Wimg] + w[3] * img[a.Wimg + 1];
+  }
+  G.tok[(size_t)tok * a.Ctok + co] = (acc + G.bias[co]) + G.pos[(size_t)rem * a.Ctok + co];
+}
+
+__global__ __launch_bounds__(256) void k_patch_bwd(PatchArgs a) {
+  const int total = a.B * a.Cimg * a.Himg * a.Wimg;
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= total) return;
+  const int x = id % a.Wimg;
+  const int y = (id / a.Wimg) % a.Himg;
+  const int ch = (id / (a.Wimg * a.Himg)) % a.Cimg;
+  const int b = id / (a.Wimg * a.Himg * a.Cimg);
+  float acc = 0.f;
+  for (int g = 0; g < a.ngroups; ++g) {
+    const PatchGroup& G = a.g[g];
+    if (ch < G.cin_off || ch >= G.cin_off + G.cin) continue;
+    const int ci = ch - G.cin_off;
+    const int Wo = a.Wimg / 2, Ho = a.Himg / 2;
+    const int tok = (b * Ho + (y >> 1)) * Wo + (x >> 1);
+    const float* dt = G.dtok + (size_t)tok * a.Ctok;
+    const float* w = G.w + (size_t)ci * 4 + (y & 1) * 2 + (x & 1);
+    const size_t wstride = (size_t)G.cin * 4;
+    for (int co = 0; co < a.Ctok; ++co) acc += dt[co] * w[co * wstride];
+  }
+  if (a.add_img) acc += a.add_img[id];
+  a.img_out[id] = acc;
+}
+
+// ConvTranspose2d(Ctok -> cout, k=s=2) with Dec_net's mean/std channel reorder (quirk Q2)
+__device__ __forceinline__ bool unembed_chan(const PatchArgs& a, int ch, int& g, int& co) {
+  for (g = 0; g < a.ngroups; ++g) {
+    const PatchGroup& G = a.g[g];
+    const int half = G.cout / 2;
+    if (ch >= G.mean_off && ch < G.mean_off + half) {
+      co = ch - G.mean_off;
+      return true;
+    }
+    if (ch >= G.std_off && ch < G.std_off + (G.cout - half)) {
+      co = half + ch - G.std_off;
+      return true;
+    }
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_unembed_fwd(PatchArgs a) {
+  const int total = a.B * a.climit * a.Himg * a.Wimg;
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= total) return;
+  const int x = id % a.Wimg;
+  const int y = (id / a.Wimg) % a.Himg;
+  const int ch = (id / (a.Wimg * a.Himg)) % a.climit;
+  const int b = id / (a.Wimg * a.Himg * a.climit);
+  int g, co;
+  if (!unembed_chan(a, ch, g, co)) return;
+  const PatchGroup& G = a.g[g];
+  const int Wo = a.Wimg / 2, Ho = a.Himg / 2;
+  const int tok = (b * Ho + (y >> 1)) * Wo + (x >> 1);
+  const float* t = G.tok + (size_t)tok * a.Ctok;
+  const float* w = G.w + (size_t)co * 4 + (y & 1) * 2 + (x & 1);
+  const size_t wstride = (size_t)G.cout * 4;
+  float acc = 0.f;
+  for (int ci = 0; ci < a.Ctok; ++ci) acc += t[ci] * w[ci * wstride];
+  a.img_out[(((size_t)b * a.Cimg + ch) * a.Himg + y) * a.Wimg + x] = acc + G.bias[co];
+}
+
+__global__ __launch_bounds__(256) void k_unembed_bwd(PatchArgs a) {
+  const PatchGroup G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2;
+  const int total = a.B * Ho * Wo * a.Ctok;
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= total) return;
+  const int ci = id % a.Ctok;
+  const int tok = id / a.Ctok;
+  const int b = tok / (Ho * Wo);
+  const int rem = tok - b * Ho * Wo;
+  const int ho = rem / Wo, wo = rem - ho * Wo;
+  const int half = G.cout / 2;
+  float acc = 0.f;
+  for (int co = 0; co < G.cout; ++co) {
+    const int ch = co < half ? G.mean_off + co : G.std_off + co - half;
+    if (ch >= a.climit) continue;
+    const float* d = a.img + (((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
+    const float* w = G.w + ((size_t)ci * G.cout + co) * 4;
+    acc += w[0] * d[0] + w[1] * d[1] + w[2] * d[a.Wimg] + w[3] * d[a.Wimg + 1];
+  }
+  G.tok[(size_t)tok * a.Ctok + ci] = acc;
+}
+
+hipError_t patch_embed_fwd(const PatchArgs& a, hipStream_t s) {
+  const int total = a.B * (a.Himg / 2) * (a.Wimg / 2) * a.Ctok;
+  hipLaunchKernelGGL(k_patch_fwd, dim3((total + 255) / 256, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t patch_embed_bwd(const PatchArgs& a, hipStream_t s) {
+  const int total = a.B * a.Cimg * a.Himg * a.Wimg;
+  hipLaunchKernelGGL(k_patch_bwd, dim3((total + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t patch_unembed_fwd(const PatchArgs& a, hipStream_t s) {
+  const int total = a.B * a.climit * a.Himg * a.Wimg;
+  hipLaunchKernelGGL(k_unembed_fwd, dim3((total + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t patch_unembed_bwd(const PatchArgs& a, hipStream_t s) {
+  const int total = a.B * (a.Himg / 2) * (a.Wimg / 2) * a.Ctok;
+  hipLaunchKernelGGL(k_unembed_bwd, dim3((total + 255) / 256, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// Misfit  J_o = 1/2 sum H (x - yo)^2 / R   (da_4dvar.py:1207) and its adjoint
+// ============================================================================
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  T t = 0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  }
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_misfit_fwd(MisfitArgs a) {
+  __shared__ double red[4];
+  const int HW = a.Hs * a.Ws;
+  const int n = a.C * HW;
+  double acc = 0.0;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    const int c = id / HW;
+    const int p = id - c * HW;
+    float v = a.net[(size_t)c * HW + p] * a.scale[c];
+    if (a.scale2) v = v * a.scale2[c];
+    if (a.xb) v = v + a.xb[id];
+    if (a.offset) v = v + a.offset[c];
+    a.x_out[id] = v;
+    if (a.flow_in) a.flow_in[id] = (v - a.mean[c]) / a.std_[c];
+    const float d = v - a.yo[id];
+    acc += (double)((a.Hm[id] * (d * d)) / a.R[id]);
+  }
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) a.partial[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_misfit_bwd(MisfitBwdArgs a) {
+  const int HW = a.Hs * a.Ws;
+  const int n = a.C * HW;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    const int c = id / HW;
+    const int p = id - c * HW;
+    float g = a.coeff * ((a.Hm[id] * (a.x[id] - a.yo[id])) / a.R[id]);
+    if (a.g_carry) g += a.g_carry[id];
+    a.g_net[(size_t)c * HW + p] = g * a.scale[c];
+  }
+}
+
+hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
+  if (a.mi || a.mj || a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorNotSupported;
+  hipLaunchKernelGGL(k_misfit_fwd, dim3(a.nblk), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
+  if (a.mi || a.mj || a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorNotSupported;
+  hipLaunchKernelGGL(k_misfit_bwd, dim3(1024), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_scale_channels(const float* in, float* out, const float* std_, int C, int HW,
+                                                        const float* add) {
+  const int n = C * HW;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    float v = in[id] / std_[id / HW];
+    if (add) v += add[id];
+    out[id] = v;
+  }
+}
+hipError_t scale_channels(const float* in, float* out, const float* std_, int C, int HW, const float* add,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_channels, dim3(1024), dim3(256), 0, s, in, out, std_, C, HW, add);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// reductions and vector primitives (torch/optim/lbfgs.py two-loop + line search, adam.py)
+// ============================================================================
+__global__ __launch_bounds__(256) void k_sumsq(const float* x, int64_t n, double* partial) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = x[i];
+    acc += v * v;
+  }
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(256) void k_dot(const float* a, const float* b, int64_t n, double* partial) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += (double)a[i] * (double)b[i];
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(256) void k_abssum(const float* a, int64_t n, double* partial) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) acc += fabs((double)a[i]);
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(256) void k_absmax(const float* a, int64_t n, float* partial) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, fabsf(a[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+__global__ __launch_bounds__(256) void k_final_d(const double* partial, int n, double* out) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += partial[i];
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = t;
+}
+__global__ __launch_bounds__(256) void k_final_max(const float* partial, int n, float* out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, partial[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+hipError_t reduce_sumsq(const float* x, int64_t n, double* partial, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(k_sumsq, dim3(nblk), dim3(256), 0, s, x, n, partial);
+  return hipGetLastError();
+}
+hipError_t reduce_final(const double* partial, int n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_final_d, dim3(1), dim3(256), 0, s, partial, n, out);
+  return hipGetLastError();
+}
+hipError_t vec_dot(const float* a, const float* b, int64_t n, double* partial, int nblk, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, a, b, n, partial);
+  hipLaunchKernelGGL(k_final_d, dim3(1), dim3(256), 0, s, partial, nblk, out);
+  return hipGetLastError();
+}
+hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_abssum, dim3(nblk), dim3(256), 0, s, x, n, partial);
+  hipLaunchKernelGGL(k_final_d, dim3(1), dim3(256), 0, s, partial, nblk, out);
+  return hipGetLastError();
+}
+hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_absmax, dim3(nblk), dim3(256), 0, s, x, n, partial);
+  hipLaunchKernelGGL(k_final_max, dim3(1), dim3(256), 0, s, partial, nblk, out);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_axpby(float* out, const float* x, float a, const float* y, float b,
+                                               int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = (y ? b * y[i] : 0.f) + a * x[i];
+}
+__global__ __launch_bounds__(256) void k_axpy(float* y, const float* x, float a, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] = y[i] + a * x[i];
+}
+__global__ __launch_bounds__(256) void k_scale(float* y, float a, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] = y[i] * a;
+}
+__global__ __launch_bounds__(256) void k_fill(float* y, float v, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] = v;
+}
+static int vgrid(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 2048); }
+hipError_t vec_axpy(float* y, const float* x, float alpha, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_axpy, dim3(vgrid(n)), dim3(256), 0, s, y, x, alpha, n);
+  return hipGetLastError();
+}
+hipError_t vec_axpby(float* out, const float* x, float a, const float* y, float b, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_axpby, dim3(vgrid(n)), dim3(256), 0, s, out, x, a, y, b, n);
+  return hipGetLastError();
+}
+hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale, dim3(vgrid(n)), dim3(256), 0, s, y, alpha, n);
+  return hipGetLastError();
+}
+hipError_t fill(float* p, float v, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(vgrid(n)), dim3(256), 0, s, p, v, n);
+  return hipGetLastError();
+}
+
+// Adam (torch/optim/adam.py single-tensor path, no weight decay, no amsgrad):
+//   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ __launch_bounds__(256) void k_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                                              float b1, float b2, float eps, float bc1, float bc2_sqrt) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i];
+    const float mi = m[i] + (gi - m[i]) * (1.0f - b1);  // torch: exp_avg.lerp_(grad, 1-beta1)
+    const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - (lr / bc1) * (mi / denom);
+  }
+}
+hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                     float bc1, float bc2_sqrt, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam, dim3(vgrid(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, bc1, bc2_sqrt);
+  return hipGetLastError();
+}
+
+// 32x32 LDS-tiled transpose (weights W [N][K] -> W^T [K][N], once at load time)
+__global__ __launch_bounds__(256) void k_transpose(const float* in, float* out, int rows, int cols) {
+  __shared__ float t[32][33];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int j = ty; j < 32; j += 8) {
+    const int r = by + j, c = bx + tx;
+    if (r < rows && c < cols) t[j][tx] = in[(size_t)r * cols + c];
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int r = bx + j, c = by + tx;  // out row = in col
+    if (r < cols && c < rows) out[(size_t)r * rows + c] = t[tx][j];
+  }
+}
+hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStream_t s) {
+  hipLaunchKernelGGL(k_transpose, dim3((cols + 31) / 32, (rows + 31) / 32), dim3(256), 0, s, in, out, rows, cols);
+  return hipGetLastError();
+}
+
+}  // namespace vv

@@ -1,0 +1,53 @@
+"""The vae4dvar analysis step on the HIP engine — mirror of cyclic_4dvar.one_step_DA(..., 'vae4dvar')
+(da_4dvar.py:1179-1306), without the CPU WRMSE/Bias logging of :1256-1269.
+
+  z = zeros(1,32,128,256)                                  (:1238)
+  LBFGS(history_size=10, max_iter=10, strong_wolfe)        (:1240)
+  for kk in range(Nit+1): cal_loss(z) ; lbfgs.step(closure) while kk < Nit   (:1255-1299)
+  xa = decoder_hr(z)[0]*stdTr*std + xb                     (:1301-1306)
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from .engine import DAProblem
+from .lbfgs import LBFGS, Adam
+
+
+def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10, optimizer: str = "lbfgs",
+                lr: float | None = None, log_terms: bool = True, log=None):
+    """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, seconds)."""
+    dev = prob.xb.device
+    z = torch.zeros(prob.latent_shape, device=dev, dtype=torch.float32)
+    ctx = prob.ctx
+    if optimizer == "lbfgs":
+        opt = LBFGS(ctx, z, lr=1 if lr is None else lr, history_size=history_size, max_iter=max_iter,
+                    line_search_fn="strong_wolfe")
+    elif optimizer == "adam":
+        opt = Adam(ctx, z, lr=1e-3 if lr is None else lr)
+    else:
+        raise ValueError(optimizer)
+
+    def closure(zz, g):
+        jb, jo = prob.closure(zz, g)
+        return prob.loss_f32(jb, jo)
+
+    js = []
+    n0 = prob.n_evals
+    t0 = time.time()
+    for kk in range(nit + 1):
+        if log_terms:
+            jb, jo = prob.closure(z, None)  # cal_loss (:1210-1236): no gradient
+            js.append((jb, jo))
+            if log is not None:
+                log(kk, jb, jo)
+        if kk < nit:
+            opt.step(closure)
+    xa = prob.analysis(z)
+    torch.cuda.synchronize()
+    n_log = (nit + 1) if log_terms else 0
+    n_iter = opt.state["n_iter"] if optimizer == "lbfgs" else opt.t
+    return {"xa": xa, "z": z, "J": js, "n_eval": prob.n_evals - n0 - n_log, "n_iter": n_iter,
+            "seconds": time.time() - t0}

@@ -1,0 +1,266 @@
+"""Host-side mirror of the reference's module protocol over libvaevar.
+
+  LGUnet       ~ networks_old.transformer.LGUnet_all (transformer.py:716-752): state_dict-keyed weights,
+                 __call__ is a differentiable forward (torch.autograd.Function over the HIP path)
+  VAE_lr       ~ nf_model/vae.py:53-90 decoder half: .decoder(z), .decoder_hr(z)
+  DAProblem    ~ the closure state of one_step_DA 'vae4dvar' (da_4dvar.py:1179-1251)
+
+torch is plumbing here (device memory, streams); every FLOP runs in libvaevar.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import VVConfig, check, lib
+
+
+def _ptr(t: torch.Tensor):
+    if not t.is_cuda:
+        raise ValueError("libvaevar compute entry points take device tensors")
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError("expected a contiguous float32 tensor")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Context:
+    """One libvaevar context per device (vv_ctx_create)."""
+
+    _by_dev: dict = {}
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.h = ctypes.c_void_p()
+        check(lib.vv_ctx_create(device, ctypes.byref(self.h)), "ctx_create")
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Context":
+        if device not in cls._by_dev:
+            cls._by_dev[device] = cls(device)
+        return cls._by_dev[device]
+
+    # --- vector primitives (torch/optim/lbfgs.py arithmetic) ---
+    def dot(self, a, b) -> float:
+        out = ctypes.c_double()
+        check(lib.vv_dot(self.h, _ptr(a), _ptr(b), a.numel(), ctypes.byref(out), _stream()), "dot")
+        return out.value
+
+    def abssum(self, a) -> float:
+        out = ctypes.c_double()
+        check(lib.vv_abssum(self.h, _ptr(a), a.numel(), ctypes.byref(out), _stream()), "abssum")
+        return out.value
+
+    def absmax(self, a) -> float:
+        out = ctypes.c_float()
+        check(lib.vv_absmax(self.h, _ptr(a), a.numel(), ctypes.byref(out), _stream()), "absmax")
+        return out.value
+
+    def axpy(self, y, x, alpha: float):
+        check(lib.vv_axpy(self.h, _ptr(y), _ptr(x), float(alpha), y.numel(), _stream()), "axpy")
+
+    def axpby(self, out, x, a: float, y, b: float):
+        yp = _ptr(y) if y is not None else None
+        check(lib.vv_axpby(self.h, _ptr(out), _ptr(x), float(a), yp, float(b), out.numel(), _stream()), "axpby")
+
+    def scale(self, y, alpha: float):
+        check(lib.vv_scale(self.h, _ptr(y), float(alpha), y.numel(), _stream()), "scale")
+
+    def copy(self, dst, src):
+        check(lib.vv_copy(self.h, _ptr(dst), _ptr(src), dst.numel(), _stream()), "copy")
+
+    def adam(self, p, g, m, v, lr, beta1, beta2, eps, step):
+        check(lib.vv_adam(self.h, _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), lr, beta1, beta2, eps, step,
+                          _stream()), "adam")
+
+    def gemm(self, A, B, bias=None, tile=-1):
+        M, K = A.shape
+        N = B.shape[0]
+        C = torch.empty(M, N, device=A.device, dtype=torch.float32)
+        bp = _ptr(bias) if bias is not None else None
+        check(lib.vv_gemm(self.h, M, N, K, _ptr(A), _ptr(B), bp, _ptr(C), tile, _stream()), "gemm")
+        return C
+
+
+class _NetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, net, slot, out_limit):
+        out = net.forward_raw(x, slot, out_limit)
+        ctx.net, ctx.slot, ctx.out_limit, ctx.shape = net, slot, out_limit, x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        dx = torch.empty(ctx.shape, device=g.device, dtype=torch.float32)
+        ctx.net.backward_raw(g.contiguous(), dx, ctx.slot, ctx.out_limit)
+        return dx, None, None, None
+
+
+class LGUnet:
+    """networks_old.transformer.LGUnet_all on the HIP engine.
+
+    Weights are the reference's state_dict entries (module./max_logvar filtering as in
+    da_4dvar.py:594-601 is applied by `load_state_dict`). Input gradients only (quirk Q5).
+    """
+
+    def __init__(self, cfg: dict, batch: int = 1, n_slots: int = 1, device: int = 0):
+        self.cfg = dict(cfg)
+        self.ctx = Context.get(device)
+        self.device = torch.device("cuda", device)
+        self.batch, self.n_slots = batch, n_slots
+        self._c = VVConfig.from_dict(cfg)
+        mid = ctypes.c_int()
+        check(lib.vv_model_create(self.ctx.h, ctypes.byref(self._c), batch, n_slots, ctypes.byref(mid)),
+              "model_create")
+        self.id = mid.value
+        self.params = _lib.param_list(cfg)
+        self.in_ch = int(sum(cfg["inchans_list"]))
+        self.out_ch = int(sum(cfg["outchans_list"]))
+        self.H, self.W = cfg["img_size"]
+
+    def workspace_bytes(self) -> int:
+        b = ctypes.c_int64()
+        check(lib.vv_model_workspace_bytes(self.ctx.h, self.id, ctypes.byref(b)), "workspace_bytes")
+        return b.value
+
+    def load_state_dict(self, sd: dict, prefix: str = ""):
+        clean = {}
+        for k, v in sd.items():
+            name = k[7:] if k.startswith("module.") else k
+            if name in ("max_logvar", "min_logvar"):
+                continue
+            clean[name] = v
+        keep = []
+        ptrs = (ctypes.c_void_p * len(self.params))()
+        for i, (name, shape) in enumerate(self.params):
+            key = prefix + name
+            if key not in clean:
+                raise KeyError(f"missing parameter {key}")
+            v = clean[key]
+            if isinstance(v, np.ndarray):
+                v = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32))
+            v = v.detach().to(torch.float32).contiguous()
+            if tuple(v.shape) != tuple(shape):
+                raise ValueError(f"{key}: shape {tuple(v.shape)} != {shape}")
+            keep.append(v)
+            ptrs[i] = v.data_ptr()
+        check(lib.vv_load_weights(self.ctx.h, self.id, ptrs, len(self.params)), "load_weights")
+        return self
+
+    def load_synthetic(self, base_seed: int = 20250620, prefix: str = ""):
+        from .synth import param_value
+
+        sd = {prefix + n: param_value(prefix + n, s, base_seed) for n, s in self.params}
+        return self.load_state_dict(sd, prefix)
+
+    # raw device entry points (no autograd)
+    def forward_raw(self, x: torch.Tensor, slot: int = 0, out_limit: int = 0, out=None):
+        if tuple(x.shape) != (self.batch, self.in_ch, self.H, self.W):
+            raise ValueError(f"input shape {tuple(x.shape)} != {(self.batch, self.in_ch, self.H, self.W)}")
+        x = x.contiguous()
+        if out is None:
+            out = torch.empty(self.batch, self.out_ch, self.H, self.W, device=x.device, dtype=torch.float32)
+        check(lib.vv_model_forward(self.ctx.h, self.id, slot, _ptr(x), _ptr(out), out_limit, _stream()), "forward")
+        return out
+
+    def backward_raw(self, g: torch.Tensor, dx: torch.Tensor, slot: int = 0, out_limit: int = 0, add=None):
+        ap = _ptr(add) if add is not None else None
+        check(lib.vv_model_backward(self.ctx.h, self.id, slot, _ptr(g), _ptr(dx), ap, out_limit, _stream()),
+              "backward")
+        return dx
+
+    def __call__(self, x: torch.Tensor, slot: int = 0, out_limit: int = 0):
+        """Differentiable forward (input gradient). One pending backward per slot."""
+        return _NetFn.apply(x, self, slot, out_limit)
+
+
+class VAE_lr:
+    """Decoder half of nf_model/vae.py:53-90 (VAE_lr.dec is networks_old LGUnet_all)."""
+
+    def __init__(self, dec_cfg: dict, device: int = 0, state_grid=None):
+        self.dec = LGUnet(dec_cfg, 1, 1, device)
+        self.state_grid = tuple(state_grid) if state_grid else tuple(dec_cfg["img_size"])
+
+    def decoder(self, z):
+        return self.dec(z)
+
+    def decoder_hr(self, z):
+        x = self.dec(z)
+        if self.state_grid != tuple(x.shape[-2:]):
+            # nearest interpolation to the state grid (vae.py:90); the maps run in torch for now
+            x = torch.nn.functional.interpolate(x, self.state_grid)
+        return x
+
+
+class DAProblem:
+    """The vae4dvar closure (da_4dvar.py:1183-1208) bound to device buffers; evaluated by libvaevar."""
+
+    def __init__(self, dec: LGUnet, prob: dict, flow: LGUnet | None = None, obs_coeff: float = 1.0, device: int = 0):
+        dev = torch.device("cuda", device)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32).to(dev)
+        self.xb, self.yo, self.H, self.R = t(prob["xb"]), t(prob["yo"]), t(prob["H"]), t(prob["R"])
+        self.mean, self.std, self.std_tr = t(prob["mean"]), t(prob["std"]), t(prob["std_tr"])
+        self.T, self.C = self.yo.shape[0], self.yo.shape[1]
+        self.Hs, self.Ws = self.yo.shape[2:]
+        self.dec, self.flow, self.obs_coeff = dec, flow, float(obs_coeff)
+        self.ctx = dec.ctx
+        self.latent_shape = (1, dec.in_ch, dec.H, dec.W)
+        fid = flow.id if flow is not None else -1
+        check(lib.vv_bind_problem(self.ctx.h, dec.id, fid, self.T, self.C, self.Hs, self.Ws, _ptr(self.xb),
+                                  _ptr(self.yo), _ptr(self.H), _ptr(self.R), _ptr(self.mean), _ptr(self.std),
+                                  _ptr(self.std_tr), self.obs_coeff), "bind_problem")
+        self.n_evals = 0
+
+    def closure(self, z: torch.Tensor, grad: torch.Tensor | None):
+        """Returns (J_b, J_o) as Python floats (double sums); grad <- dJ/dz if given."""
+        jb, jo = ctypes.c_double(), ctypes.c_double()
+        gp = _ptr(grad) if grad is not None else None
+        check(lib.vv_closure(self.ctx.h, _ptr(z), gp, ctypes.byref(jb), ctypes.byref(jo), _stream()), "closure")
+        self.n_evals += 1
+        return jb.value, jo.value
+
+    def loss_f32(self, jb: float, jo: float) -> float:
+        """loss_reg + obs_coeff * loss_obs with the reference's fp32 scalar arithmetic (quirk Q7)."""
+        return float(np.float32(jb) + np.float32(np.float32(self.obs_coeff) * np.float32(jo)))
+
+    def analysis(self, z: torch.Tensor) -> torch.Tensor:
+        xa = torch.empty(self.C, self.Hs, self.Ws, device=z.device, dtype=torch.float32)
+        check(lib.vv_decode(self.ctx.h, _ptr(z), _ptr(xa), _stream()), "decode")
+        return xa
+
+    def trajectory(self) -> torch.Tensor:
+        """x_t (T,C,Hs,Ws) of the last closure (a copy)."""
+        p = ctypes.c_void_p()
+        check(lib.vv_state_ptr(self.ctx.h, ctypes.byref(p)), "state_ptr")
+        n = self.T * self.C * self.Hs * self.Ws
+        out = torch.empty(n, device=self.xb.device, dtype=torch.float32)
+        check(lib.vv_copy(self.ctx.h, _ptr(out), p, n, _stream()), "copy")
+        return out.view(self.T, self.C, self.Hs, self.Ws)
+
+
+class _ClosureFn(torch.autograd.Function):
+    """J(z) as a differentiable scalar, so torch.optim.LBFGS can drive the HIP closure unchanged."""
+
+    @staticmethod
+    def forward(ctx, z, prob):
+        g = torch.empty_like(z)
+        jb, jo = prob.closure(z.detach().contiguous(), g)
+        ctx.save_for_backward(g)
+        return torch.tensor(prob.loss_f32(jb, jo), device=z.device, dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (g,) = ctx.saved_tensors
+        return g * gout, None
+
+
+def loss(prob: DAProblem, z: torch.Tensor) -> torch.Tensor:
+    """Drop-in for the reference's `loss(z)` (da_4dvar.py:1183-1208)."""
+    return _ClosureFn.apply(z, prob)

@@ -1,0 +1,274 @@
+"""On-device L-BFGS with strong-Wolfe line search: a statement-by-statement mirror of
+torch.optim.LBFGS (torch/optim/lbfgs.py:12-537, torch 2.10) — the optimiser the reference
+constructs as `optim.LBFGS([z], history_size=10, max_iter=10, line_search_fn="strong_wolfe")`
+(da_4dvar.py:1240).
+
+Vectors (1,048,576 floats for the 32x128x256 latent) stay in HBM and every vector operation
+(dot, axpy, scale, abs-max, abs-sum) is a libvaevar kernel; only scalars come to the host.
+Scalar types follow torch's promotion rules (quirk Q7): quantities that are 0-d fp32 tensors in
+torch (dot products, ys, ro, H_diag, al, be, gtd, ...) are numpy float32 here (numpy 2 treats
+Python floats as weak scalars exactly like torch), the loss is a Python float.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+f32 = np.float32
+
+
+def _cubic_interpolate(x1, f1, g1, x2, f2, g2, bounds=None):
+    # torch/optim/lbfgs.py:12-37
+    if bounds is not None:
+        xmin_bound, xmax_bound = bounds
+    else:
+        xmin_bound, xmax_bound = (x1, x2) if x1 <= x2 else (x2, x1)
+    d1 = g1 + g2 - 3 * (f1 - f2) / (x1 - x2)
+    d2_square = d1 ** 2 - g1 * g2
+    if d2_square >= 0:
+        d2 = np.sqrt(d2_square)
+        if x1 <= x2:
+            min_pos = x2 - (x2 - x1) * ((g2 + d2 - d1) / (g2 - g1 + 2 * d2))
+        else:
+            min_pos = x1 - (x1 - x2) * ((g1 + d2 - d1) / (g1 - g2 + 2 * d2))
+        return min(max(min_pos, xmin_bound), xmax_bound)
+    return (xmin_bound + xmax_bound) / 2.0
+
+
+class LBFGS:
+    """torch.optim.LBFGS over one flat fp32 device parameter, vector math in libvaevar.
+
+    closure(z, grad_out) -> float evaluates J at z and writes dJ/dz into grad_out.
+    """
+
+    def __init__(self, ctx, z: torch.Tensor, lr=1, max_iter=20, max_eval=None, tolerance_grad=1e-7,
+                 tolerance_change=1e-9, history_size=100, line_search_fn=None):
+        if max_eval is None:
+            max_eval = max_iter * 5 // 4
+        self.ctx, self.z = ctx, z
+        self.lr, self.max_iter, self.max_eval = lr, max_iter, max_eval
+        self.tolerance_grad, self.tolerance_change = tolerance_grad, tolerance_change
+        self.history_size, self.line_search_fn = history_size, line_search_fn
+        self.state = {"func_evals": 0, "n_iter": 0}
+
+    # --- vector helpers ---------------------------------------------------
+    def _dot(self, a, b):
+        return f32(self.ctx.dot(a.view(-1), b.view(-1)))
+
+    def _absmax(self, a):
+        return f32(self.ctx.absmax(a.view(-1)))
+
+    def _abssum(self, a):
+        return f32(self.ctx.abssum(a.view(-1)))
+
+    def _new(self):
+        return torch.empty_like(self.z)
+
+    def _add_grad(self, step_size, update):
+        self.ctx.axpy(self.z, update, float(step_size))
+
+    def _directional_evaluate(self, closure, x, t, d):
+        # lbfgs.py:325-331
+        self._add_grad(t, d)
+        g = self._new()
+        loss = float(closure(self.z, g))
+        self.ctx.copy(self.z, x)
+        return loss, g
+
+    def _strong_wolfe(self, obj_func, x, t, d, f, g, gtd, c1=1e-4, c2=0.9, tolerance_change=1e-9, max_ls=25):
+        # lbfgs.py:40-209
+        d_norm = self._absmax(d)
+        g = g.clone()
+        f_new, g_new = obj_func(x, t, d)
+        ls_func_evals = 1
+        gtd_new = self._dot(g_new, d)
+        t_prev, f_prev, g_prev, gtd_prev = 0, f, g, gtd
+        done = False
+        ls_iter = 0
+        while ls_iter < max_ls:
+            if f_new > (f + c1 * t * gtd) or (ls_iter > 1 and f_new >= f_prev):
+                bracket, bracket_f = [t_prev, t], [f_prev, f_new]
+                bracket_g, bracket_gtd = [g_prev, g_new.clone()], [gtd_prev, gtd_new]
+                break
+            if abs(gtd_new) <= -c2 * gtd:
+                bracket, bracket_f, bracket_g = [t], [f_new], [g_new]
+                done = True
+                break
+            if gtd_new >= 0:
+                bracket, bracket_f = [t_prev, t], [f_prev, f_new]
+                bracket_g, bracket_gtd = [g_prev, g_new.clone()], [gtd_prev, gtd_new]
+                break
+            min_step = t + 0.01 * (t - t_prev)
+            max_step = t * 10
+            tmp = t
+            t = _cubic_interpolate(t_prev, f_prev, gtd_prev, t, f_new, gtd_new, bounds=(min_step, max_step))
+            t_prev, f_prev, g_prev, gtd_prev = tmp, f_new, g_new.clone(), gtd_new
+            f_new, g_new = obj_func(x, t, d)
+            ls_func_evals += 1
+            gtd_new = self._dot(g_new, d)
+            ls_iter += 1
+        if ls_iter == max_ls:
+            bracket, bracket_f, bracket_g = [0, t], [f, f_new], [g, g_new]
+
+        insuf_progress = False
+        low_pos, high_pos = (0, 1) if bracket_f[0] <= bracket_f[-1] else (1, 0)
+        while not done and ls_iter < max_ls:
+            if abs(bracket[1] - bracket[0]) * d_norm < tolerance_change:
+                break
+            t = _cubic_interpolate(bracket[0], bracket_f[0], bracket_gtd[0], bracket[1], bracket_f[1],
+                                   bracket_gtd[1])
+            eps = 0.1 * (max(bracket) - min(bracket))
+            if min(max(bracket) - t, t - min(bracket)) < eps:
+                if insuf_progress or t >= max(bracket) or t <= min(bracket):
+                    if abs(t - max(bracket)) < abs(t - min(bracket)):
+                        t = max(bracket) - eps
+                    else:
+                        t = min(bracket) + eps
+                    insuf_progress = False
+                else:
+                    insuf_progress = True
+            else:
+                insuf_progress = False
+            f_new, g_new = obj_func(x, t, d)
+            ls_func_evals += 1
+            gtd_new = self._dot(g_new, d)
+            ls_iter += 1
+            if f_new > (f + c1 * t * gtd) or f_new >= bracket_f[low_pos]:
+                bracket[high_pos] = t
+                bracket_f[high_pos] = f_new
+                bracket_g[high_pos] = g_new.clone()
+                bracket_gtd[high_pos] = gtd_new
+                low_pos, high_pos = (0, 1) if bracket_f[0] <= bracket_f[1] else (1, 0)
+            else:
+                if abs(gtd_new) <= -c2 * gtd:
+                    done = True
+                elif gtd_new * (bracket[high_pos] - bracket[low_pos]) >= 0:
+                    bracket[high_pos] = bracket[low_pos]
+                    bracket_f[high_pos] = bracket_f[low_pos]
+                    bracket_g[high_pos] = bracket_g[low_pos]
+                    bracket_gtd[high_pos] = bracket_gtd[low_pos]
+                bracket[low_pos] = t
+                bracket_f[low_pos] = f_new
+                bracket_g[low_pos] = g_new.clone()
+                bracket_gtd[low_pos] = gtd_new
+        t = bracket[low_pos]
+        return bracket_f[low_pos], bracket_g[low_pos], t, ls_func_evals
+
+    def step(self, closure):
+        # lbfgs.py:333-535
+        lr, max_iter, max_eval = self.lr, self.max_iter, self.max_eval
+        tolerance_grad, tolerance_change = self.tolerance_grad, self.tolerance_change
+        state = self.state
+        flat_grad = self._new()
+        orig_loss = closure(self.z, flat_grad)
+        loss = float(orig_loss)
+        current_evals = 1
+        state["func_evals"] += 1
+        opt_cond = self._absmax(flat_grad) <= tolerance_grad
+        if opt_cond:
+            return orig_loss
+        d, t = state.get("d"), state.get("t")
+        old_dirs, old_stps, ro = state.get("old_dirs"), state.get("old_stps"), state.get("ro")
+        H_diag, prev_flat_grad, prev_loss = state.get("H_diag"), state.get("prev_flat_grad"), state.get("prev_loss")
+        n_iter = 0
+        while n_iter < max_iter:
+            n_iter += 1
+            state["n_iter"] += 1
+            if state["n_iter"] == 1:
+                d = self._new()
+                self.ctx.axpby(d, flat_grad, -1.0, None, 0.0)
+                old_dirs, old_stps, ro = [], [], []
+                H_diag = 1
+            else:
+                y = self._new()
+                self.ctx.axpby(y, flat_grad, 1.0, prev_flat_grad, -1.0)
+                s = self._new()
+                self.ctx.axpby(s, d, float(t), None, 0.0)
+                ys = self._dot(y, s)
+                if ys > 1e-10:
+                    if len(old_dirs) == self.history_size:
+                        old_dirs.pop(0)
+                        old_stps.pop(0)
+                        ro.pop(0)
+                    old_dirs.append(y)
+                    old_stps.append(s)
+                    ro.append(1.0 / ys)
+                    H_diag = ys / self._dot(y, y)
+                num_old = len(old_dirs)
+                if "al" not in state:
+                    state["al"] = [None] * self.history_size
+                al = state["al"]
+                q = self._new()
+                self.ctx.axpby(q, flat_grad, -1.0, None, 0.0)
+                for i in range(num_old - 1, -1, -1):
+                    al[i] = self._dot(old_stps[i], q) * ro[i]
+                    self.ctx.axpy(q, old_dirs[i], float(-al[i]))
+                self.ctx.scale(q, float(H_diag))
+                d = r = q
+                for i in range(num_old):
+                    be_i = self._dot(old_dirs[i], r) * ro[i]
+                    self.ctx.axpy(r, old_stps[i], float(al[i] - be_i))
+            if prev_flat_grad is None:
+                prev_flat_grad = flat_grad.clone()
+            else:
+                self.ctx.copy(prev_flat_grad, flat_grad)
+            prev_loss = loss
+            if state["n_iter"] == 1:
+                t = min(1.0, 1.0 / self._abssum(flat_grad)) * lr
+            else:
+                t = lr
+            gtd = self._dot(flat_grad, d)
+            if gtd > -tolerance_change:
+                break
+            ls_func_evals = 0
+            if self.line_search_fn is not None:
+                if self.line_search_fn != "strong_wolfe":
+                    raise RuntimeError("only 'strong_wolfe' is supported")
+                x_init = self.z.clone()
+
+                def obj_func(x, t, d):
+                    return self._directional_evaluate(closure, x, t, d)
+
+                loss, flat_grad, t, ls_func_evals = self._strong_wolfe(obj_func, x_init, t, d, loss, flat_grad, gtd,
+                                                                       max_ls=max_eval - current_evals)
+                self._add_grad(t, d)
+                opt_cond = self._absmax(flat_grad) <= tolerance_grad
+            else:
+                self._add_grad(t, d)
+                if n_iter != max_iter:
+                    flat_grad = self._new()
+                    loss = float(closure(self.z, flat_grad))
+                    opt_cond = self._absmax(flat_grad) <= tolerance_grad
+                    ls_func_evals = 1
+            current_evals += ls_func_evals
+            state["func_evals"] += ls_func_evals
+            if n_iter == max_iter:
+                break
+            if current_evals >= max_eval:
+                break
+            if opt_cond:
+                break
+            if f32(abs(t)) * self._absmax(d) <= tolerance_change:
+                break
+            if abs(loss - prev_loss) < tolerance_change:
+                break
+        state.update(d=d, t=t, old_dirs=old_dirs, old_stps=old_stps, ro=ro, H_diag=H_diag,
+                     prev_flat_grad=prev_flat_grad, prev_loss=prev_loss)
+        return orig_loss
+
+
+class Adam:
+    """torch.optim.Adam (defaults lr=1e-3, betas=(0.9, 0.999), eps=1e-8; adam.py:34) on libvaevar."""
+
+    def __init__(self, ctx, z, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.ctx, self.z, self.lr, self.betas, self.eps = ctx, z, lr, betas, eps
+        self.m = torch.zeros_like(z)
+        self.v = torch.zeros_like(z)
+        self.t = 0
+
+    def step(self, closure):
+        g = torch.empty_like(self.z)
+        loss = closure(self.z, g)
+        self.t += 1
+        self.ctx.adam(self.z, g, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps, self.t)
+        return loss
