@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Benchmark of the VAE-Var 4D-Var inner loop on MI355X (BASELINE.json metric).
+
+Workload (N=1): BASELINE config 2 — 3D-Var with the full VAE decoder (nf_model/parameters0_old.yaml,
+216M parameters), 69-channel 128x256 state, L-BFGS(history 10, max_iter 10, strong Wolfe) as in
+da_4dvar.py:1240, synthetic weights and observations (no checkpoints ship with the reference).
+
+  step   = one outer `lbfgs.step(closure)` (<= 10 L-BFGS iterations, <= 12 closure evaluations);
+           --steps 10 is the reference's converged budget for config 2 (Nit 10 x max_iter 10 = 100 iters).
+  value  = L-BFGS iterations per second over the whole job (sum over ranks / max time over ranks);
+           the analysis decode and the RCCL gather of all analyses to rank 0 are inside the timed region.
+  N > 1  = ensemble: rank r runs its own analysis (seed + r), weak scaling, no inner-loop communication.
+
+Prints ONE JSON line on rank 0. See DESIGN.md §Measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vae-var_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense peak (MI355X_MICROARCH.md, chip-level table)
+PEAK_HBM_GBS = 8000.0     # HBM3E spec
+FLOPS_PER_EVAL = {1: 1787.8e9, 2: 3577.0e9, 6: 10733.7e9}  # SURVEY §8 d (input-grad only)
+
+CONFIGS = {
+    2: dict(T=1, name="config 2: 3D-Var, full VAE decoder (parameters0_old), 69ch 128x256, 100 L-BFGS iters"),
+    3: dict(T=2, name="config 3: 4D-Var, 2-step window with LGUnet flow stand-in, 69ch 128x256, 100 iters"),
+    4: dict(T=6, name="config 4: 4D-Var, 6-step window, one analysis per GPU (ensemble)"),
+}
+
+
+def cpu_baseline(prob_np, evals_per_iter, n_evals, threads):
+    """Oracle torch-CPU restatement (oracle/), weight grads on as in the reference (quirk Q5)."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+
+    torch.set_num_threads(threads)
+    p = synth_params(C.DECODER)
+    for v in p.values():
+        v.requires_grad_(True)
+    ro = oracle_problem(prob_np, p, C.DECODER)
+    z = torch.zeros(1, 32, 128, 256, requires_grad=True)
+
+    def ev():
+        for v in p.values():
+            v.grad = None
+        z.grad = None
+        ro.loss(z).backward()
+
+    ev()  # warm-up
+    t0 = time.time()
+    for _ in range(n_evals):
+        ev()
+    per_eval = (time.time() - t0) / n_evals
+    return per_eval, {"value": 1.0 / (per_eval * evals_per_iter), "unit": "L-BFGS iters/s", "cores": threads,
+                      "kind": "port",
+                      "sample": f"{n_evals} closure evaluations (J + dJ/dz, weight grads on as in the reference) of "
+                                f"config 2 at z=0 on {threads} host threads after 1 warm-up: {per_eval:.3f} s/eval; "
+                                f"iters/s = 1/(s_per_eval x {evals_per_iter:.3f} evals per iteration of the GPU run)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10, help="outer L-BFGS steps (Nit)")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-evals", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel-class profile")
+    args = ap.parse_args()
+
+    from vaevar import config as C
+    from vaevar import ensemble
+    from vaevar.da import one_step_da
+    from vaevar.engine import DAProblem, LGUnet
+    from vaevar.lbfgs import LBFGS
+    from vaevar.problem import make_problem
+
+    rank, size, local = ensemble.init()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    T = CONFIGS[args.config]["T"]
+    dec = LGUnet(C.DECODER, 1, 1, device=local).load_synthetic()
+    flow = LGUnet(C.FLOW, 1, T - 1, device=local).load_synthetic() if T > 1 else None
+    prob_np = make_problem(nch=69, Hs=128, Ws=256, T=T, seed=20250620 + rank)
+    prob = DAProblem(dec, prob_np, flow=flow, device=local)
+
+    # warm-up: W outer steps of a throw-away analysis (same path, same shapes)
+    if args.warmup > 0:
+        one_step_da(prob, nit=args.warmup, log_terms=False)
+    torch.cuda.synchronize()
+    prof = (rank == 0) and not args.no_profile
+
+    ensemble.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = one_step_da(prob, nit=args.steps, log_terms=False)
+    xs = ensemble.gather_analyses(res["xa"])
+    torch.cuda.synchronize()
+    ensemble.barrier()
+    elapsed = time.perf_counter() - t0
+    if prof:
+        # per-kernel-class HIP-event profile of the same work (a second pass of the same analysis, so the
+        # event records do not perturb the timed region above)
+        prob.ctx.profile_start()
+        res_p = one_step_da(prob, nit=args.steps, log_terms=False)
+        torch.cuda.synchronize()
+        pr = prob.ctx.profile_stop()
+        prof_elapsed = res_p["seconds"]
+    t_max = ensemble.reduce_scalar(elapsed, "max", dev)
+    iters = ensemble.reduce_scalar(res["n_iter"], "sum", dev)
+    evals = ensemble.reduce_scalar(res["n_eval"], "sum", dev)
+
+    # J before / after (not timed)
+    j_end = prob.closure(res["z"], None)
+    z0 = torch.zeros_like(res["z"])
+    j_0 = prob.closure(z0, None)
+
+    if rank != 0:
+        return
+    out = {
+        "metric": "4D-Var inner-loop iters/sec + wall-clock to convergence, 69ch 128×256 state",
+        "value": iters / t_max,
+        "unit": "L-BFGS iters/s",
+        "n_gpus": size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * t_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": CONFIGS[args.config]["name"], "analyses": size, "T": T, "outer_steps": args.steps,
+                   "parallelism": "ensemble: 1 independent analysis per GPU, RCCL gather of xa at the end"},
+        "wall_clock_to_convergence_s": t_max,
+        "iters": iters,
+        "evals": evals,
+        "evals_per_s": evals / t_max,
+        "ms_per_eval": 1e3 * t_max * size / max(evals, 1),
+        "J_start": j_0[0] + j_0[1],
+        "J_final": j_end[0] + j_end[1],
+    }
+    flops_eval = FLOPS_PER_EVAL.get(T)
+    if prof:
+        g = pr["gemm"]
+        ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                           "frac": ach / PEAK_F32_TFLOPS, "traffic": None,
+                           "kernel": "k_gemm_nt (every fp32 MFMA GEMM launch of a HIP-event-profiled repeat "
+                                     "of the timed analysis)",
+                           "launches": g["launches"], "avg_launch_us": 1e3 * g["ms"] / max(g["launches"], 1),
+                           "flops_per_launch": g["flops"] / max(g["launches"], 1)}
+        busy = sum(v["ms"] for v in pr.values())
+        out["kernel_time_ms"] = {k: round(v["ms"], 3) for k, v in pr.items()}
+        out["kernel_launches"] = {k: v["launches"] for k, v in pr.items()}
+        out["gpu_busy_frac"] = busy / (1e3 * prof_elapsed)
+        if flops_eval:
+            out["eval_roofline_frac"] = (flops_eval / (PEAK_F32_TFLOPS * 1e12)) / (t_max * size / max(evals, 1))
+    if size == 1 and not args.no_cpu_baseline and args.config == 2:
+        evals_per_iter = evals / max(iters, 1)
+        per_eval, cb = cpu_baseline(prob_np, evals_per_iter, args.cpu_evals, args.cpu_threads)
+        out["cpu_baseline"] = cb
+        out["cpu_wall_clock_to_convergence_s_extrapolated"] = per_eval * evals
+        out["speedup_vs_cpu"] = out["value"] / cb["value"]
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

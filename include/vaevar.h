@@ -103,6 +103,12 @@ int vv_copy(vv_ctx* ctx, float* dst, const float* src, int64_t n, void* stream);
 int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
             float beta2, float eps, int step, void* stream);
 
+/* live profiler: HIP events around every kernel launch, summed per kernel class
+   (0 GEMM, 1 window attention, 2 LayerNorm, 3 patch conv/convT, 4 misfit, 5 vector); ncls >= 6.
+   ms = summed launch durations, flops/bytes = algorithmic work, launches = count. stop synchronises. */
+int vv_profile_start(vv_ctx* ctx);
+int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* launches, int ncls);
+
 /* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), epi as vv::Epi */
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
             int tile, void* stream);

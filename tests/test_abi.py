@@ -1,0 +1,88 @@
+"""CPU: the C-ABI library loads and exports every entry point include/vaevar.h declares; the parameter
+enumeration equals the reference state_dict key set (pinned by the oracle); bad configs fail cleanly."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def header_symbols():
+    h = open(os.path.join(ROOT, "include", "vaevar.h")).read()
+    return sorted(set(re.findall(r"^int\s+(vv_\w+)\s*\(", h, flags=re.M)))
+
+
+def test_library_exports_header():
+    from vaevar import _lib
+
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(_lib.lib, s), s
+    assert set(syms) == set(_lib.EXPORTED), set(syms) ^ set(_lib.EXPORTED)
+    assert _lib.lib.vv_version() >= 100
+
+
+@pytest.mark.parametrize("name", ["TINY", "TINY_FLOW", "DECODER", "FLOW"])
+def test_param_enumeration_matches_oracle(name):
+    from oracle.lgunet_ref import param_shapes
+    from vaevar import _lib, config as C
+
+    cfg = getattr(C, name)
+    pl = _lib.param_list(cfg)
+    ps = param_shapes(cfg)
+    assert [n for n, _ in pl] == list(dict.fromkeys(n for n, _ in pl))  # unique
+    assert set(n for n, _ in pl) == set(ps)
+    assert all(ps[n] == s for n, s in pl)
+
+
+def test_decoder_param_count():
+    from vaevar import _lib, config as C
+    import numpy as np
+
+    n = sum(int(np.prod(s)) for _, s in _lib.param_list(C.DECODER))
+    assert n == 215_880_165  # VAE_lr.dec parameters (buffers excluded)
+
+
+def test_bad_config_rejected():
+    from vaevar import _lib, config as C
+
+    cfg = dict(C.TINY)
+    cfg["window_size"] = 6
+    with pytest.raises(_lib.VVError, match="window_size"):
+        _lib.param_list(cfg)
+    cfg = dict(C.TINY)
+    cfg["enc_depths"] = [2, 2, 2]
+    cfg["enc_heads"] = [2, 4, 4]
+    with pytest.raises(_lib.VVError, match="encoder levels"):
+        _lib.param_list(cfg)
+
+
+def test_problem_construction():
+    import numpy as np
+    from vaevar.problem import make_problem, obs_variance
+    from vaevar import config as C
+
+    p = make_problem(nch=69, Hs=32, Ws=64, T=2, seed=1, obs_frac=0.05)
+    assert p["yo"].shape == (2, 69, 32, 64) and p["xb"].shape == (69, 32, 64)
+    assert np.array_equal(p["H"][0], p["H"][1]) and np.all(p["H"][:, 0] == p["H"][:, 68])  # column mask
+    std = np.asarray(C.MODEL_STD, np.float32)
+    v = obs_variance(69, 0.005, 2, std)
+    # da_4dvar.py:106-127, modify_tp == 2
+    assert np.isclose(v[0], 0.005 ** 2 * std[0] ** 2, rtol=1e-6)
+    assert np.isclose(v[2], 0.005 ** 2 * std[2] ** 2 / 16, rtol=1e-6)
+    assert np.isclose(v[60], 0.005 ** 2 * std[60] ** 2 / 16, rtol=1e-6)
+    assert np.allclose(p["R"][1], p["R"][0])  # q_type -1: R[t] = obs_var
+
+
+def test_no_gpu_ctx_fails_cleanly():
+    import torch
+    from vaevar import _lib
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = _lib.lib.vv_ctx_create(0, ctypes.byref(h))
+    assert rc != 0 and _lib.last_error()

@@ -1,0 +1,118 @@
+"""CPU: the oracle restatement (oracle/) against the golden fixtures generated from the real reference
+(oracle/make_golden.py imports /root/reference in the survey container). Pins the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLD
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+def test_g1_tiny_decoder():
+    from oracle.lgunet_ref import lgunet_forward, synth_params
+    from vaevar import config as C
+
+    g = gold("g1_tiny_decoder.npz")
+    p = synth_params(C.TINY)
+    z = torch.from_numpy(g["z"]).requires_grad_(True)
+    out = lgunet_forward(p, C.TINY, z)
+    (out * torch.from_numpy(g["cot"])).sum().backward()
+    assert rel(out.detach(), g["out"]) < 1e-6
+    assert rel(z.grad, g["grad"]) < 1e-6
+
+
+@pytest.mark.parametrize("shift", [0, 2])
+def test_g2_swin_block(shift):
+    from oracle.lgunet_ref import swin_block, shift_mask, rel_pos_index
+    from vaevar.synth import param_value
+
+    g = gold("g2_swin_block.npz")
+    pre = f"g2.s{shift}"
+    C = 32
+    shapes = {"norm1.weight": (C,), "norm1.bias": (C,), "attn.relative_position_bias_table": (49, 2),
+              "attn.qkv.weight": (3 * C, C), "attn.qkv.bias": (3 * C,), "attn.proj.weight": (C, C),
+              "attn.proj.bias": (C,), "norm2.weight": (C,), "norm2.bias": (C,), "mlp.fc1.weight": (4 * C, C),
+              "mlp.fc1.bias": (4 * C,), "mlp.fc2.weight": (C, 4 * C), "mlp.fc2.bias": (C,)}
+    p = {f"{pre}.{k}": torch.from_numpy(param_value(f"{pre}.{k}", s)) for k, s in shapes.items()}
+    x = torch.from_numpy(g[f"x_s{shift}"]).requires_grad_(True)
+    y = swin_block(x, p, pre, 2, 4, shift)
+    (y * torch.from_numpy(g[f"cot_s{shift}"])).sum().backward()
+    assert rel(y.detach(), g[f"out_s{shift}"]) < 1e-6
+    assert rel(x.grad, g[f"grad_s{shift}"]) < 1e-6
+    if shift:
+        assert np.array_equal(shift_mask(16, 32, 4, 2).numpy(), g["attn_mask_s2"])  # quirk Q1
+        assert np.array_equal(rel_pos_index(4).numpy(), g["rel_index"])
+
+
+def test_g4_nearest_maps():
+    """F.interpolate(mode='nearest') index maps (quirk Q3): src = floor(dst * in/out) in fp32."""
+    g = gold("g4_nearest_maps.npz")
+    for key, (a, b) in (("lat_721_to_128", (721, 128)), ("lat_128_to_721", (128, 721)),
+                        ("lon_1440_to_256", (1440, 256)), ("lon_256_to_1440", (256, 1440))):
+        scale = np.float32(a) / np.float32(b)
+        m = np.minimum(np.floor(np.arange(b, dtype=np.float32) * scale).astype(np.int64), a - 1)
+        assert np.array_equal(m, g[key]), key
+
+
+def _tiny_problem(T):
+    from vaevar.problem import make_problem
+
+    return make_problem(nch=4, Hs=32, Ws=64, T=T, seed=777, obs_frac=0.1)
+
+
+def test_g5b_tiny_4dvar_closure():
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+
+    g = gold("g5b_tiny_4dvar.npz")
+    ro = oracle_problem(_tiny_problem(2), synth_params(C.TINY), C.TINY, synth_params(C.TINY_FLOW), C.TINY_FLOW)
+    z = torch.from_numpy(g["z"]).requires_grad_(True)
+    r, o = ro.loss_terms(z)
+    (r + o).backward()
+    assert abs(float(r) - g["J_b"]) / g["J_b"] < 1e-6
+    assert abs(float(o) - g["J_o"]) / g["J_o"] < 1e-6
+    assert rel(z.grad, g["grad"]) < 1e-6
+
+
+def test_g5_tiny_lbfgs_trajectory():
+    from oracle.da_ref import one_step_da_ref, oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+
+    g = gold("g5_tiny_lbfgs.npz")
+    ro = oracle_problem(_tiny_problem(1), synth_params(C.TINY), C.TINY)
+    xa, z, js, nev, nit = one_step_da_ref(ro, 2, (4, 32, 64))
+    assert np.allclose(np.array(js), g["J"], rtol=1e-5)
+    assert nev == int(g["n_eval"]) and nit == int(g["n_iter"])
+    assert rel(xa, g["xa"]) < 1e-5
+
+
+def test_g3_full_decoder_oracle():
+    """Full parameters0_old decoder at 128x256 (216M params): oracle vs the reference's sampled outputs."""
+    from oracle.lgunet_ref import lgunet_forward, synth_params
+    from vaevar import config as C
+    from vaevar.synth import smooth_field, uniform_sym
+
+    g = gold("g3_full_decoder.npz")
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    p = synth_params(C.DECODER)
+    z = torch.from_numpy(0.5 * smooth_field(401, (1, 32, 128, 256))).requires_grad_(True)
+    cot = torch.from_numpy(uniform_sym(402, (1, 69, 128, 256), 1.0))
+    out = lgunet_forward(p, C.DECODER, z)
+    (out * cot).sum().backward()
+    o = out.detach().numpy().reshape(-1)
+    gr = z.grad.numpy().reshape(-1)
+    assert rel(o[g["idx_out"]], g["out_sample"]) < 1e-6
+    assert rel(gr[g["idx_grad"]], g["grad_sample"]) < 1e-6

@@ -1331,6 +1331,19 @@ int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n
   return 0;
 }
 
+int vv_profile_start(vv_ctx* ctx) {
+  if (!ctx) return fail(VV_E_ARG, "null ctx");
+  vv::prof_enable(true);
+  return 0;
+}
+
+int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* launches, int ncls) {
+  if (!ctx || ncls < vv::PC_N) return fail(VV_E_ARG, "need %d class slots", (int)vv::PC_N);
+  vv::prof_read(ms, flops, bytes, launches);
+  vv::prof_enable(false);
+  return 0;
+}
+
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C, int tile,
             void* stream) {
   if (!ctx || !A || !B || !C) return fail(VV_E_ARG, "null argument");

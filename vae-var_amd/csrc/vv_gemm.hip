@@ -196,12 +196,20 @@ hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint) {
   if (a.K % BK != 0 || a.ksplit % BK != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
+  const int ph = prof_begin(s);
+  hipError_t e;
   switch (t) {
-    case 0: return launch_tile<128, 128, 2, 2>(a, s);
-    case 1: return launch_tile<128, 64, 2, 2>(a, s);
-    case 2: return launch_tile<64, 64, 2, 2>(a, s);
+    case 0: e = launch_tile<128, 128, 2, 2>(a, s); break;
+    case 1: e = launch_tile<128, 64, 2, 2>(a, s); break;
+    case 2: e = launch_tile<64, 64, 2, 2>(a, s); break;
     default: return hipErrorInvalidValue;
   }
+  // algorithmic: 2MNK flops; bytes = A + B + C (+R/aux) once each
+  const double G = a.ngroups;
+  double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);
+  if (a.epi == EPI_RESID || a.epi == EPI_GELU || a.epi == EPI_DGELU) bytes += 4.0 * G * (double)a.M * a.N;
+  prof_end(ph, s, PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
+  return e;
 }
 
 }  // namespace vv

@@ -190,6 +190,16 @@ hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float
 hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
 hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                      float eps, float bc1, float bc2_sqrt, hipStream_t s);
+// ---------------------------------------------------------------------------
+// live profiler: HIP events around every launch, bucketed by kernel class
+// ---------------------------------------------------------------------------
+enum ProfClass : int { PC_GEMM = 0, PC_ATTN = 1, PC_LN = 2, PC_PATCH = 3, PC_MISFIT = 4, PC_VEC = 5, PC_N = 6 };
+int prof_begin(hipStream_t s);                                        // -1 when disabled
+void prof_end(int h, hipStream_t s, int cls, double flops, double bytes);
+void prof_enable(bool on);
+// sums since enable: ms, flops, bytes, launches per class (synchronises)
+void prof_read(double* ms, double* flops, double* bytes, int* n);
+
 hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStream_t s);
 hipError_t fill(float* p, float v, int64_t n, hipStream_t s);
 

@@ -5,7 +5,61 @@
 //   misfit J_o and its adjoint, vector primitives of L-BFGS / Adam
 #include "vv_kernels.h"
 
+#include <vector>
+
 namespace vv {
+
+// ============================================================================
+// live profiler
+// ============================================================================
+namespace {
+struct ProfRec {
+  int cls;
+  double flops, bytes;
+};
+bool g_prof_on = false;
+std::vector<hipEvent_t> g_ev;  // pairs
+std::vector<ProfRec> g_rec;
+size_t g_used = 0;
+}  // namespace
+
+void prof_enable(bool on) {
+  g_prof_on = on;
+  g_used = 0;
+  g_rec.clear();
+}
+int prof_begin(hipStream_t s) {
+  if (!g_prof_on) return -1;
+  if (2 * g_used + 2 > g_ev.size()) {
+    for (int i = 0; i < 512; ++i) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+      g_ev.push_back(e);
+    }
+  }
+  const int h = (int)g_used++;
+  (void)hipEventRecord(g_ev[2 * h], s);
+  return h;
+}
+void prof_end(int h, hipStream_t s, int cls, double flops, double bytes) {
+  if (h < 0) return;
+  (void)hipEventRecord(g_ev[2 * h + 1], s);
+  if ((int)g_rec.size() <= h) g_rec.resize(h + 1);
+  g_rec[h] = {cls, flops, bytes};
+}
+void prof_read(double* ms, double* flops, double* bytes, int* n) {
+  for (int c = 0; c < PC_N; ++c) ms[c] = flops[c] = bytes[c] = 0, n[c] = 0;
+  if (g_used) (void)hipEventSynchronize(g_ev[2 * (g_used - 1) + 1]);
+  for (size_t h = 0; h < g_used && h < g_rec.size(); ++h) {
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, g_ev[2 * h], g_ev[2 * h + 1]);
+    const int c = g_rec[h].cls;
+    ms[c] += t;
+    flops[c] += g_rec[h].flops;
+    bytes[c] += g_rec[h].bytes;
+    n[c] += 1;
+  }
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -107,12 +161,16 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
 
 hipError_t layernorm_fwd(const LnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_ln_fwd, dim3((a.rows + 3) / 4, a.ngroups), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_LN, 8.0 * a.rows * a.C * a.ngroups, 8.0 * a.rows * a.C * a.ngroups);
   return hipGetLastError();
 }
 hipError_t layernorm_bwd(const LnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_ln_bwd, dim3((a.rows + 3) / 4, a.ngroups), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_LN, 12.0 * a.rows * a.C * a.ngroups, (a.g[0].res ? 16.0 : 12.0) * a.rows * a.C * a.ngroups);
   return hipGetLastError();
 }
 
@@ -263,14 +321,20 @@ hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
   if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   const int hd = a.C / a.heads;
   const size_t lds = (3 * WN_ * (hd + 1) + WN_ * 17) * sizeof(float);
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
+  prof_end(ph, s, PC_ATTN, 4.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
+           4.0 * a.ngroups * ((double)a.nwin * WN_ * 4 * a.C + (double)a.nwin * a.heads * WN_ * WN_));
   return hipGetLastError();
 }
 hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
   if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   const int hd = a.C / a.heads;
   const size_t lds = (4 * WN_ * (hd + 1) + 2 * WN_ * 17) * sizeof(float);
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
+  prof_end(ph, s, PC_ATTN, 8.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
+           4.0 * a.ngroups * ((double)a.nwin * WN_ * 7 * a.C + (double)a.nwin * a.heads * WN_ * WN_));
   return hipGetLastError();
 }
 
@@ -384,22 +448,30 @@ __global__ __launch_bounds__(256) void k_unembed_bwd(PatchArgs a) {
 
 hipError_t patch_embed_fwd(const PatchArgs& a, hipStream_t s) {
   const int total = a.B * (a.Himg / 2) * (a.Wimg / 2) * a.Ctok;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_patch_fwd, dim3((total + 255) / 256, a.ngroups), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
   return hipGetLastError();
 }
 hipError_t patch_embed_bwd(const PatchArgs& a, hipStream_t s) {
   const int total = a.B * a.Cimg * a.Himg * a.Wimg;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_patch_bwd, dim3((total + 255) / 256), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
   return hipGetLastError();
 }
 hipError_t patch_unembed_fwd(const PatchArgs& a, hipStream_t s) {
   const int total = a.B * a.climit * a.Himg * a.Wimg;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_unembed_fwd, dim3((total + 255) / 256), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
   return hipGetLastError();
 }
 hipError_t patch_unembed_bwd(const PatchArgs& a, hipStream_t s) {
   const int total = a.B * (a.Himg / 2) * (a.Wimg / 2) * a.Ctok;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_unembed_bwd, dim3((total + 255) / 256, a.ngroups), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
   return hipGetLastError();
 }
 
@@ -455,12 +527,16 @@ __global__ __launch_bounds__(256) void k_misfit_bwd(MisfitBwdArgs a) {
 
 hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
   if (a.mi || a.mj || a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorNotSupported;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_misfit_fwd, dim3(a.nblk), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_MISFIT, 6.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * ((a.xb ? 6 : 5) + (a.flow_in ? 1 : 0)));
   return hipGetLastError();
 }
 hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
   if (a.mi || a.mj || a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorNotSupported;
+  const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_misfit_bwd, dim3(1024), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_MISFIT, 5.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * (a.g_carry ? 6 : 5));
   return hipGetLastError();
 }
 

@@ -87,6 +87,8 @@ _SIGS = {
     "vv_copy": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "vv_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                         c_float, c_int, c_void_p]),
+    "vv_profile_start": (c_int, [c_void_p]),
+    "vv_profile_stop": (c_int, [c_void_p, P(c_double), P(c_double), P(c_double), P(c_int), c_int]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 

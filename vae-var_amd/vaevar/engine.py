@@ -80,6 +80,20 @@ class Context:
         check(lib.vv_adam(self.h, _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), lr, beta1, beta2, eps, step,
                           _stream()), "adam")
 
+    PROF_CLASSES = ("gemm", "attention", "layernorm", "patch", "misfit", "vector")
+
+    def profile_start(self):
+        check(lib.vv_profile_start(self.h), "profile_start")
+
+    def profile_stop(self) -> dict:
+        """{class: dict(ms, flops, bytes, launches)} of every launch since profile_start (HIP events)."""
+        n = len(self.PROF_CLASSES)
+        ms, fl, by = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
+        cnt = (ctypes.c_int * n)()
+        check(lib.vv_profile_stop(self.h, ms, fl, by, cnt, n), "profile_stop")
+        return {c: {"ms": ms[i], "flops": fl[i], "bytes": by[i], "launches": cnt[i]}
+                for i, c in enumerate(self.PROF_CLASSES)}
+
     def gemm(self, A, B, bias=None, tile=-1):
         M, K = A.shape
         N = B.shape[0]
