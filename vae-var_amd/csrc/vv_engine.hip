@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -407,9 +408,24 @@ LnArgs ln_base(int rows, int C, int G, float eps) {
   return a;
 }
 
+// VAEVAR_SYNC_CHECK=1: synchronise after every launch and report the first failing op (debug only)
+bool sync_check() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VAEVAR_SYNC_CHECK");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 #define CK(expr)                                                                                   \
   do {                                                                                             \
     hipError_t e_ = (expr);                                                                        \
+    if (e_ == hipSuccess && sync_check()) {                                                        \
+      e_ = hipDeviceSynchronize();                                                                 \
+      if (e_ != hipSuccess) fprintf(stderr, "VAEVAR_SYNC_CHECK: %s:%d %s -> %s\n", __FILE__, __LINE__, \
+                                    #expr, hipGetErrorString(e_));                                 \
+    }                                                                                              \
     if (e_ != hipSuccess) return fail((int)e_, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,         \
                                       hipGetErrorString(e_));                                      \
   } while (0)

@@ -24,16 +24,95 @@ __device__ __forceinline__ float dgelu_f(float x) {
   return cdf + x * pdf;
 }
 
-constexpr int BK = 32;
-constexpr int LS = BK + 4;  // LDS row stride (floats)
+constexpr int KALIGN = 32;  // K, ksplit granularity accepted by gemm_nt (covers every BK variant)
 
-template <int BM, int BN, int WM, int WN, int EPI>
-__global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs args) {
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / WN / 32;
-  constexpr int AI = BM / 32;
-  constexpr int BI = BN / 32;
-  static_assert(WM * WN == 4, "4 waves");
+// GEMM epilogue. 32x32: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31; 16x16: row 4h + r,
+// col lane&15 (h = lane>>4). Everything an element needs (bias, output row, residual, pre-activation) is
+// loaded for the whole fragment first, so the stores are not serialised behind one dependent load each;
+// FULL tiles skip all bounds checks.
+template <int BM, int BN, int WM, int WN, int EPI, int MF, bool FULL, typename ACC>
+__device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& G, ACC& acc, int m0, int n0, int wm,
+                                         int wn, int rin, int hh) {
+  constexpr int TM = BM / WM / MF;
+  constexpr int TN = BN / WN / MF;
+  constexpr int NR = MF == 32 ? 16 : 4;
+  const int M = args.M, N = args.N;
+  float bv[TN];
+  int colv[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    colv[b] = n0 + wn * TN * MF + b * MF + rin;
+    const int cc = FULL ? colv[b] : min(colv[b], N - 1);
+    bv[b] = G.bias ? G.bias[cc] : 0.0f;
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    int ov[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int row = m0 + wm * TM * MF + a * MF + (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * hh : 4 * hh + r);
+      const int rc = FULL ? row : min(row, M - 1);
+      ov[r] = args.crow ? args.crow[rc] : rc;
+    }
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = FULL ? colv[b] : min(colv[b], N - 1);
+      float ex[NR];
+      if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int rr = args.rmod > 0 ? ov[r] % args.rmod : ov[r];
+          ex[r] = G.R[(size_t)rr * args.ldr + col];
+        }
+      } else if constexpr (EPI == EPI_DGELU) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) ex[r] = G.aux[(size_t)ov[r] * args.ldaux + col];
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        if (!FULL) {
+          const int row = m0 + wm * TM * MF + a * MF + (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * hh : 4 * hh + r);
+          if (row >= M || colv[b] >= N) continue;
+        }
+        const int o = ov[r];
+        float v = acc[a][b][r] + bv[b];
+        if constexpr (EPI == EPI_GELU) {
+          G.aux[(size_t)o * args.ldaux + col] = v;
+          v = gelu_f(v);
+        } else if constexpr (EPI == EPI_RESID) {
+          v = ex[r] + v;
+        } else if constexpr (EPI == EPI_DGELU) {
+          v = acc[a][b][r] * dgelu_f(ex[r]);
+        }
+        G.C[(size_t)o * args.ldc + col] = v;
+      }
+    }
+  }
+}
+
+// XCD-aware tile order: the dispatcher deals consecutive workgroups round-robin over the 8 XCDs; remap so
+// XCD x gets a contiguous range of logical tiles (M-major), i.e. a band of A rows that its 4 MB L2 serves
+// to all of its CUs (cdna_hip_programming.md T1, bijective form for tile counts not divisible by 8).
+__device__ __forceinline__ int xcd_remap(int bid, int nt) {
+  const int q = nt >> 3, r = nt & 7, x = bid & 7, l = bid >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int EPI, bool XCD, int MF>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int LS = BK + 4;        // LDS row stride (floats): rows land on distinct 16-B slots
+  constexpr int TPR = BK / 4;       // threads per staged row (float4 each)
+  constexpr int RPP = NT / TPR;     // rows per staging pass
+  constexpr int TM = BM / WM / MF;   // MFMA tiles per wave
+  constexpr int TN = BN / WN / MF;
+  constexpr int AI = BM / RPP;
+  constexpr int BI = BN / RPP;
+  constexpr int KG = 64 / MF;        // lane groups along k: 2 (32x32x2) or 4 (16x16x4)
+  constexpr int HALF = BK / KG;      // lane group h takes k in [h*HALF, (h+1)*HALF)
+  typedef float accv __attribute__((ext_vector_type(MF == 32 ? 16 : 4)));
+  static_assert(AI >= 1 && BI >= 1 && AI * RPP == BM && BI * RPP == BN, "staging shape");
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int tid = threadIdx.x;
@@ -41,22 +120,25 @@ __global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs args) {
   const int wave = tid >> 6;
   const GemmGroup G = args.g[blockIdx.z];
   const int M = args.M, N = args.N, K = args.K, ksplit = args.ksplit;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int lr = tid >> 3, lc = (tid & 7) * 4;
+  const int ntn = (N + BN - 1) / BN;
+  const int ntiles = ntn * ((M + BM - 1) / BM);
+  const int tile = XCD ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int lr = tid / TPR, lc = (tid % TPR) * 4;
 
   const float* a1p[AI];
   const float* a2p[AI];
   const float* bp[BI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int r = min(m0 + lr + 32 * i, M - 1);
+    const int r = min(m0 + lr + RPP * i, M - 1);
     const int ar = args.arow ? args.arow[r] : r;
     a1p[i] = G.A + (size_t)ar * args.lda + lc;
     a2p[i] = G.A2 ? G.A2 + (size_t)r * args.lda2 + lc - ksplit : a1p[i];
   }
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
-    const int n = min(n0 + lr + 32 * i, N - 1);
+    const int n = min(n0 + lr + RPP * i, N - 1);
     bp[i] = G.B + (size_t)n * K + lc;
   }
 
@@ -76,38 +158,43 @@ __global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs args) {
     float* As = smem + buf * (BM + BN) * LS;
     float* Bs = As + BM * LS;
 #pragma unroll
-    for (int i = 0; i < AI; ++i) *reinterpret_cast<f4*>(As + (lr + 32 * i) * LS + lc) = ra[i];
+    for (int i = 0; i < AI; ++i) *reinterpret_cast<f4*>(As + (lr + RPP * i) * LS + lc) = ra[i];
 #pragma unroll
-    for (int i = 0; i < BI; ++i) *reinterpret_cast<f4*>(Bs + (lr + 32 * i) * LS + lc) = rb[i];
+    for (int i = 0; i < BI; ++i) *reinterpret_cast<f4*>(Bs + (lr + RPP * i) * LS + lc) = rb[i];
   };
 
   const int wm = wave / WN, wn = wave % WN;
-  const int rin = lane & 31, hh = lane >> 5;
-  f16v acc[TM][TN];
+  const int rin = lane & (MF - 1), hh = lane / MF;
+  constexpr int NR = MF == 32 ? 16 : 4;
+  accv acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+      for (int r = 0; r < NR; ++r) acc[a][b][r] = 0.0f;
 
   auto compute = [&](int buf) {
-    const float* As = smem + buf * (BM + BN) * LS + (wm * TM * 32 + rin) * LS + hh * 16;
-    const float* Bs = smem + buf * (BM + BN) * LS + BM * LS + (wn * TN * 32 + rin) * LS + hh * 16;
+    const float* As = smem + buf * (BM + BN) * LS + (wm * TM * MF + rin) * LS + hh * HALF;
+    const float* Bs = smem + buf * (BM + BN) * LS + BM * LS + (wn * TN * MF + rin) * LS + hh * HALF;
 #pragma unroll
-    for (int kq = 0; kq < 4; ++kq) {
+    for (int kq = 0; kq < HALF / 4; ++kq) {
       f4 af[TM], bf[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a) af[a] = *reinterpret_cast<const f4*>(As + a * 32 * LS + kq * 4);
+      for (int a = 0; a < TM; ++a) af[a] = *reinterpret_cast<const f4*>(As + a * MF * LS + kq * 4);
 #pragma unroll
-      for (int b = 0; b < TN; ++b) bf[b] = *reinterpret_cast<const f4*>(Bs + b * 32 * LS + kq * 4);
+      for (int b = 0; b < TN; ++b) bf[b] = *reinterpret_cast<const f4*>(Bs + b * MF * LS + kq * 4);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
-          for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+          for (int b = 0; b < TN; ++b) {
+            if constexpr (MF == 32)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+            else
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+          }
     }
   };
 
@@ -123,51 +210,33 @@ __global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs args) {
     __syncthreads();
   }
 
-  // epilogue: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31 of the 32x32 tile
-  const float* bias = G.bias;
-#pragma unroll
-  for (int a = 0; a < TM; ++a) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      if (row >= M) continue;
-      const int o = args.crow ? args.crow[row] : row;
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = n0 + wn * TN * 32 + b * 32 + rin;
-        if (col >= N) continue;
-        float v = acc[a][b][r];
-        if (bias) v += bias[col];
-        if constexpr (EPI == EPI_GELU) {
-          G.aux[(size_t)o * args.ldaux + col] = v;
-          v = gelu_f(v);
-        } else if constexpr (EPI == EPI_RESID) {
-          const int rr = args.rmod > 0 ? o % args.rmod : o;
-          v = G.R[(size_t)rr * args.ldr + col] + v;
-        } else if constexpr (EPI == EPI_DGELU) {
-          v = v * dgelu_f(G.aux[(size_t)o * args.ldaux + col]);
-        }
-        G.C[(size_t)o * args.ldc + col] = v;
-      }
-    }
-  }
+  // epilogue: 32x32: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31;
+  //           16x16: row 4h + r, col lane&15 (h = lane>>4)
+  // Everything an element needs (bias, output row, residual, pre-activation) is loaded for the whole
+  // fragment first, so the stores are not serialised behind one dependent load each.
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, WM, WN, EPI, MF, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  else
+    epilogue<BM, BN, WM, WN, EPI, MF, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int BK, int WM, int WN, bool XCD = false, int MF = 32>
 static hipError_t launch_tile(const GemmArgs& a, hipStream_t s) {
+  constexpr int LS = BK + 4;
+  if (a.K % BK || a.ksplit % BK) return hipErrorInvalidValue;
   const size_t lds = 2 * (BM + BN) * LS * sizeof(float);
-  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, a.ngroups);
+  dim3 grid(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, a.ngroups);
   switch (a.epi) {
 #define VV_EPI(E)                                                                                   \
   case E: {                                                                                         \
     static bool init = false;                                                                       \
     if (!init) {                                                                                    \
-      hipError_t e = hipFuncSetAttribute((const void*)k_gemm_nt<BM, BN, WM, WN, E>,                 \
+      hipError_t e = hipFuncSetAttribute((const void*)k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF>,             \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
       if (e != hipSuccess) return e;                                                                \
       init = true;                                                                                  \
     }                                                                                               \
-    hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, E>), grid, dim3(256), lds, s, a);                \
+    hipLaunchKernelGGL((k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF>), grid, dim3(64 * WM * WN), lds, s, a);   \
     return hipGetLastError();                                                                       \
   }
     VV_EPI(EPI_STORE)
@@ -180,30 +249,47 @@ static hipError_t launch_tile(const GemmArgs& a, hipStream_t s) {
   }
 }
 
+// tile variants (index = tile hint)
+static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
+  switch (t) {
+    case 0: return launch_tile<128, 128, 32, 2, 2>(a, s);
+    case 1: return launch_tile<128, 64, 32, 2, 2>(a, s);
+    case 2: return launch_tile<64, 64, 32, 2, 2>(a, s);
+    case 3: return launch_tile<64, 64, 16, 2, 2>(a, s);
+    case 4: return launch_tile<32, 64, 32, 1, 2>(a, s);
+    case 5: return launch_tile<64, 32, 32, 2, 1>(a, s);
+    case 6: return launch_tile<64, 128, 32, 2, 2>(a, s);
+    case 7: return launch_tile<32, 64, 16, 1, 2>(a, s);
+    case 8: return launch_tile<64, 64, 64, 2, 2>(a, s);
+    case 9: return launch_tile<64, 64, 32, 2, 2, true>(a, s);     // 2 with the XCD remap
+    case 10: return launch_tile<64, 64, 32, 2, 2, false, 16>(a, s);   // 16x16x4 MFMA
+    case 11: return launch_tile<128, 64, 32, 2, 2, false, 16>(a, s);
+    case 12: return launch_tile<64, 128, 32, 2, 2, false, 16>(a, s);
+    case 13: return launch_tile<128, 128, 32, 2, 2, false, 16>(a, s);
+    case 14: return launch_tile<64, 64, 16, 2, 2, false, 16>(a, s);
+    case 15: return launch_tile<32, 64, 32, 1, 2, false, 16>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 static long tiles_of(const GemmArgs& a, int bm, int bn) {
   return (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.ngroups;
 }
 
-// tile choice: the largest tile that still gives every CU (256 on MI355X) work
+// tile choice (measured on MI355X, tools/gemm_bench.py; 4 WGs/CU resident): high-occupancy 64x64 tiles beat
+// larger tiles on every decoder shape at M = 2048 / 8192; 32x64 when 64x64 leaves CUs idle
 static int pick_tile(const GemmArgs& a) {
-  if (tiles_of(a, 128, 128) >= 480) return 0;
-  if (tiles_of(a, 128, 64) >= 400) return 1;
-  return 2;
+  if (tiles_of(a, 64, 64) >= 512) return 2;
+  return 4;
 }
 
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint) {
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
-  if (a.K % BK != 0 || a.ksplit % BK != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
+  if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
   const int ph = prof_begin(s);
-  hipError_t e;
-  switch (t) {
-    case 0: e = launch_tile<128, 128, 2, 2>(a, s); break;
-    case 1: e = launch_tile<128, 64, 2, 2>(a, s); break;
-    case 2: e = launch_tile<64, 64, 2, 2>(a, s); break;
-    default: return hipErrorInvalidValue;
-  }
+  const hipError_t e = launch_variant(t, a, s);
   // algorithmic: 2MNK flops; bytes = A + B + C (+R/aux) once each
   const double G = a.ngroups;
   double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);

@@ -5,6 +5,7 @@
 //   misfit J_o and its adjoint, vector primitives of L-BFGS / Adam
 #include "vv_kernels.h"
 
+#include <algorithm>
 #include <vector>
 
 namespace vv {
@@ -61,6 +62,8 @@ void prof_read(double* ms, double* flops, double* bytes, int* n) {
   }
 }
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -75,103 +78,211 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // ============================================================================
 // LayerNorm  (nn.LayerNorm: biased variance, y = (x-mean)/sqrt(var+eps)*g + b)
 // ============================================================================
-struct LnAddr {
-  // element (r, c) of the *input* row for output row r, in a buffer with row stride ld
-  int mode, C, Hin, Win;
-  const int* map;
-  __device__ __forceinline__ size_t off(int r, int c, int ld) const {
-    if (mode == LN_ROWMAP) {
-      const int ir = map ? map[r] : r;
-      return (size_t)ir * ld + c;
-    } else if (mode == LN_MERGE) {
-      const int Hh = Hin >> 1, Wh = Win >> 1;
-      const int b = r / (Hh * Wh);
-      const int rem = r - b * Hh * Wh;
-      const int h = rem / Wh, w = rem - h * Wh;
-      const int Cs = C >> 2;
-      const int q = c / Cs, cc = c - q * Cs;
-      const int tok = (b * Hin + 2 * h + (q & 1)) * Win + 2 * w + (q >> 1);
-      return (size_t)tok * ld + cc;
-    } else {  // LN_EXPAND: output grid (2Hin, 2Win); input row (b, y/2, x/2), segment (y%2)*2 + x%2
-      const int Wo = Win * 2, Ho = Hin * 2;
-      const int b = r / (Ho * Wo);
-      const int rem = r - b * Ho * Wo;
-      const int y = rem / Wo, x = rem - y * Wo;
-      const int ir = (b * Hin + (y >> 1)) * Win + (x >> 1);
-      const int seg = (y & 1) * 2 + (x & 1);
-      return (size_t)ir * ld + seg * C + c;
-    }
-  }
-};
+// One row per L-lane sub-wave, the row held in registers as float4 (NV <= 8 per lane): one HBM read of x,
+// one write of y. Gathers (window / merge / expand) keep float4 granularity (segment widths are multiples of 4).
+constexpr int LN_NVMAX = 8;
 
+template <int L>
+__device__ __forceinline__ float sub_sum(float v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// element offsets (relative to the input base, row stride ld) of this lane's float4s of output row r
+template <int L, int NV>
+__device__ __forceinline__ void ln_offsets(const LnArgs& a, int r, int sl, int ld, size_t (&eo)[NV]) {
+  const int C = a.C, f4n = C >> 2;
+  if (a.mode == LN_ROWMAP) {
+    const size_t base = (size_t)(a.map ? a.map[r] : r) * ld;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) eo[v] = base + 4 * (sl + v * L);
+  } else if (a.mode == LN_MERGE) {
+    const int Hh = a.Hin >> 1, Wh = a.Win >> 1;
+    const int b = r / (Hh * Wh);
+    const int rem = r - b * Hh * Wh;
+    const int h = rem / Wh, w = rem - h * Wh;
+    const int Cs = C >> 2;
+    size_t tb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      tb[q] = (size_t)((b * a.Hin + 2 * h + (q & 1)) * a.Win + 2 * w + (q >> 1)) * ld;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = 4 * (sl + v * L);
+      const int q = min(c / Cs, 3);
+      eo[v] = tb[q] + (c - q * Cs);
+    }
+  } else {
+    const int Wo = a.Win * 2, Ho = a.Hin * 2;
+    const int b = r / (Ho * Wo);
+    const int rem = r - b * Ho * Wo;
+    const int y = rem / Wo, x = rem - y * Wo;
+    const size_t base = (size_t)((b * a.Hin + (y >> 1)) * a.Win + (x >> 1)) * ld + ((y & 1) * 2 + (x & 1)) * C;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) eo[v] = base + 4 * (sl + v * L);
+  }
+  (void)f4n;
+}
+
+template <int L, int NV>
 __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr int RPB = 256 / L;
+  const int sl = threadIdx.x % L;
+  const int r = blockIdx.x * RPB + threadIdx.x / L;
   if (r >= a.rows) return;
   const LnGroup G = a.g[blockIdx.y];
-  const LnAddr ad{a.mode, a.C, a.Hin, a.Win, a.map};
-  const int C = a.C;
+  const int C = a.C, f4n = C >> 2;
+  size_t eo[NV];
+  ln_offsets<L, NV>(a, r, sl, a.ldx, eo);
+  f4 xv[NV];
   float s = 0.f;
-  for (int c = lane; c < C; c += 64) s += G.x[ad.off(r, c, a.ldx)];
-  const float mean = wave_sum(s) / (float)C;
-  float v = 0.f;
-  for (int c = lane; c < C; c += 64) {
-    const float d = G.x[ad.off(r, c, a.ldx)] - mean;
-    v += d * d;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (sl + v * L < f4n) {
+      xv[v] = *reinterpret_cast<const f4*>(G.x + eo[v]);
+      s += (xv[v][0] + xv[v][1]) + (xv[v][2] + xv[v][3]);
+    }
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)C + a.eps);
+  const float mean = sub_sum<L>(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (sl + v * L < f4n) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = xv[v][e] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = 1.0f / sqrtf(sub_sum<L>(q) / (float)C + a.eps);
   float* y = G.y + (size_t)r * a.ldy;
-  for (int c = lane; c < C; c += 64) {
-    const float xh = (G.x[ad.off(r, c, a.ldx)] - mean) * rstd;
-    y[c] = xh * G.gamma[c] + G.beta[c];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int j = sl + v * L;
+    if (j < f4n) {
+      const f4 g = *reinterpret_cast<const f4*>(G.gamma + 4 * j);
+      const f4 b = *reinterpret_cast<const f4*>(G.beta + 4 * j);
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (xv[v][e] - mean) * rstd * g[e] + b[e];
+      *reinterpret_cast<f4*>(y + 4 * j) = o;
+    }
   }
-  if (lane == 0 && G.stats) {
+  if (sl == 0 && G.stats) {
     G.stats[2 * r] = mean;
     G.stats[2 * r + 1] = rstd;
   }
 }
 
-// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) ; written back at the input position
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)), written back at the input position (+ res);
+// x, dx and res share the input layout (ldx == ldy == ldres, checked on the host)
+template <int L, int NV>
 __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr int RPB = 256 / L;
+  const int sl = threadIdx.x % L;
+  const int r = blockIdx.x * RPB + threadIdx.x / L;
   if (r >= a.rows) return;
   const LnGroup G = a.g[blockIdx.y];
-  const LnAddr ad{a.mode, a.C, a.Hin, a.Win, a.map};
-  const int C = a.C;
+  const int C = a.C, f4n = C >> 2;
+  size_t eo[NV];
+  ln_offsets<L, NV>(a, r, sl, a.ldx, eo);
   const float mean = G.stats[2 * r], rstd = G.stats[2 * r + 1];
   const float* dy = G.dy + (size_t)r * a.lddy;
   float s1 = 0.f, s2 = 0.f;
-  for (int c = lane; c < C; c += 64) {
-    const float gdy = G.gamma[c] * dy[c];
-    const float xh = (G.x[ad.off(r, c, a.ldx)] - mean) * rstd;
-    s1 += gdy;
-    s2 += gdy * xh;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int j = sl + v * L;
+    if (j < f4n) {
+      const f4 x = *reinterpret_cast<const f4*>(G.x + eo[v]);
+      const f4 d = *reinterpret_cast<const f4*>(dy + 4 * j);
+      const f4 g = *reinterpret_cast<const f4*>(G.gamma + 4 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gd = g[e] * d[e];
+        s1 += gd;
+        s2 += gd * ((x[e] - mean) * rstd);
+      }
+    }
   }
-  const float m1 = wave_sum(s1) / (float)C;
-  const float m2 = wave_sum(s2) / (float)C;
-  for (int c = lane; c < C; c += 64) {
-    const float gdy = G.gamma[c] * dy[c];
-    const float xh = (G.x[ad.off(r, c, a.ldx)] - mean) * rstd;
-    float dx = rstd * (gdy - m1 - xh * m2);
-    if (G.res) dx += G.res[ad.off(r, c, a.ldres)];
-    G.y[ad.off(r, c, a.ldy)] = dx;
+  const float m1 = sub_sum<L>(s1) / (float)C;
+  const float m2 = sub_sum<L>(s2) / (float)C;
+  // second pass re-reads the row (L1/L2-resident) instead of holding it in registers
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int j = sl + v * L;
+    if (j < f4n) {
+      const f4 x = *reinterpret_cast<const f4*>(G.x + eo[v]);
+      const f4 d = *reinterpret_cast<const f4*>(dy + 4 * j);
+      const f4 g = *reinterpret_cast<const f4*>(G.gamma + 4 * j);
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rstd * (g[e] * d[e] - m1 - ((x[e] - mean) * rstd) * m2);
+      if (G.res) {
+        const f4 rr = *reinterpret_cast<const f4*>(G.res + eo[v]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += rr[e];
+      }
+      *reinterpret_cast<f4*>(G.y + eo[v]) = o;
+    }
   }
+}
+
+// lanes per row: <= 3 float4 per lane up to C = 384, then a full wave (C = 1152: 4.5 float4 per lane)
+static int ln_lanes(int C) {
+  const int f4n = C / 4;
+  if (f4n <= 24) return 8;
+  if (f4n <= 48) return 16;
+  if (f4n <= 96) return 32;
+  return 64;
+}
+
+template <bool FWD>
+static hipError_t ln_launch(const LnArgs& a, hipStream_t s) {
+  if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  if ((a.C & 3) || a.C / 4 > 64 * LN_NVMAX) return hipErrorInvalidValue;
+  if ((a.ldx & 3) || (a.ldy & 3) || (a.lddy & 3) || (a.ldres & 3)) return hipErrorInvalidValue;
+  if (a.mode == LN_MERGE && ((a.C / 4) & 3)) return hipErrorInvalidValue;
+  if (!FWD && (a.ldy != a.ldx || (a.g[0].res && a.ldres != a.ldx))) return hipErrorInvalidValue;
+  const int L = ln_lanes(a.C);
+  const int need = (a.C / 4 + L - 1) / L;
+  const int NV = need <= 1 ? 1 : need <= 2 ? 2 : need <= 3 ? 3 : need <= 5 ? 5 : 8;
+  const int rpb = 256 / L;
+  dim3 grid((a.rows + rpb - 1) / rpb, a.ngroups);
+  const int key = L * 16 + NV;
+  switch (key) {
+#define LNL(LL, NN)                                                                               \
+  case LL * 16 + NN:                                                                              \
+    if (FWD)                                                                                      \
+      hipLaunchKernelGGL((k_ln_fwd<LL, NN>), grid, dim3(256), 0, s, a);                           \
+    else                                                                                          \
+      hipLaunchKernelGGL((k_ln_bwd<LL, NN>), grid, dim3(256), 0, s, a);                           \
+    break;
+    LNL(8, 1) LNL(8, 2) LNL(8, 3)
+    LNL(16, 1) LNL(16, 2) LNL(16, 3)
+    LNL(32, 1) LNL(32, 2) LNL(32, 3)
+    LNL(64, 1) LNL(64, 2) LNL(64, 3) LNL(64, 5) LNL(64, 8)
+#undef LNL
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t layernorm_fwd(const LnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_ln_fwd, dim3((a.rows + 3) / 4, a.ngroups), dim3(256), 0, s, a);
+  const hipError_t e = ln_launch<true>(a, s);
   prof_end(ph, s, PC_LN, 8.0 * a.rows * a.C * a.ngroups, 8.0 * a.rows * a.C * a.ngroups);
-  return hipGetLastError();
+  return e;
 }
 hipError_t layernorm_bwd(const LnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_ln_bwd, dim3((a.rows + 3) / 4, a.ngroups), dim3(256), 0, s, a);
+  const hipError_t e = ln_launch<false>(a, s);
   prof_end(ph, s, PC_LN, 12.0 * a.rows * a.C * a.ngroups, (a.g[0].res ? 16.0 : 12.0) * a.rows * a.C * a.ngroups);
-  return hipGetLastError();
+  return e;
 }
 
 // ============================================================================
@@ -340,139 +451,192 @@ hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
 
 // ============================================================================
 // PatchEmbed (Conv2d k=s=2) + absolute_pos_embed   (transformer.py:41-49, 392-394)
+// ConvTranspose2d(k=s=2) + Dec_net mean/std reorder (transformer.py:593-623, quirk Q2)
+// Block = 64 consecutive tokens of one tower (blockIdx.y); the tower's weights and the block's token rows /
+// 2x2 pixel patches are staged in LDS so every global access is coalesced.
 // ============================================================================
+constexpr int PT = 64;  // tokens per block
+
+__device__ __forceinline__ void tok_coords(int tok, int Ho, int Wo, int& b, int& ho, int& wo) {
+  b = tok / (Ho * Wo);
+  const int rem = tok - b * Ho * Wo;
+  ho = rem / Wo;
+  wo = rem - ho * Wo;
+}
+
+// tok[t][co] = (sum_{ci,p,q} w[co][ci][p][q] * img[cin_off+ci][2ho+p][2wo+q] + bias[co]) + pos[t][co]
 __global__ __launch_bounds__(256) void k_patch_fwd(PatchArgs a) {
-  const PatchGroup G = a.g[blockIdx.y];
-  const int Ho = a.Himg / 2, Wo = a.Wimg / 2;
-  const int total = a.B * Ho * Wo * a.Ctok;
-  const int id = blockIdx.x * 256 + threadIdx.x;
-  if (id >= total) return;
-  const int co = id % a.Ctok;
-  const int tok = id / a.Ctok;
-  const int b = tok / (Ho * Wo);
-  const int rem = tok - b * Ho * Wo;
-  const int ho = rem / Wo, wo = rem - ho * Wo;
-  float acc = 0.f;
-  for (int ci = 0; ci < G.cin; ++ci) {
-    const float* img = a.img + (((size_t)b * a.Cimg + G.cin_off + ci) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
-    const float* w = G.w + ((size_t)co * G.cin + ci) * 4;
-    acc += w[0] * img[0] + w[1] * img[1] + w[2] * img[a.Wimg] + w[3] * img[a.Wimg + 1];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const PatchGroup& G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
+  const int kc = G.cin * 4, kcp = kc + 1, C = a.Ctok;
+  float* Ws = sm;              // [C][kc+1]
+  float* Xs = Ws + C * kcp;    // [PT][kc+1]
+  const int t0 = blockIdx.x * PT;
+  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i / kc) * kcp + i % kc] = G.w[i];
+  for (int i = threadIdx.x; i < PT * kc; i += 256) {
+    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;  // rest = ci*2 + p
+    const int ci = rest >> 1, p = rest & 1;
+    const int tok = t0 + t;
+    float v = 0.f;
+    if (tok < ntok) {
+      int b, ho, wo;
+      tok_coords(tok, Ho, Wo, b, ho, wo);
+      v = a.img[(((size_t)b * a.Cimg + G.cin_off + ci) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q];
+    }
+    Xs[t * kcp + ci * 4 + p * 2 + q] = v;
   }
-  G.tok[(size_t)tok * a.Ctok + co] = (acc + G.bias[co]) + G.pos[(size_t)rem * a.Ctok + co];
+  __syncthreads();
+  for (int i = threadIdx.x; i < PT * C; i += 256) {
+    const int t = i / C, co = i - t * C;
+    const int tok = t0 + t;
+    if (tok >= ntok) continue;
+    float acc = 0.f;
+    for (int j = 0; j < kc; ++j) acc += Ws[co * kcp + j] * Xs[t * kcp + j];
+    const int rem = tok % (Ho * Wo);
+    G.tok[(size_t)tok * C + co] = (acc + G.bias[co]) + G.pos[(size_t)rem * C + co];
+  }
 }
 
+// dimg[cin_off+ci][2ho+p][2wo+q] = add + sum_co dtok[t][co] * w[co][ci][p][q]
 __global__ __launch_bounds__(256) void k_patch_bwd(PatchArgs a) {
-  const int total = a.B * a.Cimg * a.Himg * a.Wimg;
-  const int id = blockIdx.x * 256 + threadIdx.x;
-  if (id >= total) return;
-  const int x = id % a.Wimg;
-  const int y = (id / a.Wimg) % a.Himg;
-  const int ch = (id / (a.Wimg * a.Himg)) % a.Cimg;
-  const int b = id / (a.Wimg * a.Himg * a.Cimg);
-  float acc = 0.f;
-  for (int g = 0; g < a.ngroups; ++g) {
-    const PatchGroup& G = a.g[g];
-    if (ch < G.cin_off || ch >= G.cin_off + G.cin) continue;
-    const int ci = ch - G.cin_off;
-    const int Wo = a.Wimg / 2, Ho = a.Himg / 2;
-    const int tok = (b * Ho + (y >> 1)) * Wo + (x >> 1);
-    const float* dt = G.dtok + (size_t)tok * a.Ctok;
-    const float* w = G.w + (size_t)ci * 4 + (y & 1) * 2 + (x & 1);
-    const size_t wstride = (size_t)G.cin * 4;
-    for (int co = 0; co < a.Ctok; ++co) acc += dt[co] * w[co * wstride];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const PatchGroup& G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
+  const int kc = G.cin * 4, C = a.Ctok, Cp = C + 1;
+  float* Ws = sm;             // [kc][C+1]  (transposed: j-major)
+  float* Ds = Ws + kc * Cp;   // [PT][C+1]
+  const int t0 = blockIdx.x * PT;
+  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i % kc) * Cp + i / kc] = G.w[i];
+  for (int i = threadIdx.x; i < PT * C; i += 256) {
+    const int t = i / C, co = i - t * C;
+    Ds[t * Cp + co] = (t0 + t < ntok) ? G.dtok[(size_t)(t0 + t) * C + co] : 0.f;
   }
-  if (a.add_img) acc += a.add_img[id];
-  a.img_out[id] = acc;
-}
-
-// ConvTranspose2d(Ctok -> cout, k=s=2) with Dec_net's mean/std channel reorder (quirk Q2)
-__device__ __forceinline__ bool unembed_chan(const PatchArgs& a, int ch, int& g, int& co) {
-  for (g = 0; g < a.ngroups; ++g) {
-    const PatchGroup& G = a.g[g];
-    const int half = G.cout / 2;
-    if (ch >= G.mean_off && ch < G.mean_off + half) {
-      co = ch - G.mean_off;
-      return true;
-    }
-    if (ch >= G.std_off && ch < G.std_off + (G.cout - half)) {
-      co = half + ch - G.std_off;
-      return true;
-    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < PT * kc; i += 256) {
+    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;
+    const int ci = rest >> 1, p = rest & 1;
+    const int tok = t0 + t;
+    if (tok >= ntok) continue;
+    const float* wr = Ws + (ci * 4 + p * 2 + q) * Cp;
+    const float* dr = Ds + t * Cp;
+    float acc = 0.f;
+    for (int co = 0; co < C; ++co) acc += dr[co] * wr[co];
+    int b, ho, wo;
+    tok_coords(tok, Ho, Wo, b, ho, wo);
+    const size_t o = (((size_t)b * a.Cimg + G.cin_off + ci) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q;
+    if (a.add_img) acc += a.add_img[o];
+    a.img_out[o] = acc;
   }
-  return false;
 }
 
-__global__ __launch_bounds__(256) void k_unembed_fwd(PatchArgs a) {
-  const int total = a.B * a.climit * a.Himg * a.Wimg;
-  const int id = blockIdx.x * 256 + threadIdx.x;
-  if (id >= total) return;
-  const int x = id % a.Wimg;
-  const int y = (id / a.Wimg) % a.Himg;
-  const int ch = (id / (a.Wimg * a.Himg)) % a.climit;
-  const int b = id / (a.Wimg * a.Himg * a.climit);
-  int g, co;
-  if (!unembed_chan(a, ch, g, co)) return;
-  const PatchGroup& G = a.g[g];
-  const int Wo = a.Wimg / 2, Ho = a.Himg / 2;
-  const int tok = (b * Ho + (y >> 1)) * Wo + (x >> 1);
-  const float* t = G.tok + (size_t)tok * a.Ctok;
-  const float* w = G.w + (size_t)co * 4 + (y & 1) * 2 + (x & 1);
-  const size_t wstride = (size_t)G.cout * 4;
-  float acc = 0.f;
-  for (int ci = 0; ci < a.Ctok; ++ci) acc += t[ci] * w[ci * wstride];
-  a.img_out[(((size_t)b * a.Cimg + ch) * a.Himg + y) * a.Wimg + x] = acc + G.bias[co];
-}
-
-__global__ __launch_bounds__(256) void k_unembed_bwd(PatchArgs a) {
-  const PatchGroup G = a.g[blockIdx.y];
-  const int Ho = a.Himg / 2, Wo = a.Wimg / 2;
-  const int total = a.B * Ho * Wo * a.Ctok;
-  const int id = blockIdx.x * 256 + threadIdx.x;
-  if (id >= total) return;
-  const int ci = id % a.Ctok;
-  const int tok = id / a.Ctok;
-  const int b = tok / (Ho * Wo);
-  const int rem = tok - b * Ho * Wo;
-  const int ho = rem / Wo, wo = rem - ho * Wo;
+__device__ __forceinline__ int unembed_ch(const PatchGroup& G, int co) {
   const int half = G.cout / 2;
-  float acc = 0.f;
-  for (int co = 0; co < G.cout; ++co) {
-    const int ch = co < half ? G.mean_off + co : G.std_off + co - half;
-    if (ch >= a.climit) continue;
-    const float* d = a.img + (((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
-    const float* w = G.w + ((size_t)ci * G.cout + co) * 4;
-    acc += w[0] * d[0] + w[1] * d[1] + w[2] * d[a.Wimg] + w[3] * d[a.Wimg + 1];
+  return co < half ? G.mean_off + co : G.std_off + co - half;
+}
+
+// out[ch(co)][2ho+p][2wo+q] = bias[co] + sum_ci tok[t][ci] * w[ci][co][p][q]   (channels < climit only)
+__global__ __launch_bounds__(256) void k_unembed_fwd(PatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const PatchGroup& G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
+  const int kc = G.cout * 4, C = a.Ctok, Cp = C + 1;
+  float* Ws = sm;            // [kc][C+1] (transposed)
+  float* Ts = Ws + kc * Cp;  // [PT][C+1]
+  const int t0 = blockIdx.x * PT;
+  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i % kc) * Cp + i / kc] = G.w[i];
+  for (int i = threadIdx.x; i < PT * C; i += 256) {
+    const int t = i / C, ci = i - t * C;
+    Ts[t * Cp + ci] = (t0 + t < ntok) ? G.tok[(size_t)(t0 + t) * C + ci] : 0.f;
   }
-  G.tok[(size_t)tok * a.Ctok + ci] = acc;
+  __syncthreads();
+  for (int i = threadIdx.x; i < PT * kc; i += 256) {
+    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;  // rest = co*2 + p
+    const int co = rest >> 1, p = rest & 1;
+    const int tok = t0 + t;
+    const int ch = unembed_ch(G, co);
+    if (tok >= ntok || ch >= a.climit) continue;
+    const float* wr = Ws + (co * 4 + p * 2 + q) * Cp;
+    const float* tr = Ts + t * Cp;
+    float acc = 0.f;
+    for (int ci = 0; ci < C; ++ci) acc += tr[ci] * wr[ci];
+    int b, ho, wo;
+    tok_coords(tok, Ho, Wo, b, ho, wo);
+    a.img_out[(((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q] = acc + G.bias[co];
+  }
+}
+
+// dtok[t][ci] = sum_{co,p,q} dout[ch(co)][2ho+p][2wo+q] * w[ci][co][p][q]   (channels < climit only)
+__global__ __launch_bounds__(256) void k_unembed_bwd(PatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const PatchGroup& G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
+  const int kc = G.cout * 4, kcp = kc + 1, C = a.Ctok;
+  float* Ws = sm;            // [C][kc+1]
+  float* Ds = Ws + C * kcp;  // [PT][kc+1]
+  const int t0 = blockIdx.x * PT;
+  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i / kc) * kcp + i % kc] = G.w[i];
+  for (int i = threadIdx.x; i < PT * kc; i += 256) {
+    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;
+    const int co = rest >> 1, p = rest & 1;
+    const int tok = t0 + t;
+    const int ch = unembed_ch(G, co);
+    float v = 0.f;
+    if (tok < ntok && ch < a.climit) {
+      int b, ho, wo;
+      tok_coords(tok, Ho, Wo, b, ho, wo);
+      v = a.img[(((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q];
+    }
+    Ds[t * kcp + co * 4 + p * 2 + q] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < PT * C; i += 256) {
+    const int t = i / C, ci = i - t * C;
+    const int tok = t0 + t;
+    if (tok >= ntok) continue;
+    const float* wr = Ws + ci * kcp;
+    const float* dr = Ds + t * kcp;
+    float acc = 0.f;
+    for (int j = 0; j < kc; ++j) acc += dr[j] * wr[j];
+    G.tok[(size_t)tok * C + ci] = acc;
+  }
+}
+
+static int max_k(const PatchArgs& a, bool in) {
+  int m = 0;
+  for (int g = 0; g < a.ngroups; ++g) m = std::max(m, (in ? a.g[g].cin : a.g[g].cout) * 4);
+  return m;
+}
+
+template <typename K>
+static hipError_t patch_launch(K kern, const PatchArgs& a, size_t lds, hipStream_t s) {
+  if (a.ngroups <= 0 || a.ngroups > kMaxGroups || lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
+  const int ph = prof_begin(s);
+  hipLaunchKernelGGL(kern, dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
+  return hipGetLastError();
 }
 
 hipError_t patch_embed_fwd(const PatchArgs& a, hipStream_t s) {
-  const int total = a.B * (a.Himg / 2) * (a.Wimg / 2) * a.Ctok;
-  const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_patch_fwd, dim3((total + 255) / 256, a.ngroups), dim3(256), 0, s, a);
-  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
-  return hipGetLastError();
+  const int kc = max_k(a, true);
+  return patch_launch(k_patch_fwd, a, (size_t)(a.Ctok + PT) * (kc + 1) * sizeof(float), s);
 }
 hipError_t patch_embed_bwd(const PatchArgs& a, hipStream_t s) {
-  const int total = a.B * a.Cimg * a.Himg * a.Wimg;
-  const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_patch_bwd, dim3((total + 255) / 256), dim3(256), 0, s, a);
-  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
-  return hipGetLastError();
+  const int kc = max_k(a, true);
+  return patch_launch(k_patch_bwd, a, (size_t)(kc + PT) * (a.Ctok + 1) * sizeof(float), s);
 }
 hipError_t patch_unembed_fwd(const PatchArgs& a, hipStream_t s) {
-  const int total = a.B * a.climit * a.Himg * a.Wimg;
-  const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_unembed_fwd, dim3((total + 255) / 256), dim3(256), 0, s, a);
-  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
-  return hipGetLastError();
+  const int kc = max_k(a, false);
+  return patch_launch(k_unembed_fwd, a, (size_t)(kc + PT) * (a.Ctok + 1) * sizeof(float), s);
 }
 hipError_t patch_unembed_bwd(const PatchArgs& a, hipStream_t s) {
-  const int total = a.B * (a.Himg / 2) * (a.Wimg / 2) * a.Ctok;
-  const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_unembed_bwd, dim3((total + 255) / 256, a.ngroups), dim3(256), 0, s, a);
-  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
-  return hipGetLastError();
+  const int kc = max_k(a, false);
+  return patch_launch(k_unembed_bwd, a, (size_t)(a.Ctok + PT) * (kc + 1) * sizeof(float), s);
 }
 
 // ============================================================================
