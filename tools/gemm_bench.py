@@ -6,9 +6,9 @@ import torch
 from vaevar.engine import Context
 
 ctx = Context.get(0)
-shapes = [(2048, 3456, 1152), (2048, 1152, 1152), (2048, 4608, 1152), (2048, 1152, 4608), (2048, 1152, 3456),
+shapes = [(2048, 1024, 4608), (2048, 3456, 1152), (2048, 1152, 1152), (2048, 4608, 1152), (2048, 1152, 4608), (2048, 1152, 3456),
           (8192, 288, 96), (8192, 96, 384), (2048, 576, 192), (2048, 192, 768), (4096, 4608, 1152), (4096, 1152, 4608)]
-tiles = [int(t) for t in os.environ.get("TILES", "2,4,8,10,13").split(",")]
+tiles = [int(t) for t in os.environ.get("TILES", "2,16,4").split(",")]
 res = []
 for (M, N, K) in shapes:
     A = torch.rand(M, K, device="cuda") * 2 - 1

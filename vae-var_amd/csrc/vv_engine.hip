@@ -215,6 +215,7 @@ struct StageSave {
 
 struct Scratch {
   float *t1, *t2, *h, *dqkv;
+  float* ws;  // GEMM tail-split partials (vv::gemm_ws_floats())
 };
 
 struct Save {
@@ -259,6 +260,7 @@ struct vv_ctx {
   std::vector<std::unique_ptr<Model>> models;
   Problem prob;
   double* red = nullptr;   // reduction scratch
+  float* gemm_ws = nullptr;
   float* redf = nullptr;
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
@@ -448,7 +450,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
-    CK(gemm_nt(q, st));
+    CK(gemm_nt(q, st, -1, sc.ws));
     // window attention
     AttnArgs at;
     memset(&at, 0, sizeof(at));
@@ -472,7 +474,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     for (int g = 0; g < G; ++g)
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
                 nullptr};
-    CK(gemm_nt(p, st));
+    CK(gemm_nt(p, st, -1, sc.ws));
     // LN2
     LnArgs ln2 = ln_base(M, C, G, 1e-5f);
     for (int g = 0; g < G; ++g)
@@ -484,13 +486,13 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, sc.h + g * MC * 4, nullptr,
                  sv.h1[b] + g * MC * 4};
-    CK(gemm_nt(f1, st));
+    CK(gemm_nt(f1, st, -1, sc.ws));
     // fc2 + residual
     GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, sv.x[b + 1] + g * MC, sv.x1[b] + g * MC,
                  nullptr};
-    CK(gemm_nt(f2, st));
+    CK(gemm_nt(f2, st, -1, sc.ws));
   }
   return 0;
 }
@@ -506,11 +508,11 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
-    CK(gemm_nt(f2, st));
+    CK(gemm_nt(f2, st, -1, sc.ws));
     GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE);
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
-    CK(gemm_nt(f1, st));
+    CK(gemm_nt(f1, st, -1, sc.ws));
     LnArgs ln2 = ln_base(M, C, G, 1e-5f);
     for (int g = 0; g < G; ++g)
       ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
@@ -520,7 +522,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     p.arow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {gx + g * MC, nullptr, S.w[b][g].projWT, nullptr, sc.t2 + g * MC, nullptr, nullptr};
-    CK(gemm_nt(p, st));
+    CK(gemm_nt(p, st, -1, sc.ws));
     AttnArgs at;
     memset(&at, 0, sizeof(at));
     at.nwin = nwin;
@@ -540,7 +542,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
-    CK(gemm_nt(q, st));
+    CK(gemm_nt(q, st, -1, sc.ws));
     LnArgs ln1 = ln_base(M, C, G, 1e-5f);
     ln1.map = idx;
     for (int g = 0; g < G; ++g)
@@ -610,6 +612,7 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
     m->sc.t2 = P.f(mx);
     m->sc.h = P.f(mx * 4);
     m->sc.dqkv = P.f(mx * 3);
+    m->sc.ws = P.f(vv::gemm_ws_floats());
     m->xm = P.f(G * M1 * 4 * c.C0);
     m->cat = P.f(M1 * G * c.C1);
     m->dp = P.f(M1 * G * c.C1);
@@ -710,7 +713,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.xm + (size_t)g * M1 * 4 * C0, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight"), nullptr,
                 sv.enc1.x[0] + g * M1C1, nullptr, nullptr};
-  CK(gemm_nt(red, st));
+  CK(gemm_nt(red, st, -1, m.sc.ws));
   if ((r = stage_fwd(m.enc1, sv.enc1, m.sc, c.ws, st))) return r;
   float* skip1 = sv.enc1.x.back();
   // encoder norm -> concat (transformer.py:402, 567)
@@ -726,7 +729,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   ep.rmod = c.H1 * c.W1;
   ep.ldr = E;
   ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
-  CK(gemm_nt(ep, st));
+  CK(gemm_nt(ep, st, -1, m.sc.ws));
   // ---- LG_net layers
   for (size_t l = 0; l < m.lg.size(); ++l)
     if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st))) return r;
@@ -734,7 +737,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   // ---- Dec_net.proj (transformer.py:600)
   GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE);
   dp.g[0] = {lg_out, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m.dp, nullptr, nullptr};
-  CK(gemm_nt(dp, st));
+  CK(gemm_nt(dp, st, -1, m.sc.ws));
   // concat_back_dim[0]: cat(x, skip1) (transformer.py:468-469)
   GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE);
   c0.lda = G * C1;
@@ -743,14 +746,14 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   for (int g = 0; g < G; ++g)
     c0.g[g] = {m.dp + g * C1, skip1 + g * M1C1, w(dg(g) + ".concat_back_dim.0.weight"),
                w(dg(g) + ".concat_back_dim.0.bias"), sv.dec1.x[0] + g * M1C1, nullptr, nullptr};
-  CK(gemm_nt(c0, st));
+  CK(gemm_nt(c0, st, -1, m.sc.ws));
   if ((r = stage_fwd(m.dec1, sv.dec1, m.sc, c.ws, st))) return r;
   // PatchExpand: expand (no bias) + rearrange + LN(C0, eps 1e-6) (transformer.py:106-118)
   GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {sv.dec1.x.back() + g * M1C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight"), nullptr,
                sv.ex + (size_t)g * M1 * 2 * C1, nullptr, nullptr};
-  CK(gemm_nt(ex, st));
+  CK(gemm_nt(ex, st, -1, m.sc.ws));
   LnArgs lx = ln_base(M0, C0, G, 1e-6f);
   lx.mode = LN_EXPAND;
   lx.Hin = c.H1;
@@ -769,7 +772,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   for (int g = 0; g < G; ++g)
     c1.g[g] = {m.xe + g * M0C0, skip0 + g * M0C0, w(dg(g) + ".concat_back_dim.1.weight"),
                w(dg(g) + ".concat_back_dim.1.bias"), sv.dec0.x[0] + g * M0C0, nullptr, nullptr};
-  CK(gemm_nt(c1, st));
+  CK(gemm_nt(c1, st, -1, m.sc.ws));
   if ((r = stage_fwd(m.dec0, sv.dec0, m.sc, c.ws, st))) return r;
   // norm_up (transformer.py:472)
   LnArgs lu = ln_base(M0, C0, G, 1e-6f);
@@ -851,7 +854,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd0 + g * M0C0, nullptr, w(dg(g) + ".concat_back_dim.1.weight^T") + (size_t)half * C0 * C0,
                  nullptr, (half ? m.gsk0 : m.gxe) + g * M0C0, nullptr, nullptr};
-    CK(gemm_nt(cb, st));
+    CK(gemm_nt(cb, st, -1, m.sc.ws));
   }
   // PatchExpand backward: LN (expand mode) then expand^T
   LnArgs lx = ln_base(M0, C0, G, 1e-6f);
@@ -867,7 +870,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   for (int g = 0; g < G; ++g)
     ex.g[g] = {m.gex + (size_t)g * M1 * 2 * C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight^T"), nullptr,
                m.gd1 + g * M1C1, nullptr, nullptr};
-  CK(gemm_nt(ex, st));
+  CK(gemm_nt(ex, st, -1, m.sc.ws));
   if ((r = stage_bwd(m.dec1, sv.dec1, m.sc, c.ws, m.gd1, st))) return r;
   // concat_back_dim[0] backward: left -> Dec_net.proj output slice g, right -> skip1
   for (int half = 0; half < 2; ++half) {
@@ -876,19 +879,19 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd1 + g * M1C1, nullptr, w(dg(g) + ".concat_back_dim.0.weight^T") + (size_t)half * C1 * C1,
                  nullptr, half ? m.gsk1 + g * M1C1 : m.gdp + g * C1, nullptr, nullptr};
-    CK(gemm_nt(cb, st));
+    CK(gemm_nt(cb, st, -1, m.sc.ws));
   }
   // Dec_net.proj backward
   float* glg = m.glg;
   GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE);
   dp.g[0] = {m.gdp, nullptr, w("dec.proj.weight^T"), nullptr, glg, nullptr, nullptr};
-  CK(gemm_nt(dp, st));
+  CK(gemm_nt(dp, st, -1, m.sc.ws));
   for (int l = (int)m.lg.size() - 1; l >= 0; --l)
     if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st))) return r;
   // pos_embed: identity ; Enc_net.proj backward
   GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE);
   ep.g[0] = {glg, nullptr, w("enc.proj.weight^T"), nullptr, m.gcat, nullptr, nullptr};
-  CK(gemm_nt(ep, st));
+  CK(gemm_nt(ep, st, -1, m.sc.ws));
   // encoder norm backward (+ skip1 gradient), in place on gsk1
   float* skip1 = sv.enc1.x.back();
   LnArgs le = ln_base(M1, C1, G, 1e-6f);
@@ -903,7 +906,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.gsk1 + g * M1C1, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight^T"), nullptr,
                 m.gxm + (size_t)g * M1 * 4 * C0, nullptr, nullptr};
-  CK(gemm_nt(red, st));
+  CK(gemm_nt(red, st, -1, m.sc.ws));
   float* skip0 = sv.enc0.x.back();
   LnArgs lm = ln_base(M1, 4 * C0, G, 1e-6f);
   lm.mode = LN_MERGE;
@@ -1091,6 +1094,7 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipMalloc(&c->redf, kRedBlocks * sizeof(float)));
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
+  VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
   *out = c;
   return 0;
 }
@@ -1105,6 +1109,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   (void)hipFree(ctx->redf);
   (void)hipFree(ctx->dout);
   (void)hipFree(ctx->doutf);
+  (void)hipFree(ctx->gemm_ws);
   delete ctx;
   return 0;
 }
@@ -1365,7 +1370,7 @@ int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, co
   if (!ctx || !A || !B || !C) return fail(VV_E_ARG, "null argument");
   GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE);
   a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
-  VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile));
+  VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
   return 0;
 }
 

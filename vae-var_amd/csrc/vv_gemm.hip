@@ -12,6 +12,8 @@
 // one barrier per k-tile.
 #include "vv_kernels.h"
 
+#include <algorithm>
+
 namespace vv {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -98,7 +100,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nt) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int EPI, bool XCD, int MF>
+template <int BM, int BN, int BK, int WM, int WN, int EPI, bool XCD, int MF, int DEPTH>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
   constexpr int NT = 64 * WM * WN;
   constexpr int LS = BK + 4;        // LDS row stride (floats): rows land on distinct 16-B slots
@@ -122,7 +124,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
   const int M = args.M, N = args.N, K = args.K, ksplit = args.ksplit;
   const int ntn = (N + BN - 1) / BN;
   const int ntiles = ntn * ((M + BM - 1) / BM);
-  const int tile = XCD ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
+  const int nkt = K / BK;
+  int tile, kb = 0, ke = nkt, part = -1;
+  if ((int)blockIdx.x < args.tdp || args.tsplit <= 1) {
+    tile = XCD ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
+  } else {
+    part = blockIdx.x - args.tdp;  // tail item: tile tdp + part / S, k-chunk part % S
+    const int S = args.tsplit, c = part % S;
+    tile = args.tdp + part / S;
+    kb = (c * nkt) / S;
+    ke = ((c + 1) * nkt) / S;
+  }
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
   const int lr = tid / TPR, lc = (tid % TPR) * 4;
 
@@ -142,8 +154,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
     bp[i] = G.B + (size_t)n * K + lc;
   }
 
-  f4 ra[AI], rb[BI];
-  auto gload = [&](int k0) {
+  // register staging sets (named, statically indexed): DEPTH 1 = tile t+1 in flight during tile t,
+  // DEPTH 2 = tiles t+1 (landed, written to LDS after the compute) and t+2 (in flight)
+  f4 ra0[AI], rb0[BI], ra1[AI], rb1[BI];
+  auto gload = [&](int k0, f4 (&ra)[AI], f4 (&rb)[BI]) {
     if (k0 < ksplit) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) ra[i] = *reinterpret_cast<const f4*>(a1p[i] + k0);
@@ -154,7 +168,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
 #pragma unroll
     for (int i = 0; i < BI; ++i) rb[i] = *reinterpret_cast<const f4*>(bp[i] + k0);
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const f4 (&ra)[AI], const f4 (&rb)[BI]) {
     float* As = smem + buf * (BM + BN) * LS;
     float* Bs = As + BM * LS;
 #pragma unroll
@@ -198,45 +212,123 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
     }
   };
 
-  const int nk = K / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-    compute(cur);
-    if (kt + 1 < nk) sstore(cur ^ 1);
+  const int nk = ke - kb;
+  if constexpr (DEPTH == 1) {
+    gload(kb * BK, ra0, rb0);
+    sstore(0, ra0, rb0);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) gload((kb + kt + 1) * BK, ra0, rb0);
+      compute(cur);
+      if (kt + 1 < nk) sstore(cur ^ 1, ra0, rb0);
+      __syncthreads();
+    }
+  } else {
+    static_assert(DEPTH == 1 || DEPTH == 2, "depth");
+    // prologue: tile 0 -> LDS buffer 0, tile 1 -> registers set 1
+    gload(kb * BK, ra0, rb0);
+    if (nk > 1) gload((kb + 1) * BK, ra1, rb1);
+    sstore(0, ra0, rb0);
+    __syncthreads();
+    // steady state, unrolled by two so each register set is named statically
+    for (int kt = 0; kt < nk; kt += 2) {
+      // even step: compute buf 0 (tile kt); set 1 holds tile kt+1; load tile kt+2 into set 0
+      if (kt + 2 < nk) gload((kb + kt + 2) * BK, ra0, rb0);
+      compute(0);
+      if (kt + 1 < nk) sstore(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      // odd step: compute buf 1 (tile kt+1); set 0 holds tile kt+2; load tile kt+3 into set 1
+      if (kt + 3 < nk) gload((kb + kt + 3) * BK, ra1, rb1);
+      compute(1);
+      if (kt + 2 < nk) sstore(0, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // epilogue: 32x32: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31;
   //           16x16: row 4h + r, col lane&15 (h = lane>>4)
   // Everything an element needs (bias, output row, residual, pre-activation) is loaded for the whole
   // fragment first, so the stores are not serialised behind one dependent load each.
+  if (part >= 0) {
+    // tail chunk: raw fp32 partial, register-major [TM*TN*NR][NT] so the fixup reads it coalesced
+    float* w = args.ws + ((size_t)blockIdx.z * (gridDim.x - args.tdp) + part) * (size_t)(TM * TN * NR * NT);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) w[(size_t)((a * TN + b) * NR + r) * NT + tid] = acc[a][b][r];
+    return;
+  }
   if (m0 + BM <= M && n0 + BN <= N)
     epilogue<BM, BN, WM, WN, EPI, MF, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
   else
     epilogue<BM, BN, WM, WN, EPI, MF, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool XCD = false, int MF = 32>
+// Tail fixup: sums the tsplit k-chunk partials of each tail tile in chunk order (deterministic) and applies
+// the same epilogue as the main kernel. grid = (tail tiles, 1, groups), same block shape as the main kernel.
+template <int BM, int BN, int WM, int WN, int EPI, int MF>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup(GemmArgs args) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TM = BM / WM / MF;
+  constexpr int TN = BN / WN / MF;
+  constexpr int NR = MF == 32 ? 16 : 4;
+  constexpr int NREG = TM * TN * NR;
+  typedef float accv __attribute__((ext_vector_type(MF == 32 ? 16 : 4)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N;
+  const int ntn = (N + BN - 1) / BN;
+  const int S = args.tsplit;
+  const int tile = args.tdp + blockIdx.x;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const size_t items = (size_t)gridDim.x * S;
+  const float* w = args.ws + ((size_t)blockIdx.z * items + (size_t)blockIdx.x * S) * (size_t)(NREG * NT);
+  accv acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const size_t j = (size_t)((a * TN + b) * NR + r) * NT + tid;
+        float v = w[j];
+        for (int c = 1; c < S; ++c) v += w[(size_t)c * NREG * NT + j];
+        acc[a][b][r] = v;
+      }
+  const int wm = wave / WN, wn = wave % WN;
+  const int rin = lane & (MF - 1), hh = lane / MF;
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, WM, WN, EPI, MF, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  else
+    epilogue<BM, BN, WM, WN, EPI, MF, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool XCD = false, int MF = 32, int DEPTH = 1>
 static hipError_t launch_tile(const GemmArgs& a, hipStream_t s) {
   constexpr int LS = BK + 4;
   if (a.K % BK || a.ksplit % BK) return hipErrorInvalidValue;
   const size_t lds = 2 * (BM + BN) * LS * sizeof(float);
-  dim3 grid(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, a.ngroups);
+  const int T = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
+  const int tail = a.tsplit > 1 ? T - a.tdp : 0;
+  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
   switch (a.epi) {
 #define VV_EPI(E)                                                                                   \
   case E: {                                                                                         \
     static bool init = false;                                                                       \
     if (!init) {                                                                                    \
-      hipError_t e = hipFuncSetAttribute((const void*)k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF>,             \
+      hipError_t e = hipFuncSetAttribute((const void*)k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF, DEPTH>,             \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
       if (e != hipSuccess) return e;                                                                \
       init = true;                                                                                  \
     }                                                                                               \
-    hipLaunchKernelGGL((k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF>), grid, dim3(64 * WM * WN), lds, s, a);   \
+    hipLaunchKernelGGL((k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF, DEPTH>), grid, dim3(64 * WM * WN), lds, s, a);   \
+    if (tail)                                                                                       \
+      hipLaunchKernelGGL((k_gemm_fixup<BM, BN, WM, WN, E, MF>), dim3(tail, 1, a.ngroups), dim3(64 * WM * WN), 0, \
+                         s, a);                                                                     \
     return hipGetLastError();                                                                       \
   }
     VV_EPI(EPI_STORE)
@@ -268,6 +360,11 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 13: return launch_tile<128, 128, 32, 2, 2, false, 16>(a, s);
     case 14: return launch_tile<64, 64, 16, 2, 2, false, 16>(a, s);
     case 15: return launch_tile<32, 64, 32, 1, 2, false, 16>(a, s);
+    case 16: return launch_tile<64, 64, 32, 2, 2, false, 32, 2>(a, s);    // 2-deep register prefetch
+    case 17: return launch_tile<64, 128, 32, 2, 2, false, 32, 2>(a, s);
+    case 18: return launch_tile<32, 64, 32, 1, 2, false, 32, 2>(a, s);
+    case 19: return launch_tile<64, 64, 64, 2, 2, false, 32, 2>(a, s);
+    case 20: return launch_tile<64, 64, 16, 2, 2, false, 32, 2>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -283,11 +380,56 @@ static int pick_tile(const GemmArgs& a) {
   return 4;
 }
 
-hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint) {
+static int g_num_cu = 0;
+constexpr size_t kWsFloats = (size_t)1 << 21;  // 8 MB: tail partials of up to 512 chunks of a 64x64 tile
+
+size_t gemm_ws_floats() { return kWsFloats; }
+
+// tile edge of each variant (for the tail split)
+static void variant_tile(int t, int& bm, int& bn, int& bk) {
+  static const int tab[][3] = {{128, 128, 32}, {128, 64, 32}, {64, 64, 32}, {64, 64, 16}, {32, 64, 32}, {64, 32, 32},
+                               {64, 128, 32}, {32, 64, 16}, {64, 64, 64}, {64, 64, 32}, {64, 64, 32}, {128, 64, 32},
+                               {64, 128, 32}, {128, 128, 32}, {64, 64, 16}, {32, 64, 32}, {64, 64, 32}, {64, 128, 32},
+                               {32, 64, 32}, {64, 64, 64}, {64, 64, 16}};
+  bm = tab[t][0];
+  bn = tab[t][1];
+  bk = tab[t][2];
+}
+
+hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
+  GemmArgs a = a_in;
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
+  if (t < 0 || t > 20) return hipErrorInvalidValue;
+  // data-parallel rounds of whole tiles + the remaining tiles split along K over the idle CUs
+  if (!g_num_cu) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) g_num_cu = p.multiProcessorCount;
+    if (g_num_cu <= 0) g_num_cu = 256;
+  }
+  a.tdp = 0;
+  a.tsplit = 1;
+  a.ws = ws;
+  if (ws && a.ngroups == 1) {
+    int bm, bn, bk;
+    variant_tile(t, bm, bn, bk);
+    const int T = ((a.N + bn - 1) / bn) * ((a.M + bm - 1) / bm);
+    const int P = g_num_cu, nkt = a.K / bk;
+    const int tdp = (T / P) * P, tail = T - tdp;
+    if (tdp > 0 && tail > 0 && tail <= P / 2) {
+      // chunks of >= 12 k-tiles: below that the fixup launch and partial traffic cost more than the tail
+      int S = std::min(P / tail, nkt / 12);
+      const size_t tile_f = (size_t)bm * bn;
+      while (S > 1 && (size_t)tail * S * tile_f > kWsFloats) --S;
+      if (S > 1) {
+        a.tdp = tdp;
+        a.tsplit = S;
+      }
+    }
+  }
   const int ph = prof_begin(s);
   const hipError_t e = launch_variant(t, a, s);
   // algorithmic: 2MNK flops; bytes = A + B + C (+R/aux) once each

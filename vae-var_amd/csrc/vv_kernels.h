@@ -39,10 +39,16 @@ struct GemmArgs {
   const int* crow;
   int epi;
   int ngroups;
+  // tail split (filled in by gemm_nt): the first tdp tiles run whole; each remaining tile is split into
+  // tsplit k-chunks whose fp32 partials go to ws and are summed (in chunk order) by the fixup kernel
+  int tdp, tsplit;
+  float* ws;
   GemmGroup g[kMaxGroups];
 };
 
-hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1);
+// ws: scratch of at least gemm_ws_floats() floats (may be null: no tail split)
+hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);
+size_t gemm_ws_floats();
 
 // ---------------------------------------------------------------------------
 // LayerNorm over the last dim, one wave per output row.

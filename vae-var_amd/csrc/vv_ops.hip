@@ -307,34 +307,48 @@ __device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* 
   return b;
 }
 
+// LDS row stride for a [16][hd] tile: hd + 4 keeps rows 16-B aligned and puts the 16 rows of a
+// ds_read_b128 lane group on distinct 16-B slots (hd % 64 in {0, 32}: (hd+4)/4 is odd).
+__device__ __forceinline__ int attn_ld(int hd) { return hd + 4; }
+
+__device__ __forceinline__ void attn_load(const float* __restrict__ src, int ldsrc, float* dst, int st, int hd,
+                                          int lane) {
+  const int q4 = hd >> 2;
+  for (int idx = lane; idx < WN_ * q4; idx += 64) {
+    const int t = idx / q4, d = (idx - t * q4) * 4;
+    *reinterpret_cast<f4*>(dst + t * st + d) = *reinterpret_cast<const f4*>(src + (size_t)t * ldsrc + d);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_attn_fwd(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int win = blockIdx.x, h = blockIdx.y;
   const AttnGroup G = a.g[blockIdx.z];
   const int lane = threadIdx.x;
   const int C = a.C, hd = C / a.heads, ldq = 3 * C;
-  const int st = hd + 1;
+  const int st = attn_ld(hd);
   float* q = sm;
   float* k = q + WN_ * st;
   float* v = k + WN_ * st;
   float* p = v + WN_ * st;  // [16][17]
   const float* base = G.qkv + (size_t)win * WN_ * ldq + h * hd;
-  for (int idx = lane; idx < WN_ * hd; idx += 64) {
-    const int t = idx / hd, d = idx - t * hd;
-    const float* row = base + (size_t)t * ldq + d;
-    q[t * st + d] = row[0];
-    k[t * st + d] = row[C];
-    v[t * st + d] = row[2 * C];
-  }
+  attn_load(base, ldq, q, st, hd, lane);
+  attn_load(base + C, ldq, k, st, hd, lane);
+  attn_load(base + 2 * C, ldq, v, st, hd, lane);
   __syncthreads();
+  // S = (q * scale) k^T : lane -> row i, columns j0..j0+3 (swinblock.py:151-152)
   const int i = lane >> 2, j0 = (lane & 3) * 4;
   float sv[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int d = 0; d < hd; ++d) {
-    const float qd = q[i * st + d] * a.scale;
+  for (int d = 0; d < hd; d += 4) {
+    f4 qd = *reinterpret_cast<const f4*>(q + i * st + d);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) sv[jj] += qd * k[(j0 + jj) * st + d];
+    for (int e = 0; e < 4; ++e) qd[e] *= a.scale;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const f4 kd = *reinterpret_cast<const f4*>(k + (j0 + jj) * st + d);
+      sv[jj] += qd[0] * kd[0] + qd[1] * kd[1] + qd[2] * kd[2] + qd[3] * kd[3];
+    }
   }
-  // NOTE: the reference scales q before the product (q = q * scale; q @ k^T, swinblock.py:151-152)
   float mx = -INFINITY;
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
@@ -352,21 +366,29 @@ __global__ __launch_bounds__(64) void k_attn_fwd(AttnArgs a) {
   sum += __shfl_xor(sum, 1);
   sum += __shfl_xor(sum, 2);
   const float inv = 1.0f / sum;
-  float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
+  f4 pv;
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
-    const float pv = sv[jj] * inv;
-    p[i * 17 + j0 + jj] = pv;
-    Pg[i * WN_ + j0 + jj] = pv;
+    pv[jj] = sv[jj] * inv;
+    p[i * 17 + j0 + jj] = pv[jj];
   }
+  float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
+  *reinterpret_cast<f4*>(Pg + i * WN_ + j0) = pv;
   __syncthreads();
+  // O = P v : lane -> (t, 4 consecutive d)
   float* ob = G.o + (size_t)win * WN_ * C + h * hd;
-  for (int idx = lane; idx < WN_ * hd; idx += 64) {
-    const int t = idx / hd, d = idx - t * hd;
-    float acc = 0.f;
+  const int q4 = hd >> 2;
+  for (int idx = lane; idx < WN_ * q4; idx += 64) {
+    const int t = idx / q4, d = (idx - t * q4) * 4;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int jj = 0; jj < WN_; ++jj) acc += p[t * 17 + jj] * v[jj * st + d];
-    ob[(size_t)t * C + d] = acc;
+    for (int jj = 0; jj < WN_; ++jj) {
+      const float pj = p[t * 17 + jj];
+      const f4 vv = *reinterpret_cast<const f4*>(v + jj * st + d);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += pj * vv[e];
+    }
+    *reinterpret_cast<f4*>(ob + (size_t)t * C + d) = acc;
   }
 }
 
@@ -376,7 +398,7 @@ __global__ __launch_bounds__(64) void k_attn_bwd(AttnArgs a) {
   const AttnGroup G = a.g[blockIdx.z];
   const int lane = threadIdx.x;
   const int C = a.C, hd = C / a.heads, ldq = 3 * C;
-  const int st = hd + 1;
+  const int st = attn_ld(hd);
   float* q = sm;
   float* k = q + WN_ * st;
   float* v = k + WN_ * st;
@@ -384,24 +406,23 @@ __global__ __launch_bounds__(64) void k_attn_bwd(AttnArgs a) {
   float* p = dO + WN_ * st;  // [16][17]
   float* ds = p + WN_ * 17;  // [16][17]
   const float* base = G.qkv + (size_t)win * WN_ * ldq + h * hd;
-  const float* dob = G.dO + (size_t)win * WN_ * C + h * hd;
-  for (int idx = lane; idx < WN_ * hd; idx += 64) {
-    const int t = idx / hd, d = idx - t * hd;
-    const float* row = base + (size_t)t * ldq + d;
-    q[t * st + d] = row[0];
-    k[t * st + d] = row[C];
-    v[t * st + d] = row[2 * C];
-    dO[t * st + d] = dob[(size_t)t * C + d];
-  }
+  attn_load(base, ldq, q, st, hd, lane);
+  attn_load(base + C, ldq, k, st, hd, lane);
+  attn_load(base + 2 * C, ldq, v, st, hd, lane);
+  attn_load(G.dO + (size_t)win * WN_ * C + h * hd, C, dO, st, hd, lane);
   const float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
   for (int idx = lane; idx < WN_ * WN_; idx += 64) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
   __syncthreads();
+  // dP = dO v^T ; dS = P * (dP - rowsum(P * dP))
   const int i = lane >> 2, j0 = (lane & 3) * 4;
   float dp[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int d = 0; d < hd; ++d) {
-    const float od = dO[i * st + d];
+  for (int d = 0; d < hd; d += 4) {
+    const f4 od = *reinterpret_cast<const f4*>(dO + i * st + d);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) dp[jj] += od * v[(j0 + jj) * st + d];
+    for (int jj = 0; jj < 4; ++jj) {
+      const f4 vd = *reinterpret_cast<const f4*>(v + (j0 + jj) * st + d);
+      dp[jj] += od[0] * vd[0] + od[1] * vd[1] + od[2] * vd[2] + od[3] * vd[3];
+    }
   }
   float rd = 0.f;
 #pragma unroll
@@ -411,27 +432,42 @@ __global__ __launch_bounds__(64) void k_attn_bwd(AttnArgs a) {
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) ds[i * 17 + j0 + jj] = p[i * 17 + j0 + jj] * (dp[jj] - rd);
   __syncthreads();
+  // dQ[t] = scale sum_j dS[t][j] k[j] ; dK[t] = scale sum_i dS[i][t] q[i] ; dV[t] = sum_i P[i][t] dO[i]
   float* gb = G.dqkv + (size_t)win * WN_ * ldq + h * hd;
-  for (int idx = lane; idx < WN_ * hd; idx += 64) {
-    const int t = idx / hd, d = idx - t * hd;
-    float aq = 0.f, ak = 0.f, av = 0.f;
+  const int q4 = hd >> 2;
+  for (int idx = lane; idx < WN_ * q4; idx += 64) {
+    const int t = idx / q4, d = (idx - t * q4) * 4;
+    f4 aq = {0.f, 0.f, 0.f, 0.f}, ak = aq, av = aq;
 #pragma unroll
     for (int u = 0; u < WN_; ++u) {
-      aq += ds[t * 17 + u] * k[u * st + d];   // dQ[t] = sum_j dS[t][j] k[j]
-      ak += ds[u * 17 + t] * q[u * st + d];   // dK[t] = sum_i dS[i][t] q[i]
-      av += p[u * 17 + t] * dO[u * st + d];   // dV[t] = sum_i P[i][t] dO[i]
+      const float s_tu = ds[t * 17 + u], s_ut = ds[u * 17 + t], p_ut = p[u * 17 + t];
+      const f4 kk = *reinterpret_cast<const f4*>(k + u * st + d);
+      const f4 qq = *reinterpret_cast<const f4*>(q + u * st + d);
+      const f4 oo = *reinterpret_cast<const f4*>(dO + u * st + d);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        aq[e] += s_tu * kk[e];
+        ak[e] += s_ut * qq[e];
+        av[e] += p_ut * oo[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      aq[e] *= a.scale;
+      ak[e] *= a.scale;
     }
     float* row = gb + (size_t)t * ldq + d;
-    row[0] = aq * a.scale;
-    row[C] = ak * a.scale;
-    row[2 * C] = av;
+    *reinterpret_cast<f4*>(row) = aq;
+    *reinterpret_cast<f4*>(row + C) = ak;
+    *reinterpret_cast<f4*>(row + 2 * C) = av;
   }
 }
 
 hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
   if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   const int hd = a.C / a.heads;
-  const size_t lds = (3 * WN_ * (hd + 1) + WN_ * 17) * sizeof(float);
+  if (hd & 3) return hipErrorInvalidValue;
+  const size_t lds = (3 * WN_ * (hd + 4) + WN_ * 17) * sizeof(float);
   const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
   prof_end(ph, s, PC_ATTN, 4.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
@@ -441,7 +477,8 @@ hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
 hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
   if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   const int hd = a.C / a.heads;
-  const size_t lds = (4 * WN_ * (hd + 1) + 2 * WN_ * 17) * sizeof(float);
+  if (hd & 3) return hipErrorInvalidValue;
+  const size_t lds = (4 * WN_ * (hd + 4) + 2 * WN_ * 17) * sizeof(float);
   const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
   prof_end(ph, s, PC_ATTN, 8.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
