@@ -36,6 +36,8 @@ CONFIGS = {
     2: dict(T=1, name="config 2: 3D-Var, full VAE decoder (parameters0_old), 69ch 128x256, 100 L-BFGS iters"),
     3: dict(T=2, name="config 3: 4D-Var, 2-step window with LGUnet flow stand-in, 69ch 128x256, 100 iters"),
     4: dict(T=6, name="config 4: 4D-Var, 6-step window, one analysis per GPU (ensemble)"),
+    5: dict(T=2, grid=(721, 1440), name="config 5: 4D-Var at 0.25 deg (69ch 721x1440 state, nearest-interpolated "
+                                          "to the 128x256 networks), T=2, 50 iters"),
 }
 
 
@@ -70,6 +72,17 @@ def cpu_baseline(prob_np, evals_per_iter, n_evals, threads):
                                 f"iters/s = 1/(s_per_eval x {evals_per_iter:.3f} evals per iteration of the GPU run)"}
 
 
+def gemm_traffic():
+    """HBM bytes per k_gemm_nt launch from the committed rocprofv3 --pmc passes (FETCH_SIZE x2 + WRITE_SIZE,
+    gfx950 corrections, tools/pmc_traffic.py) of `bench.py --config 2`; PMC counters cannot be read live."""
+    path = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,7 +108,8 @@ def main():
     T = CONFIGS[args.config]["T"]
     dec = LGUnet(C.DECODER, 1, 1, device=local).load_synthetic()
     flow = LGUnet(C.FLOW, 1, T - 1, device=local).load_synthetic() if T > 1 else None
-    prob_np = make_problem(nch=69, Hs=128, Ws=256, T=T, seed=20250620 + rank)
+    Hs, Ws = CONFIGS[args.config].get("grid", (128, 256))
+    prob_np = make_problem(nch=69, Hs=Hs, Ws=Ws, T=T, seed=20250620 + rank)
     prob = DAProblem(dec, prob_np, flow=flow, device=local)
 
     # warm-up: W outer steps of a throw-away analysis (same path, same shapes)
@@ -159,7 +173,7 @@ def main():
         g = pr["gemm"]
         ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
         out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                           "frac": ach / PEAK_F32_TFLOPS, "traffic": None,
+                           "frac": ach / PEAK_F32_TFLOPS, "traffic": gemm_traffic(),
                            "kernel": "k_gemm_nt (every fp32 MFMA GEMM launch of a HIP-event-profiled repeat "
                                      "of the timed analysis)",
                            "launches": g["launches"], "avg_launch_us": 1e3 * g["ms"] / max(g["launches"], 1),

@@ -16,6 +16,7 @@
  *
  * Conventions: every function returns 0 on success, a non-zero status otherwise (HIP error code or
  * VV_E_*), never throws; vv_last_error() describes the last failure of the calling thread.
+ *   vv_nearest_map                F.interpolate(mode='nearest') index maps (nf_model/vae.py:90, da_4dvar.py:671,679)
  * All float pointers passed to compute entry points are DEVICE pointers (fp32, 16-byte aligned)
  * owned by the caller; `stream` is a hipStream_t (NULL = default stream). A context is bound to
  * one device and is not thread-safe. All work is enqueued on the given stream; only functions
@@ -78,6 +79,8 @@ int vv_model_backward(vv_ctx* ctx, int model_id, int slot, const float* dout, fl
 int vv_model_workspace_bytes(vv_ctx* ctx, int model_id, int64_t* bytes);
 
 /* one_step_DA 'vae4dvar' problem: state (C,Hs,Ws), window of T times; flow_model_id < 0 when T == 1.
+   When (Hs,Ws) differs from the network grid (e.g. 721x1440 vs 128x256) the decoder output and each forecast are
+   nearest-up-sampled to the state grid and the forecast input nearest-down-sampled, as decoder_hr / integrate do.
    xb (C,Hs,Ws); yo, Hmask, R (T,C,Hs,Ws); mean, std, std_tr (C). Buffers stay owned by the caller. */
 int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int C, int Hs, int Ws,
                     const float* xb, const float* yo, const float* Hmask, const float* R, const float* mean,
@@ -108,6 +111,10 @@ int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n
    ms = summed launch durations, flops/bytes = algorithmic work, launches = count. stop synchronises. */
 int vv_profile_start(vv_ctx* ctx);
 int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* launches, int ncls);
+
+/* F.interpolate(mode='nearest') source index map for in_size -> out_size (quirk Q3), as used by
+   decoder_hr (nf_model/vae.py:90) and integrate (da_4dvar.py:671, 679); map has out_size entries (host) */
+int vv_nearest_map(int in_size, int out_size, int* map);
 
 /* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), epi as vv::Epi */
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,

@@ -202,3 +202,61 @@ def test_oracle_on_box_tiny_adam():
     e = np.linalg.norm(xa - xa_ref) / np.linalg.norm(xa_ref)
     print(f"config 1 (Adam x20): xa rel-L2 {e:.2e}")
     assert e < 1e-4
+
+
+def test_interpolated_grid_4dvar():
+    """State grid 45x90 != network grid 32x64 (non-integer ratio, like 721x1440 vs 128x256): decoder_hr
+    up-sampling, integrate down/up-sampling and their adjoints, T=2, against the oracle restatement."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.engine import DAProblem, LGUnet
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    p = make_problem(nch=4, Hs=45, Ws=90, T=2, seed=778, obs_frac=0.2)
+    dec = LGUnet(C.TINY, 1, 1).load_synthetic()
+    flow = LGUnet(C.TINY_FLOW, 1, 1).load_synthetic()
+    prob = DAProblem(dec, p, flow=flow)
+    z = torch.from_numpy(0.3 * smooth_field(304, (1, 4, 32, 64), sigma=2.0))
+    g = torch.empty(1, 4, 32, 64, device="cuda")
+    jb, jo = prob.closure(z.cuda(), g)
+    ro = oracle_problem(p, synth_params(C.TINY), C.TINY, synth_params(C.TINY_FLOW), C.TINY_FLOW)
+    zr = z.clone().requires_grad_(True)
+    rb, rob = ro.loss_terms(zr)
+    (rb + rob).backward()
+    e_j = abs(jo - float(rob)) / abs(float(rob))
+    e_g = rel(g.cpu(), zr.grad)
+    xa = prob.analysis(z.cuda()).cpu().numpy()
+    with torch.no_grad():
+        e_x = rel(xa, ro.analysis(z).numpy())
+    print(f"interpolated grid T=2: J_o rel {e_j:.2e} grad rel {e_g:.2e} xa rel {e_x:.2e}")
+    assert e_j < 1e-5 and e_g < 1e-5 and e_x < 1e-6
+
+
+def test_config5_grid_closure():
+    """BASELINE config 5 grid: full decoder, 69ch 721x1440 state, T=1, one closure vs the oracle (CPU)."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    p = make_problem(nch=69, Hs=721, Ws=1440, T=1, seed=20250621)
+    from vaevar.engine import LGUnet
+
+    dec = LGUnet(C.DECODER, 1, 1).load_synthetic()
+    prob = DAProblem(dec, p)
+    z = torch.from_numpy(0.3 * smooth_field(405, (1, 32, 128, 256)))
+    g = torch.empty(1, 32, 128, 256, device="cuda")
+    jb, jo = prob.closure(z.cuda(), g)
+    torch.set_num_threads(16)
+    ro = oracle_problem(p, synth_params(C.DECODER), C.DECODER)
+    zr = z.clone().requires_grad_(True)
+    rb, rob = ro.loss_terms(zr)
+    (rb + rob).backward()
+    e_j = abs(jo - float(rob)) / abs(float(rob))
+    e_g = rel(g.cpu(), zr.grad)
+    print(f"config-5 grid closure: J_o rel {e_j:.2e} grad rel {e_g:.2e}")
+    assert e_j < 1e-4 and e_g < 1e-4

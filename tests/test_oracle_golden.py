@@ -65,6 +65,16 @@ def test_g4_nearest_maps():
         assert np.array_equal(m, g[key]), key
 
 
+def test_g4_engine_nearest_maps():
+    """The engine's own index maps (vv_nearest_map, used by the misfit kernels) equal the reference's."""
+    from vaevar import _lib
+
+    g = gold("g4_nearest_maps.npz")
+    for key, (a, b) in (("lat_721_to_128", (721, 128)), ("lat_128_to_721", (128, 721)),
+                        ("lon_1440_to_256", (1440, 256)), ("lon_256_to_1440", (256, 1440))):
+        assert np.array_equal(np.array(_lib.nearest_map(a, b)), g[key]), key
+
+
 def _tiny_problem(T):
     from vaevar.problem import make_problem
 

@@ -1,0 +1,33 @@
+"""Per-launch HBM traffic of the GEMM kernels from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are in KB; FETCH_SIZE reports exactly
+half of the bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is exact for 16-B
+streaming stores. Usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+"""
+import csv, json, statistics, sys
+
+
+def per_kernel(path, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        vals.setdefault(r["Dispatch_Id"], [r["Kernel_Name"], 0.0])[1] += float(r["Counter_Value"])
+    return vals
+
+
+f = per_kernel(sys.argv[1], "FETCH_SIZE")
+w = per_kernel(sys.argv[2], "WRITE_SIZE")
+gf = [v for n, v in f.values() if "k_gemm_nt" in n]
+gw = [v for n, v in w.values() if "k_gemm_nt" in n]
+out = {
+    "kernel": "k_gemm_nt",
+    "launches_fetch": len(gf), "launches_write": len(gw),
+    "fetch_bytes_per_launch_raw": 1024 * statistics.mean(gf),
+    "fetch_bytes_per_launch": 2 * 1024 * statistics.mean(gf),
+    "write_bytes_per_launch": 1024 * statistics.mean(gw),
+}
+out["hbm_bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
+out["note"] = "FETCH_SIZE doubled (gfx950 wide-load undercount), both in KB -> bytes; mean over every GEMM launch"
+json.dump(out, open(sys.argv[3], "w"), indent=1)
+print(json.dumps(out))

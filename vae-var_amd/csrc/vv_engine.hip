@@ -8,6 +8,7 @@
 // ([N][K], forward operand) plus a transposed copy ([K][N], backward operand).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdarg>
@@ -244,7 +245,11 @@ struct Model {
 
 struct Problem {
   bool bound = false;
-  int dec = -1, flow = -1, T = 1, C = 0, Hs = 0, Ws = 0;
+  int dec = -1, flow = -1, T = 1, C = 0, Hs = 0, Ws = 0, Hl = 0, Wl = 0;
+  bool interp = false;                 // state grid != network grid: nearest maps (quirk Q3)
+  int *mi = nullptr, *mj = nullptr;    // state -> net (decoder_hr / integrate up-sampling)
+  int *ri0 = nullptr, *rj0 = nullptr;  // net -> first state row/col mapping onto it (adjoint ranges)
+  int *di = nullptr, *dj = nullptr;    // net -> state (integrate down-sampling)
   const float *xb, *yo, *Hm, *R, *mean, *std_, *std_tr;
   float obs_coeff = 1.f;
   std::unique_ptr<Arena> arena;
@@ -273,6 +278,22 @@ constexpr int kRedBlocks = 1024;
 int set_dev(vv_ctx* ctx) {
   VV_HIP(hipSetDevice(ctx->device));
   return 0;
+}
+
+// torch nearest_idx (aten/src/ATen/native/UpSample.h): identity when equal, >>1 for exact 2x, otherwise
+// min(floor(dst * (float)in/out), in-1) in fp32 (quirk Q3; pinned by tests/golden/g4_nearest_maps.npz)
+std::vector<int> nearest_map(int in, int out) {
+  std::vector<int> m(out);
+  const float scale = (float)in / (float)out;
+  for (int i = 0; i < out; ++i) {
+    if (in == out)
+      m[i] = i;
+    else if (out == 2 * in)
+      m[i] = i >> 1;
+    else
+      m[i] = std::min((int)floorf((float)i * scale), in - 1);
+  }
+  return m;
 }
 
 std::vector<int> window_map(int B, int H, int W, int ws, int shift) {
@@ -942,21 +963,29 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
 // ----------------------------------------------------------------------------
 // closure  (da_4dvar.py:1183-1208 loss(z) + backward)
 // ----------------------------------------------------------------------------
+void set_maps(const Problem& P, MisfitArgs& m) {
+  m.Hl = P.Hl;
+  m.Wl = P.Wl;
+  m.mi = P.interp ? P.mi : nullptr;
+  m.mj = P.interp ? P.mj : nullptr;
+}
+
 int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   Problem& P = ctx->prob;
   if (!P.bound) return fail(VV_E_STATE, "vv_bind_problem first");
   Model& D = *ctx->models[P.dec];
   Model* F = P.flow >= 0 ? ctx->models[P.flow].get() : nullptr;
-  const int C = P.C, HW = P.Hs * P.Ws;
-  const size_t CHW = (size_t)C * HW;
+  const int C = P.C, HW = P.Hs * P.Ws, HWl = P.Hl * P.Wl;
+  const size_t CHW = (size_t)C * HW, CHWl = (size_t)C * HWl;
   int r;
   // forward: x_0 = decoder(z)*stdTr*std + xb
   if ((r = model_fwd(D, 0, z, P.dec_out, C, st))) return r;
   MisfitArgs ma;
   memset(&ma, 0, sizeof(ma));
   ma.C = C;
-  ma.Hs = ma.Hl = P.Hs;
-  ma.Ws = ma.Wl = P.Ws;
+  ma.Hs = P.Hs;
+  ma.Ws = P.Ws;
+  set_maps(P, ma);
   ma.net = P.dec_out;
   ma.scale = P.std_tr;
   ma.scale2 = P.std_;
@@ -971,11 +1000,12 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   ma.partial = P.partial;
   ma.nblk = P.nblk;
   CK(misfit_fwd(ma, st));
+  if (P.T > 1 && P.interp) CK(flow_input(P.X, P.FI, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
   for (int t = 1; t < P.T; ++t) {
     // x_t = integrate(x_{t-1}) = flow((x - mean)/std)[:C]*std + mean   (da_4dvar.py:666-681)
-    if ((r = model_fwd(*F, t - 1, P.FI + (t - 1) * CHW, P.FO + (size_t)(t - 1) * F->cfg.Cout * HW, C, st))) return r;
+    if ((r = model_fwd(*F, t - 1, P.FI + (t - 1) * CHWl, P.FO + (size_t)(t - 1) * F->cfg.Cout * HWl, C, st))) return r;
     MisfitArgs mt = ma;
-    mt.net = P.FO + (size_t)(t - 1) * F->cfg.Cout * HW;
+    mt.net = P.FO + (size_t)(t - 1) * F->cfg.Cout * HWl;
     mt.scale = P.std_;
     mt.scale2 = nullptr;
     mt.xb = nullptr;
@@ -984,9 +1014,11 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     mt.Hm = P.Hm + t * CHW;
     mt.R = P.R + t * CHW;
     mt.x_out = P.X + t * CHW;
-    mt.flow_in = t < P.T - 1 ? P.FI + t * CHW : nullptr;
+    mt.flow_in = t < P.T - 1 ? P.FI + t * CHWl : nullptr;
     mt.partial = P.partial + (size_t)t * P.nblk;
     CK(misfit_fwd(mt, st));
+    if (t < P.T - 1 && P.interp)
+      CK(flow_input(P.X + t * CHW, P.FI + t * CHWl, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
   }
   CK(reduce_final(P.partial, P.nblk * P.T, P.dJ + 1, st));
   CK(reduce_sumsq(z, (int64_t)D.B * D.cfg.Cin * D.cfg.Himg * D.cfg.Wimg, P.partial + (size_t)P.T * P.nblk, P.nblk, st));
@@ -998,8 +1030,12 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     MisfitBwdArgs mb;
     memset(&mb, 0, sizeof(mb));
     mb.C = C;
-    mb.Hs = mb.Hl = P.Hs;
-    mb.Ws = mb.Wl = P.Ws;
+    mb.Hs = P.Hs;
+    mb.Ws = P.Ws;
+    mb.Hl = P.Hl;
+    mb.Wl = P.Wl;
+    mb.ri0 = P.interp ? P.ri0 : nullptr;
+    mb.rj0 = P.interp ? P.rj0 : nullptr;
     mb.x = P.X + t * CHW;
     mb.yo = P.yo + t * CHW;
     mb.Hm = P.Hm + t * CHW;
@@ -1011,14 +1047,21 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     mb.net_cstride = F->cfg.Cout;
     CK(misfit_bwd(mb, st));
     if ((r = model_bwd(*F, t - 1, P.GFO, P.GFI, nullptr, C, st))) return r;
-    CK(scale_channels(P.GFI, P.carry, P.std_, C, HW, nullptr, st));
+    if (P.interp)
+      CK(flow_input_adjoint(P.GFI, P.carry, P.di, P.dj, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
+    else
+      CK(scale_channels(P.GFI, P.carry, P.std_, C, HW, nullptr, st));
     carry = P.carry;
   }
   MisfitBwdArgs mb;
   memset(&mb, 0, sizeof(mb));
   mb.C = C;
-  mb.Hs = mb.Hl = P.Hs;
-  mb.Ws = mb.Wl = P.Ws;
+  mb.Hs = P.Hs;
+  mb.Ws = P.Ws;
+  mb.Hl = P.Hl;
+  mb.Wl = P.Wl;
+  mb.ri0 = P.interp ? P.ri0 : nullptr;
+  mb.rj0 = P.interp ? P.rj0 : nullptr;
   mb.x = P.X;
   mb.yo = P.yo;
   mb.Hm = P.Hm;
@@ -1177,9 +1220,8 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   if (T < 1 || C < 1) return fail(VV_E_ARG, "bad T/C");
   if (D->B != 1) return fail(VV_E_ARG, "closure needs a batch-1 decoder");
   if (D->cfg.Cout < C) return fail(VV_E_ARG, "decoder produces %d channels < C=%d", D->cfg.Cout, C);
-  if (Hs != D->cfg.Himg || Ws != D->cfg.Wimg)
-    return fail(VV_E_ARG, "state grid %dx%d != network grid %dx%d (nearest-interpolated grids not yet supported)", Hs,
-                Ws, D->cfg.Himg, D->cfg.Wimg);
+  if (Hs < D->cfg.Himg || Ws < D->cfg.Wimg)
+    return fail(VV_E_ARG, "state grid %dx%d coarser than the network grid %dx%d", Hs, Ws, D->cfg.Himg, D->cfg.Wimg);
   Model* F = nullptr;
   if (T > 1) {
     F = get_model(ctx, flow_model_id);
@@ -1187,7 +1229,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     if (F->cfg.Cin != C || F->cfg.Cout < C || F->nslots < T - 1 || F->B != 1)
       return fail(VV_E_ARG, "flow model shape/slots incompatible (Cin %d Cout %d slots %d)", F->cfg.Cin, F->cfg.Cout,
                   F->nslots);
-    if (F->cfg.Himg != Hs || F->cfg.Wimg != Ws) return fail(VV_E_ARG, "flow grid mismatch");
+    if (F->cfg.Himg != D->cfg.Himg || F->cfg.Wimg != D->cfg.Wimg) return fail(VV_E_ARG, "flow grid mismatch");
   }
   if (!xb || !yo || !Hmask || !R || !mean || !std_ || !std_tr) return fail(VV_E_ARG, "null problem buffer");
   int r = set_dev(ctx);
@@ -1208,31 +1250,60 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   P.std_ = std_;
   P.std_tr = std_tr;
   P.obs_coeff = obs_coeff;
+  P.Hl = D->cfg.Himg;
+  P.Wl = D->cfg.Wimg;
+  P.interp = (Hs != P.Hl || Ws != P.Wl);
   const size_t CHW = (size_t)C * Hs * Ws;
-  const size_t HW = (size_t)Hs * Ws;
+  const size_t HWl = (size_t)P.Hl * P.Wl;
+  const size_t CHWl = (size_t)C * HWl;
   const int fcout = F ? F->cfg.Cout : 0;
   for (int pass = 0; pass < 2; ++pass) {
     Planner pl;
     if (pass) pl.base = P.arena->base;
     P.X = pl.f(CHW * T);
-    P.dec_out = pl.f((size_t)D->cfg.Cout * HW);
-    P.gdec = pl.f((size_t)D->cfg.Cout * HW);
+    P.dec_out = pl.f((size_t)D->cfg.Cout * HWl);
+    P.gdec = pl.f((size_t)D->cfg.Cout * HWl);
     P.prod = pl.f(C);
-    P.FI = pl.f(CHW * std::max(T - 1, 1));
-    P.FO = pl.f((size_t)fcout * HW * std::max(T - 1, 1) + 1);
-    P.GFO = pl.f((size_t)fcout * HW + 1);
-    P.GFI = pl.f(CHW);
+    P.FI = pl.f(CHWl * std::max(T - 1, 1));
+    P.FO = pl.f((size_t)fcout * HWl * std::max(T - 1, 1) + 1);
+    P.GFO = pl.f((size_t)fcout * HWl + 1);
+    P.GFI = pl.f(CHWl);
     P.carry = pl.f(CHW);
+    float* maps = pl.f((size_t)Hs + Ws + 2 * (P.Hl + 1) + 2 * (P.Wl + 1));
     double* pd = reinterpret_cast<double*>(pl.f((size_t)2 * P.nblk * (T + 1) + 8));
     if (pass) {
       P.partial = pd;
       P.dJ = pd + (size_t)P.nblk * (T + 1) + 2;
+      int* mp = reinterpret_cast<int*>(maps);
+      P.mi = mp;
+      P.mj = P.mi + Hs;
+      P.ri0 = P.mj + Ws;
+      P.rj0 = P.ri0 + P.Hl + 1;
+      P.di = P.rj0 + P.Wl + 1;
+      P.dj = P.di + P.Hl;
     }
     if (!pass) {
       P.arena = std::make_unique<Arena>();
       if (hipMalloc(&P.arena->base, pl.bytes) != hipSuccess) return fail(VV_E_ALLOC, "problem arena");
       P.arena->cap = pl.bytes;
     }
+  }
+  {
+    // nearest maps (F.interpolate mode='nearest', quirk Q3) and the adjoint row/col ranges
+    std::vector<int> mi = nearest_map(P.Hl, Hs), mj = nearest_map(P.Wl, Ws);
+    std::vector<int> di = nearest_map(Hs, P.Hl), dj = nearest_map(Ws, P.Wl);
+    auto ranges = [](const std::vector<int>& m, int n) {
+      std::vector<int> r(n + 1, (int)m.size());
+      for (int k = (int)m.size() - 1; k >= 0; --k) r[m[k]] = k;
+      for (int a = n - 1; a >= 0; --a) r[a] = std::min(r[a], r[a + 1]);
+      return r;
+    };
+    for (size_t k = 1; k < mi.size(); ++k)
+      if (mi[k] < mi[k - 1]) return fail(VV_E_ARG, "non-monotone nearest map");
+    std::vector<int> ri0 = ranges(mi, P.Hl), rj0 = ranges(mj, P.Wl);
+    std::vector<int> all;
+    for (auto* v : {&mi, &mj, &ri0, &rj0, &di, &dj}) all.insert(all.end(), v->begin(), v->end());
+    VV_HIP(hipMemcpy(P.mi, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   hipLaunchKernelGGL(k_prod, dim3((C + 255) / 256), dim3(256), 0, 0, std_tr, std_, P.prod, C);
   VV_HIP(hipGetLastError());
@@ -1277,8 +1348,9 @@ int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream) {
   MisfitArgs ma;
   memset(&ma, 0, sizeof(ma));
   ma.C = P.C;
-  ma.Hs = ma.Hl = P.Hs;
-  ma.Ws = ma.Wl = P.Ws;
+  ma.Hs = P.Hs;
+  ma.Ws = P.Ws;
+  set_maps(P, ma);
   ma.net = P.dec_out;
   ma.scale = P.std_tr;
   ma.scale2 = P.std_;
@@ -1362,6 +1434,13 @@ int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* 
   if (!ctx || ncls < vv::PC_N) return fail(VV_E_ARG, "need %d class slots", (int)vv::PC_N);
   vv::prof_read(ms, flops, bytes, launches);
   vv::prof_enable(false);
+  return 0;
+}
+
+int vv_nearest_map(int in_size, int out_size, int* map) {
+  if (in_size <= 0 || out_size <= 0 || !map) return fail(VV_E_ARG, "bad argument");
+  auto m = nearest_map(in_size, out_size);
+  std::copy(m.begin(), m.end(), map);
   return 0;
 }
 

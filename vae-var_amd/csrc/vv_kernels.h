@@ -180,7 +180,14 @@ struct MisfitBwdArgs {
   float* g_state;         // scratch (C,Hs,Ws) (needed when maps are not identity)
 };
 hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s);
-// g_x(prev step) = g_flow_in / std (+ nothing else): flow input normalisation adjoint
+// general (nearest-interpolated) grids, F.interpolate mode='nearest' (quirk Q3):
+//   flow_in[c][a][b] = (x[c][di[a]][dj[b]] - mean[c]) / std[c]          (integrate: down-sample, da_4dvar.py:668-671)
+hipError_t flow_input(const float* x, float* flow_in, const int* di, const int* dj, const float* mean,
+                      const float* std_, int C, int Hs, int Ws, int Hl, int Wl, hipStream_t s);
+//   carry[c][i][j] = sum over (a,b) with (di[a],dj[b]) == (i,j) of gfi[c][a][b] / std[c]   (adjoint of the above)
+hipError_t flow_input_adjoint(const float* gfi, float* carry, const int* di, const int* dj, const float* std_, int C,
+                              int Hs, int Ws, int Hl, int Wl, hipStream_t s);
+// g_x(prev step) = g_flow_in / std (+ nothing else): flow input normalisation adjoint (identity grids)
 hipError_t scale_channels(const float* in, float* out, const float* inv_std, int C, int HW, const float* add,
                           hipStream_t s);
 

@@ -697,16 +697,22 @@ __global__ __launch_bounds__(256) void k_misfit_fwd(MisfitArgs a) {
   __shared__ double red[4];
   const int HW = a.Hs * a.Ws;
   const int n = a.C * HW;
+  const int HWl = a.Hl * a.Wl;
   double acc = 0.0;
   for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
     const int c = id / HW;
     const int p = id - c * HW;
-    float v = a.net[(size_t)c * HW + p] * a.scale[c];
+    int q = p;  // network-grid pixel (decoder_hr / integrate up-sampling, nearest)
+    if (a.mi) {
+      const int i = p / a.Ws, j = p - i * a.Ws;
+      q = a.mi[i] * a.Wl + a.mj[j];
+    }
+    float v = a.net[(size_t)c * HWl + q] * a.scale[c];
     if (a.scale2) v = v * a.scale2[c];
     if (a.xb) v = v + a.xb[id];
     if (a.offset) v = v + a.offset[c];
     a.x_out[id] = v;
-    if (a.flow_in) a.flow_in[id] = (v - a.mean[c]) / a.std_[c];
+    if (a.flow_in && !a.mi) a.flow_in[id] = (v - a.mean[c]) / a.std_[c];
     const float d = v - a.yo[id];
     acc += (double)((a.Hm[id] * (d * d)) / a.R[id]);
   }
@@ -726,17 +732,86 @@ __global__ __launch_bounds__(256) void k_misfit_bwd(MisfitBwdArgs a) {
   }
 }
 
+// adjoint of the nearest up-sampling for general grids: each network pixel (a,b) sums the state rectangle
+// [ri0[a], ri0[a+1]) x [rj0[b], rj0[b+1]) that maps onto it (mi/mj are monotone), deterministic order
+__global__ __launch_bounds__(256) void k_misfit_bwd_gather(MisfitBwdArgs a) {
+  const int HWl = a.Hl * a.Wl, HW = a.Hs * a.Ws;
+  const int n = a.C * HWl;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    const int c = id / HWl;
+    const int q = id - c * HWl;
+    const int ra = q / a.Wl, cb = q - ra * a.Wl;
+    float g = 0.f;
+    for (int i = a.ri0[ra]; i < a.ri0[ra + 1]; ++i)
+      for (int j = a.rj0[cb]; j < a.rj0[cb + 1]; ++j) {
+        const size_t e = (size_t)c * HW + (size_t)i * a.Ws + j;
+        float v = a.coeff * ((a.Hm[e] * (a.x[e] - a.yo[e])) / a.R[e]);
+        if (a.g_carry) v += a.g_carry[e];
+        g += v;
+      }
+    a.g_net[(size_t)c * HWl + q] = g * a.scale[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_flow_input(const float* x, float* fi, const int* di, const int* dj,
+                                                    const float* mean, const float* std_, int C, int Hs, int Ws,
+                                                    int Hl, int Wl) {
+  const int HWl = Hl * Wl;
+  const int n = C * HWl;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    const int c = id / HWl, q = id - c * HWl;
+    const int ra = q / Wl, cb = q - ra * Wl;
+    fi[id] = (x[((size_t)c * Hs + di[ra]) * Ws + dj[cb]] - mean[c]) / std_[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_flow_input_adj(const float* gfi, float* carry, const int* di, const int* dj,
+                                                        const float* std_, int C, int Hs, int Ws, int Hl, int Wl) {
+  const int HWl = Hl * Wl;
+  const int n = C * HWl;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    const int c = id / HWl, q = id - c * HWl;
+    const int ra = q / Wl, cb = q - ra * Wl;
+    // di/dj are injective when down-sampling (Hs >= Hl), so every target is written at most once
+    carry[((size_t)c * Hs + di[ra]) * Ws + dj[cb]] = gfi[id] / std_[c];
+  }
+}
+
+hipError_t flow_input(const float* x, float* fi, const int* di, const int* dj, const float* mean, const float* std_,
+                      int C, int Hs, int Ws, int Hl, int Wl, hipStream_t s) {
+  const int ph = prof_begin(s);
+  hipLaunchKernelGGL(k_flow_input, dim3(1024), dim3(256), 0, s, x, fi, di, dj, mean, std_, C, Hs, Ws, Hl, Wl);
+  prof_end(ph, s, PC_MISFIT, 2.0 * C * Hl * Wl, 8.0 * C * Hl * Wl);
+  return hipGetLastError();
+}
+
+hipError_t flow_input_adjoint(const float* gfi, float* carry, const int* di, const int* dj, const float* std_, int C,
+                              int Hs, int Ws, int Hl, int Wl, hipStream_t s) {
+  if (Hs < Hl || Ws < Wl) return hipErrorNotSupported;
+  hipError_t e = hipMemsetAsync(carry, 0, (size_t)C * Hs * Ws * sizeof(float), s);
+  if (e != hipSuccess) return e;
+  const int ph = prof_begin(s);
+  hipLaunchKernelGGL(k_flow_input_adj, dim3(1024), dim3(256), 0, s, gfi, carry, di, dj, std_, C, Hs, Ws, Hl, Wl);
+  prof_end(ph, s, PC_MISFIT, 1.0 * C * Hl * Wl, 8.0 * C * Hl * Wl);
+  return hipGetLastError();
+}
+
 hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
-  if (a.mi || a.mj || a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorNotSupported;
+  if ((a.mi == nullptr) != (a.mj == nullptr)) return hipErrorInvalidValue;
+  if (!a.mi && (a.Hs != a.Hl || a.Ws != a.Wl)) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_misfit_fwd, dim3(a.nblk), dim3(256), 0, s, a);
   prof_end(ph, s, PC_MISFIT, 6.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * ((a.xb ? 6 : 5) + (a.flow_in ? 1 : 0)));
   return hipGetLastError();
 }
 hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
-  if (a.mi || a.mj || a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorNotSupported;
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_misfit_bwd, dim3(1024), dim3(256), 0, s, a);
+  if (a.ri0) {
+    hipLaunchKernelGGL(k_misfit_bwd_gather, dim3(1024), dim3(256), 0, s, a);
+  } else {
+    if (a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_misfit_bwd, dim3(1024), dim3(256), 0, s, a);
+  }
   prof_end(ph, s, PC_MISFIT, 5.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * (a.g_carry ? 6 : 5));
   return hipGetLastError();
 }

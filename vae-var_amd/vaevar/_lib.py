@@ -89,6 +89,7 @@ _SIGS = {
                         c_float, c_int, c_void_p]),
     "vv_profile_start": (c_int, [c_void_p]),
     "vv_profile_stop": (c_int, [c_void_p, P(c_double), P(c_double), P(c_double), P(c_int), c_int]),
+    "vv_nearest_map": (c_int, [c_int, c_int, P(c_int)]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 
@@ -126,6 +127,13 @@ def last_error() -> str:
 def check(rc: int, what: str = "") -> None:
     if rc != 0:
         raise VVError(f"libvaevar {what} failed (status {rc}): {last_error()}")
+
+
+def nearest_map(in_size: int, out_size: int):
+    """F.interpolate(mode='nearest') source indices used by the engine (quirk Q3)."""
+    m = (c_int * out_size)()
+    check(lib.vv_nearest_map(in_size, out_size, m), "nearest_map")
+    return list(m)
 
 
 def param_list(cfg: dict):
