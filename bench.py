@@ -29,6 +29,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense peak (MI355X_MICROARCH.md, chip-level table)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X bf16 MFMA dense peak; the split GEMM spends 6 bf16 products per fp32 product
+PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
 FLOPS_PER_EVAL = {1: 1787.8e9, 2: 3577.0e9, 6: 10733.7e9}  # SURVEY §8 d (input-grad only)
 
@@ -172,10 +174,16 @@ def main():
     if prof:
         g = pr["gemm"]
         ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
-        out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                           "frac": ach / PEAK_F32_TFLOPS, "traffic": gemm_traffic(),
-                           "kernel": "k_gemm_nt (every fp32 MFMA GEMM launch of a HIP-event-profiled repeat "
+        split = prob.ctx.gemm_math == "split"
+        peak = PEAK_SPLIT_TFLOPS if split else PEAK_F32_TFLOPS
+        out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                           "frac": ach / peak, "traffic": gemm_traffic(),
+                           "kernel": "k_gemm_bs / k_gemm_nt (every fp32 GEMM launch of a HIP-event-profiled repeat "
                                      "of the timed analysis)",
+                           "gemm_math": ("bf16x6 split (fp32 operands as 3 bf16 planes, 6 v_mfma_f32_32x32x16_bf16 "
+                                         "products; peak = 2.5 PF bf16 / 6)") if split else
+                                        "exact f32 MFMA (v_mfma_f32_32x32x2_f32; peak 157.3 TF)",
+                           "frac_of_f32_mfma_peak": ach / PEAK_F32_TFLOPS,
                            "launches": g["launches"], "avg_launch_us": 1e3 * g["ms"] / max(g["launches"], 1),
                            "flops_per_launch": g["flops"] / max(g["launches"], 1)}
         busy = sum(v["ms"] for v in pr.values())

@@ -24,6 +24,8 @@ def _ref_gemm(A, B, bias):
 @pytest.mark.parametrize("M,N,K,tile", [
     (256, 96, 96, -1), (2048, 1152, 1152, 0), (2048, 1152, 1152, 1), (2048, 1152, 1152, 2),
     (2048, 3456, 1152, -1), (2048, 1152, 4608, -1), (8192, 288, 96, -1), (100, 70, 64, 2), (130, 200, 32, 0),
+    (2048, 1152, 1152, 21), (2048, 1152, 1152, 24), (100, 70, 64, 21), (130, 200, 32, 24), (300, 96, 384, 23),
+    (2048, 4608, 1152, 26), (130, 200, 64, 25), (130, 200, 64, 22),
 ])
 def test_gemm_nt(ctx, M, N, K, tile):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
@@ -32,10 +34,39 @@ def test_gemm_nt(ctx, M, N, K, tile):
     bias = torch.rand(N, generator=g) - 0.5
     C = ctx.gemm(A.cuda(), B.cuda(), bias.cuda(), tile=tile).cpu().double()
     ref = _ref_gemm(A, B, bias)
-    # exact-f32 MFMA: error ~1e-7 * sum|a*b| per element (cdna_hip_programming.md §3)
+    # exact-f32 MFMA (tiles < 21) and the bf16x6 split (tiles >= 21): error ~1e-7 * sum|a*b| per element
     scale = (A.abs().double() @ B.abs().double().t()).max()
     err = (C - ref).abs().max() / scale
     assert err < 2e-6, float(err)
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 1152, 4608), (8192, 96, 384), (777, 300, 96)])
+def test_gemm_split_accuracy(ctx, M, N, K):
+    """bf16x6 split GEMM (tiles >= 21) vs fp64: element error / sum|a*b| no larger than the exact-f32
+    MFMA's on the same operands (x1.5 margin) and below 1e-6; randn operands, weight-like B scale."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) * 0.03
+    ref = A.double() @ B.double().t()
+    scale = A.double().abs() @ B.double().abs().t()
+    A, B = A.cuda(), B.cuda()
+    e32 = float(((ctx.gemm(A, B, tile=2).cpu().double() - ref).abs() / scale).max())
+    for t in (21, 24):
+        es = float(((ctx.gemm(A, B, tile=t).cpu().double() - ref).abs() / scale).max())
+        print(f"gemm {M}x{N}x{K}: f32 {e32:.2e} split t{t} {es:.2e}")
+        assert es < 1e-6 and es < 1.5 * e32, (t, es, e32)
+
+
+def test_gemm_math_switch(ctx):
+    assert ctx.gemm_math in ("split", "f32")
+    old = ctx.gemm_math
+    try:
+        ctx.gemm_math = "f32"
+        assert ctx.gemm_math == "f32"
+        ctx.gemm_math = "split"
+        assert ctx.gemm_math == "split"
+    finally:
+        ctx.gemm_math = old
 
 
 def test_gemm_asymmetric_identity(ctx):

@@ -113,6 +113,31 @@ def test_full_closure_g3(full_dec):
     assert e_b < 1e-5 and e_o < 1e-4 and e_g < 1e-4
 
 
+def test_full_closure_g3_exact_f32(full_dec):
+    """The same G3 closure with every GEMM on the exact-f32 MFMA (VV_GEMM_F32) instead of the bf16x6 split."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    g = gold("g3_full_decoder.npz")
+    ctx = full_dec.ctx
+    old = ctx.gemm_math
+    ctx.gemm_math = "f32"
+    try:
+        prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+        z = torch.from_numpy(0.3 * smooth_field(403, (1, 32, 128, 256))).cuda()
+        grad = torch.empty_like(z)
+        jb, jo = prob.closure(z, grad)
+    finally:
+        ctx.gemm_math = old
+    gr = grad.cpu().numpy().reshape(-1).astype(np.float64)
+    e_b = abs(jb - g["J_b"]) / g["J_b"]
+    e_o = abs(jo - g["J_o"]) / g["J_o"]
+    e_g = rel(gr[g["idx_grad"]], g["cgrad_sample"])
+    print(f"G3 closure (exact f32 GEMM): J_b rel {e_b:.2e} J_o rel {e_o:.2e} grad rel {e_g:.2e}")
+    assert e_b < 1e-5 and e_o < 1e-4 and e_g < 1e-4
+
+
 def _tiny_problem(T):
     from vaevar.problem import make_problem
 

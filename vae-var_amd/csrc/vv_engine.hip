@@ -232,6 +232,7 @@ struct Model {
   std::vector<float*> pptr;  // device pointer per param
   std::unordered_map<std::string, const float*> W;   // name -> weights ; name + "^T" -> transposed
   std::unique_ptr<Arena> warena, aarena;
+  std::unique_ptr<Arena> parena;  // bf16 split planes of warena (3 x 2 B per float), GEMM_SPLIT B operands
   Stage enc0, enc1, dec1, dec0;
   std::vector<Stage> lg;
   std::vector<Save> saves;
@@ -269,6 +270,12 @@ struct vv_ctx {
   float* redf = nullptr;
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
+  struct SplitW {
+    const float* base;
+    size_t n;
+    unsigned short* planes;
+  };
+  std::vector<SplitW> split_owned;  // vv_gemm_register_weight planes
 };
 
 namespace {
@@ -596,6 +603,12 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
   m->warena = std::make_unique<Arena>();
   if (hipMalloc(&m->warena->base, wbytes) != hipSuccess) return fail(VV_E_ALLOC, "weights: %zu bytes", wbytes);
   m->warena->cap = wbytes;
+  m->parena = std::make_unique<Arena>();
+  if (hipMalloc(&m->parena->base, wbytes / 4 * 3 * sizeof(unsigned short)) != hipSuccess)
+    return fail(VV_E_ALLOC, "weight split planes: %zu bytes", wbytes / 4 * 6);
+  m->parena->cap = wbytes / 4 * 6;
+  vv::register_split_arena(reinterpret_cast<const float*>(m->warena->base), wbytes / 4,
+                           reinterpret_cast<const unsigned short*>(m->parena->base));
   size_t off = 0;
   for (auto& p : m->params) {
     float* d = reinterpret_cast<float*>(m->warena->base + off);
@@ -1138,6 +1151,7 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
+  if (const char* e = getenv("VAEVAR_GEMM_MATH")) vv::set_gemm_math(strcmp(e, "f32") == 0 ? vv::GEMM_F32 : vv::GEMM_SPLIT);
   *out = c;
   return 0;
 }
@@ -1146,8 +1160,14 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   if (!ctx) return 0;
   (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();
-  for (auto& m : ctx->models)
+  for (auto& m : ctx->models) {
     for (int* p : m->maps_owned) (void)hipFree(p);
+    if (m->warena) vv::unregister_split_arena(reinterpret_cast<const float*>(m->warena->base));
+  }
+  for (auto& w : ctx->split_owned) {
+    vv::unregister_split_arena(w.base);
+    (void)hipFree(w.planes);
+  }
   (void)hipFree(ctx->red);
   (void)hipFree(ctx->redf);
   (void)hipFree(ctx->dout);
@@ -1178,6 +1198,16 @@ int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
     auto it = m->W.find(p.name + "^T");
     if (it == m->W.end()) continue;
     VV_HIP(vv::transpose2d(m->W[p.name], const_cast<float*>(it->second), (int)p.shape[0], (int)p.shape[1], 0));
+  }
+  // bf16 split planes of every GEMM weight and its transpose (GEMM_SPLIT B operands)
+  const float* wbase = reinterpret_cast<const float*>(m->warena->base);
+  unsigned short* pbase = reinterpret_cast<unsigned short*>(m->parena->base);
+  for (auto& p : m->params) {
+    auto it = m->W.find(p.name + "^T");
+    if (it == m->W.end()) continue;
+    const size_t n = numel(p.shape);
+    VV_HIP(vv::split_planes(m->W[p.name], pbase + 3 * (size_t)(m->W[p.name] - wbase), n, (int)p.shape[1], 0));
+    VV_HIP(vv::split_planes(it->second, pbase + 3 * (size_t)(it->second - wbase), n, (int)p.shape[0], 0));
   }
   VV_HIP(hipDeviceSynchronize());
   m->loaded = true;
@@ -1441,6 +1471,44 @@ int vv_nearest_map(int in_size, int out_size, int* map) {
   if (in_size <= 0 || out_size <= 0 || !map) return fail(VV_E_ARG, "bad argument");
   auto m = nearest_map(in_size, out_size);
   std::copy(m.begin(), m.end(), map);
+  return 0;
+}
+
+int vv_set_gemm_math(vv_ctx* ctx, int math) {
+  if (!ctx || (math != VV_GEMM_F32 && math != VV_GEMM_SPLIT)) return fail(VV_E_ARG, "bad gemm math %d", math);
+  vv::set_gemm_math(math);
+  return 0;
+}
+
+int vv_get_gemm_math(vv_ctx* ctx, int* math) {
+  if (!ctx || !math) return fail(VV_E_ARG, "null argument");
+  *math = vv::gemm_math();
+  return 0;
+}
+
+int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K) {
+  if (!ctx || !B || N <= 0 || K <= 0) return fail(VV_E_ARG, "bad argument");
+  int r = set_dev(ctx);
+  if (r) return r;
+  unsigned short* planes = nullptr;
+  const size_t n = (size_t)N * K;
+  // a registration overlapping this range is stale (its weight was freed and the memory reused): drop it
+  VV_HIP(hipDeviceSynchronize());
+  for (size_t i = 0; i < ctx->split_owned.size();) {
+    auto& w = ctx->split_owned[i];
+    if (w.base < B + n && B < w.base + w.n) {
+      vv::unregister_split_arena(w.base);
+      (void)hipFree(w.planes);
+      ctx->split_owned.erase(ctx->split_owned.begin() + i);
+    } else {
+      ++i;
+    }
+  }
+  if (hipMalloc(&planes, n * 3 * sizeof(unsigned short)) != hipSuccess) return fail(VV_E_ALLOC, "planes");
+  VV_HIP(vv::split_planes(B, planes, n, K, 0));
+  VV_HIP(hipDeviceSynchronize());
+  vv::register_split_arena(B, n, planes);
+  ctx->split_owned.push_back({B, n, planes});
   return 0;
 }
 

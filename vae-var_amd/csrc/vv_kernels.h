@@ -29,6 +29,8 @@ struct GemmGroup {
   float* C;
   const float* R;
   float* aux;
+  const unsigned short* Bp;  // filled in by gemm_nt: bf16 split planes of B (registered weight arena) or null
+  const unsigned short* Ap;  // bf16 split planes of A, rows [3][lda] (caller-provided or registered), or null
 };
 
 struct GemmArgs {
@@ -49,6 +51,18 @@ struct GemmArgs {
 // ws: scratch of at least gemm_ws_floats() floats (may be null: no tail split)
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);
 size_t gemm_ws_floats();
+
+// GEMM arithmetic: GEMM_F32 = v_mfma_f32_32x32x2_f32 (exact f32 fma chain); GEMM_SPLIT = the fp32 operands
+// split into three bf16 planes, six v_mfma_f32_32x32x16_bf16 products (fp32-level error, 2.67x the rate)
+enum GemmMath : int { GEMM_F32 = 0, GEMM_SPLIT = 1 };
+void set_gemm_math(int m);
+int gemm_math();
+// weight arenas whose bf16 split planes exist: for B inside [base, base+n), row r of the [N][K] operand at
+// float offset o = B - base has its planes at planes + 3*(o + r*K): h[K], m[K], l[K]
+void register_split_arena(const float* base, size_t n, const unsigned short* planes);
+void unregister_split_arena(const float* base);
+// dst[n/K][3][K] = exact bf16 split of the rows of src[n/K][K] (h = bf16(x), m = bf16(x-h), l = bf16(x-h-m))
+hipError_t split_planes(const float* src, unsigned short* dst, size_t n, int K, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // LayerNorm over the last dim, one wave per output row.

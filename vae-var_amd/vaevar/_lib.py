@@ -90,6 +90,9 @@ _SIGS = {
     "vv_profile_start": (c_int, [c_void_p]),
     "vv_profile_stop": (c_int, [c_void_p, P(c_double), P(c_double), P(c_double), P(c_int), c_int]),
     "vv_nearest_map": (c_int, [c_int, c_int, P(c_int)]),
+    "vv_set_gemm_math": (c_int, [c_void_p, c_int]),
+    "vv_get_gemm_math": (c_int, [c_void_p, P(c_int)]),
+    "vv_gemm_register_weight": (c_int, [c_void_p, c_void_p, c_int, c_int]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 

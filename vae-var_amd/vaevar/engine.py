@@ -94,6 +94,23 @@ class Context:
         return {c: {"ms": ms[i], "flops": fl[i], "bytes": by[i], "launches": cnt[i]}
                 for i, c in enumerate(self.PROF_CLASSES)}
 
+    GEMM_MATH = {"f32": 0, "split": 1}
+
+    @property
+    def gemm_math(self) -> str:
+        """'split' (bf16x6 split planes, fp32-level error, default) or 'f32' (exact f32 MFMA); process-wide."""
+        v = ctypes.c_int()
+        check(lib.vv_get_gemm_math(self.h, ctypes.byref(v)), "get_gemm_math")
+        return {0: "f32", 1: "split"}[v.value]
+
+    @gemm_math.setter
+    def gemm_math(self, name: str):
+        check(lib.vv_set_gemm_math(self.h, self.GEMM_MATH[name]), "set_gemm_math")
+
+    def gemm_register_weight(self, B):
+        """Precompute B's bf16 split planes (B must outlive the context and stay unchanged)."""
+        check(lib.vv_gemm_register_weight(self.h, _ptr(B), B.shape[0], B.shape[1]), "gemm_register_weight")
+
     def gemm(self, A, B, bias=None, tile=-1):
         M, K = A.shape
         N = B.shape[0]
