@@ -224,6 +224,7 @@ enum ProfClass : int { PC_GEMM = 0, PC_ATTN = 1, PC_LN = 2, PC_PATCH = 3, PC_MIS
 int prof_begin(hipStream_t s);                                        // -1 when disabled
 void prof_end(int h, hipStream_t s, int cls, double flops, double bytes);
 void prof_enable(bool on);
+bool prof_enabled();
 // sums since enable: ms, flops, bytes, launches per class (synchronises)
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 

@@ -24,6 +24,7 @@ std::vector<ProfRec> g_rec;
 size_t g_used = 0;
 }  // namespace
 
+bool prof_enabled() { return g_prof_on; }
 void prof_enable(bool on) {
   g_prof_on = on;
   g_used = 0;
