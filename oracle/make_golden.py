@@ -13,6 +13,7 @@ are stored):
   g4_nearest_maps.npz   G4: nearest index maps of F.interpolate 721<->128, 1440<->256
   g5_tiny_lbfgs.npz     G5: restated vae4dvar loop on the tiny decoder (Nit=2): J per outer pass, xa
   g5b_tiny_4dvar.npz    tiny decoder + tiny flow, T=2: J terms and dJ/dz of one closure
+  g7_tiny_lgunet1.npz   G7: tiny networks.LGUnet_all_1 (RoPE, -inf mask, global LG window, 3 levels): out
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
                         and one config-2 closure (J_b, J_o, sampled dJ/dz)
 """
@@ -207,6 +208,36 @@ def g3(tr):
     np.savez(os.path.join(GOLD, "g3_full_decoder.npz"), **res)
 
 
+def ref_cfg_l1(cfg):
+    c = {k: v for k, v in cfg.items() if k != "arch"}
+    c.update(in_chans=sum(cfg["inchans_list"]), out_chans=sum(cfg["outchans_list"]), Weather_T=1, drop_path=0.0,
+             use_checkpoint=False, inp_length=1, use_mlp=False)
+    return c
+
+
+def g7():
+    """G7: the real networks.LGUnet_all_1 on TINY_FCST with synthetic weights; pins oracle/lgunet1_ref.py."""
+    import importlib
+
+    from oracle.lgunet1_ref import lgunet1_forward, synth_params as synth1
+
+    L1 = importlib.import_module("networks.LGUnet_all")
+    cfg = C.TINY_FCST
+    torch.manual_seed(0)
+    m = L1.LGUnet_all_1(**ref_cfg_l1(cfg))
+    p = synth1(cfg)
+    sd = m.state_dict()
+    assert set(sd) == set(p), (set(sd) ^ set(p))
+    m.load_state_dict(p, strict=True)
+    m.eval()
+    x = torch.from_numpy(smooth_field(701, (1, C.in_channels(cfg)) + tuple(cfg["img_size"])))
+    with torch.no_grad():
+        y = m(x)
+        yo = lgunet1_forward(p, cfg, x)
+    print(f"G7 tiny LGUnet_all_1: out {tuple(y.shape)} oracle rel {rel(yo, y):.2e}")
+    np.savez(os.path.join(GOLD, "g7_tiny_lgunet1.npz"), out=y.numpy())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also generate G3 (full decoder, ~1 min)")
@@ -217,7 +248,8 @@ def main():
     cwd = os.getcwd()
     tr, sb = ref_harness.import_reference()
     os.chdir(cwd)
-    steps = {"g1": lambda: g1(tr), "g2": lambda: g2(sb), "g4": g4, "g5": lambda: g5(tr), "g5b": lambda: g5b(tr)}
+    steps = {"g1": lambda: g1(tr), "g2": lambda: g2(sb), "g4": g4, "g5": lambda: g5(tr), "g5b": lambda: g5b(tr),
+             "g7": g7}
     if a.full:
         steps["g3"] = lambda: g3(tr)
     for k, f in steps.items():

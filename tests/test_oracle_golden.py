@@ -126,3 +126,17 @@ def test_g3_full_decoder_oracle():
     gr = z.grad.numpy().reshape(-1)
     assert rel(o[g["idx_out"]], g["out_sample"]) < 1e-6
     assert rel(gr[g["idx_grad"]], g["grad_sample"]) < 1e-6
+
+
+def test_g7_tiny_lgunet1_oracle():
+    """networks.LGUnet_all_1 restatement (RoPE, -inf mask, global LG window, 3 levels, patch (3,2)/s2)."""
+    from oracle.lgunet1_ref import lgunet1_forward, synth_params
+    from vaevar import config as C
+    from vaevar.synth import smooth_field
+
+    g = gold("g7_tiny_lgunet1.npz")
+    cfg = C.TINY_FCST
+    x = torch.from_numpy(smooth_field(701, (1, C.in_channels(cfg)) + tuple(cfg["img_size"])))
+    with torch.no_grad():
+        y = lgunet1_forward(synth_params(cfg), cfg, x)
+    assert rel(y, g["out"]) < 1e-6
