@@ -5,13 +5,16 @@
  * protocol. Each entry point below replaces one piece of that protocol:
  *
  *   vv_lgunet_param_count/_info   the state_dict key set of networks_old.transformer.LGUnet_all
- *                                 (networks_old/transformer.py:716-745, swinblock.py:189-262)
+ *                                 (networks_old/transformer.py:716-745, swinblock.py:189-262), or with
+ *                                 arch = VV_ARCH_LGUNET1 of networks.LGUnet_all.LGUnet_all_1 (LGUnet_all.py:742-776)
  *   vv_model_create/load_weights  LGUnet_all(**cfg) + load_state_dict (da_4dvar.py:590-603, 571-588)
  *   vv_model_forward              LGUnet_all.forward (transformer.py:747-752) = VAE_lr.decoder (vae.py:83-85)
  *   vv_model_backward             autograd of the above w.r.t. its input (input gradient only, quirk Q5)
  *   vv_bind_problem               the closure state of one_step_DA 'vae4dvar' (da_4dvar.py:1179-1251)
  *   vv_closure                    closure() -> loss(z); backward (da_4dvar.py:1183-1208, 1242-1246)
  *   vv_decode                     the analysis xa = decoder_hr(z)*stdTr*std + xb (da_4dvar.py:1301-1306)
+ *   vv_integrate                  integrate(x, model, 1) (da_4dvar.py:666-681): the outer-cycle forecast with
+ *                                 the 0.25-degree LGUnet_all_1 (da_4dvar.py:1329, :652), forward only
  *   vv_dot/axpy/... , vv_adam     vector arithmetic of torch/optim/lbfgs.py:333-535 and adam.py
  *
  * Conventions: every function returns 0 on success, a non-zero status otherwise (HIP error code or
@@ -36,7 +39,11 @@ extern "C" {
 
 typedef struct vv_ctx vv_ctx;
 
-/* networks_old.transformer.LGUnet_all keyword arguments (nf_model/parameters0_old.yaml:49-96) */
+#define VV_ARCH_LGUNET 0   /* networks_old.transformer.LGUnet_all (VAE decoder, flow model): fwd + input bwd */
+#define VV_ARCH_LGUNET1 1  /* networks.LGUnet_all.LGUnet_all_1 (forecast model): forward only */
+
+/* LGUnet_all keyword arguments (nf_model/parameters0_old.yaml:49-96; for VV_ARCH_LGUNET1
+   output/model/model_0.25degree/training_options.yaml:64-119). Zero-initialise, then fill. */
 typedef struct vv_lgunet_config {
   int img_size[2];
   int patch_size[2];   /* must equal stride: (2,2) */
@@ -53,6 +60,9 @@ typedef struct vv_lgunet_config {
   int n_lg_layers;
   int lg_depths[8];
   int lg_heads[8];
+  /* appended for VV_ARCH_LGUNET1 (ignored by VV_ARCH_LGUNET, whose window is window_size x window_size) */
+  int arch;            /* VV_ARCH_* */
+  int window_hw[2];    /* [wh, ww] (LGUnet_all_1 window_size); patch_size may then exceed stride (3,2)/(2,2) */
 } vv_lgunet_config;
 
 int vv_version(void);
@@ -91,6 +101,11 @@ int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* 
 int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, void* stream);
 /* analysis state xa (C,Hs,Ws) */
 int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
+/* out = integrate(x, model, steps) (da_4dvar.py:666-681): z = (x - mean)/std (nearest to the model grid when
+   (Hs,Ws) differs, interpolation=True); `steps` times z = model(z)[:, :C]; nearest back to (Hs,Ws); *std + mean.
+   x, out (C,Hs,Ws); mean, std (C). The model (either arch, batch 1) must map C channels to >= C. */
+int vv_integrate(vv_ctx* ctx, int model_id, const float* x, float* out, int C, int Hs, int Ws, const float* mean,
+                 const float* std_, int steps, void* stream);
 /* trajectory x_t (T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
 int vv_state_ptr(vv_ctx* ctx, const float** x);
 

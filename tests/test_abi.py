@@ -86,3 +86,18 @@ def test_no_gpu_ctx_fails_cleanly():
     h = ctypes.c_void_p()
     rc = _lib.lib.vv_ctx_create(0, ctypes.byref(h))
     assert rc != 0 and _lib.last_error()
+
+
+def test_fcst_param_enumeration_matches_reference_keys():
+    """vv_lgunet_param_info for LGUnet_all_1 (arch lgunet1) == the state_dict key set / shapes of the reference
+    (the oracle's param_shapes is pinned to the real module by oracle/make_golden.py::g7)."""
+    from oracle.lgunet1_ref import param_shapes
+    from vaevar import _lib
+    from vaevar import config as C
+
+    for cfg in (C.TINY_FCST, C.MID_FCST, C.FCST):
+        got = dict(_lib.param_list(cfg))
+        want = param_shapes(cfg)
+        assert set(got) == set(want)
+        for k, v in want.items():
+            assert tuple(got[k]) == tuple(v), k

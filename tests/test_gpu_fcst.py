@@ -1,0 +1,99 @@
+"""Forecast network networks.LGUnet_all.LGUnet_all_1 and integrate() (a12 / f1) on the HIP
+engine, against the G7 golden (real reference) and the oracle restatement (oracle/lgunet1_ref.py, itself pinned
+bit-exact to the reference by G7). Forward only, as the reference uses it (da_4dvar.py:652, 1329).
+
+Tolerance: out rel <= 1e-5 (tiny, G7) / 1e-4 (mid size), rel = max|a-b| / max|b|."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLD
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+def _model(cfg):
+    from vaevar.engine import LGUnet
+
+    return LGUnet(cfg, 1, 1).load_synthetic()
+
+
+def test_fcst_tiny_g7():
+    from vaevar import config as C
+    from vaevar.synth import smooth_field
+
+    cfg = C.TINY_FCST
+    g = np.load(os.path.join(GOLD, "g7_tiny_lgunet1.npz"))
+    x = torch.from_numpy(smooth_field(701, (1, C.in_channels(cfg)) + tuple(cfg["img_size"]))).cuda()
+    out = _model(cfg).forward_raw(x)
+    e = rel(out.cpu(), g["out"])
+    print(f"G7 tiny LGUnet_all_1: out rel {e:.2e}")
+    assert e < 1e-5
+
+
+def test_fcst_mid_vs_oracle():
+    """Real FCST widths/heads/window on a 97x192 image: head_dim 32/32/64/192, [6,12] windows with the -inf
+    row mask, 288-token global LG window, patch (3,2)/stride 2 conv and overlapping ConvTranspose."""
+    from oracle.lgunet1_ref import lgunet1_forward, synth_params
+    from vaevar import config as C
+    from vaevar.synth import smooth_field
+
+    cfg = C.MID_FCST
+    x = smooth_field(702, (1, C.in_channels(cfg)) + tuple(cfg["img_size"]))
+    out = _model(cfg).forward_raw(torch.from_numpy(x).cuda())
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        ref = lgunet1_forward(synth_params(cfg), cfg, torch.from_numpy(x))
+    e = rel(out.cpu(), ref)
+    print(f"mid LGUnet_all_1 (97x192): out rel {e:.2e}")
+    assert e < 1e-4
+
+
+def test_fcst_backward_refused():
+    from vaevar import config as C
+    from vaevar._lib import VVError
+
+    m = _model(C.TINY_FCST)
+    x = torch.zeros(1, 5, 49, 96, device="cuda")
+    m.forward_raw(x)
+    with pytest.raises(VVError):
+        m.backward_raw(torch.zeros(1, 10, 49, 96, device="cuda"), torch.empty_like(x))
+
+
+@pytest.mark.parametrize("grid", [(49, 96), (61, 120)])
+def test_integrate_forecast(grid):
+    """integrate(x, forecast_model, 1): (x-mean)/std -> model -> [:C] -> *std+mean; a state grid other than
+    the model grid goes through the nearest maps both ways (interpolation=True, quirk Q3)."""
+    from oracle.lgunet1_ref import lgunet1_forward, synth_params
+    from vaevar import config as C
+    from vaevar.engine import integrate
+    from vaevar.synth import smooth_field
+
+    cfg = dict(C.TINY_FCST, outchans_list=[4, 6])   # in 5 channels -> out 10 (mean halves first: 2+3)
+    Cs = C.in_channels(cfg)
+    Hs, Ws = grid
+    mean = torch.linspace(-1.0, 2.0, Cs)
+    std = torch.linspace(0.5, 3.0, Cs)
+    x = torch.from_numpy(smooth_field(703, (Cs, Hs, Ws))) * std.view(-1, 1, 1) + mean.view(-1, 1, 1)
+    m = _model(cfg)
+    out = integrate(m, x.cuda(), mean, std, steps=1)
+    z = ((x - mean.view(-1, 1, 1)) / std.view(-1, 1, 1)).unsqueeze(0)
+    H, W = cfg["img_size"]
+    if (Hs, Ws) != (H, W):
+        z = torch.nn.functional.interpolate(z, (H, W))
+    with torch.no_grad():
+        y = lgunet1_forward(synth_params(cfg), cfg, z)[:, :Cs]
+    if (Hs, Ws) != (H, W):
+        y = torch.nn.functional.interpolate(y, (Hs, Ws))
+    ref = y.reshape(Cs, Hs, Ws) * std.view(-1, 1, 1) + mean.view(-1, 1, 1)
+    e = rel(out.cpu(), ref)
+    print(f"integrate {grid}: rel {e:.2e}")
+    assert e < 1e-5

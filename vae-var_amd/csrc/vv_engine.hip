@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/vaevar.h"
+#include "vv_fcst.h"
 #include "vv_kernels.h"
 
 namespace {
@@ -242,6 +243,8 @@ struct Model {
   std::vector<int*> maps_owned;
   bool loaded = false;
   int64_t workspace = 0;
+  vvf::FModel* fm = nullptr;  // VV_ARCH_LGUNET1: the forward-only forecast engine (vv_fcst.hip)
+  ~Model() { vvf::destroy(fm); }
 };
 
 struct Problem {
@@ -1154,6 +1157,14 @@ int vv_last_error(char* buf, int cap) {
 }
 
 int vv_lgunet_param_count(const vv_lgunet_config* cfg, int* count) {
+  if (cfg && cfg->arch == VV_ARCH_LGUNET1) {
+    std::vector<vvf::ParamInfo> v;
+    std::string err;
+    const int r = vvf::params(cfg, v, err);
+    if (r) return fail(r, "%s", err.c_str());
+    *count = (int)v.size();
+    return 0;
+  }
   Cfg c;
   int r = parse_cfg(cfg, c);
   if (r) return r;
@@ -1163,6 +1174,18 @@ int vv_lgunet_param_count(const vv_lgunet_config* cfg, int* count) {
 
 int vv_lgunet_param_info(const vv_lgunet_config* cfg, int index, char* name, int name_cap, int64_t* shape,
                          int* ndim) {
+  if (cfg && cfg->arch == VV_ARCH_LGUNET1) {
+    std::vector<vvf::ParamInfo> v;
+    std::string err;
+    const int r = vvf::params(cfg, v, err);
+    if (r) return fail(r, "%s", err.c_str());
+    if (index < 0 || index >= (int)v.size()) return fail(VV_E_ARG, "param index %d out of range", index);
+    if (name) snprintf(name, name_cap, "%s", v[index].name.c_str());
+    if (ndim) *ndim = (int)v[index].shape.size();
+    if (shape)
+      for (size_t i = 0; i < v[index].shape.size(); ++i) shape[i] = v[index].shape[i];
+    return 0;
+  }
   Cfg c;
   int r = parse_cfg(cfg, c);
   if (r) return r;
@@ -1217,15 +1240,41 @@ int vv_ctx_destroy(vv_ctx* ctx) {
 }
 
 int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_slots, int* model_id) {
-  if (!ctx || !model_id) return fail(VV_E_ARG, "null argument");
+  if (!ctx || !model_id || !cfg) return fail(VV_E_ARG, "null argument");
   int r = set_dev(ctx);
   if (r) return r;
+  if (cfg->arch == VV_ARCH_LGUNET1) {
+    auto m = std::make_unique<Model>();
+    std::string err;
+    if ((r = vvf::create(cfg, batch, &m->fm, err))) return fail(r, "%s", err.c_str());
+    m->B = batch;
+    m->nslots = 1;
+    m->workspace = vvf::workspace_bytes(m->fm);
+    m->cfg.raw = *cfg;
+    m->cfg.Cin = vvf::in_channels(m->fm);
+    m->cfg.Cout = vvf::out_channels(m->fm);
+    m->cfg.Himg = vvf::img_h(m->fm);
+    m->cfg.Wimg = vvf::img_w(m->fm);
+    ctx->models.push_back(std::move(m));
+    *model_id = (int)ctx->models.size() - 1;
+    return 0;
+  }
+  if (cfg->arch != VV_ARCH_LGUNET) return fail(VV_E_ARG, "unknown arch %d", cfg->arch);
   return create_model(ctx, cfg, batch, n_slots, model_id);
 }
 
 int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
   Model* m = get_model(ctx, model_id);
   if (!m || !ptrs) return fail(VV_E_ARG, "bad model or ptrs");
+  if (m->fm) {
+    int r = set_dev(ctx);
+    if (r) return r;
+    std::string err;
+    if ((r = vvf::load(m->fm, ptrs, n, err))) return fail(r, "%s", err.c_str());
+    drop_graphs(ctx);
+    m->loaded = true;
+    return 0;
+  }
   if (n != (int)m->params.size()) return fail(VV_E_ARG, "expected %zu params, got %d", m->params.size(), n);
   int r = set_dev(ctx);
   if (r) return r;
@@ -1267,6 +1316,11 @@ int vv_model_forward(vv_ctx* ctx, int model_id, int slot, const float* in, float
   if (slot < 0 || slot >= m->nslots) return fail(VV_E_ARG, "slot %d out of range", slot);
   int r = set_dev(ctx);
   if (r) return r;
+  if (m->fm) {
+    std::string err;
+    if ((r = vvf::forward(m->fm, in, out, out_limit, (hipStream_t)stream, err))) return fail(r, "%s", err.c_str());
+    return 0;
+  }
   return model_fwd(*m, slot, in, out, out_limit, (hipStream_t)stream);
 }
 
@@ -1274,6 +1328,7 @@ int vv_model_backward(vv_ctx* ctx, int model_id, int slot, const float* dout, fl
                       int out_limit, void* stream) {
   Model* m = get_model(ctx, model_id);
   if (!m || !dout || !din) return fail(VV_E_ARG, "bad model or pointers");
+  if (m->fm) return fail(VV_E_STATE, "LGUnet_all_1 (forecast model) is forward-only");
   if (!m->loaded) return fail(VV_E_STATE, "weights not loaded");
   if (slot < 0 || slot >= m->nslots) return fail(VV_E_ARG, "slot %d out of range", slot);
   int r = set_dev(ctx);
@@ -1286,6 +1341,8 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
                     const float* std_tr, float obs_coeff) {
   Model* D = get_model(ctx, dec_model_id);
   if (!D) return fail(VV_E_ARG, "bad decoder model");
+  if (D->fm || (flow_model_id >= 0 && get_model(ctx, flow_model_id) && get_model(ctx, flow_model_id)->fm))
+    return fail(VV_E_ARG, "the closure needs differentiable networks_old LGUnet_all models");
   if (T < 1 || C < 1) return fail(VV_E_ARG, "bad T/C");
   drop_graphs(ctx);
   if (D->B != 1) return fail(VV_E_ARG, "closure needs a batch-1 decoder");
@@ -1550,6 +1607,60 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math) {
   if (!ctx || !math) return fail(VV_E_ARG, "null argument");
   *math = vv::gemm_math();
   return 0;
+}
+
+int vv_integrate(vv_ctx* ctx, int model_id, const float* x, float* out, int C, int Hs, int Ws, const float* mean,
+                 const float* std_, int steps, void* stream) {
+  Model* m = get_model(ctx, model_id);
+  if (!m || !x || !out || !mean || !std_) return fail(VV_E_ARG, "bad model or pointers");
+  if (!m->loaded) return fail(VV_E_STATE, "weights not loaded");
+  if (steps < 1) return fail(VV_E_ARG, "steps must be >= 1");
+  const int Hl = m->cfg.Himg, Wl = m->cfg.Wimg;
+  if (m->B != 1 || m->cfg.Cin != C || m->cfg.Cout < C)
+    return fail(VV_E_ARG, "model must map C=%d channels to >= C (has %d -> %d, batch %d)", C, m->cfg.Cin,
+                m->cfg.Cout, m->B);
+  if (C < 1 || Hs < 1 || Ws < 1) return fail(VV_E_ARG, "bad state shape");
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  // nearest maps (quirk Q3) when the state grid differs from the model grid (integrate(interpolation=True))
+  const bool interp = Hs != Hl || Ws != Wl;
+  const size_t nin = (size_t)C * Hl * Wl, nout = (size_t)m->cfg.Cout * Hl * Wl;
+  std::vector<int> maps;
+  if (interp) {
+    for (auto& v : {nearest_map(Hs, Hl), nearest_map(Ws, Wl), nearest_map(Hl, Hs), nearest_map(Wl, Ws)})
+      maps.insert(maps.end(), v.begin(), v.end());
+  }
+  float *a = nullptr, *b = nullptr;
+  int* dm = nullptr;
+  VV_HIP(hipMallocAsync((void**)&a, nin * sizeof(float), st));
+  VV_HIP(hipMallocAsync((void**)&b, nout * sizeof(float), st));
+  if (interp) {
+    VV_HIP(hipMallocAsync((void**)&dm, maps.size() * sizeof(int), st));
+    VV_HIP(hipMemcpyAsync(dm, maps.data(), maps.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  }
+  const int* di = interp ? dm : nullptr;
+  const int* dj = interp ? dm + Hl : nullptr;
+  const int* mi = interp ? dm + Hl + Wl : nullptr;
+  const int* mj = interp ? dm + Hl + Wl + Hs : nullptr;
+  // z = (x - mean)/std (-> model grid); z = model(z)[:, :C] `steps` times (da_4dvar.py:667-676)
+  VV_HIP(vvf::normalize_resample(x, a, di, dj, mean, std_, C, Hs, Ws, Hl, Wl, st));
+  for (int k = 0; k < steps && !r; ++k) {
+    if (m->fm) {
+      std::string err;
+      r = vvf::forward(m->fm, a, b, C, st, err);
+      if (r) fail(r, "%s", err.c_str());
+    } else {
+      r = model_fwd(*m, 0, a, b, C, st);
+    }
+    if (!r && k + 1 < steps) VV_HIP(hipMemcpyAsync(a, b, nin * sizeof(float), hipMemcpyDeviceToDevice, st));
+  }
+  // (-> state grid) * std + mean (:678-681)
+  if (!r) VV_HIP(vvf::denormalize_resample(b, m->cfg.Cout, out, mi, mj, mean, std_, C, Hs, Ws, Hl, Wl, st));
+  (void)hipFreeAsync(a, st);
+  (void)hipFreeAsync(b, st);
+  if (dm) (void)hipFreeAsync(dm, st);
+  return r;
 }
 
 int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K) {

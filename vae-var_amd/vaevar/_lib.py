@@ -33,6 +33,8 @@ class VVConfig(ctypes.Structure):
         ("n_lg_layers", c_int),
         ("lg_depths", c_int * 8),
         ("lg_heads", c_int * 8),
+        ("arch", c_int),
+        ("window_hw", c_int * 2),
     ]
 
     @classmethod
@@ -51,9 +53,13 @@ class VVConfig(ctypes.Structure):
         c.embed_dim = cfg["embed_dim"]
         ws = cfg["window_size"]
         c.window_size = ws if isinstance(ws, int) else int(ws[0])
+        c.arch = {"lgunet": 0, "lgunet1": 1}[cfg.get("arch", "lgunet")]
+        c.window_hw[:] = [ws, ws] if isinstance(ws, int) else [int(ws[0]), int(ws[1])]
         c.n_enc_levels = len(cfg["enc_depths"])
         c.enc_depths[: c.n_enc_levels] = list(cfg["enc_depths"])
         c.enc_heads[: c.n_enc_levels] = list(cfg["enc_heads"])
+        if len(cfg["enc_heads"]) != c.n_enc_levels or len(cfg["lg_heads"]) != len(cfg["lg_depths"]):
+            raise ValueError("enc_heads / lg_heads must match enc_depths / lg_depths in length")
         c.n_lg_layers = len(cfg["lg_depths"])
         c.lg_depths[: c.n_lg_layers] = list(cfg["lg_depths"])
         c.lg_heads[: c.n_lg_layers] = list(cfg["lg_heads"])
@@ -91,6 +97,8 @@ _SIGS = {
     "vv_profile_stop": (c_int, [c_void_p, P(c_double), P(c_double), P(c_double), P(c_int), c_int]),
     "vv_nearest_map": (c_int, [c_int, c_int, P(c_int)]),
     "vv_set_gemm_math": (c_int, [c_void_p, c_int]),
+    "vv_integrate": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                             c_int, c_void_p]),
     "vv_get_gemm_math": (c_int, [c_void_p, P(c_int)]),
     "vv_gemm_register_weight": (c_int, [c_void_p, c_void_p, c_int, c_int]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),

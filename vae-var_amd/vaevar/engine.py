@@ -135,7 +135,8 @@ class _NetFn(torch.autograd.Function):
 
 
 class LGUnet:
-    """networks_old.transformer.LGUnet_all on the HIP engine.
+    """networks_old.transformer.LGUnet_all on the HIP engine, or with cfg["arch"] == "lgunet1" the
+    forecast network networks.LGUnet_all.LGUnet_all_1 (forward only, LGUnet_all.py:742-776).
 
     Weights are the reference's state_dict entries (module./max_logvar filtering as in
     da_4dvar.py:594-601 is applied by `load_state_dict`). Input gradients only (quirk Q5).
@@ -210,6 +211,22 @@ class LGUnet:
     def __call__(self, x: torch.Tensor, slot: int = 0, out_limit: int = 0):
         """Differentiable forward (input gradient). One pending backward per slot."""
         return _NetFn.apply(x, self, slot, out_limit)
+
+
+def integrate(model: LGUnet, x: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, steps: int = 1,
+              out: torch.Tensor = None) -> torch.Tensor:
+    """`cyclic_4dvar.integrate(x, model, steps)` (da_4dvar.py:666-681) on libvaevar (vv_integrate): the
+    outer-cycle forecast x_b = integrate(x_a, forecast_model, 1) (:1329). x: (C, Hs, Ws) on the device; a
+    state grid other than the model grid is nearest-resampled both ways (interpolation=True)."""
+    C, Hs, Ws = x.shape
+    x = x.contiguous()
+    mean = mean.to(x.device, torch.float32).contiguous()
+    std = std.to(x.device, torch.float32).contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib.vv_integrate(model.ctx.h, model.id, _ptr(x), _ptr(out), C, Hs, Ws, _ptr(mean), _ptr(std), steps,
+                           _stream()), "integrate")
+    return out
 
 
 class VAE_lr:
