@@ -39,21 +39,23 @@ def test_fcst_tiny_g7():
     assert e < 1e-5
 
 
-def test_fcst_mid_vs_oracle():
+@pytest.mark.parametrize("name", ["MID_FCST", "BIG_FCST"])
+def test_fcst_mid_vs_oracle(name):
     """Real FCST widths/heads/window on a 97x192 image: head_dim 32/32/64/192, [6,12] windows with the -inf
-    row mask, 288-token global LG window, patch (3,2)/stride 2 conv and overlapping ConvTranspose."""
+    row mask, 288-token global LG window (streaming kernel), patch (3,2)/stride 2 conv and overlapping
+    ConvTranspose; on 193x384 the 1152-token global window runs as split GEMMs + row softmax."""
     from oracle.lgunet1_ref import lgunet1_forward, synth_params
     from vaevar import config as C
     from vaevar.synth import smooth_field
 
-    cfg = C.MID_FCST
+    cfg = getattr(C, name)
     x = smooth_field(702, (1, C.in_channels(cfg)) + tuple(cfg["img_size"]))
     out = _model(cfg).forward_raw(torch.from_numpy(x).cuda())
     torch.set_num_threads(16)
     with torch.no_grad():
         ref = lgunet1_forward(synth_params(cfg), cfg, torch.from_numpy(x))
     e = rel(out.cpu(), ref)
-    print(f"mid LGUnet_all_1 (97x192): out rel {e:.2e}")
+    print(f"{name} LGUnet_all_1 {cfg['img_size']}: out rel {e:.2e}")
     assert e < 1e-4
 
 

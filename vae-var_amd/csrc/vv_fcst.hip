@@ -241,6 +241,93 @@ __global__ void k_convT(ConvArgs a) {
   }
 }
 
+// PatchEmbed as a GEMM: im2col rows [pix][k], k = (ci*kh + ky)*kw + kx, zero-padded to Kp (multiple of 32)
+__global__ void k_im2col(ConvArgs a, float* col0, int Kp, size_t gstride) {
+  const int g = blockIdx.y;
+  const int cin = a.cin[g], kk = a.kh * a.kw, K = cin * kk;
+  const size_t total = (size_t)a.B * a.Ho * a.Wo * Kp;
+  float* col = col0 + g * gstride;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(t % Kp);
+    const size_t pix = t / Kp;
+    float v = 0.f;
+    if (k < K) {
+      const int ci = k / kk, ky = (k % kk) / a.kw, kx = k % a.kw;
+      const int b = (int)(pix / ((size_t)a.Ho * a.Wo));
+      const int p = (int)(pix % ((size_t)a.Ho * a.Wo));
+      const int oy = p / a.Wo, ox = p % a.Wo;
+      v = a.img[(((size_t)b * a.Cimg + a.cin_off[g] + ci) * a.Himg + (size_t)oy * a.sh + ky) * a.Wimg +
+                (size_t)ox * a.sw + kx];
+    }
+    col[t] = v;
+  }
+}
+
+// ConvTranspose2d after the GEMM Y[pix][(co*kh + ky)*kw + kx] = tok[pix] . w[:, co, ky, kx]: col2im gather of
+// the (overlapping) taps + bias, quirk Q2 channel placement
+__global__ void k_col2im(ConvArgs a, const float* Y0, int ldy, size_t gstride) {
+  const int g = blockIdx.z, co = blockIdx.y;
+  const int cout = a.cout[g];
+  if (co >= cout) return;
+  const int oc = co < cout / 2 ? a.mean_off[g] + co : a.std_off[g] + (co - cout / 2);
+  if (a.climit > 0 && oc >= a.climit) return;
+  const float* Y = Y0 + g * gstride;
+  const size_t npix = (size_t)a.B * a.Himg * a.Wimg;
+  const float b0 = a.bias[g][co];
+  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    const int x = (int)(p % a.Wimg);
+    const int y = (int)((p / a.Wimg) % a.Himg);
+    const int b = (int)(p / ((size_t)a.Himg * a.Wimg));
+    float acc = 0.f;
+    for (int ky = 0; ky < a.kh; ++ky) {
+      const int yy = y - ky;
+      if (yy < 0 || yy % a.sh) continue;
+      const int iy = yy / a.sh;
+      if (iy >= a.Ho) continue;
+      for (int kx = 0; kx < a.kw; ++kx) {
+        const int xx = x - kx;
+        if (xx < 0 || xx % a.sw) continue;
+        const int ix = xx / a.sw;
+        if (ix >= a.Wo) continue;
+        acc += Y[(((size_t)b * a.Ho + iy) * a.Wo + ix) * ldy + (co * a.kh + ky) * a.kw + kx];
+      }
+    }
+    a.img_out[(((size_t)b * a.Ctot + oc) * a.Himg + y) * a.Wimg + x] = acc + b0;
+  }
+}
+
+// Global-window attention as GEMMs (LG layer 0, Hg*Wg tokens): V^T per head, zero-padded to Np columns
+__global__ void k_vt(const float* qkv, float* vt, int N, int Np, int C, int heads, int hd) {
+  const size_t total = (size_t)heads * hd * Np;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % Np);
+    const size_t hdrow = t / Np;
+    const int d = (int)(hdrow % hd), h = (int)(hdrow / hd);
+    vt[t] = j < N ? qkv[(size_t)j * 3 * C + 2 * C + h * hd + d] : 0.f;
+  }
+}
+
+// row softmax of S [rows][Np] (first N columns), in place; pad columns set to 0 (they feed the P.V GEMM's K)
+__global__ __launch_bounds__(256) void k_softmax_rows(float* S, int N, int Np) {
+  __shared__ float red[8];
+  float* row = S + (size_t)blockIdx.x * Np;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float mx = -INFINITY;
+  for (int j = tid; j < N; j += 256) mx = fmaxf(mx, row[j]);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) red[wv] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int j = tid; j < N; j += 256) sum += expf(row[j] - mx);
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  __syncthreads();
+  if (lane == 0) red[4 + wv] = sum;
+  __syncthreads();
+  const float inv = 1.f / ((red[4] + red[5]) + (red[6] + red[7]));
+  for (int j = tid; j < Np; j += 256) row[j] = j < N ? expf(row[j] - mx) * inv : 0.f;
+}
+
 __global__ void k_norm_resample(const float* x, float* y, const int* di, const int* dj, const float* mean,
                                 const float* sd, int C, int Hs, int Ws, int Hl, int Wl) {
   const size_t n = (size_t)C * Hl * Wl;
@@ -461,6 +548,10 @@ std::vector<int> window_map(int B, int H, int W, int wh, int ww, int sh, int sw)
 
 }  // namespace
 
+// windows of at least this many tokens (the global LG window at 0.25 degree: 16,200) run as two split GEMMs
+// (S = Q K^T, O = softmax(S) V) instead of the streaming kernel
+constexpr int kGemmAttnMin = 1024;
+
 struct FBlock {
   const float *n1g, *n1b, *qkvW, *qkvb, *projW, *projb, *n2g, *n2b, *fc1W, *fc1b, *fc2W, *fc2b;
 };
@@ -490,6 +581,15 @@ struct FModel {
   std::vector<void*> owned;
   int64_t bytes = 0;
   bool loaded = false;
+  // PatchEmbed / ConvTranspose2d as GEMMs: per tower the conv weight [C0][Kp] (zero-padded K) and the transposed
+  // ConvTranspose weight [NT][C0] (rows (co*kh+ky)*kw+kx, zero rows up to the widest tower)
+  float* convw = nullptr;
+  unsigned short* convp = nullptr;
+  size_t conv_floats = 0;
+  std::vector<float*> Wp, W2;
+  int Kp = 0, NT = 0;
+  // global-window attention through the split GEMM when the window is large: S/P [heads][N][Np], V^T [heads][hd][Np]
+  float *att_s = nullptr, *att_vt = nullptr;
 };
 
 namespace {
@@ -653,8 +753,10 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     ra.c2 = S.c2;
     ra.s2 = S.s2;
     ra.scale = (float)std::pow((double)S.hd, -0.5);
+    int ph = prof_begin(st);
     hipLaunchKernelGGL(k_rope, dim3(grid_for((size_t)M * S.heads * (S.hd / 2)), G), dim3(256), 0, st, ra);
     FH(hipGetLastError());
+    prof_end(ph, st, PC_ATTN, 6.0 * G * M * C, 16.0 * G * M * C);
     FlashArgs fa;
     memset(&fa, 0, sizeof(fa));
     for (int g = 0; g < G; ++g) {
@@ -671,7 +773,38 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     fa.sh = sh;
     fa.nWh = S.H / S.wh;
     fa.nWw = S.W / S.ww;
-    FH(flash(fa, S.hd, nwin, G, st));
+    if (S.global && N >= kGemmAttnMin && m.att_s && G == 1) {
+      // S_h = Q_h K_h^T (heads as GEMM groups; q rotated + scaled, k rotated), P = softmax_rows(S), O_h = P V_h
+      const int Np = (N + 31) / 32 * 32, hd = S.hd;
+      for (int b0 = 0; b0 < nwin; ++b0) {
+        const float* qkv = m.qkv + (size_t)b0 * N * 3 * C;
+        GemmArgs sq = gbase(N, N, hd, S.heads, EPI_STORE);
+        sq.lda = 3 * C;
+        sq.ldb = 3 * C;
+        sq.ldc = Np;
+        for (int hh = 0; hh < S.heads; ++hh)
+          sq.g[hh] = {qkv + hh * hd, nullptr, qkv + C + hh * hd, nullptr, m.att_s + (size_t)hh * N * Np, nullptr,
+                      nullptr};
+        FH(gemm_nt(sq, st, -1, nullptr));
+        ph = prof_begin(st);
+        hipLaunchKernelGGL(k_softmax_rows, dim3(S.heads * N), dim3(256), 0, st, m.att_s, N, Np);
+        FH(hipGetLastError());
+        hipLaunchKernelGGL(k_vt, dim3(grid_for((size_t)C * Np)), dim3(256), 0, st, qkv, m.att_vt, N, Np, C, S.heads,
+                           hd);
+        FH(hipGetLastError());
+        prof_end(ph, st, PC_ATTN, 4.0 * S.heads * N * (double)Np, 12.0 * S.heads * N * (double)Np);
+        GemmArgs pv = gbase(N, hd, Np, S.heads, EPI_STORE);
+        pv.ldc = C;
+        for (int hh = 0; hh < S.heads; ++hh)
+          pv.g[hh] = {m.att_s + (size_t)hh * N * Np, nullptr, m.att_vt + (size_t)hh * hd * Np, nullptr,
+                      m.t2 + (size_t)b0 * N * C + hh * hd, nullptr, nullptr};
+        FH(gemm_nt(pv, st, -1, nullptr));
+      }
+    } else {
+      ph = prof_begin(st);
+      FH(flash(fa, S.hd, nwin, G, st));
+      prof_end(ph, st, PC_ATTN, 4.0 * G * (double)M * N * C, 16.0 * G * (double)M * C);
+    }
     // proj + window reverse / roll back + residual, in place
     GemmArgs p = gbase(M, C, C, G, EPI_RESID);
     p.crow = idx;
@@ -708,6 +841,7 @@ int params(const vv_lgunet_config* cfg, std::vector<ParamInfo>& out, std::string
 void destroy(FModel* m) {
   if (!m) return;
   if (m->warena) unregister_split_arena(m->warena);
+  if (m->convw) unregister_split_arena(m->convw);
   for (void* p : m->owned) (void)hipFree(p);
   delete m;
 }
@@ -762,6 +896,31 @@ int create(const vv_lgunet_config* cfg, int batch, FModel** out, std::string& er
       (r = dalloc(*m, S[0], &m->yn, err)) || (r = dalloc(*m, Mg * c.E, &m->lgx, err)) ||
       (r = dalloc(*m, gemm_ws_floats(), &m->ws, err)))
     return bail(r);
+  {
+    int kmax = 0, nmax = 0;
+    for (int g = 0; g < G; ++g) {
+      kmax = std::max(kmax, c.raw.inchans[g] * c.kh * c.kw);
+      nmax = std::max(nmax, c.raw.outchans[g] * c.kh * c.kw);
+    }
+    m->Kp = (kmax + 31) / 32 * 32;
+    m->NT = nmax;
+    const size_t per = (size_t)c.Cl[0] * m->Kp + (size_t)m->NT * c.Cl[0];
+    m->conv_floats = per * G;
+    if ((r = dalloc(*m, m->conv_floats, &m->convw, err))) return bail(r);
+    void* cp = nullptr;
+    if (hipMalloc(&cp, m->conv_floats * 3 * sizeof(unsigned short)) != hipSuccess)
+      return bail(ferr(err, VV_E_ALLOC, "conv split planes"));
+    m->owned.push_back(cp);
+    m->convp = reinterpret_cast<unsigned short*>(cp);
+    register_split_arena(m->convw, m->conv_floats, m->convp);
+    for (int g = 0; g < G; ++g) {
+      m->Wp.push_back(m->convw + g * per);
+      m->W2.push_back(m->convw + g * per + (size_t)c.Cl[0] * m->Kp);
+    }
+    // im2col rows and the ConvTranspose GEMM output live in the MLP scratch (4 x the widest level)
+    if ((size_t)B * c.Hl[0] * c.Wl[0] * std::max(m->Kp, m->NT) * G > 4 * smax)
+      return bail(ferr(err, VV_E_ARG, "conv GEMM scratch too small"));
+  }
   m->enc.resize(L);
   m->dec.resize(L);
   for (int l = 0; l < L; ++l) {
@@ -775,6 +934,14 @@ int create(const vv_lgunet_config* cfg, int batch, FModel** out, std::string& er
   for (size_t li = 0; li < m->lg.size(); ++li)
     if ((r = init_stage(*m, m->lg[li], 1, c.Hg, c.Wg, c.E, c.lg_heads[li], c.lg_depth[li], li == 0, m->lgx, err)))
       return bail(r);
+  {
+    const size_t N = (size_t)c.Hg * c.Wg, Np = (N + 31) / 32 * 32;
+    if (N >= (size_t)kGemmAttnMin) {
+      const int hmax = *std::max_element(c.lg_heads.begin(), c.lg_heads.end());
+      if ((r = dalloc(*m, (size_t)hmax * N * Np, &m->att_s, err)) || (r = dalloc(*m, (size_t)c.E * Np, &m->att_vt, err)))
+        return bail(r);
+    }
+  }
   *out = m;
   return 0;
 }
@@ -792,6 +959,34 @@ int load(FModel* m, const void* const* ptrs, int n, std::string& err) {
   }
   FH(hipDeviceSynchronize());
   const FCfg& c = m->c;
+  {
+    const int C0 = c.Cl[0], kk = c.kh * c.kw;
+    std::vector<float> host;
+    for (int g = 0; g < c.G; ++g) {
+      // conv: [C0][cin][kh][kw] -> [C0][Kp]
+      const int cin = c.raw.inchans[g];
+      host.resize((size_t)C0 * cin * kk);
+      FH(hipMemcpy(host.data(), m->W.at("enc.enc_list." + std::to_string(g) + ".patch_embed.proj.weight"),
+                   host.size() * 4, hipMemcpyDeviceToHost));
+      std::vector<float> wp((size_t)C0 * m->Kp, 0.f);
+      for (int co = 0; co < C0; ++co)
+        for (int k = 0; k < cin * kk; ++k) wp[(size_t)co * m->Kp + k] = host[(size_t)co * cin * kk + k];
+      FH(hipMemcpy(m->Wp[g], wp.data(), wp.size() * 4, hipMemcpyHostToDevice));
+      // convT: [C0][cout][kh][kw] -> [(co*kh+ky)*kw+kx][C0], zero rows up to NT
+      const int cout = c.raw.outchans[g];
+      host.resize((size_t)C0 * cout * kk);
+      FH(hipMemcpy(host.data(), m->W.at("dec.final_proj_list." + std::to_string(g) + ".weight"), host.size() * 4,
+                   hipMemcpyDeviceToHost));
+      std::vector<float> w2((size_t)m->NT * C0, 0.f);
+      for (int ci = 0; ci < C0; ++ci)
+        for (int j = 0; j < cout * kk; ++j) w2[(size_t)j * C0 + ci] = host[(size_t)ci * cout * kk + j];
+      FH(hipMemcpy(m->W2[g], w2.data(), w2.size() * 4, hipMemcpyHostToDevice));
+      // split planes (rows of K = Kp for Wp, C0 for W2)
+      FH(split_planes(m->Wp[g], m->convp + 3 * (size_t)(m->Wp[g] - m->convw), (size_t)C0 * m->Kp, m->Kp, 0));
+      FH(split_planes(m->W2[g], m->convp + 3 * (size_t)(m->W2[g] - m->convw), (size_t)m->NT * C0, C0, 0));
+    }
+    FH(hipDeviceSynchronize());
+  }
   for (int g = 0; g < c.G; ++g) {
     const std::string e = "enc.enc_list." + std::to_string(g), d = "dec.dec_list." + std::to_string(g);
     for (int l = 0; l < c.L; ++l) {
@@ -847,8 +1042,18 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     pa.cin_off[g] = off;
     pa.cin[g] = c.raw.inchans[g];
   }
-  hipLaunchKernelGGL(k_conv_patch, dim3(grid_for(S[0]), G), dim3(256), 0, st, pa);
+  // PatchEmbed = im2col + GEMM (+bias, +absolute_pos_embed in the epilogue)
+  const size_t colg = (size_t)M[0] * m->Kp;
+  int ph = prof_begin(st);
+  hipLaunchKernelGGL(k_im2col, dim3(grid_for(colg), G), dim3(256), 0, st, pa, m->h, m->Kp, colg);
   FH(hipGetLastError());
+  prof_end(ph, st, PC_PATCH, 0.0, 8.0 * G * colg);
+  GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID);
+  pe.rmod = c.Hl[0] * c.Wl[0];
+  pe.ldr = c.Cl[0];
+  for (int g = 0; g < G; ++g)
+    pe.g[g] = {m->h + g * colg, nullptr, m->Wp[g], pa.bias[g], pa.tok[g], pa.pos[g], nullptr};
+  FH(gemm_nt(pe, st, -1, m->ws));
   for (int l = 0; l < L; ++l) {
     if (l > 0) {
       // PatchMerging (LGUnet_all.py:77-96): gather + LN(4C) + reduction, BEFORE the blocks (:236-246)
@@ -957,8 +1162,16 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     so += co - co / 2;
     maxc = std::max(maxc, co);
   }
-  hipLaunchKernelGGL(k_convT, dim3(grid_for((size_t)B * c.Himg * c.Wimg), maxc, G), dim3(256), 0, st, pu);
+  // ConvTranspose2d = GEMM (tokens x transposed weight) + col2im of the overlapping taps
+  const size_t yg = (size_t)M[0] * m->NT;
+  GemmArgs ct = gbase(M[0], m->NT, c.Cl[0], G, EPI_STORE);
+  for (int g = 0; g < G; ++g) ct.g[g] = {pu.tok[g], nullptr, m->W2[g], nullptr, m->h + g * yg, nullptr, nullptr};
+  FH(gemm_nt(ct, st, -1, m->ws));
+  ph = prof_begin(st);
+  hipLaunchKernelGGL(k_col2im, dim3(grid_for((size_t)B * c.Himg * c.Wimg), maxc, G), dim3(256), 0, st, pu, m->h,
+                     m->NT, yg);
   FH(hipGetLastError());
+  prof_end(ph, st, PC_PATCH, 0.0, 4.0 * G * (yg + (size_t)c.Cout * c.Himg * c.Wimg / G));
   return 0;
 }
 

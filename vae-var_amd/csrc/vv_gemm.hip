@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int n = min(n0 + lr + RPP * i, N - 1);
-    bp[i] = G.B + (size_t)n * K + lc;
+    bp[i] = G.B + (size_t)n * (args.ldb ? args.ldb : K) + lc;
   }
 
   // register staging sets (named, statically indexed): DEPTH 1 = tile t+1 in flight during tile t,
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int n = min(n0 + lr + RPP * i, N - 1);
-      bp[i] = G.B + (size_t)n * K + lc;
+      bp[i] = G.B + (size_t)n * (args.ldb ? args.ldb : K) + lc;
     }
   }
   const size_t ps = K;  // planes of one B row: [h | m | l] x K
@@ -844,7 +844,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   GemmArgs a = a_in;
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
-  if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3)) return hipErrorInvalidValue;
+  if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
   if (t < 0 || t > 33) return hipErrorInvalidValue;
   // data-parallel rounds of whole tiles + the remaining tiles split along K over the idle CUs
@@ -858,7 +858,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   a.tsplit = 1;
   a.ws = ws;
   for (int g = 0; g < a.ngroups; ++g) {
-    a.g[g].Bp = t >= 21 ? split_planes_of(a.g[g].B) : nullptr;
+    a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     a.g[g].Ap = (t >= 21 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_of(a.g[g].A) : a.g[g].Ap;
   }
   if (ws && a.ngroups == 1) {

@@ -36,6 +36,7 @@ struct GemmGroup {
 struct GemmArgs {
   int M, N, K, ksplit;
   int lda, lda2, ldc, ldr, ldaux;
+  int ldb;  // row stride of B (0 = K); a registered weight (split planes) is always contiguous
   int rmod;
   const int* arow;
   const int* crow;
