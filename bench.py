@@ -185,7 +185,10 @@ def main():
                                         "exact f32 MFMA (v_mfma_f32_32x32x2_f32; peak 157.3 TF)",
                            "frac_of_f32_mfma_peak": ach / PEAK_F32_TFLOPS,
                            "launches": g["launches"], "avg_launch_us": 1e3 * g["ms"] / max(g["launches"], 1),
-                           "flops_per_launch": g["flops"] / max(g["launches"], 1)}
+                           "flops_per_launch": g["flops"] / max(g["launches"], 1),
+                           "algorithmic_bytes_per_launch": g["bytes"] / max(g["launches"], 1),
+                           "traffic_source": "profiles/r01/gemm_traffic.json: rocprofv3 --pmc FETCH_SIZE / "
+                                             "WRITE_SIZE passes of bench.py (tools/pmc_traffic.py)"}
         busy = sum(v["ms"] for v in pr.values())
         out["kernel_time_ms"] = {k: round(v["ms"], 3) for k, v in pr.items()}
         out["kernel_launches"] = {k: v["launches"] for k, v in pr.items()}

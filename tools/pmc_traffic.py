@@ -18,10 +18,11 @@ def per_kernel(path, counter):
 
 f = per_kernel(sys.argv[1], "FETCH_SIZE")
 w = per_kernel(sys.argv[2], "WRITE_SIZE")
-gf = [v for n, v in f.values() if "k_gemm_nt" in n]
-gw = [v for n, v in w.values() if "k_gemm_nt" in n]
+KEY = ("k_gemm_nt", "k_gemm_bs")
+gf = [v for n, v in f.values() if any(k in n for k in KEY)]
+gw = [v for n, v in w.values() if any(k in n for k in KEY)]
 out = {
-    "kernel": "k_gemm_nt",
+    "kernel": "k_gemm_bs / k_gemm_nt (every GEMM main-kernel launch)",
     "launches_fetch": len(gf), "launches_write": len(gw),
     "fetch_bytes_per_launch_raw": 1024 * statistics.mean(gf),
     "fetch_bytes_per_launch": 2 * 1024 * statistics.mean(gf),
