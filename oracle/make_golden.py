@@ -13,6 +13,8 @@ are stored):
   g4_nearest_maps.npz   G4: nearest index maps of F.interpolate 721<->128, 1440<->256
   g5_tiny_lbfgs.npz     G5: restated vae4dvar loop on the tiny decoder (Nit=2): J per outer pass, xa
   g5b_tiny_4dvar.npz    tiny decoder + tiny flow, T=2: J terms and dJ/dz of one closure
+  g6_one_step_da_c5.npz G6 (--g6, ~5 min): the genuine cyclic_4dvar.one_step_DA(..., 'vae4dvar') at 721x1440, T=2,
+                        Nit=1 (config 5): printed J per outer pass, sampled xa + sums
   g7_tiny_lgunet1.npz   G7: tiny networks.LGUnet_all_1 (RoPE, -inf mask, global LG window, 3 levels): out
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
                         and one config-2 closure (J_b, J_o, sampled dJ/dz)
@@ -238,10 +240,73 @@ def g7():
     np.savez(os.path.join(GOLD, "g7_tiny_lgunet1.npz"), out=y.numpy())
 
 
+def g6(tr):
+    """G6: run the reference's own one_step_DA vae4dvar branch (da_4dvar.py:1179-1306) on CPU at 721x1440 with
+    T=2 (flow stand-in), Nit=1, synthetic weights and the make_problem(seed=20250620) inputs (SURVEY §8 c2 iv:
+    object.__new__ + attributes, device 'cuda' rewritten to 'cpu')."""
+    import contextlib
+    import importlib
+    import io
+    import re
+
+    from torch.overrides import TorchFunctionMode
+
+    class CPUMode(TorchFunctionMode):
+        def __torch_function__(self, func, types, args=(), kwargs=None):
+            kwargs = dict(kwargs or {})
+            if "device" in kwargs and kwargs["device"] is not None and str(kwargs["device"]).startswith("cuda"):
+                kwargs["device"] = "cpu"
+            return func(*args, **kwargs)
+
+    cwd = os.getcwd()
+    os.chdir(ref_harness.REF)
+    da = importlib.import_module("da_4dvar")
+    metrics = importlib.import_module("utils.metrics")
+    vae_mod = importlib.import_module("nf_model.vae")
+    vae = vae_mod.VAE_lr("parameters0_old")
+    os.chdir(cwd)
+    dec_p = synth_params(C.DECODER)
+    missing, unexpected = vae.dec.load_state_dict(dec_p, strict=False)
+    assert not unexpected and all(k.endswith(("relative_position_index", "attn_mask")) for k in missing)
+    flow_cfg = {k: v for k, v in C.FLOW.items() if k != "arch"}
+    flow = tr.LGUnet_all(rank=0, **flow_cfg)
+    missing, unexpected = flow.load_state_dict(synth_params(C.FLOW), strict=False)
+    assert not unexpected and all(k.endswith(("relative_position_index", "attn_mask")) for k in missing)
+    a = object.__new__(da.cyclic_4dvar)
+    a.device = "cpu"
+    a.da_win, a.obs_type, a.obs_coeff, a.Nit, a.use_eval = 2, "synthetic", 1.0, 1, False
+    a.nchannel, a.nlev, a.nlat, a.nlon, a.current_time = 69, 13, 721, 1440, "G6"
+    a.metric = metrics.Metrics()
+    a.metrics_list = {"bg_wrmse": [], "bg_bias": [], "ana_wrmse": [], "ana_bias": []}
+    a.model_mean, a.model_std, a.model_mean_gpu, a.model_std_gpu = a.get_model_mean_std()
+    a.vae, a.flow_model = vae, flow
+    prob = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250620)
+    t = lambda k: torch.from_numpy(prob[k])
+    old_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *args, **kw: self
+    buf = io.StringIO()
+    t0 = time.time()
+    try:
+        with CPUMode(), contextlib.redirect_stdout(buf):
+            xa = a.one_step_DA(t("gt"), t("xb"), t("yo"), t("H"), t("R"), "vae4dvar")
+    finally:
+        torch.Tensor.cuda = old_cuda
+    log = buf.getvalue()
+    J = [(float(m.group(1)), float(m.group(2))) for m in re.finditer(r"loss reg: ([-0-9.e+]+) loss obs: ([-0-9.e+]+)", log)]
+    xa = xa.detach().numpy().astype(np.float32)
+    idx = sample_idx(xa.size, 8192, 606)
+    flat = xa.reshape(-1).astype(np.float64)
+    print(f"G6 one_step_DA 721x1440 T=2 Nit=1: {time.time() - t0:.0f}s, J per pass {J}")
+    np.savez(os.path.join(GOLD, "g6_one_step_da_c5.npz"), J=np.array(J), idx_xa=idx, xa_sample=xa.reshape(-1)[idx],
+             xa_sum=flat.sum(), xa_sumsq=(flat * flat).sum(),
+             dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also generate G3 (full decoder, ~1 min)")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--g6", action="store_true", help="also generate G6 (genuine one_step_DA at 721x1440, ~5 min)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.set_num_threads(8)
@@ -252,6 +317,8 @@ def main():
              "g7": g7}
     if a.full:
         steps["g3"] = lambda: g3(tr)
+    if a.g6:
+        steps["g6"] = lambda: g6(tr)
     for k, f in steps.items():
         if a.only and k not in a.only.split(","):
             continue

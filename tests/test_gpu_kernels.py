@@ -57,6 +57,29 @@ def test_gemm_split_accuracy(ctx, M, N, K):
         assert es < 1e-6 and es < 1.5 * e32, (t, es, e32)
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 1152, 4608), (300, 200, 96), (4096, 384, 1152),
+                                   (2048, 3456, 1152)])
+def test_gemm_pipelined_registered(ctx, M, N, K):
+    """Pipelined 128x128 split kernel (tile 34) on a registered weight (pre-split planes), incl. ragged edges and
+    the split-K tail: same fp32-level error bound as the other variants."""
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) * 0.03
+    ref = A.double() @ B.double().t()
+    scale = A.double().abs() @ B.double().abs().t()
+    Bd = B.cuda()
+    ctx.gemm_register_weight(Bd)
+    for t in (35, 34, 31, 24):
+        C = ctx.gemm(A.cuda(), Bd, tile=t).cpu().double()
+        es = float(((C - ref).abs() / scale).max())
+        print(f"registered gemm {M}x{N}x{K} t{t}: {es:.2e}")
+        assert es < 1e-6, (t, es)
+    _keep.append(Bd)   # a registered weight must stay alive while the context lives
+
+
+_keep = []
+
+
 def test_gemm_math_switch(ctx):
     assert ctx.gemm_math in ("split", "f32")
     old = ctx.gemm_math

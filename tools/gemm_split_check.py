@@ -9,6 +9,7 @@ ctx = Context.get(0)
 tiles = [int(t) for t in os.environ.get("TILES", "2,21,22,23,24,25,26").split(",")]
 shapes = [tuple(int(x) for x in sh.split("x")) for sh in os.environ["SHAPES"].split(",")] if os.environ.get("SHAPES") else [(2048, 4608, 1152), (2048, 1152, 4608), (2048, 3456, 1152), (2048, 1152, 1152), (2048, 1024, 4608),
           (8192, 288, 96), (8192, 96, 384), (2048, 576, 192), (49152, 384, 96), (49152, 96, 384)]
+keep = []   # registered operands must stay alive while the context lives
 for (M, N, K) in shapes:
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     A = torch.randn(M, K, device="cuda", generator=g)
@@ -17,6 +18,7 @@ for (M, N, K) in shapes:
         ctx.gemm_register_weight(B)
     if os.environ.get("APRE"):
         ctx.gemm_register_weight(A)
+    keep += [A, B]
     ref = A.double() @ B.double().t()
     scale = (A.double().abs() @ B.double().abs().t())
     row = {"M": M, "N": N, "K": K}

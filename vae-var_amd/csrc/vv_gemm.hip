@@ -13,6 +13,7 @@
 #include "vv_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace vv {
 
@@ -318,6 +319,41 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup(GemmArgs args) {
     epilogue<BM, BN, WM, WN, EPI, MF, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
   else
     epilogue<BM, BN, WM, WN, EPI, MF, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+}
+
+// Split-K tail fixup, one workgroup per (tail tile, 32x32 sub-block (a, b)): each thread sums the S chunk
+// partials of its 16 accumulator registers of that sub-block in chunk order (deterministic) and runs the
+// epilogue on them; TM*TN times the parallelism of k_gemm_fixup for tiles with several sub-blocks per wave.
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup_sub(GemmArgs args) {
+  constexpr int NT = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32, NREG = TM * TN * 16;
+  typedef float accv __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int S = args.tsplit;
+  const int tile = args.tdp + blockIdx.x;
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb);
+  const int a = blockIdx.y / TN, b = blockIdx.y % TN;
+  const int wm = wave / WN, wn = wave % WN;
+  const size_t items = (size_t)gridDim.x * S;
+  const float* w = args.ws + ((size_t)blockIdx.z * items + (size_t)blockIdx.x * S) * (size_t)(NREG * NT);
+  accv acc[1][1];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const size_t j = (size_t)((a * TN + b) * 16 + r) * NT + tid;
+    float v = w[j];
+    for (int c = 1; c < S; ++c) v += w[(size_t)c * NREG * NT + j];
+    acc[0][0][r] = v;
+  }
+  const int m0 = mb * BM + wm * TM * 32 + a * 32, n0 = nb * BN + wn * TN * 32 + b * 32;
+  const int rin = lane & 31, hh = lane >> 5;
+  if (m0 + 32 <= M && n0 + 32 <= N)
+    epilogue<32, 32, 1, 1, EPI, 32, true>(args, G, acc, m0, n0, 0, 0, rin, hh);
+  else
+    epilogue<32, 32, 1, 1, EPI, 32, false>(args, G, acc, m0, n0, 0, 0, rin, hh);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -664,8 +700,8 @@ static hipError_t launch_bs_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   }
   hipLaunchKernelGGL((k_gemm_bs<BM, BN, WM, WN, EPI, BPRE, DEPTH, NBUF, APRE>), grid, dim3(64 * WM * WN), lds, s, a);
   if (tail)
-    hipLaunchKernelGGL((k_gemm_fixup<BM, BN, WM, WN, EPI, 32, true>), dim3(tail, 1, a.ngroups), dim3(64 * WM * WN),
-                       0, s, a);
+    hipLaunchKernelGGL((k_gemm_fixup_sub<BM, BN, WM, WN, EPI>),
+                       dim3(tail, (BM / WM / 32) * (BN / WN / 32), a.ngroups), dim3(64 * WM * WN), 0, s, a);
   return hipGetLastError();
 }
 
@@ -731,6 +767,505 @@ static hipError_t launch_tile(const GemmArgs& a, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Pipelined split GEMM: 128x128x32 tile, 4 waves of 64x64, two LDS buffers, ONE barrier per k-tile.
+// Iteration kt reads all fragments of tile kt from buf[kt&1] and, while its 48 MFMAs run, splits tile kt+1
+// (already in registers since iteration kt-1) into buf[(kt+1)&1] and issues the global loads of tile kt+2;
+// sched_group_barrier interleaves the split VALU, the LDS writes and the loads between the MFMAs so the matrix
+// pipe is never waiting for the staging (k_gemm_bs serialises them: split, barrier, MFMAs, barrier).
+template <int EPI, bool APRE>
+__global__ __launch_bounds__(256, 1) void k_gemm_bs2(GemmArgs args) {
+  constexpr int BM = 128, BN = 128, BK = 32, NT = 256, WN = 2, TM = 2, TN = 2;
+  constexpr int LSB = BK, PLANE = (BM + BN) * LSB;
+  constexpr int TPR = BK / 4, RPP = NT / TPR;   // fp32 A staging: 8 threads per row, 32 rows per pass
+  constexpr int AI = APRE ? 1 : BM / RPP;       // 4
+  constexpr int AQ = BM * 4 / NT;               // 2 (16-B chunks per thread per plane)
+  constexpr int BQ = BN * 4 / NT;               // 2
+  typedef float accv __attribute__((ext_vector_type(16)));
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N, K = args.K, ksplit = args.ksplit;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nkt = K / BK;
+  int tile, kb = 0, ke = nkt, part = -1;
+  if (args.tsplit <= 1) {
+    tile = xcd_remap(blockIdx.x, ntm * ntn);
+  } else if ((int)blockIdx.x < args.tdp) {
+    tile = xcd_remap(blockIdx.x, args.tdp);
+  } else {
+    part = blockIdx.x - args.tdp;
+    const int S = args.tsplit, c = part % S;
+    tile = args.tdp + part / S;
+    kb = (c * nkt) / S;
+    ke = ((c + 1) * nkt) / S;
+  }
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lr = tid / TPR, lc = (tid % TPR) * 4;
+  auto swz = [](int row, int k) { return row * LSB + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); };
+
+  const float* a1p[AI];
+  const float* a2p[AI];
+  const unsigned short* aq[AQ];
+  if constexpr (APRE) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int c = tid + NT * i;
+      const int r = min(m0 + c / 4, M - 1);
+      const int ar = args.arow ? args.arow[r] : r;
+      aq[i] = G.Ap + (size_t)ar * 3 * args.lda + (c % 4) * 8;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int r = min(m0 + lr + RPP * i, M - 1);
+      const int ar = args.arow ? args.arow[r] : r;
+      a1p[i] = G.A + (size_t)ar * args.lda + lc;
+      a2p[i] = G.A2 ? G.A2 + (size_t)r * args.lda2 + lc - ksplit : a1p[i];
+    }
+  }
+  const unsigned short* bq[BQ];
+#pragma unroll
+  for (int i = 0; i < BQ; ++i) {
+    const int c = tid + NT * i;
+    const int n = min(n0 + c / 4, N - 1);
+    bq[i] = G.Bp + (size_t)n * 3 * K + (c % 4) * 8;
+  }
+
+  f4 ra[AI];
+  u4v qa[AQ][3], rq[BQ][3];
+  auto gload = [&](int k0) {
+    if constexpr (APRE) {
+#pragma unroll
+      for (int i = 0; i < AQ; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) qa[i][p] = *reinterpret_cast<const u4v*>(aq[i] + p * args.lda + k0);
+    } else if (k0 < ksplit) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) ra[i] = *reinterpret_cast<const f4*>(a1p[i] + k0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) ra[i] = *reinterpret_cast<const f4*>(a2p[i] + k0);
+    }
+#pragma unroll
+    for (int i = 0; i < BQ; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) rq[i][p] = *reinterpret_cast<const u4v*>(bq[i] + p * K + k0);
+  };
+  auto sstore = [&](int buf) {
+    unsigned short* P = lds16 + buf * 3 * PLANE;
+    if constexpr (APRE) {
+#pragma unroll
+      for (int i = 0; i < AQ; ++i) {
+        const int c = tid + NT * i;
+        const int o = swz(c / 4, (c % 4) * 8);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<u4v*>(P + p * PLANE + o) = qa[i][p];
+      }
+    } else {
+      u2v h, m, l;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        split3t(ra[i], h, m, l);
+        const int o = swz(lr + RPP * i, lc);
+        *reinterpret_cast<u2v*>(P + o) = h;
+        *reinterpret_cast<u2v*>(P + PLANE + o) = m;
+        *reinterpret_cast<u2v*>(P + 2 * PLANE + o) = l;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BQ; ++i) {
+      const int c = tid + NT * i;
+      const int o = swz(BM + c / 4, (c % 4) * 8);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u4v*>(P + p * PLANE + o) = rq[i][p];
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int rin = lane & 31, hh = lane >> 5;
+  accv acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  const int nk = ke - kb;
+  gload(kb * BK);
+  sstore(0);
+  if (nk > 1) gload((kb + 1) * BK);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned short* P = lds16 + (kt & 1) * 3 * PLANE;
+    const unsigned short* As = P + (wm * TM * 32 + rin) * LSB;
+    const unsigned short* Bs = P + (BM + wn * TN * 32 + rin) * LSB;
+    bf8v fa[2][TM][3], fb[2][TN][3];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ck = ((2 * s + hh) ^ ((rin >> 2) & 3)) * 8;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fa[s][a][p] = *reinterpret_cast<const bf8v*>(As + p * PLANE + a * 32 * LSB + ck);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[s][b][p] = *reinterpret_cast<const bf8v*>(Bs + p * PLANE + b * 32 * LSB + ck);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 48 MFMA slots, each followed by a small, fixed piece of the staging work (source order is kept by
+    // sched_barrier): slots 0-15 split one element of tile kt+1's A chunk, 16-19 pack + write a chunk's planes,
+    // 20-25 write the B planes, 26-35 issue tile kt+2's global loads. Branch-free: on the last two iterations
+    // the staging re-reads the last k-tile and writes a buffer nobody reads again.
+    unsigned short* Pn = lds16 + ((kt + 1) & 1) * 3 * PLANE;
+    const int k2 = min(kb + kt + 2, ke - 1) * BK;
+    unsigned xb[AI][4], mbv[AI][4], lbv[AI][4];
+#pragma unroll
+    for (int i = 0; i < 48; ++i) {
+      // MFMA i: step s, product p (smallest first), chain (a, b) fastest -> consecutive MFMAs independent
+      const int st = i / 24, pr = (i % 24) / 4, a = (i % 4) / 2, b = i % 2;
+      const bf8v& xa = fa[st][a][pr == 0 ? 2 : pr == 1 ? 0 : pr == 2 ? 1 : pr == 3 ? 1 : 0];
+      const bf8v& xbv = fb[st][b][pr == 0 ? 0 : pr == 1 ? 2 : pr == 2 ? 1 : pr == 3 ? 0 : pr == 4 ? 1 : 0];
+      const bf8v& xa2 = (pr == 4 || pr == 5) ? fa[st][a][0] : xa;
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa2, xbv, acc[a][b], 0, 0, 0);
+      if constexpr (!APRE) {
+        if (i < 16) {
+          const int c = i / 4, e = i % 4;
+          const unsigned xv = __float_as_uint(ra[c][e]);
+          const float r1 = ra[c][e] - __uint_as_float(xv & 0xffff0000u);
+          xb[c][e] = xv;
+          mbv[c][e] = __float_as_uint(r1);
+          lbv[c][e] = __float_as_uint(r1 - __uint_as_float(mbv[c][e] & 0xffff0000u));
+        } else if (i < 20) {
+          const int c = i - 16;
+          u2v h, m, l;
+          h[0] = __builtin_amdgcn_perm(xb[c][1], xb[c][0], 0x07060302u);
+          h[1] = __builtin_amdgcn_perm(xb[c][3], xb[c][2], 0x07060302u);
+          m[0] = __builtin_amdgcn_perm(mbv[c][1], mbv[c][0], 0x07060302u);
+          m[1] = __builtin_amdgcn_perm(mbv[c][3], mbv[c][2], 0x07060302u);
+          l[0] = __builtin_amdgcn_perm(lbv[c][1], lbv[c][0], 0x07060302u);
+          l[1] = __builtin_amdgcn_perm(lbv[c][3], lbv[c][2], 0x07060302u);
+          const int o = swz(lr + RPP * c, lc);
+          *reinterpret_cast<u2v*>(Pn + o) = h;
+          *reinterpret_cast<u2v*>(Pn + PLANE + o) = m;
+          *reinterpret_cast<u2v*>(Pn + 2 * PLANE + o) = l;
+        }
+      } else {
+        if (i < 6) {
+          const int c = tid + NT * (i / 3);
+          *reinterpret_cast<u4v*>(Pn + (i % 3) * PLANE + swz(c / 4, (c % 4) * 8)) = qa[i / 3][i % 3];
+        }
+      }
+      if (i >= 20 && i < 26) {
+        const int q = (i - 20) / 3, p = (i - 20) % 3;
+        const int c = tid + NT * q;
+        *reinterpret_cast<u4v*>(Pn + p * PLANE + swz(BM + c / 4, (c % 4) * 8)) = rq[q][p];
+      }
+      if (i >= 26 && i < 26 + (APRE ? 3 * AQ : AI)) {
+        const int j = i - 26;
+        if constexpr (APRE) {
+          qa[j / 3][j % 3] = *reinterpret_cast<const u4v*>(aq[j / 3] + (j % 3) * args.lda + k2);
+        } else {
+          ra[j] = *reinterpret_cast<const f4*>((k2 < ksplit ? a1p[j] : a2p[j]) + k2);
+        }
+      }
+      if (i >= 36 && i < 42) {
+        const int q = (i - 36) / 3, p = (i - 36) % 3;
+        rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + p * K + k2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+
+  if (part >= 0) {
+    float* w = args.ws + ((size_t)blockIdx.z * (gridDim.x - args.tdp) + part) * (size_t)(TM * TN * 16 * NT);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[(size_t)((a * TN + b) * 16 + r) * NT + tid] = acc[a][b][r];
+    return;
+  }
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, 2, WN, EPI, 32, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  else
+    epilogue<BM, BN, 2, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+}
+
+template <int EPI, bool APRE>
+static hipError_t launch_bs2_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail) {
+  static bool init = false;
+  if (!init) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_gemm_bs2<EPI, APRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    init = true;
+  }
+  hipLaunchKernelGGL((k_gemm_bs2<EPI, APRE>), grid, dim3(256), lds, s, a);
+  if (tail)
+    hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// requires pre-split B planes for every group (registered weights); falls back to k_gemm_bs otherwise
+static hipError_t launch_bs2(const GemmArgs& a, hipStream_t s) {
+  if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
+  bool pre = true, apre = true;
+  for (int g = 0; g < a.ngroups; ++g) {
+    pre = pre && a.g[g].Bp;
+    apre = apre && a.g[g].Ap;
+  }
+  if (!pre) return launch_bs<128, 128, 2, 2, 1, 1>(a, s);
+  const size_t lds = 2 * 3 * 256 * 32 * sizeof(unsigned short);
+  const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
+  const int tail = a.tsplit > 1 ? T - a.tdp : 0;
+  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  if (apre && a.epi == EPI_STORE) return launch_bs2_k<EPI_STORE, true>(a, s, grid, lds, tail);
+  switch (a.epi) {
+    case EPI_STORE: return launch_bs2_k<EPI_STORE, false>(a, s, grid, lds, tail);
+    case EPI_GELU: return launch_bs2_k<EPI_GELU, false>(a, s, grid, lds, tail);
+    case EPI_RESID: return launch_bs2_k<EPI_RESID, false>(a, s, grid, lds, tail);
+    case EPI_DGELU: return launch_bs2_k<EPI_DGELU, false>(a, s, grid, lds, tail);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Split GEMM with a 3-buffer LDS ring and half-step fragment prefetch: 128x128x32 tile, 4 waves of 64x64.
+// Tile kt is consumed from ring slot kt%3 while tile kt+2 is split/written into slot (kt+2)%3 and tile kt+3 is
+// loaded into registers. The MFMAs of each half k-tile (16-deep step) run on fragments read during the previous
+// half, so the ONE barrier per k-tile is the only point where a wave waits on LDS; the staging work is
+// hand-interleaved between the MFMAs (sched_barrier keeps the source order).
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void k_gemm_bs3(GemmArgs args) {
+  constexpr int BM = 128, BN = 128, BK = 32, NT = 256, WN = 2, TM = 2, TN = 2;
+  constexpr int LSB = BK, PLANE = (BM + BN) * LSB, RING = 3 * PLANE;
+  constexpr int TPR = BK / 4, RPP = NT / TPR, AI = BM / RPP, BQ = BN * 4 / NT;
+  typedef float accv __attribute__((ext_vector_type(16)));
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N, K = args.K, ksplit = args.ksplit;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nkt = K / BK;
+  int tile, kb = 0, ke = nkt, part = -1;
+  if (args.tsplit <= 1) {
+    tile = xcd_remap(blockIdx.x, ntm * ntn);
+  } else if ((int)blockIdx.x < args.tdp) {
+    tile = xcd_remap(blockIdx.x, args.tdp);
+  } else {
+    part = blockIdx.x - args.tdp;
+    const int S = args.tsplit, c = part % S;
+    tile = args.tdp + part / S;
+    kb = (c * nkt) / S;
+    ke = ((c + 1) * nkt) / S;
+  }
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lr = tid / TPR, lc = (tid % TPR) * 4;
+  auto swz = [](int row, int k) { return row * LSB + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); };
+
+  const float* a1p[AI];
+  const float* a2p[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = min(m0 + lr + RPP * i, M - 1);
+    const int ar = args.arow ? args.arow[r] : r;
+    a1p[i] = G.A + (size_t)ar * args.lda + lc;
+    a2p[i] = G.A2 ? G.A2 + (size_t)r * args.lda2 + lc - ksplit : a1p[i];
+  }
+  const unsigned short* bq[BQ];
+#pragma unroll
+  for (int i = 0; i < BQ; ++i) {
+    const int c = tid + NT * i;
+    const int n = min(n0 + c / 4, N - 1);
+    bq[i] = G.Bp + (size_t)n * 3 * K + (c % 4) * 8;
+  }
+
+  f4 ra[AI];
+  u4v rq[BQ][3];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) ra[i] = *reinterpret_cast<const f4*>((k0 < ksplit ? a1p[i] : a2p[i]) + k0);
+#pragma unroll
+    for (int i = 0; i < BQ; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) rq[i][p] = *reinterpret_cast<const u4v*>(bq[i] + p * K + k0);
+  };
+  auto sstore = [&](unsigned short* P) {
+    u2v h, m, l;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      split3t(ra[i], h, m, l);
+      const int o = swz(lr + RPP * i, lc);
+      *reinterpret_cast<u2v*>(P + o) = h;
+      *reinterpret_cast<u2v*>(P + PLANE + o) = m;
+      *reinterpret_cast<u2v*>(P + 2 * PLANE + o) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BQ; ++i) {
+      const int c = tid + NT * i;
+      const int o = swz(BM + c / 4, (c % 4) * 8);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u4v*>(P + p * PLANE + o) = rq[i][p];
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int rin = lane & 31, hh = lane >> 5;
+  // fragments of one 16-deep step: A [TM][3 planes], B [TN][3 planes]
+  auto frags = [&](const unsigned short* P, int s, bf8v (&fa)[TM][3], bf8v (&fb)[TN][3]) {
+    const unsigned short* As = P + (wm * TM * 32 + rin) * LSB;
+    const unsigned short* Bs = P + (BM + wn * TN * 32 + rin) * LSB;
+    const int ck = ((2 * s + hh) ^ ((rin >> 2) & 3)) * 8;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[a][p] = *reinterpret_cast<const bf8v*>(As + p * PLANE + a * 32 * LSB + ck);
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[b][p] = *reinterpret_cast<const bf8v*>(Bs + p * PLANE + b * 32 * LSB + ck);
+  };
+  accv acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  // 24 MFMA slots of one half-step; slot j of half `half` also does staging piece q = 24*half + j:
+  //   q 0-19: A chunk c = q/5: elements 0-3 split (q%5 < 4), then pack + write the 3 planes (q%5 == 4)
+  //   q 20-25: B plane writes; q 26-29: A loads of tile kt+3; q 36-41: B loads of tile kt+3
+  unsigned xs[4], ms[4], ls[4];
+  auto half_step = [&](const bf8v (&fa)[TM][3], const bf8v (&fb)[TN][3], int half, unsigned short* Pw, int k3) {
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      const int pr = j / 4, a = (j % 4) / 2, b = j % 2;
+      const int pa = pr == 0 ? 2 : (pr == 2 || pr == 3) ? 1 : 0;
+      const int pb = pr == 1 ? 2 : (pr == 2 || pr == 4) ? 1 : 0;
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][pa], fb[b][pb], acc[a][b], 0, 0, 0);
+      const int q = 24 * half + j;
+      if (q < 20) {
+        const int c = q / 5, e = q % 5;
+        if (e < 4) {
+          const unsigned xv = __float_as_uint(ra[c][e]);
+          const float r1 = ra[c][e] - __uint_as_float(xv & 0xffff0000u);
+          xs[e] = xv;
+          ms[e] = __float_as_uint(r1);
+          ls[e] = __float_as_uint(r1 - __uint_as_float(ms[e] & 0xffff0000u));
+        } else {
+          u2v h, m, l;
+          h[0] = __builtin_amdgcn_perm(xs[1], xs[0], 0x07060302u);
+          h[1] = __builtin_amdgcn_perm(xs[3], xs[2], 0x07060302u);
+          m[0] = __builtin_amdgcn_perm(ms[1], ms[0], 0x07060302u);
+          m[1] = __builtin_amdgcn_perm(ms[3], ms[2], 0x07060302u);
+          l[0] = __builtin_amdgcn_perm(ls[1], ls[0], 0x07060302u);
+          l[1] = __builtin_amdgcn_perm(ls[3], ls[2], 0x07060302u);
+          const int o = swz(lr + RPP * c, lc);
+          *reinterpret_cast<u2v*>(Pw + o) = h;
+          *reinterpret_cast<u2v*>(Pw + PLANE + o) = m;
+          *reinterpret_cast<u2v*>(Pw + 2 * PLANE + o) = l;
+        }
+      } else if (q < 26) {
+        const int i = (q - 20) / 3, p = (q - 20) % 3;
+        const int c = tid + NT * i;
+        *reinterpret_cast<u4v*>(Pw + p * PLANE + swz(BM + c / 4, (c % 4) * 8)) = rq[i][p];
+      } else if (q < 30) {
+        const int i = q - 26;
+        ra[i] = *reinterpret_cast<const f4*>((k3 < ksplit ? a1p[i] : a2p[i]) + k3);
+      } else if (q >= 36 && q < 42) {
+        const int i = (q - 36) / 3, p = (q - 36) % 3;
+        rq[i][p] = *reinterpret_cast<const u4v*>(bq[i] + p * K + k3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const int nk = ke - kb;
+  gload(kb * BK);
+  sstore(lds16);
+  gload(min(kb + 1, ke - 1) * BK);
+  sstore(lds16 + RING);
+  gload(min(kb + 2, ke - 1) * BK);
+  __syncthreads();
+  bf8v x0a[TM][3], x0b[TN][3], x1a[TM][3], x1b[TN][3];
+  frags(lds16, 0, x0a, x0b);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int nxt = cur == 2 ? 0 : cur + 1, wr = nxt == 2 ? 0 : nxt + 1;
+    unsigned short* Pc = lds16 + cur * RING;
+    unsigned short* Pw = lds16 + wr * RING;
+    const int k3 = min(kb + kt + 3, ke - 1) * BK;
+    frags(Pc, 1, x1a, x1b);
+    __builtin_amdgcn_sched_barrier(0);
+    half_step(x0a, x0b, 0, Pw, k3);
+    frags(lds16 + nxt * RING, 0, x0a, x0b);
+    __builtin_amdgcn_sched_barrier(0);
+    half_step(x1a, x1b, 1, Pw, k3);
+    __syncthreads();
+    cur = nxt;
+  }
+
+  if (part >= 0) {
+    float* w = args.ws + ((size_t)blockIdx.z * (gridDim.x - args.tdp) + part) * (size_t)(TM * TN * 16 * NT);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[(size_t)((a * TN + b) * 16 + r) * NT + tid] = acc[a][b][r];
+    return;
+  }
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, 2, WN, EPI, 32, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  else
+    epilogue<BM, BN, 2, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+}
+
+template <int EPI>
+static hipError_t launch_bs3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail) {
+  static bool init = false;
+  if (!init) {
+    hipError_t e =
+        hipFuncSetAttribute((const void*)k_gemm_bs3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    init = true;
+  }
+  hipLaunchKernelGGL((k_gemm_bs3<EPI>), grid, dim3(256), lds, s, a);
+  if (tail)
+    hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+static hipError_t launch_bs3(const GemmArgs& a, hipStream_t s) {
+  if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
+  bool pre = true;
+  for (int g = 0; g < a.ngroups; ++g) pre = pre && a.g[g].Bp;
+  if (!pre) return launch_bs<128, 128, 2, 2, 1, 1>(a, s);
+  const size_t lds = 3 * 3 * 256 * 32 * sizeof(unsigned short);
+  const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
+  const int tail = a.tsplit > 1 ? T - a.tdp : 0;
+  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  switch (a.epi) {
+    case EPI_STORE: return launch_bs3_k<EPI_STORE>(a, s, grid, lds, tail);
+    case EPI_GELU: return launch_bs3_k<EPI_GELU>(a, s, grid, lds, tail);
+    case EPI_RESID: return launch_bs3_k<EPI_RESID>(a, s, grid, lds, tail);
+    case EPI_DGELU: return launch_bs3_k<EPI_DGELU>(a, s, grid, lds, tail);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // tile variants (index = tile hint)
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
@@ -769,6 +1304,8 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 31: return launch_bs<128, 128, 2, 2, 1, 1>(a, s);
     case 32: return launch_bs<128, 128, 2, 4, 2, 1>(a, s);
     case 33: return launch_bs<64, 128, 2, 2, 2, 2>(a, s);
+    case 34: return launch_bs2(a, s);   // pipelined 128x128, one barrier per k-tile
+    case 35: return launch_bs3(a, s);   // 3-buffer ring + half-step fragment prefetch
     default: return hipErrorInvalidValue;
   }
 }
@@ -782,6 +1319,7 @@ static long tiles_of(const GemmArgs& a, int bm, int bn) {
 
 static int g_num_cu = 0;
 static int g_math = GEMM_SPLIT;
+static int g_tail_occ = -1;  // VAEVAR_TAIL_OCC=1: size the split-K tail by workgroups per CU (measured slower)
 void set_gemm_math(int m) { g_math = m; }
 int gemm_math() { return g_math; }
 
@@ -804,6 +1342,11 @@ void unregister_split_arena(const float* base) {
       return;
     }
 }
+static const unsigned short* split_planes_exact(const float* A) {
+  for (int i = 0; i < g_nsplit; ++i)
+    if (A == g_split[i].base) return g_split[i].planes;
+  return nullptr;
+}
 static const unsigned short* split_planes_of(const float* B) {
   for (int i = 0; i < g_nsplit; ++i)
     if (B >= g_split[i].base && B < g_split[i].base + g_split[i].n) return g_split[i].planes + 3 * (size_t)(B - g_split[i].base);
@@ -816,8 +1359,10 @@ size_t gemm_ws_floats() { return kWsFloats; }
 // tile choice (measured on MI355X, tools/gemm_bench.py, tools/gemm_split_check.py)
 static int pick_tile(const GemmArgs& a) {
   if (g_math == GEMM_SPLIT) {
-    // 128x128 with 64x64 per wave, one LDS buffer (2 WGs / CU) when it fills the chip; else 64x64
-    if (tiles_of(a, 128, 128) >= 256) return 31;
+    // pipelined 128x128 (64x64 per wave, one barrier per k-tile) for the deep-K GEMMs that fill the chip with
+    // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline)
+    const long t128 = tiles_of(a, 128, 128);
+    if (a.K >= 768 && (t128 >= 256 || (t128 >= 128 && a.K <= 1536))) return 34;
     return 24;
   }
   // f32 MFMA: high-occupancy 64x64 tiles beat larger tiles on every decoder shape at M = 2048 / 8192;
@@ -834,7 +1379,7 @@ static void variant_tile(int t, int& bm, int& bn, int& bk) {
                                {32, 64, 32}, {64, 64, 64}, {64, 64, 16}, {128, 128, 32}, {128, 128, 32},
                                {128, 64, 32}, {64, 64, 32}, {64, 128, 32}, {128, 64, 32}, {128, 128, 32},
                                {128, 128, 32}, {64, 64, 32}, {128, 64, 32}, {128, 128, 32}, {128, 128, 32},
-                               {64, 128, 32}};
+                               {64, 128, 32}, {128, 128, 32}, {128, 128, 32}};
   bm = tab[t][0];
   bn = tab[t][1];
   bk = tab[t][2];
@@ -846,8 +1391,12 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
-  if (t < 0 || t > 33) return hipErrorInvalidValue;
+  if (t < 0 || t > 35) return hipErrorInvalidValue;
   // data-parallel rounds of whole tiles + the remaining tiles split along K over the idle CUs
+  if (g_tail_occ < 0) {
+    const char* e = getenv("VAEVAR_TAIL_OCC");
+    g_tail_occ = (e && e[0] == '1') ? 1 : 0;
+  }
   if (!g_num_cu) {
     int dev = 0;
     hipDeviceProp_t p;
@@ -859,13 +1408,16 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   a.ws = ws;
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
-    a.g[g].Ap = (t >= 21 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_of(a.g[g].A) : a.g[g].Ap;
+    // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start
+    a.g[g].Ap = (t >= 21 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_exact(a.g[g].A) : a.g[g].Ap;
   }
   if (ws && a.ngroups == 1) {
     int bm, bn, bk;
     variant_tile(t, bm, bn, bk);
     const int T = ((a.N + bn - 1) / bn) * ((a.M + bm - 1) / bm);
-    const int P = g_num_cu, nkt = a.K / bk;
+    // concurrent workgroups per CU of the split variants (LDS-limited): 64x64 3, 128x128 single-buffer 2
+    const int occ = g_tail_occ ? (t == 24 || t == 29 ? 3 : (t == 31 || t == 28 ? 2 : 1)) : 1;
+    const int P = g_num_cu * occ, nkt = a.K / bk;
     const int tdp = (T / P) * P, tail = T - tdp;
     if (tdp > 0 && tail > 0 && tail <= P / 2) {
       // chunks of >= 12 k-tiles: below that the fixup launch and partial traffic cost more than the tail
