@@ -279,17 +279,6 @@ struct vv_ctx {
     unsigned short* planes;
   };
   std::vector<SplitW> split_owned;  // vv_gemm_register_weight planes
-  // hipGraph cache of the closure, keyed by its buffers: the second evaluation with the same (z, grad, d_J)
-  // is captured once on cap_stream and every later one is a single hipGraphLaunch on the caller's stream
-  struct ClosureGraph {
-    const float* z;
-    float* grad;
-    double* dJ;
-    int seen;
-    hipGraphExec_t exec;
-  };
-  std::vector<ClosureGraph> graphs;
-  hipStream_t cap_stream = nullptr;
 };
 
 namespace {
@@ -1127,20 +1116,6 @@ int closure_enqueue(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hip
   return 0;
 }
 
-bool graphs_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VAEVAR_GRAPH");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
-void drop_graphs(vv_ctx* ctx) {
-  for (auto& g : ctx->graphs)
-    if (g.exec) (void)hipGraphExecDestroy(g.exec);
-  ctx->graphs.clear();
-}
 }  // namespace
 
 // ============================================================================
@@ -1228,8 +1203,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
     vv::unregister_split_arena(w.base);
     (void)hipFree(w.planes);
   }
-  drop_graphs(ctx);
-  if (ctx->cap_stream) (void)hipStreamDestroy(ctx->cap_stream);
+
   (void)hipFree(ctx->red);
   (void)hipFree(ctx->redf);
   (void)hipFree(ctx->dout);
@@ -1271,7 +1245,6 @@ int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
     if (r) return r;
     std::string err;
     if ((r = vvf::load(m->fm, ptrs, n, err))) return fail(r, "%s", err.c_str());
-    drop_graphs(ctx);
     m->loaded = true;
     return 0;
   }
@@ -1344,7 +1317,6 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   if (D->fm || (flow_model_id >= 0 && get_model(ctx, flow_model_id) && get_model(ctx, flow_model_id)->fm))
     return fail(VV_E_ARG, "the closure needs differentiable networks_old LGUnet_all models");
   if (T < 1 || C < 1) return fail(VV_E_ARG, "bad T/C");
-  drop_graphs(ctx);
   if (D->B != 1) return fail(VV_E_ARG, "closure needs a batch-1 decoder");
   if (D->cfg.Cout < C) return fail(VV_E_ARG, "decoder produces %d channels < C=%d", D->cfg.Cout, C);
   if (Hs < D->cfg.Himg || Ws < D->cfg.Wimg)
@@ -1443,37 +1415,7 @@ int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, vo
   if (!ctx || !z) return fail(VV_E_ARG, "null argument");
   int r = set_dev(ctx);
   if (r) return r;
-  hipStream_t st = (hipStream_t)stream;
-  if (!graphs_enabled() || vv::prof_enabled() || sync_check()) return closure_enqueue(ctx, z, grad_z, d_J, st);
-  vv_ctx::ClosureGraph* g = nullptr;
-  for (auto& e : ctx->graphs)
-    if (e.z == z && e.grad == grad_z && e.dJ == d_J) g = &e;
-  if (!g) {
-    // first evaluation with these buffers runs eagerly (also performs every one-time kernel attribute set-up)
-    if (ctx->graphs.size() >= 8) drop_graphs(ctx);
-    ctx->graphs.push_back({z, grad_z, d_J, 1, nullptr});
-    return closure_enqueue(ctx, z, grad_z, d_J, st);
-  }
-  if (!g->exec) {
-    if (!ctx->cap_stream) VV_HIP(hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking));
-    VV_HIP(hipStreamBeginCapture(ctx->cap_stream, hipStreamCaptureModeRelaxed));
-    r = closure_enqueue(ctx, z, grad_z, d_J, ctx->cap_stream);
-    hipGraph_t graph = nullptr;
-    const hipError_t ec = hipStreamEndCapture(ctx->cap_stream, &graph);
-    if (r) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return r;
-    }
-    VV_HIP(ec);
-    const hipError_t ei = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) {
-      g->exec = nullptr;
-      return fail((int)ei, "closure graph instantiate: %s", hipGetErrorString(ei));
-    }
-  }
-  VV_HIP(hipGraphLaunch(g->exec, st));
-  return 0;
+  return closure_enqueue(ctx, z, grad_z, d_J, (hipStream_t)stream);
 }
 
 int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream) {
@@ -1598,7 +1540,6 @@ int vv_nearest_map(int in_size, int out_size, int* map) {
 
 int vv_set_gemm_math(vv_ctx* ctx, int math) {
   if (!ctx || (math != VV_GEMM_F32 && math != VV_GEMM_SPLIT)) return fail(VV_E_ARG, "bad gemm math %d", math);
-  if (math != vv::gemm_math()) drop_graphs(ctx);
   vv::set_gemm_math(math);
   return 0;
 }
