@@ -31,6 +31,7 @@ import torch  # noqa: E402
 PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense peak (MI355X_MICROARCH.md, chip-level table)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X bf16 MFMA dense peak; the split GEMM spends 6 bf16 products per fp32 product
 PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
+PEAK_SPLIT16_TFLOPS = 2500.0 / 3  # fp16 MFMA dense peak (= bf16); the fp16x3 split spends 3 products per fp32 one
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
 FLOPS_PER_EVAL = {1: 1787.8e9, 2: 3577.0e9, 6: 10733.7e9}  # SURVEY §8 d (input-grad only)
 
@@ -83,14 +84,15 @@ def cpu_baseline(prob_np, evals_per_iter, n_evals, threads):
                                 f"{evals_per_iter:.3f} evals per iteration of the GPU run)"}
 
 
-def gemm_traffic():
-    """HBM bytes per k_gemm_nt launch from the committed rocprofv3 --pmc passes (FETCH_SIZE x2 + WRITE_SIZE,
-    gfx950 corrections, tools/pmc_traffic.py) of `bench.py --config 2`; PMC counters cannot be read live."""
+def gemm_traffic(kernel):
+    """HBM bytes per launch of `kernel` ("k_gemm_h3" or "all") from the committed rocprofv3 --pmc passes
+    (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections, tools/pmc_traffic.py) of `bench.py --config 2`; PMC counters
+    cannot be read live."""
     path = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f)["hbm_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
+            return json.load(f)[kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -181,21 +183,37 @@ def main():
     }
     flops_eval = FLOPS_PER_EVAL.get(T)
     if prof:
-        g = pr["gemm"]
-        ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
-        split = prob.ctx.gemm_math == "split"
-        peak = PEAK_SPLIT_TFLOPS if split else PEAK_F32_TFLOPS
+        math = prob.ctx.gemm_math
+        g16, g6 = pr["gemm16"], pr["gemm"]
+        allg = {k: g16[k] + g6[k] for k in ("ms", "flops", "bytes", "launches")}
+        if math == "split16":
+            dom, peak, tkey = g16, PEAK_SPLIT16_TFLOPS, "k_gemm_h3"
+            kname = ("k_rowscale + k_gemm_h3 (+ split-K fixup): every GEMM launch that ran the fp16x3 kernel in a "
+                     "HIP-event-profiled repeat of the timed analysis")
+            desc = ("fp16x3 split: fp32 operands scaled per row by 2^e and split into 2 fp16 planes, 3 "
+                    "v_mfma_f32_32x32x16_f16 products per fp32 product; peak = 2.5 PF fp16 dense / 3")
+        elif math == "split":
+            dom, peak, tkey = allg, PEAK_SPLIT_TFLOPS, "all"
+            kname = "every GEMM launch (k_gemm_bs*) of a HIP-event-profiled repeat of the timed analysis"
+            desc = "bf16x6 split (fp32 operands as 3 bf16 planes, 6 v_mfma_f32_32x32x16_bf16 products; peak = 2.5 PF / 6)"
+        else:
+            dom, peak, tkey = allg, PEAK_F32_TFLOPS, "all"
+            kname = "every GEMM launch (k_gemm_nt) of a HIP-event-profiled repeat of the timed analysis"
+            desc = "exact f32 MFMA (v_mfma_f32_32x32x2_f32; peak 157.3 TF)"
+        ach = dom["flops"] / max(dom["ms"] * 1e-3, 1e-12) / 1e12
+        n = max(dom["launches"], 1)
+        all_ach = allg["flops"] / max(allg["ms"] * 1e-3, 1e-12) / 1e12
         out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                           "frac": ach / peak, "traffic": gemm_traffic(),
-                           "kernel": "k_gemm_bs / k_gemm_nt (every fp32 GEMM launch of a HIP-event-profiled repeat "
-                                     "of the timed analysis)",
-                           "gemm_math": ("bf16x6 split (fp32 operands as 3 bf16 planes, 6 v_mfma_f32_32x32x16_bf16 "
-                                         "products; peak = 2.5 PF bf16 / 6)") if split else
-                                        "exact f32 MFMA (v_mfma_f32_32x32x2_f32; peak 157.3 TF)",
+                           "frac": ach / peak, "traffic": gemm_traffic(tkey),
+                           "kernel": kname, "gemm_math": desc,
                            "frac_of_f32_mfma_peak": ach / PEAK_F32_TFLOPS,
-                           "launches": g["launches"], "avg_launch_us": 1e3 * g["ms"] / max(g["launches"], 1),
-                           "flops_per_launch": g["flops"] / max(g["launches"], 1),
-                           "algorithmic_bytes_per_launch": g["bytes"] / max(g["launches"], 1),
+                           "launches": dom["launches"], "avg_launch_us": 1e3 * dom["ms"] / n,
+                           "flops_per_launch": dom["flops"] / n,
+                           "algorithmic_bytes_per_launch": dom["bytes"] / n,
+                           "share_of_gemm_time": dom["ms"] / max(allg["ms"], 1e-12),
+                           "all_gemm": {"achieved": all_ach, "launches": allg["launches"],
+                                        "avg_launch_us": 1e3 * allg["ms"] / max(allg["launches"], 1),
+                                        "frac_of_f32_mfma_peak": all_ach / PEAK_F32_TFLOPS},
                            "traffic_source": "profiles/r01/gemm_traffic.json: rocprofv3 --pmc FETCH_SIZE / "
                                              "WRITE_SIZE passes of bench.py (tools/pmc_traffic.py)"}
         busy = sum(v["ms"] for v in pr.values())

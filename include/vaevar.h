@@ -131,18 +131,22 @@ int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* 
    decoder_hr (nf_model/vae.py:90) and integrate (da_4dvar.py:671, 679); map has out_size entries (host) */
 int vv_nearest_map(int in_size, int out_size, int* map);
 
-/* GEMM arithmetic for every nn.Linear of the engine (process-wide; default VV_GEMM_SPLIT, or the
-   VAEVAR_GEMM_MATH=f32|split environment variable at vv_ctx_create):
-   VV_GEMM_F32   = v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (torch fp32 matmul semantics);
-   VV_GEMM_SPLIT = each fp32 operand split exactly into three bf16 planes (x = h + m + l) and the six
-                   products of order >= 2^-16 accumulated in fp32 by v_mfma_f32_32x32x16_bf16: fp32-level
-                   error (measured vs fp64 no larger than VV_GEMM_F32's) at 2.67x the arithmetic rate. */
+/* GEMM arithmetic for every nn.Linear of the engine (process-wide; default VV_GEMM_SPLIT16, or the
+   VAEVAR_GEMM_MATH=f32|split|split16 environment variable at vv_ctx_create):
+   VV_GEMM_F32     = v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (torch fp32 matmul semantics);
+   VV_GEMM_SPLIT   = each fp32 operand split exactly into three bf16 planes (x = h + m + l) and the six
+                     products of order >= 2^-16 accumulated in fp32 by v_mfma_f32_32x32x16_bf16;
+   VV_GEMM_SPLIT16 = each fp32 operand scaled by a power of two (A per row and 32-wide k-chunk, B per row) and
+                     split into two fp16 planes (x = h + l, 22 bits), three products (hh, hl, lh) accumulated
+                     in fp32 by v_mfma_f32_32x32x16_f16.
+   Both split modes have fp32-level error (measured vs fp64, tests/test_gpu_kernels.py). */
 #define VV_GEMM_F32 0
 #define VV_GEMM_SPLIT 1
+#define VV_GEMM_SPLIT16 2
 int vv_set_gemm_math(vv_ctx* ctx, int math);
 int vv_get_gemm_math(vv_ctx* ctx, int* math);
 
-/* give a device weight B[N][K] (used as the B operand of vv_gemm) precomputed bf16 split planes, as the
+/* give a device weight B[N][K] (used as the B operand of vv_gemm) precomputed split planes, as the
    engine does for every model weight at vv_load_weights; B must stay alive and unchanged until
    vv_ctx_destroy (which frees the planes) */
 int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K);

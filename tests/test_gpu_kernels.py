@@ -60,8 +60,8 @@ def test_gemm_split_accuracy(ctx, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 1152, 4608), (300, 200, 96), (4096, 384, 1152),
                                    (2048, 3456, 1152)])
 def test_gemm_pipelined_registered(ctx, M, N, K):
-    """Pipelined 128x128 split kernel (tile 34) on a registered weight (pre-split planes), incl. ragged edges and
-    the split-K tail: same fp32-level error bound as the other variants."""
+    """Pipelined 128x128 split kernels (tile 34/35 bf16x6, 36 fp16x3) on a registered weight (pre-split planes),
+    incl. ragged edges and the split-K tail: same fp32-level error bound as the other variants."""
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
     A = torch.randn(M, K, generator=g)
     B = torch.randn(N, K, generator=g) * 0.03
@@ -69,7 +69,7 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
     scale = A.double().abs() @ B.double().abs().t()
     Bd = B.cuda()
     ctx.gemm_register_weight(Bd)
-    for t in (35, 34, 31, 24):
+    for t in (36, 35, 34, 31, 24):
         C = ctx.gemm(A.cuda(), Bd, tile=t).cpu().double()
         es = float(((C - ref).abs() / scale).max())
         print(f"registered gemm {M}x{N}x{K} t{t}: {es:.2e}")
@@ -80,14 +80,39 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
 _keep = []
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
+def test_gemm_split16_dynamic_range(ctx, M, N, K):
+    """fp16x3 split (tile 36) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
+    (per-chunk scales), B rows span 2^+-8, with zeros, a zero row and huge/tiny values: no overflow, no flush."""
+    g = torch.Generator().manual_seed(M + N + K + 1)
+    A = torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-12, 12, generator=g)) \
+        * torch.exp(torch.empty(1, K).uniform_(-3, 3, generator=g))
+    A[5] = 0.0
+    A[:, 7] = 0.0
+    A[9, 11] = 3.0e30
+    A[10] *= 1e-25
+    B = torch.randn(N, K, generator=g) * 0.03 * torch.exp(torch.empty(N, 1).uniform_(-6, 6, generator=g))
+    ref = A.double() @ B.double().t()
+    scale = (A.double().abs() @ B.double().abs().t()).clamp_min(1e-300)
+    Bd = B.cuda()
+    ctx.gemm_register_weight(Bd)
+    e32 = float(((ctx.gemm(A.cuda(), Bd, tile=2).cpu().double() - ref).abs() / scale).max())
+    C = ctx.gemm(A.cuda(), Bd, tile=36).cpu().double()
+    assert torch.isfinite(C).all()
+    es = float(((C - ref).abs() / scale).max())
+    print(f"split16 dynamic range {M}x{N}x{K}: f32 {e32:.2e} split16 {es:.2e}")
+    assert es < 1e-6 and es < 2.0 * e32, (es, e32)
+    assert torch.all(C[5] == 0)
+    _keep.append(Bd)
+
+
 def test_gemm_math_switch(ctx):
-    assert ctx.gemm_math in ("split", "f32")
+    assert ctx.gemm_math in ("split16", "split", "f32")
     old = ctx.gemm_math
     try:
-        ctx.gemm_math = "f32"
-        assert ctx.gemm_math == "f32"
-        ctx.gemm_math = "split"
-        assert ctx.gemm_math == "split"
+        for m in ("f32", "split", "split16"):
+            ctx.gemm_math = m
+            assert ctx.gemm_math == m
     finally:
         ctx.gemm_math = old
 

@@ -18,17 +18,30 @@ def per_kernel(path, counter):
 
 f = per_kernel(sys.argv[1], "FETCH_SIZE")
 w = per_kernel(sys.argv[2], "WRITE_SIZE")
-KEY = ("k_gemm_nt", "k_gemm_bs")
-gf = [v for n, v in f.values() if any(k in n for k in KEY)]
-gw = [v for n, v in w.values() if any(k in n for k in KEY)]
+
+
+def summary(keys, what):
+    gf = [v for n, v in f.values() if any(k in n for k in keys)]
+    gw = [v for n, v in w.values() if any(k in n for k in keys)]
+    if not gf or not gw:
+        return None
+    o = {"kernel": what, "launches_fetch": len(gf), "launches_write": len(gw),
+         "fetch_bytes_per_launch_raw": 1024 * statistics.mean(gf),
+         "fetch_bytes_per_launch": 2 * 1024 * statistics.mean(gf),
+         "write_bytes_per_launch": 1024 * statistics.mean(gw)}
+    o["hbm_bytes_per_launch"] = o["fetch_bytes_per_launch"] + o["write_bytes_per_launch"]
+    return o
+
+
 out = {
-    "kernel": "k_gemm_bs / k_gemm_nt (every GEMM main-kernel launch)",
-    "launches_fetch": len(gf), "launches_write": len(gw),
-    "fetch_bytes_per_launch_raw": 1024 * statistics.mean(gf),
-    "fetch_bytes_per_launch": 2 * 1024 * statistics.mean(gf),
-    "write_bytes_per_launch": 1024 * statistics.mean(gw),
+    # one fp16x3 GEMM = k_rowscale (reads A) + k_gemm_h3 (+ fixup): counted per k_gemm_h3 launch
+    "k_gemm_h3": summary(("k_gemm_h3",), "k_gemm_h3 main-kernel launches"),
+    "k_rowscale": summary(("k_rowscale",), "k_rowscale launches (one per fp16x3 GEMM)"),
+    "all": summary(("k_gemm_nt", "k_gemm_bs", "k_gemm_h3"), "every GEMM main-kernel launch"),
+    "note": "FETCH_SIZE doubled (gfx950 wide-load undercount), both in KB -> bytes; means over launches",
 }
-out["hbm_bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
-out["note"] = "FETCH_SIZE doubled (gfx950 wide-load undercount), both in KB -> bytes; mean over every GEMM launch"
+if out["k_gemm_h3"] and out["k_rowscale"]:
+    out["k_gemm_h3"]["hbm_bytes_per_launch_incl_rowscale"] = (out["k_gemm_h3"]["hbm_bytes_per_launch"] +
+                                                              out["k_rowscale"]["hbm_bytes_per_launch"])
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(out))

@@ -607,9 +607,9 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
   if (hipMalloc(&m->warena->base, wbytes) != hipSuccess) return fail(VV_E_ALLOC, "weights: %zu bytes", wbytes);
   m->warena->cap = wbytes;
   m->parena = std::make_unique<Arena>();
-  if (hipMalloc(&m->parena->base, wbytes / 4 * 3 * sizeof(unsigned short)) != hipSuccess)
-    return fail(VV_E_ALLOC, "weight split planes: %zu bytes", wbytes / 4 * 6);
-  m->parena->cap = wbytes / 4 * 6;
+  const size_t pbytes = vv::split_arena_bytes(wbytes / 4);
+  if (hipMalloc(&m->parena->base, pbytes) != hipSuccess) return fail(VV_E_ALLOC, "weight split planes: %zu bytes", pbytes);
+  m->parena->cap = pbytes;
   vv::register_split_arena(reinterpret_cast<const float*>(m->warena->base), wbytes / 4,
                            reinterpret_cast<const unsigned short*>(m->parena->base));
   size_t off = 0;
@@ -1186,7 +1186,8 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
-  if (const char* e = getenv("VAEVAR_GEMM_MATH")) vv::set_gemm_math(strcmp(e, "f32") == 0 ? vv::GEMM_F32 : vv::GEMM_SPLIT);
+  if (const char* e = getenv("VAEVAR_GEMM_MATH"))
+    vv::set_gemm_math(strcmp(e, "f32") == 0 ? vv::GEMM_F32 : strcmp(e, "split") == 0 ? vv::GEMM_SPLIT : vv::GEMM_SPLIT16);
   *out = c;
   return 0;
 }
@@ -1260,15 +1261,13 @@ int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
     if (it == m->W.end()) continue;
     VV_HIP(vv::transpose2d(m->W[p.name], const_cast<float*>(it->second), (int)p.shape[0], (int)p.shape[1], 0));
   }
-  // bf16 split planes of every GEMM weight and its transpose (GEMM_SPLIT B operands)
-  const float* wbase = reinterpret_cast<const float*>(m->warena->base);
-  unsigned short* pbase = reinterpret_cast<unsigned short*>(m->parena->base);
+  // split planes (bf16 and fp16) of every GEMM weight and its transpose (GEMM_SPLIT / GEMM_SPLIT16 B operands)
   for (auto& p : m->params) {
     auto it = m->W.find(p.name + "^T");
     if (it == m->W.end()) continue;
     const size_t n = numel(p.shape);
-    VV_HIP(vv::split_planes(m->W[p.name], pbase + 3 * (size_t)(m->W[p.name] - wbase), n, (int)p.shape[1], 0));
-    VV_HIP(vv::split_planes(it->second, pbase + 3 * (size_t)(it->second - wbase), n, (int)p.shape[0], 0));
+    VV_HIP(vv::split_registered(m->W[p.name], n, (int)p.shape[1], 0));
+    VV_HIP(vv::split_registered(it->second, n, (int)p.shape[0], 0));
   }
   VV_HIP(hipDeviceSynchronize());
   m->loaded = true;
@@ -1539,7 +1538,8 @@ int vv_nearest_map(int in_size, int out_size, int* map) {
 }
 
 int vv_set_gemm_math(vv_ctx* ctx, int math) {
-  if (!ctx || (math != VV_GEMM_F32 && math != VV_GEMM_SPLIT)) return fail(VV_E_ARG, "bad gemm math %d", math);
+  if (!ctx || (math != VV_GEMM_F32 && math != VV_GEMM_SPLIT && math != VV_GEMM_SPLIT16))
+    return fail(VV_E_ARG, "bad gemm math %d", math);
   vv::set_gemm_math(math);
   return 0;
 }
@@ -1622,10 +1622,14 @@ int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K) {
       ++i;
     }
   }
-  if (hipMalloc(&planes, n * 3 * sizeof(unsigned short)) != hipSuccess) return fail(VV_E_ALLOC, "planes");
-  VV_HIP(vv::split_planes(B, planes, n, K, 0));
-  VV_HIP(hipDeviceSynchronize());
+  if (hipMalloc(&planes, vv::split_arena_bytes(n)) != hipSuccess) return fail(VV_E_ALLOC, "planes");
   vv::register_split_arena(B, n, planes);
+  const hipError_t se = vv::split_registered(B, n, K, 0);
+  if (se != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    vv::unregister_split_arena(B);
+    (void)hipFree(planes);
+    return fail((int)se, "split planes: %s", hipGetErrorString(se));
+  }
   ctx->split_owned.push_back({B, n, planes});
   return 0;
 }

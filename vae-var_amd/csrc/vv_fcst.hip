@@ -869,7 +869,7 @@ int create(const vv_lgunet_config* cfg, int batch, FModel** out, std::string& er
   m->wfloats = off;
   if ((r = dalloc(*m, off, &m->warena, err))) return bail(r);
   void* pl = nullptr;
-  if (hipMalloc(&pl, off * 3 * sizeof(unsigned short)) != hipSuccess)
+  if (hipMalloc(&pl, split_arena_bytes(off)) != hipSuccess)
     return bail(ferr(err, VV_E_ALLOC, "weight split planes"));
   m->owned.push_back(pl);
   m->planes = reinterpret_cast<unsigned short*>(pl);
@@ -908,7 +908,7 @@ int create(const vv_lgunet_config* cfg, int batch, FModel** out, std::string& er
     m->conv_floats = per * G;
     if ((r = dalloc(*m, m->conv_floats, &m->convw, err))) return bail(r);
     void* cp = nullptr;
-    if (hipMalloc(&cp, m->conv_floats * 3 * sizeof(unsigned short)) != hipSuccess)
+    if (hipMalloc(&cp, split_arena_bytes(m->conv_floats)) != hipSuccess)
       return bail(ferr(err, VV_E_ALLOC, "conv split planes"));
     m->owned.push_back(cp);
     m->convp = reinterpret_cast<unsigned short*>(cp);
@@ -955,7 +955,7 @@ int load(FModel* m, const void* const* ptrs, int n, std::string& err) {
   for (size_t i = 0; i < m->params.size(); ++i) {
     const auto& p = m->params[i];
     if (p.shape.size() != 2) continue;
-    FH(split_planes(m->pptr[i], m->planes + 3 * (size_t)(m->pptr[i] - m->warena), numel(p.shape), (int)p.shape[1], 0));
+    FH(split_registered(m->pptr[i], numel(p.shape), (int)p.shape[1], 0));
   }
   FH(hipDeviceSynchronize());
   const FCfg& c = m->c;
@@ -982,8 +982,8 @@ int load(FModel* m, const void* const* ptrs, int n, std::string& err) {
         for (int j = 0; j < cout * kk; ++j) w2[(size_t)j * C0 + ci] = host[(size_t)ci * cout * kk + j];
       FH(hipMemcpy(m->W2[g], w2.data(), w2.size() * 4, hipMemcpyHostToDevice));
       // split planes (rows of K = Kp for Wp, C0 for W2)
-      FH(split_planes(m->Wp[g], m->convp + 3 * (size_t)(m->Wp[g] - m->convw), (size_t)C0 * m->Kp, m->Kp, 0));
-      FH(split_planes(m->W2[g], m->convp + 3 * (size_t)(m->W2[g] - m->convw), (size_t)m->NT * C0, C0, 0));
+      FH(split_registered(m->Wp[g], (size_t)C0 * m->Kp, m->Kp, 0));
+      FH(split_registered(m->W2[g], (size_t)m->NT * C0, C0, 0));
     }
     FH(hipDeviceSynchronize());
   }

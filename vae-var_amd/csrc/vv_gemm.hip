@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 namespace vv {
 
@@ -1266,6 +1267,288 @@ static hipError_t launch_bs3(const GemmArgs& a, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// fp32 GEMM as three fp16 MFMA products (GEMM_SPLIT16; v_mfma_f32_32x32x16_f16, half the MFMAs of the bf16x6
+// split for the same fp32-level error).
+//
+// An fp16 pair carries 22 significant bits (x = h + l + O(2^-22 x)) but only a 5-bit exponent, so each operand
+// row is first scaled by a power of two that puts its maximum in [2^14, 2^15): B (weights) at load time
+// (k_split16_rows), A (activations) by k_rowscale just before the GEMM (one pass over A, max over the whole
+// logical row incl. the A2 part and the arow gather). Then
+//   a.b = (h_a h_b + h_a l_b + l_a h_b) 2^-(e_a + e_b)      (dropped: l_a l_b and the residuals, ~2^-22 |a b|)
+// Products of fp16 values are exact in fp32; both scales are applied once, after the k loop. A is split while
+// the k-tile is staged (h = fp16(a 2^e), l = fp16(a 2^e - h), round-to-nearest, the residual exact in fp32).
+// Tile 128x128x32, 4 waves of 64x64, two LDS buffers with the same swizzle as k_gemm_bs2, ONE barrier per
+// k-tile: the MFMAs of tile kt run while tile kt+1 (in registers) is split into the other buffer and tile kt+2
+// is loaded; same split-K tail and epilogues.
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+
+// s[r] = 2^(141 - exponent(max_k |A(r,k)|)) for the logical rows of a GEMM (one wave per row; grid.z = group)
+__global__ __launch_bounds__(256) void k_rowscale(GemmArgs args, float* __restrict__ out) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= args.M) return;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int ar = args.arow ? args.arow[r] : r;
+  const float* a = G.A + (size_t)ar * args.lda;
+  unsigned mx = 0;
+  for (int k = lane * 4; k < args.ksplit; k += 256) {
+    const f4 v = *reinterpret_cast<const f4*>(a + k);
+    mx = max(mx, max(max(__float_as_uint(fabsf(v[0])), __float_as_uint(fabsf(v[1]))),
+                     max(__float_as_uint(fabsf(v[2])), __float_as_uint(fabsf(v[3])))));
+  }
+  if (G.A2) {
+    const float* a2 = G.A2 + (size_t)r * args.lda2;
+    for (int k = lane * 4; k < args.K - args.ksplit; k += 256) {
+      const f4 v = *reinterpret_cast<const f4*>(a2 + k);
+      mx = max(mx, max(max(__float_as_uint(fabsf(v[0])), __float_as_uint(fabsf(v[1]))),
+                       max(__float_as_uint(fabsf(v[2])), __float_as_uint(fabsf(v[3])))));
+    }
+  }
+  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  if (lane == 0) out[(size_t)blockIdx.z * args.M + r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
+}
+
+// XP != 0: timing experiments only (wrong results): 1 no global loads in the k loop, 2 no MFMAs, 3 no A split
+// arithmetic
+template <int EPI, int XP = 0>
+__global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* __restrict__ ascale) {
+  constexpr int BM = 128, BN = 128, BK = 32, NT = 256, WN = 2, TM = 2, TN = 2;
+  constexpr int LSB = BK, PLANE = (BM + BN) * LSB;  // unsigned shorts
+  constexpr int BUF = 2 * PLANE;                    // fp16 planes h, l of the A and B rows
+  constexpr int TPR = BK / 4, RPP = NT / TPR, AI = BM / RPP, BQ = BN * 4 / NT;  // 8, 32, 4, 2
+  typedef float accv __attribute__((ext_vector_type(16)));
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N, K = args.K, ksplit = args.ksplit;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nkt = K / BK;
+  int tile, kb = 0, ke = nkt, part = -1;
+  if (args.tsplit <= 1) {
+    tile = xcd_remap(blockIdx.x, ntm * ntn);
+  } else if ((int)blockIdx.x < args.tdp) {
+    tile = xcd_remap(blockIdx.x, args.tdp);
+  } else {
+    part = blockIdx.x - args.tdp;
+    const int S = args.tsplit, c = part % S;
+    tile = args.tdp + part / S;
+    kb = (c * nkt) / S;
+    ke = ((c + 1) * nkt) / S;
+  }
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lr = tid / TPR, lc = (tid % TPR) * 4;
+  auto swz = [](int row, int k) { return row * LSB + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); };
+  const float* rs = ascale + (size_t)blockIdx.z * M;
+
+  const float* a1p[AI];
+  const float* a2p[AI];
+  float sa[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = min(m0 + lr + RPP * i, M - 1);
+    const int ar = args.arow ? args.arow[r] : r;
+    a1p[i] = G.A + (size_t)ar * args.lda + lc;
+    a2p[i] = G.A2 ? G.A2 + (size_t)r * args.lda2 + lc - ksplit : a1p[i];
+    sa[i] = rs[r];
+  }
+  const unsigned short* bq[BQ];
+#pragma unroll
+  for (int i = 0; i < BQ; ++i) {
+    const int c = tid + NT * i;
+    const int n = min(n0 + c / 4, N - 1);
+    bq[i] = G.Bh + (size_t)n * 2 * K + (c % 4) * 8;
+  }
+
+  f4 ra[AI];
+  u4v rq[BQ][2];
+  auto aload = [&](int i, int k0) { ra[i] = *reinterpret_cast<const f4*>((k0 < ksplit ? a1p[i] : a2p[i]) + k0); };
+  auto bload = [&](int q, int p, int k0) { rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + p * K + k0); };
+  auto asplit = [&](unsigned short* P, int i) {
+    const int o = swz(lr + RPP * i, lc);
+    if constexpr (XP == 3) {
+      *reinterpret_cast<u2v*>(P + o) = u2v{__float_as_uint(ra[i][0]), __float_as_uint(ra[i][1])};
+      *reinterpret_cast<u2v*>(P + PLANE + o) = u2v{__float_as_uint(ra[i][2]), __float_as_uint(ra[i][3])};
+      return;
+    }
+    h4v hv, lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v = ra[i][e] * sa[i];
+      hv[e] = (_Float16)v;
+      lv[e] = (_Float16)(v - (float)hv[e]);
+    }
+    *reinterpret_cast<h4v*>(P + o) = hv;
+    *reinterpret_cast<h4v*>(P + PLANE + o) = lv;
+  };
+  auto bstore = [&](unsigned short* P, int q, int p) {
+    const int c = tid + NT * q;
+    *reinterpret_cast<u4v*>(P + p * PLANE + swz(BM + c / 4, (c % 4) * 8)) = rq[q][p];
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int rin = lane & 31, hh = lane >> 5;
+  accv acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  const int nk = ke - kb;
+#pragma unroll
+  for (int i = 0; i < AI; ++i) aload(i, kb * BK);
+#pragma unroll
+  for (int q = 0; q < BQ; ++q)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) bload(q, p, kb * BK);
+#pragma unroll
+  for (int i = 0; i < AI; ++i) asplit(lds16, i);
+#pragma unroll
+  for (int q = 0; q < BQ; ++q)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) bstore(lds16, q, p);
+  {
+    const int k1 = min(kb + 1, ke - 1) * BK;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) aload(i, k1);
+#pragma unroll
+    for (int q = 0; q < BQ; ++q)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) bload(q, p, k1);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned short* P = lds16 + (kt & 1) * BUF;
+    const unsigned short* As = P + (wm * TM * 32 + rin) * LSB;
+    const unsigned short* Bs = P + (BM + wn * TN * 32 + rin) * LSB;
+    h8v fa[2][TM][2], fb[2][TN][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ck = ((2 * s + hh) ^ ((rin >> 2) & 3)) * 8;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) fa[s][a][p] = *reinterpret_cast<const h8v*>(As + p * PLANE + a * 32 * LSB + ck);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) fb[s][b][p] = *reinterpret_cast<const h8v*>(Bs + p * PLANE + b * 32 * LSB + ck);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned short* Pn = lds16 + ((kt + 1) & 1) * BUF;
+    const int k2 = min(kb + kt + 2, ke - 1) * BK;
+    // 24 MFMA slots: step s, product (l h, h l, h h: smallest first), chain (a, b) fastest. Branch-free staging:
+    // on the last two iterations it re-reads the last k-tile and writes a buffer nobody reads again.
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      const int st = i / 12, pr = (i % 12) / 4, a = (i % 4) / 2, b = i % 2;
+      const h8v& xa = fa[st][a][pr == 0 ? 1 : 0];
+      const h8v& xb = fb[st][b][pr == 1 ? 1 : 0];
+      if constexpr (XP == 2) {
+        if (i < 4) acc[a][b][0] += (float)xa[0] + (float)xb[1];
+      } else {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa, xb, acc[a][b], 0, 0, 0);
+      }
+      if (i < 2 * AI && (i & 1)) asplit(Pn, i / 2);
+      if (i >= 8 && i < 12) bstore(Pn, (i - 8) / 2, (i - 8) % 2);
+      if (XP != 1 && i >= 12 && i < 12 + AI) aload(i - 12, k2);
+      if (XP != 1 && i >= 16 && i < 20) bload((i - 16) / 2, (i - 16) % 2, k2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+
+  // undo the scales: rows of A (2^-e_a), rows of B = columns of C (2^-e_b)
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = min(n0 + wn * TN * 32 + b * 32 + rin, N - 1);
+    const float sb = G.Bs[(size_t)col * (K / 32)];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = min(m0 + wm * TM * 32 + a * 32 + 8 * j + 4 * hh + q, M - 1);
+          const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));   // 2^-e_a
+          acc[a][b][4 * j + q] *= ia * sb;
+        }
+  }
+
+  if (part >= 0) {
+    float* w = args.ws + ((size_t)blockIdx.z * (gridDim.x - args.tdp) + part) * (size_t)(TM * TN * 16 * NT);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[(size_t)((a * TN + b) * 16 + r) * NT + tid] = acc[a][b][r];
+    return;
+  }
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, 2, WN, EPI, 32, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  else
+    epilogue<BM, BN, 2, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+}
+
+template <int EPI, int XP = 0>
+static hipError_t launch_h3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc) {
+  static bool init = false;
+  if (!init) {
+    hipError_t e =
+        hipFuncSetAttribute((const void*)k_gemm_h3<EPI, XP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    init = true;
+  }
+  hipLaunchKernelGGL((k_gemm_h3<EPI, XP>), grid, dim3(256), lds, s, a, sc);
+  if (tail)
+    hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+constexpr size_t kWsFloats = (size_t)1 << 21;      // 8 MB: tail partials of up to 512 chunks of a 64x64 tile
+constexpr size_t kScaleFloats = (size_t)1 << 19;   // then the A row scales of GEMM_SPLIT16 (groups x M)
+
+// requires fp16 planes for every group's B (registered weights) and a workspace for the A row scales; the
+// bf16x6 pipelined kernel otherwise
+static bool h3_ready(const GemmArgs& a) {
+  bool pre = a.ws && (size_t)a.ngroups * a.M <= kScaleFloats;
+  for (int g = 0; g < a.ngroups; ++g) pre = pre && a.g[g].Bh && a.g[g].Bs;
+  return pre;
+}
+
+static hipError_t launch_h3(const GemmArgs& a, hipStream_t s, int xp = 0) {
+  if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
+  if (!h3_ready(a)) return launch_bs2(a, s);
+  float* sc = a.ws + kWsFloats;
+  hipLaunchKernelGGL(k_rowscale, dim3((a.M + 3) / 4, 1, a.ngroups), dim3(256), 0, s, a, sc);
+  const size_t lds = 2 * (2 * 256 * 32) * sizeof(unsigned short);
+  const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
+  const int tail = a.tsplit > 1 ? T - a.tdp : 0;
+  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  if (xp && a.epi == EPI_STORE) {
+    switch (xp) {
+      case 1: return launch_h3_k<EPI_STORE, 1>(a, s, grid, lds, tail, sc);
+      case 2: return launch_h3_k<EPI_STORE, 2>(a, s, grid, lds, tail, sc);
+      case 3: return launch_h3_k<EPI_STORE, 3>(a, s, grid, lds, tail, sc);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  switch (a.epi) {
+    case EPI_STORE: return launch_h3_k<EPI_STORE>(a, s, grid, lds, tail, sc);
+    case EPI_GELU: return launch_h3_k<EPI_GELU>(a, s, grid, lds, tail, sc);
+    case EPI_RESID: return launch_h3_k<EPI_RESID>(a, s, grid, lds, tail, sc);
+    case EPI_DGELU: return launch_h3_k<EPI_DGELU>(a, s, grid, lds, tail, sc);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // tile variants (index = tile hint)
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
@@ -1306,6 +1589,9 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 33: return launch_bs<64, 128, 2, 2, 2, 2>(a, s);
     case 34: return launch_bs2(a, s);   // pipelined 128x128, one barrier per k-tile
     case 35: return launch_bs3(a, s);   // 3-buffer ring + half-step fragment prefetch
+    // fp16x3 split (fp32-accurate)
+    case 36: return launch_h3(a, s);
+    case 37: case 38: case 39: return launch_h3(a, s, t - 36);   // timing experiments (wrong results)
     default: return hipErrorInvalidValue;
   }
 }
@@ -1318,7 +1604,7 @@ static long tiles_of(const GemmArgs& a, int bm, int bn) {
 // larger tiles on every decoder shape at M = 2048 / 8192; 32x64 when 64x64 leaves CUs idle
 
 static int g_num_cu = 0;
-static int g_math = GEMM_SPLIT;
+static int g_math = GEMM_SPLIT16;
 static int g_tail_occ = -1;  // VAEVAR_TAIL_OCC=1: size the split-K tail by workgroups per CU (measured slower)
 void set_gemm_math(int m) { g_math = m; }
 int gemm_math() { return g_math; }
@@ -1328,37 +1614,98 @@ struct SplitArena {
   size_t n;
   const unsigned short* planes;
 };
-static SplitArena g_split[16];
-static int g_nsplit = 0;
+static std::vector<SplitArena> g_split;   // registered weight arenas (host-side lookup per GEMM launch)
+
+static size_t split16_scale_off(size_t n) { return (10 * n + 255) & ~size_t(255); }  // bytes
+size_t split_arena_bytes(size_t n) { return split16_scale_off(n) + (n / 32 + 1) * sizeof(float); }
 
 void register_split_arena(const float* base, size_t n, const unsigned short* planes) {
   unregister_split_arena(base);
-  if (g_nsplit < 16) g_split[g_nsplit++] = {base, n, planes};
+  g_split.push_back({base, n, planes});
 }
 void unregister_split_arena(const float* base) {
-  for (int i = 0; i < g_nsplit; ++i)
+  for (size_t i = 0; i < g_split.size(); ++i)
     if (g_split[i].base == base) {
-      g_split[i] = g_split[--g_nsplit];
+      g_split.erase(g_split.begin() + i);
       return;
     }
 }
+static const SplitArena* arena_of(const float* B) {
+  for (const SplitArena& a : g_split)
+    if (B >= a.base && B < a.base + a.n) return &a;
+  return nullptr;
+}
 static const unsigned short* split_planes_exact(const float* A) {
-  for (int i = 0; i < g_nsplit; ++i)
-    if (A == g_split[i].base) return g_split[i].planes;
+  for (const SplitArena& a : g_split)
+    if (A == a.base) return a.planes;
   return nullptr;
 }
 static const unsigned short* split_planes_of(const float* B) {
-  for (int i = 0; i < g_nsplit; ++i)
-    if (B >= g_split[i].base && B < g_split[i].base + g_split[i].n) return g_split[i].planes + 3 * (size_t)(B - g_split[i].base);
-  return nullptr;
+  const SplitArena* a = arena_of(B);
+  return a ? a->planes + 3 * (size_t)(B - a->base) : nullptr;
 }
-constexpr size_t kWsFloats = (size_t)1 << 21;  // 8 MB: tail partials of up to 512 chunks of a 64x64 tile
+// fp16 planes and row scales of B (GEMM_SPLIT16); null unless B's offset in its arena is a multiple of 32
+static void split16_of(const float* B, int K, const unsigned short*& h, const float*& sc) {
+  h = nullptr;
+  sc = nullptr;
+  const SplitArena* a = arena_of(B);
+  if (!a || K % 32) return;
+  const size_t o = (size_t)(B - a->base);
+  if (o % 32) return;
+  h = a->planes + 3 * a->n + 2 * o;
+  sc = reinterpret_cast<const float*>(reinterpret_cast<const char*>(a->planes) + split16_scale_off(a->n)) + o / 32;
+}
 
-size_t gemm_ws_floats() { return kWsFloats; }
+// fp16 split of whole rows (one workgroup per row): e = 141 - exponent(max |x|) puts the row maximum in
+// [2^14, 2^15); h = fp16(x 2^e), l = fp16(x 2^e - h) (both round-to-nearest, the residual is exact in fp32);
+// row scale 2^-e at sc[r * K / 32]
+__global__ __launch_bounds__(256) void k_split16_rows(const float* __restrict__ src, unsigned short* __restrict__ dst,
+                                                      float* __restrict__ sc, int K) {
+  __shared__ unsigned red[4];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float* x = src + (size_t)r * K;
+  unsigned mx = 0;
+  for (int k = tid; k < K; k += 256) mx = max(mx, __float_as_uint(fabsf(x[k])));
+  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = max(max(red[0], red[1]), max(red[2], red[3]));
+  const unsigned E = max(mx >> 23, 15u);
+  const float s = __uint_as_float((268u - E) << 23);
+  unsigned short* d = dst + (size_t)r * 2 * K;
+  for (int k = tid; k < K; k += 256) {
+    const float v = x[k] * s;
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)(v - (float)h);
+    d[k] = __builtin_bit_cast(unsigned short, h);
+    d[K + k] = __builtin_bit_cast(unsigned short, l);
+  }
+  if (tid == 0) sc[(size_t)r * K / 32] = __uint_as_float((E - 14u) << 23);
+}
+
+hipError_t split_registered(const float* W, size_t n, int K, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (K <= 0 || n % K) return hipErrorInvalidValue;
+  const SplitArena* a = arena_of(W);
+  if (!a || W + n > a->base + a->n) return hipErrorInvalidValue;
+  hipError_t e = split_planes(W, const_cast<unsigned short*>(a->planes) + 3 * (size_t)(W - a->base), n, K, s);
+  if (e != hipSuccess) return e;
+  const unsigned short* h;
+  const float* sc;
+  split16_of(W, K, h, sc);
+  if (!h) return hipSuccess;  // K or offset not 32-aligned: no GEMM can use the fp16 planes anyway
+  hipLaunchKernelGGL(k_split16_rows, dim3((unsigned)(n / K)), dim3(256), 0, s, W, const_cast<unsigned short*>(h),
+                     const_cast<float*>(sc), K);
+  return hipGetLastError();
+}
+size_t gemm_ws_floats() { return kWsFloats + kScaleFloats; }
 
 // tile choice (measured on MI355X, tools/gemm_bench.py, tools/gemm_split_check.py)
 static int pick_tile(const GemmArgs& a) {
-  if (g_math == GEMM_SPLIT) {
+  if (g_math == GEMM_SPLIT16 || g_math == GEMM_SPLIT) {
+    // GEMM_SPLIT16: fp16x3 128x128 for the deep-K GEMMs that give >= 128 tiles; the bf16x6 64x64 kernel for the
+    // short-K / few-tile GEMMs of the Swin towers (its pipeline prologue and epilogue dominate there)
+    if (g_math == GEMM_SPLIT16 && a.K >= 768 && tiles_of(a, 128, 128) >= 128) return 36;
     // pipelined 128x128 (64x64 per wave, one barrier per k-tile) for the deep-K GEMMs that fill the chip with
     // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline)
     const long t128 = tiles_of(a, 128, 128);
@@ -1379,7 +1726,8 @@ static void variant_tile(int t, int& bm, int& bn, int& bk) {
                                {32, 64, 32}, {64, 64, 64}, {64, 64, 16}, {128, 128, 32}, {128, 128, 32},
                                {128, 64, 32}, {64, 64, 32}, {64, 128, 32}, {128, 64, 32}, {128, 128, 32},
                                {128, 128, 32}, {64, 64, 32}, {128, 64, 32}, {128, 128, 32}, {128, 128, 32},
-                               {64, 128, 32}, {128, 128, 32}, {128, 128, 32}};
+                               {64, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32},
+                               {128, 128, 32}, {128, 128, 32}};
   bm = tab[t][0];
   bn = tab[t][1];
   bk = tab[t][2];
@@ -1391,7 +1739,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
-  if (t < 0 || t > 35) return hipErrorInvalidValue;
+  if (t < 0 || t > 39) return hipErrorInvalidValue;
   // data-parallel rounds of whole tiles + the remaining tiles split along K over the idle CUs
   if (g_tail_occ < 0) {
     const char* e = getenv("VAEVAR_TAIL_OCC");
@@ -1409,7 +1757,10 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start
-    a.g[g].Ap = (t >= 21 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_exact(a.g[g].A) : a.g[g].Ap;
+    a.g[g].Ap = (t >= 21 && t <= 35 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_exact(a.g[g].A) : a.g[g].Ap;
+    a.g[g].Bh = nullptr;
+    a.g[g].Bs = nullptr;
+    if (t >= 36 && (!a.ldb || a.ldb == a.K)) split16_of(a.g[g].B, a.K, a.g[g].Bh, a.g[g].Bs);
   }
   if (ws && a.ngroups == 1) {
     int bm, bn, bk;
@@ -1436,7 +1787,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   const double G = a.ngroups;
   double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);
   if (a.epi == EPI_RESID || a.epi == EPI_GELU || a.epi == EPI_DGELU) bytes += 4.0 * G * (double)a.M * a.N;
-  prof_end(ph, s, PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
+  prof_end(ph, s, t == 36 && h3_ready(a) ? PC_GEMM16 : PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
   return e;
 }
 

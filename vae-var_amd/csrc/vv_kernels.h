@@ -31,6 +31,8 @@ struct GemmGroup {
   float* aux;
   const unsigned short* Bp;  // filled in by gemm_nt: bf16 split planes of B (registered weight arena) or null
   const unsigned short* Ap;  // bf16 split planes of A, rows [3][lda] (caller-provided or registered), or null
+  const unsigned short* Bh;  // filled in by gemm_nt (GEMM_SPLIT16): fp16 planes of B, per row [h | l] x K, or null
+  const float* Bs;           // ... and the row scales: row n of B has 2^-e = Bs[n * K / 32]
 };
 
 struct GemmArgs {
@@ -53,15 +55,24 @@ struct GemmArgs {
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);
 size_t gemm_ws_floats();
 
-// GEMM arithmetic: GEMM_F32 = v_mfma_f32_32x32x2_f32 (exact f32 fma chain); GEMM_SPLIT = the fp32 operands
-// split into three bf16 planes, six v_mfma_f32_32x32x16_bf16 products (fp32-level error, 2.67x the rate)
-enum GemmMath : int { GEMM_F32 = 0, GEMM_SPLIT = 1 };
+// GEMM arithmetic:
+//   GEMM_F32     v_mfma_f32_32x32x2_f32 (exact f32 fma chain)
+//   GEMM_SPLIT   fp32 operands split into three bf16 planes, six v_mfma_f32_32x32x16_bf16 products
+//   GEMM_SPLIT16 fp32 operands scaled by a power of two (A: per row and 32-wide k-chunk, B: per row) and split
+//                into two fp16 planes, three v_mfma_f32_32x32x16_f16 products (both fp32-level error)
+enum GemmMath : int { GEMM_F32 = 0, GEMM_SPLIT = 1, GEMM_SPLIT16 = 2 };
 void set_gemm_math(int m);
 int gemm_math();
-// weight arenas whose bf16 split planes exist: for B inside [base, base+n), row r of the [N][K] operand at
-// float offset o = B - base has its planes at planes + 3*(o + r*K): h[K], m[K], l[K]
+// Weight arenas with precomputed split planes. The planes buffer of an arena of n floats holds, at these
+// offsets (split_arena_bytes(n) bytes in all):
+//   bf16: [0, 3n) unsigned shorts; row r of the [N][K] operand at float offset o = B - base: 3*(o + r*K) = h[K], m[K], l[K]
+//   fp16: [3n, 5n) unsigned shorts; at 3n + 2*(o + r*K): h[K], l[K] of the row scaled by 2^e
+//   row scales: floats after that; 2^-e of the row starting at float offset f at index f / 32
+size_t split_arena_bytes(size_t n);
 void register_split_arena(const float* base, size_t n, const unsigned short* planes);
 void unregister_split_arena(const float* base);
+// fill the planes of the rows of W[n/K][K], which lies inside a registered arena (W - base and K multiples of 32)
+hipError_t split_registered(const float* W, size_t n, int K, hipStream_t s);
 // dst[n/K][3][K] = exact bf16 split of the rows of src[n/K][K] (h = bf16(x), m = bf16(x-h), l = bf16(x-h-m))
 hipError_t split_planes(const float* src, unsigned short* dst, size_t n, int K, hipStream_t s);
 
@@ -221,7 +232,9 @@ hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, fl
 // ---------------------------------------------------------------------------
 // live profiler: HIP events around every launch, bucketed by kernel class
 // ---------------------------------------------------------------------------
-enum ProfClass : int { PC_GEMM = 0, PC_ATTN = 1, PC_LN = 2, PC_PATCH = 3, PC_MISFIT = 4, PC_VEC = 5, PC_N = 6 };
+// PC_GEMM16: the GEMMs that ran the fp16x3 kernel (k_rowscale + k_gemm_h3 [+ fixup]); PC_GEMM: every other GEMM
+enum ProfClass : int { PC_GEMM = 0, PC_ATTN = 1, PC_LN = 2, PC_PATCH = 3, PC_MISFIT = 4, PC_VEC = 5, PC_GEMM16 = 6,
+                       PC_N = 7 };
 int prof_begin(hipStream_t s);                                        // -1 when disabled
 void prof_end(int h, hipStream_t s, int cls, double flops, double bytes);
 void prof_enable(bool on);

@@ -80,7 +80,7 @@ class Context:
         check(lib.vv_adam(self.h, _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), lr, beta1, beta2, eps, step,
                           _stream()), "adam")
 
-    PROF_CLASSES = ("gemm", "attention", "layernorm", "patch", "misfit", "vector")
+    PROF_CLASSES = ("gemm", "attention", "layernorm", "patch", "misfit", "vector", "gemm16")
 
     def profile_start(self):
         check(lib.vv_profile_start(self.h), "profile_start")
@@ -94,21 +94,23 @@ class Context:
         return {c: {"ms": ms[i], "flops": fl[i], "bytes": by[i], "launches": cnt[i]}
                 for i, c in enumerate(self.PROF_CLASSES)}
 
-    GEMM_MATH = {"f32": 0, "split": 1}
+    GEMM_MATH = {"f32": 0, "split": 1, "split16": 2}
 
     @property
     def gemm_math(self) -> str:
-        """'split' (bf16x6 split planes, fp32-level error, default) or 'f32' (exact f32 MFMA); process-wide."""
+        """'split16' (fp16x3 scaled split, default), 'split' (bf16x6 split) or 'f32' (exact f32 MFMA); process-wide.
+
+        Both split modes carry fp32-level error (measured against fp64 in tests/test_gpu_kernels.py)."""
         v = ctypes.c_int()
         check(lib.vv_get_gemm_math(self.h, ctypes.byref(v)), "get_gemm_math")
-        return {0: "f32", 1: "split"}[v.value]
+        return {0: "f32", 1: "split", 2: "split16"}[v.value]
 
     @gemm_math.setter
     def gemm_math(self, name: str):
         check(lib.vv_set_gemm_math(self.h, self.GEMM_MATH[name]), "set_gemm_math")
 
     def gemm_register_weight(self, B):
-        """Precompute B's bf16 split planes (B must outlive the context and stay unchanged)."""
+        """Precompute B's split planes (bf16 and fp16; B must outlive the context and stay unchanged)."""
         check(lib.vv_gemm_register_weight(self.h, _ptr(B), B.shape[0], B.shape[1]), "gemm_register_weight")
 
     def gemm(self, A, B, bias=None, tile=-1):
