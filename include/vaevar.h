@@ -117,6 +117,11 @@ int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void*
 int vv_axpby(vv_ctx* ctx, float* out, const float* x, float a, const float* y, float b, int64_t n, void* stream);
 int vv_scale(vv_ctx* ctx, float* y, float alpha, int64_t n, void* stream);
 int vv_copy(vv_ctx* ctx, float* dst, const float* src, int64_t n, void* stream);
+/* L-BFGS two-loop recursion (torch/optim/lbfgs.py:404-442): q holds -g on entry and the direction d on return;
+   S, Y: host arrays of m device vectors (old_stps, old_dirs, oldest first), ro[m] = 1/(y.s) (host, fp32),
+   m <= 256. The dot products and coefficients stay on the device (fp32 as torch's 0-d tensors); no sync. */
+int vv_lbfgs_two_loop(vv_ctx* ctx, float* q, const float* const* S, const float* const* Y, const float* ro, int m,
+                      float H_diag, int64_t n, void* stream);
 /* torch.optim.Adam step (no weight decay / amsgrad): step is the 1-based step count */
 int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
             float beta2, float eps, int step, void* stream);

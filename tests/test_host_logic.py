@@ -28,6 +28,18 @@ class CpuPrims:
     def copy(self, dst, src):
         dst.copy_(src)
 
+    def lbfgs_two_loop(self, q, stps, dirs, ro, H_diag):
+        # k_twoloop_coef's arithmetic: fp64-accumulated dot rounded to fp32, times ro[i] in fp32
+        f32 = np.float32
+        al = [None] * len(stps)
+        for i in range(len(stps) - 1, -1, -1):
+            al[i] = f32(self.dot(stps[i], q)) * f32(ro[i])
+            q.add_(dirs[i], alpha=float(-al[i]))
+        q.mul_(float(H_diag))
+        for i in range(len(stps)):
+            be = f32(self.dot(dirs[i], q)) * f32(ro[i])
+            q.add_(stps[i], alpha=float(al[i] - be))
+
     def adam(self, p, g, m, v, lr, b1, b2, eps, step):
         m.lerp_(g, 1 - b1)
         v.mul_(b2).addcmul_(g, g, value=1 - b2)

@@ -273,6 +273,7 @@ struct vv_ctx {
   float* redf = nullptr;
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
+  float* twoloop = nullptr;  // L-BFGS two-loop scalars: al[kMaxHistory], coef
   struct SplitW {
     const float* base;
     size_t n;
@@ -284,6 +285,7 @@ struct vv_ctx {
 namespace {
 
 constexpr int kRedBlocks = 1024;
+constexpr int kMaxHistory = 256;  // L-BFGS history pairs accepted by vv_lbfgs_two_loop
 
 int set_dev(vv_ctx* ctx) {
   VV_HIP(hipSetDevice(ctx->device));
@@ -1183,6 +1185,7 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipSetDevice(device));
   VV_HIP(hipMalloc(&c->red, kRedBlocks * sizeof(double)));
   VV_HIP(hipMalloc(&c->redf, kRedBlocks * sizeof(float)));
+  VV_HIP(hipMalloc(&c->twoloop, (kMaxHistory + 1) * sizeof(float)));
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
@@ -1206,6 +1209,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   }
 
   (void)hipFree(ctx->red);
+  (void)hipFree(ctx->twoloop);
   (void)hipFree(ctx->redf);
   (void)hipFree(ctx->dout);
   (void)hipFree(ctx->doutf);
@@ -1501,6 +1505,16 @@ int vv_axpby(vv_ctx* ctx, float* out, const float* x, float a, const float* y, f
 int vv_scale(vv_ctx* ctx, float* y, float alpha, int64_t n, void* stream) {
   if (!ctx || !y) return fail(VV_E_ARG, "null argument");
   VV_HIP(vv::vec_scale(y, alpha, n, (hipStream_t)stream));
+  return 0;
+}
+int vv_lbfgs_two_loop(vv_ctx* ctx, float* q, const float* const* S, const float* const* Y, const float* ro, int m,
+                      float H_diag, int64_t n, void* stream) {
+  if (!ctx || !q || (m > 0 && (!S || !Y || !ro))) return fail(VV_E_ARG, "null argument");
+  if (m < 0 || m > kMaxHistory) return fail(VV_E_ARG, "history size out of range");
+  for (int i = 0; i < m; ++i)
+    if (!S[i] || !Y[i]) return fail(VV_E_ARG, "null history vector");
+  VV_HIP(vv::lbfgs_two_loop(q, S, Y, ro, m, H_diag, n, ctx->red, kRedBlocks, ctx->twoloop, ctx->twoloop + kMaxHistory,
+                            (hipStream_t)stream));
   return 0;
 }
 int vv_copy(vv_ctx* ctx, float* dst, const float* src, int64_t n, void* stream) {

@@ -91,6 +91,8 @@ _SIGS = {
     "vv_axpby": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_float, c_int64, c_void_p]),
     "vv_scale": (c_int, [c_void_p, c_void_p, c_float, c_int64, c_void_p]),
     "vv_copy": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "vv_lbfgs_two_loop": (c_int, [c_void_p, c_void_p, P(c_void_p), P(c_void_p), P(c_float), c_int, c_float, c_int64,
+                                  c_void_p]),
     "vv_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                         c_float, c_int, c_void_p]),
     "vv_profile_start": (c_int, [c_void_p]),

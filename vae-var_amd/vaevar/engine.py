@@ -76,6 +76,14 @@ class Context:
     def copy(self, dst, src):
         check(lib.vv_copy(self.h, _ptr(dst), _ptr(src), dst.numel(), _stream()), "copy")
 
+    def lbfgs_two_loop(self, q, stps, dirs, ro, H_diag: float):
+        """q = -g in, the L-BFGS direction out (lbfgs.py:404-442), dot products and coefficients on the device."""
+        m = len(stps)
+        S = (ctypes.c_void_p * max(m, 1))(*[_ptr(v).value for v in stps])
+        Y = (ctypes.c_void_p * max(m, 1))(*[_ptr(v).value for v in dirs])
+        r = (ctypes.c_float * max(m, 1))(*[float(x) for x in ro])
+        check(lib.vv_lbfgs_two_loop(self.h, _ptr(q), S, Y, r, m, float(H_diag), q.numel(), _stream()), "two_loop")
+
     def adam(self, p, g, m, v, lr, beta1, beta2, eps, step):
         check(lib.vv_adam(self.h, _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), lr, beta1, beta2, eps, step,
                           _stream()), "adam")

@@ -42,13 +42,14 @@ class LBFGS:
     """
 
     def __init__(self, ctx, z: torch.Tensor, lr=1, max_iter=20, max_eval=None, tolerance_grad=1e-7,
-                 tolerance_change=1e-9, history_size=100, line_search_fn=None):
+                 tolerance_change=1e-9, history_size=100, line_search_fn=None, device_two_loop=True):
         if max_eval is None:
             max_eval = max_iter * 5 // 4
         self.ctx, self.z = ctx, z
         self.lr, self.max_iter, self.max_eval = lr, max_iter, max_eval
         self.tolerance_grad, self.tolerance_change = tolerance_grad, tolerance_change
         self.history_size, self.line_search_fn = history_size, line_search_fn
+        self.device_two_loop = device_two_loop  # False: the two loops with host scalars (one sync per dot)
         self.state = {"func_evals": 0, "n_iter": 0}
 
     # --- vector helpers ---------------------------------------------------
@@ -194,20 +195,25 @@ class LBFGS:
                     old_stps.append(s)
                     ro.append(1.0 / ys)
                     H_diag = ys / self._dot(y, y)
-                num_old = len(old_dirs)
-                if "al" not in state:
-                    state["al"] = [None] * self.history_size
-                al = state["al"]
                 q = self._new()
                 self.ctx.axpby(q, flat_grad, -1.0, None, 0.0)
-                for i in range(num_old - 1, -1, -1):
-                    al[i] = self._dot(old_stps[i], q) * ro[i]
-                    self.ctx.axpy(q, old_dirs[i], float(-al[i]))
-                self.ctx.scale(q, float(H_diag))
-                d = r = q
-                for i in range(num_old):
-                    be_i = self._dot(old_dirs[i], r) * ro[i]
-                    self.ctx.axpy(r, old_stps[i], float(al[i] - be_i))
+                if self.device_two_loop:
+                    # the two loops below with al / be kept on the device (same fp32 arithmetic, no host sync)
+                    self.ctx.lbfgs_two_loop(q, old_stps, old_dirs, ro, H_diag)
+                    d = q
+                else:
+                    num_old = len(old_dirs)
+                    if "al" not in state:
+                        state["al"] = [None] * self.history_size
+                    al = state["al"]
+                    for i in range(num_old - 1, -1, -1):
+                        al[i] = self._dot(old_stps[i], q) * ro[i]
+                        self.ctx.axpy(q, old_dirs[i], float(-al[i]))
+                    self.ctx.scale(q, float(H_diag))
+                    d = r = q
+                    for i in range(num_old):
+                        be_i = self._dot(old_dirs[i], r) * ro[i]
+                        self.ctx.axpy(r, old_stps[i], float(al[i] - be_i))
             if prev_flat_grad is None:
                 prev_flat_grad = flat_grad.clone()
             else:
