@@ -287,7 +287,7 @@ hipError_t layernorm_bwd(const LnArgs& a, hipStream_t s) {
 }
 
 // ============================================================================
-// Window attention, 4x4 windows (N = 16 tokens), one wave per (window, head)
+// Window attention, 4x4 windows (N = 16 tokens), one workgroup per (window, chunk of heads)
 // ============================================================================
 constexpr int WN_ = 16;
 
@@ -308,154 +308,187 @@ __device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* 
   return b;
 }
 
-// LDS row stride for a [16][hd] tile: hd + 4 keeps rows 16-B aligned and puts the 16 rows of a
-// ds_read_b128 lane group on distinct 16-B slots (hd % 64 in {0, 32}: (hd+4)/4 is odd).
-__device__ __forceinline__ int attn_ld(int hd) { return hd + 4; }
+// One workgroup (256 threads) per (window, chunk of HPB heads), HPB * hd <= 192: for the LG stage (hd 192) one
+// head per block with the 64 score quads split four ways along d; for the Swin towers (hd 32) all heads of a
+// window per block, so every token row is one contiguous HPB*hd-float load of q, k and v. Tokens of a window
+// are 16 consecutive rows (window order, made by the LayerNorm gather).
+//   scores: entry e = (head hl, row i, column quad jq), DP lanes per entry along d (interleaved 16-B steps),
+//           reduced by xor shuffles; softmax over the 4 jq lanes of a row (same wave)
+//   outputs: item = (token t, head hl, 4 consecutive d), d fastest -> coalesced row writes
+// LDS: rows of HPB*hd + 4 floats (16-B aligned, consecutive rows start 4 banks apart).
+constexpr int kAttnThreads = 256;
 
-__device__ __forceinline__ void attn_load(const float* __restrict__ src, int ldsrc, float* dst, int st, int hd,
-                                          int lane) {
-  const int q4 = hd >> 2;
-  for (int idx = lane; idx < WN_ * q4; idx += 64) {
+struct AttnShape {
+  int hd, hpb, dp, st;  // head dim, heads per block, lanes per score quad, LDS row stride
+};
+__device__ __forceinline__ AttnShape attn_shape(const AttnArgs& a) {
+  AttnShape s;
+  s.hd = a.C / a.heads;
+  s.hpb = a.heads / gridDim.y;
+  const int e = s.hpb * 64;
+  s.dp = e >= kAttnThreads ? 1 : kAttnThreads / e;  // 1, 2 or 4 (e in {64, 128, 192, 256, ...})
+  s.st = s.hpb * s.hd + 4;
+  return s;
+}
+
+// rows [16][n] (n floats from src row t at src + t * ld) -> LDS rows of stride st
+__device__ __forceinline__ void attn_rows(const float* __restrict__ src, int ld, float* dst, int st, int n) {
+  const int q4 = n >> 2;
+  for (int idx = threadIdx.x; idx < WN_ * q4; idx += kAttnThreads) {
     const int t = idx / q4, d = (idx - t * q4) * 4;
-    *reinterpret_cast<f4*>(dst + t * st + d) = *reinterpret_cast<const f4*>(src + (size_t)t * ldsrc + d);
+    *reinterpret_cast<f4*>(dst + t * st + d) = *reinterpret_cast<const f4*>(src + (size_t)t * ld + d);
   }
 }
 
-__global__ __launch_bounds__(64) void k_attn_fwd(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int win = blockIdx.x, h = blockIdx.y;
-  const AttnGroup G = a.g[blockIdx.z];
-  const int lane = threadIdx.x;
-  const int C = a.C, hd = C / a.heads, ldq = 3 * C;
-  const int st = attn_ld(hd);
-  float* q = sm;
-  float* k = q + WN_ * st;
-  float* v = k + WN_ * st;
-  float* p = v + WN_ * st;  // [16][17]
-  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * hd;
-  attn_load(base, ldq, q, st, hd, lane);
-  attn_load(base + C, ldq, k, st, hd, lane);
-  attn_load(base + 2 * C, ldq, v, st, hd, lane);
-  __syncthreads();
-  // S = (q * scale) k^T : lane -> row i, columns j0..j0+3 (swinblock.py:151-152)
-  const int i = lane >> 2, j0 = (lane & 3) * 4;
-  float sv[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int d = 0; d < hd; d += 4) {
-    f4 qd = *reinterpret_cast<const f4*>(q + i * st + d);
+// sv[jj] = sum_d x[i][hl*hd + d] y[j0+jj][hl*hd + d] over this lane's d-part, then over the DP lanes
+__device__ __forceinline__ void attn_quad(const float* x, const float* y, const AttnShape& S, int hl, int i, int j0,
+                                          int dpi, float sv[4]) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) qd[e] *= a.scale;
+  for (int jj = 0; jj < 4; ++jj) sv[jj] = 0.0f;
+  const float* xr = x + i * S.st + hl * S.hd;
+  const float* yr = y + j0 * S.st + hl * S.hd;
+  for (int d = dpi * 4; d < S.hd; d += 4 * S.dp) {
+    const f4 xd = *reinterpret_cast<const f4*>(xr + d);
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const f4 kd = *reinterpret_cast<const f4*>(k + (j0 + jj) * st + d);
-      sv[jj] += qd[0] * kd[0] + qd[1] * kd[1] + qd[2] * kd[2] + qd[3] * kd[3];
+      const f4 yd = *reinterpret_cast<const f4*>(yr + jj * S.st + d);
+      sv[jj] += xd[0] * yd[0] + xd[1] * yd[1] + xd[2] * yd[2] + xd[3] * yd[3];
     }
   }
-  float mx = -INFINITY;
+  for (int o = 1; o < S.dp; o <<= 1)
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    sv[jj] += attn_bias_mask(a, G.table, win, h, i, j0 + jj);
-    mx = fmaxf(mx, sv[jj]);
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 1));
-  mx = fmaxf(mx, __shfl_xor(mx, 2));
-  float sum = 0.f;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    sv[jj] = expf(sv[jj] - mx);
-    sum += sv[jj];
-  }
-  sum += __shfl_xor(sum, 1);
-  sum += __shfl_xor(sum, 2);
-  const float inv = 1.0f / sum;
-  f4 pv;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    pv[jj] = sv[jj] * inv;
-    p[i * 17 + j0 + jj] = pv[jj];
-  }
-  float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
-  *reinterpret_cast<f4*>(Pg + i * WN_ + j0) = pv;
+    for (int jj = 0; jj < 4; ++jj) sv[jj] += __shfl_xor(sv[jj], o);
+}
+
+__global__ __launch_bounds__(kAttnThreads) void k_attn_fwd(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const AttnShape S = attn_shape(a);
+  const int win = blockIdx.x, h0 = blockIdx.y * S.hpb, tid = threadIdx.x;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int C = a.C, ldq = 3 * C, W = S.hpb * S.hd;
+  float* q = sm;
+  float* k = q + WN_ * S.st;
+  float* v = k + WN_ * S.st;
+  float* p = v + WN_ * S.st;  // [hpb][16][17]
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h0 * S.hd;
+  attn_rows(base, ldq, q, S.st, W);
+  attn_rows(base + C, ldq, k, S.st, W);
+  attn_rows(base + 2 * C, ldq, v, S.st, W);
   __syncthreads();
-  // O = P v : lane -> (t, 4 consecutive d)
-  float* ob = G.o + (size_t)win * WN_ * C + h * hd;
-  const int q4 = hd >> 2;
-  for (int idx = lane; idx < WN_ * q4; idx += 64) {
-    const int t = idx / q4, d = (idx - t * q4) * 4;
+  // S = (q k^T) scale + bias + mask -> softmax (swinblock.py:151-168)
+  const int dpi = tid % S.dp;
+  for (int e = tid / S.dp; e < S.hpb * 64; e += kAttnThreads / S.dp) {
+    const int hl = e >> 6, i = (e >> 2) & 15, j0 = (e & 3) * 4, h = h0 + hl;
+    float sv[4];
+    attn_quad(q, k, S, hl, i, j0, dpi, sv);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      sv[jj] = sv[jj] * a.scale + attn_bias_mask(a, G.table, win, h, i, j0 + jj);
+      mx = fmaxf(mx, sv[jj]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, S.dp));
+    mx = fmaxf(mx, __shfl_xor(mx, 2 * S.dp));
+    float sum = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      sv[jj] = expf(sv[jj] - mx);
+      sum += sv[jj];
+    }
+    sum += __shfl_xor(sum, S.dp);
+    sum += __shfl_xor(sum, 2 * S.dp);
+    const float inv = 1.0f / sum;
+    if (dpi == 0) {
+      f4 pv;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        pv[jj] = sv[jj] * inv;
+        p[(hl * WN_ + i) * 17 + j0 + jj] = pv[jj];
+      }
+      *reinterpret_cast<f4*>(G.P + (((size_t)win * a.heads + h) * WN_ + i) * WN_ + j0) = pv;
+    }
+  }
+  __syncthreads();
+  // O = P v
+  float* ob = G.o + (size_t)win * WN_ * C + h0 * S.hd;
+  const int q4 = S.hd >> 2;
+  for (int idx = tid; idx < WN_ * S.hpb * q4; idx += kAttnThreads) {
+    const int t = idx / (S.hpb * q4), r = idx - t * S.hpb * q4, hl = r / q4, d = hl * S.hd + (r - hl * q4) * 4;
+    const float* pr = p + (hl * WN_ + t) * 17;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int jj = 0; jj < WN_; ++jj) {
-      const float pj = p[t * 17 + jj];
-      const f4 vv = *reinterpret_cast<const f4*>(v + jj * st + d);
+      const float pj = pr[jj];
+      const f4 vv = *reinterpret_cast<const f4*>(v + jj * S.st + d);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e] += pj * vv[e];
+      for (int c = 0; c < 4; ++c) acc[c] += pj * vv[c];
     }
     *reinterpret_cast<f4*>(ob + (size_t)t * C + d) = acc;
   }
 }
 
-__global__ __launch_bounds__(64) void k_attn_bwd(AttnArgs a) {
+__global__ __launch_bounds__(kAttnThreads) void k_attn_bwd(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int win = blockIdx.x, h = blockIdx.y;
+  const AttnShape S = attn_shape(a);
+  const int win = blockIdx.x, h0 = blockIdx.y * S.hpb, tid = threadIdx.x;
   const AttnGroup G = a.g[blockIdx.z];
-  const int lane = threadIdx.x;
-  const int C = a.C, hd = C / a.heads, ldq = 3 * C;
-  const int st = attn_ld(hd);
+  const int C = a.C, ldq = 3 * C, W = S.hpb * S.hd;
   float* q = sm;
-  float* k = q + WN_ * st;
-  float* v = k + WN_ * st;
-  float* dO = v + WN_ * st;
-  float* p = dO + WN_ * st;  // [16][17]
-  float* ds = p + WN_ * 17;  // [16][17]
-  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * hd;
-  attn_load(base, ldq, q, st, hd, lane);
-  attn_load(base + C, ldq, k, st, hd, lane);
-  attn_load(base + 2 * C, ldq, v, st, hd, lane);
-  attn_load(G.dO + (size_t)win * WN_ * C + h * hd, C, dO, st, hd, lane);
-  const float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
-  for (int idx = lane; idx < WN_ * WN_; idx += 64) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
+  float* k = q + WN_ * S.st;
+  float* v = k + WN_ * S.st;
+  float* dO = v + WN_ * S.st;
+  float* p = dO + WN_ * S.st;       // [hpb][16][17]
+  float* ds = p + S.hpb * WN_ * 17;  // [hpb][16][17]
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h0 * S.hd;
+  attn_rows(base, ldq, q, S.st, W);
+  attn_rows(base + C, ldq, k, S.st, W);
+  attn_rows(base + 2 * C, ldq, v, S.st, W);
+  attn_rows(G.dO + (size_t)win * WN_ * C + h0 * S.hd, C, dO, S.st, W);
+  const float* Pg = G.P + ((size_t)win * a.heads + h0) * WN_ * WN_;
+  for (int idx = tid; idx < S.hpb * WN_ * WN_; idx += kAttnThreads) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
   __syncthreads();
-  // dP = dO v^T ; dS = P * (dP - rowsum(P * dP))
-  const int i = lane >> 2, j0 = (lane & 3) * 4;
-  float dp[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int d = 0; d < hd; d += 4) {
-    const f4 od = *reinterpret_cast<const f4*>(dO + i * st + d);
+  // dP = dO v^T ; dS = P (dP - rowsum(P dP))
+  const int dpi = tid % S.dp;
+  for (int e = tid / S.dp; e < S.hpb * 64; e += kAttnThreads / S.dp) {
+    const int hl = e >> 6, i = (e >> 2) & 15, j0 = (e & 3) * 4;
+    float dp[4];
+    attn_quad(dO, v, S, hl, i, j0, dpi, dp);
+    const float* pr = p + (hl * WN_ + i) * 17 + j0;
+    float rd = 0.f;
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const f4 vd = *reinterpret_cast<const f4*>(v + (j0 + jj) * st + d);
-      dp[jj] += od[0] * vd[0] + od[1] * vd[1] + od[2] * vd[2] + od[3] * vd[3];
-    }
+    for (int jj = 0; jj < 4; ++jj) rd += pr[jj] * dp[jj];
+    rd += __shfl_xor(rd, S.dp);
+    rd += __shfl_xor(rd, 2 * S.dp);
+    if (dpi == 0)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) ds[(hl * WN_ + i) * 17 + j0 + jj] = pr[jj] * (dp[jj] - rd);
   }
-  float rd = 0.f;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) rd += p[i * 17 + j0 + jj] * dp[jj];
-  rd += __shfl_xor(rd, 1);
-  rd += __shfl_xor(rd, 2);
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) ds[i * 17 + j0 + jj] = p[i * 17 + j0 + jj] * (dp[jj] - rd);
   __syncthreads();
-  // dQ[t] = scale sum_j dS[t][j] k[j] ; dK[t] = scale sum_i dS[i][t] q[i] ; dV[t] = sum_i P[i][t] dO[i]
-  float* gb = G.dqkv + (size_t)win * WN_ * ldq + h * hd;
-  const int q4 = hd >> 2;
-  for (int idx = lane; idx < WN_ * q4; idx += 64) {
-    const int t = idx / q4, d = (idx - t * q4) * 4;
+  // dQ[t] = scale sum_u dS[t][u] k[u] ; dK[t] = scale sum_u dS[u][t] q[u] ; dV[t] = sum_u P[u][t] dO[u]
+  float* gb = G.dqkv + (size_t)win * WN_ * ldq + h0 * S.hd;
+  const int q4 = S.hd >> 2;
+  for (int idx = tid; idx < WN_ * S.hpb * q4; idx += kAttnThreads) {
+    const int t = idx / (S.hpb * q4), r = idx - t * S.hpb * q4, hl = r / q4, d = hl * S.hd + (r - hl * q4) * 4;
+    const float* dsh = ds + hl * WN_ * 17;
+    const float* ph = p + hl * WN_ * 17;
     f4 aq = {0.f, 0.f, 0.f, 0.f}, ak = aq, av = aq;
 #pragma unroll
     for (int u = 0; u < WN_; ++u) {
-      const float s_tu = ds[t * 17 + u], s_ut = ds[u * 17 + t], p_ut = p[u * 17 + t];
-      const f4 kk = *reinterpret_cast<const f4*>(k + u * st + d);
-      const f4 qq = *reinterpret_cast<const f4*>(q + u * st + d);
-      const f4 oo = *reinterpret_cast<const f4*>(dO + u * st + d);
+      const float s_tu = dsh[t * 17 + u], s_ut = dsh[u * 17 + t], p_ut = ph[u * 17 + t];
+      const f4 kk = *reinterpret_cast<const f4*>(k + u * S.st + d);
+      const f4 qq = *reinterpret_cast<const f4*>(q + u * S.st + d);
+      const f4 oo = *reinterpret_cast<const f4*>(dO + u * S.st + d);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        aq[e] += s_tu * kk[e];
-        ak[e] += s_ut * qq[e];
-        av[e] += p_ut * oo[e];
+      for (int c = 0; c < 4; ++c) {
+        aq[c] += s_tu * kk[c];
+        ak[c] += s_ut * qq[c];
+        av[c] += p_ut * oo[c];
       }
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      aq[e] *= a.scale;
-      ak[e] *= a.scale;
+    for (int c = 0; c < 4; ++c) {
+      aq[c] *= a.scale;
+      ak[c] *= a.scale;
     }
     float* row = gb + (size_t)t * ldq + d;
     *reinterpret_cast<f4*>(row) = aq;
@@ -464,24 +497,36 @@ __global__ __launch_bounds__(64) void k_attn_bwd(AttnArgs a) {
   }
 }
 
-hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
-  if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+// heads per block: the largest divisor of heads with hpb * hd <= 192
+static int attn_hpb(const AttnArgs& a) {
   const int hd = a.C / a.heads;
-  if (hd & 3) return hipErrorInvalidValue;
-  const size_t lds = (3 * WN_ * (hd + 4) + WN_ * 17) * sizeof(float);
+  int hpb = 1;
+  for (int c = 1; c <= a.heads; ++c)
+    if (a.heads % c == 0 && c * hd <= 192) hpb = c;
+  return hpb;
+}
+static bool attn_ok(const AttnArgs& a) {
+  if (a.ws != 4 || a.heads <= 0 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return false;
+  const int hd = a.C / a.heads;
+  return (hd & 3) == 0 && hd <= 256;
+}
+
+hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
+  if (!attn_ok(a)) return hipErrorInvalidValue;
+  const int hpb = attn_hpb(a), st = hpb * (a.C / a.heads) + 4;
+  const size_t lds = (3 * WN_ * st + hpb * WN_ * 17) * sizeof(float);
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
+  hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
   prof_end(ph, s, PC_ATTN, 4.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
            4.0 * a.ngroups * ((double)a.nwin * WN_ * 4 * a.C + (double)a.nwin * a.heads * WN_ * WN_));
   return hipGetLastError();
 }
 hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
-  if (a.ws != 4 || a.C % a.heads != 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
-  const int hd = a.C / a.heads;
-  if (hd & 3) return hipErrorInvalidValue;
-  const size_t lds = (4 * WN_ * (hd + 4) + 2 * WN_ * 17) * sizeof(float);
+  if (!attn_ok(a)) return hipErrorInvalidValue;
+  const int hpb = attn_hpb(a), st = hpb * (a.C / a.heads) + 4;
+  const size_t lds = (4 * WN_ * st + 2 * hpb * WN_ * 17) * sizeof(float);
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads, a.ngroups), dim3(64), lds, s, a);
+  hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
   prof_end(ph, s, PC_ATTN, 8.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
            4.0 * a.ngroups * ((double)a.nwin * WN_ * 7 * a.C + (double)a.nwin * a.heads * WN_ * WN_));
   return hipGetLastError();
