@@ -13,6 +13,7 @@
  *   vv_bind_problem               the closure state of one_step_DA 'vae4dvar' (da_4dvar.py:1179-1251)
  *   vv_closure                    closure() -> loss(z); backward (da_4dvar.py:1183-1208, 1242-1246)
  *   vv_decode                     the analysis xa = decoder_hr(z)*stdTr*std + xb (da_4dvar.py:1301-1306)
+ *   vv_set_obs_operator/_augment  the real-observation operator obs_interpolater (da_4dvar.py:62-94, :1196-1206)
  *   vv_integrate                  integrate(x, model, 1) (da_4dvar.py:666-681): the outer-cycle forecast with
  *                                 the 0.25-degree LGUnet_all_1 (da_4dvar.py:1329, :652), forward only
  *   vv_dot/axpy/... , vv_adam     vector arithmetic of torch/optim/lbfgs.py:333-535 and adam.py
@@ -106,6 +107,16 @@ int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
    x, out (C,Hs,Ws); mean, std (C). The model (either arch, batch 1) must map C channels to >= C. */
 int vv_integrate(vv_ctx* ctx, int model_id, const float* x, float* out, int C, int Hs, int Ws, const float* mean,
                  const float* std_, int steps, void* stream);
+/* real-observation operator (da_4dvar.py:62-94 obs_interpolater; the loss's x_aug, :1196-1206): after
+   vv_bind_problem, the bound yo, Hmask, R become (T, 4 + 5*n_out, Hs, Ws) observation-space fields. Channels 0..3
+   are observed directly; for each of the five 13-level variables i (z, q, u, v, t) x_aug[4 + n_out*i + o] =
+   sum_j interp[o][j] x[4 + n_in*i + j]. interp: (n_out, n_in) fp32, host or device, copied. Needs C = 4 + 5*n_in,
+   n_in <= 16, n_out <= 64; n_out = 0 restores the identity operator (synthetic observations). */
+int vv_set_obs_operator(vv_ctx* ctx, int n_out, int n_in, const float* interp);
+/* x_aug (T, 4 + 5*n_out, Hs, Ws) = the operator applied to x (T, 4 + 5*n_in, Hs, Ws); interp on the device.
+   Also get_R_matrix_from_gt (da_4dvar.py:729-756) when applied to R. */
+int vv_obs_augment(vv_ctx* ctx, const float* interp, int n_out, int n_in, const float* x, float* x_aug, int T,
+                   int Hs, int Ws, void* stream);
 /* trajectory x_t (T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
 int vv_state_ptr(vv_ctx* ctx, const float** x);
 

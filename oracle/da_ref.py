@@ -6,6 +6,9 @@ vae4dvar inner loop of `da_4dvar.py`.
   integrate      da_4dvar.py:666-681 (interpolation=True, detach=False)
   one_step_DA    da_4dvar.py:1179-1306 (vae4dvar branch, without the CPU
                  metric logging of :1256-1269)
+  x_aug          da_4dvar.py:1196-1206 (obs_type 'real*': F.linear of each
+                 13-level variable by obs_interpolater.interp, :62-94)
+  R_aug          get_R_matrix_from_gt, da_4dvar.py:729-756
   decoder_hr     nf_model/vae.py:87-90, with the target grid parametrised
                  (the reference hard-codes 721x1440; at 128x256 every
                  nearest interpolation is the identity, SURVEY §8 d)
@@ -26,11 +29,41 @@ def oracle_problem(prob, dec_p, dec_cfg, flow_p=None, flow_cfg=None, obs_coeff=1
     """RefProblem over the oracle's own network restatement."""
     dec_fn = lambda z: lgunet_forward(dec_p, dec_cfg, z)
     flow_fn = (lambda x: lgunet_forward(flow_p, flow_cfg, x)) if flow_p is not None else None
-    return RefProblem(prob, dec_fn, dec_cfg["img_size"], flow_fn, obs_coeff)
+    return RefProblem(prob, dec_fn, dec_cfg["img_size"], flow_fn, obs_coeff, interp=prob.get("interp"))
+
+
+def obs_interp_ref(dim_in=13, dim_out=40):
+    """obs_interpolater.get_interp / get_interp_inv (da_4dvar.py:62-94), torch fp32 matrices."""
+    import numpy as np
+
+    hl = [50, 100, 150, 200, 250, 300, 400, 500, 600, 700, 850, 925, 1000]
+    hn = np.round(np.exp(np.linspace(3.91202301, 6.90775528, dim_out)))
+
+    def table(a, b):
+        m = torch.zeros(len(a), len(b))
+        for i in range(len(a)):
+            for j in range(len(b)):
+                if a[i] == b[j]:
+                    m[i, j] = 1
+                elif a[i] > b[j] and a[i] < b[j + 1]:
+                    m[i, j] = (np.log(b[j + 1]) - np.log(a[i])) / (np.log(b[j + 1]) - np.log(b[j]))
+                    m[i, j + 1] = (np.log(a[i]) - np.log(b[j])) / (np.log(b[j + 1]) - np.log(b[j]))
+        return m
+
+    return table(hn, hl), table(hl, hn)
+
+
+def x_aug_ref(x_pred, interp, nlev=13):
+    """da_4dvar.py:1196-1206 on (T, 69, H, W)."""
+    parts = [x_pred[:, :4]]
+    for i in range(5):
+        mat = x_pred[:, 4 + i * nlev:4 + (i + 1) * nlev]
+        parts.append(F.linear(mat.transpose(1, 3), interp).transpose(1, 3))
+    return torch.cat(parts, 1)
 
 
 class RefProblem:
-    def __init__(self, prob: dict, dec_fn, lat, flow_fn=None, obs_coeff: float = 1.0):
+    def __init__(self, prob: dict, dec_fn, lat, flow_fn=None, obs_coeff: float = 1.0, interp=None):
         """dec_fn(z) / flow_fn(x): the decoder and flow networks (the oracle's
         `lgunet_forward` restatement, or the reference modules themselves
         when make_golden.py pins this restatement)."""
@@ -43,6 +76,7 @@ class RefProblem:
         self.dec_fn, self.flow_fn = dec_fn, flow_fn
         self.obs_coeff = obs_coeff
         self.lat = tuple(lat)
+        self.interp = None if interp is None else t(interp)
 
     def decoder_hr(self, z):
         x = self.dec_fn(z)
@@ -68,6 +102,8 @@ class RefProblem:
     def loss_terms(self, z):
         loss_reg = torch.sum(z ** 2) / 2
         xp = self.trajectory(z)
+        if self.interp is not None:
+            xp = x_aug_ref(xp, self.interp)
         loss_obs = torch.sum(self.H * (xp - self.yo) ** 2 / self.R) / 2
         return loss_reg, loss_obs
 

@@ -15,6 +15,9 @@ are stored):
   g5b_tiny_4dvar.npz    tiny decoder + tiny flow, T=2: J terms and dJ/dz of one closure
   g6_one_step_da_c5.npz G6 (--g6, ~5 min): the genuine cyclic_4dvar.one_step_DA(..., 'vae4dvar') at 721x1440, T=2,
                         Nit=1 (config 5): printed J per outer pass, sampled xa + sums
+  g8_real_obs.npz       G8 (--g8, ~3 min): the genuine obs_interpolater(13, 40) matrices, get_R_matrix_from_gt on a
+                        small R, and cyclic_4dvar.one_step_DA(..., 'vae4dvar') with obs_type 'real' at 721x1440,
+                        T=1, Nit=1 (J per outer pass, sampled xa)
   g7_tiny_lgunet1.npz   G7: tiny networks.LGUnet_all_1 (RoPE, -inf mask, global LG window, 3 levels): out
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
                         and one config-2 closure (J_b, J_o, sampled dJ/dz)
@@ -302,11 +305,81 @@ def g6(tr):
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
 
+def g8(tr):
+    """G8: the real-observation operator of the genuine reference — obs_interpolater (da_4dvar.py:
+    62-94), get_R_matrix_from_gt (:729-756) and the vae4dvar loss with x_aug (:1196-1206) inside the genuine
+    one_step_DA at 721x1440, T=1, Nit=1, on make_real_problem(seed=20250622) inputs and synthetic weights."""
+    import contextlib
+    import importlib
+    import io
+    import re
+
+    from torch.overrides import TorchFunctionMode
+    from vaevar.problem import make_real_problem
+
+    class CPUMode(TorchFunctionMode):
+        def __torch_function__(self, func, types, args=(), kwargs=None):
+            kwargs = dict(kwargs or {})
+            if "device" in kwargs and kwargs["device"] is not None and str(kwargs["device"]).startswith("cuda"):
+                kwargs["device"] = "cpu"
+            return func(*args, **kwargs)
+
+    cwd = os.getcwd()
+    os.chdir(ref_harness.REF)
+    da = importlib.import_module("da_4dvar")
+    metrics = importlib.import_module("utils.metrics")
+    vae_mod = importlib.import_module("nf_model.vae")
+    vae = vae_mod.VAE_lr("parameters0_old")
+    os.chdir(cwd)
+    old_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *args, **kw: self
+    try:
+        oi = da.obs_interpolater(13, 40)
+        interp, interp_inv = oi.interp.numpy().copy(), oi.interp_inv.numpy().copy()
+        # get_R_matrix_from_gt on a small spatially varying R (T=2, 69, 4, 8)
+        a = object.__new__(da.cyclic_4dvar)
+        a.nlev, a.obs_interp = 13, oi
+        rs = make_problem(nch=69, Hs=4, Ws=8, T=2, seed=811)["R"]
+        rs = (rs * (1.0 + 0.5 * smooth_field(812, rs.shape, sigma=1.0) ** 2)).astype(np.float32)
+        a.static_info = {"R": torch.from_numpy(rs)}
+        r_aug = a.get_R_matrix_from_gt(None, None).numpy().copy()
+        # the genuine one_step_DA with obs_type 'real'
+        dec_p = synth_params(C.DECODER)
+        missing, unexpected = vae.dec.load_state_dict(dec_p, strict=False)
+        assert not unexpected and all(k.endswith(("relative_position_index", "attn_mask")) for k in missing)
+        b = object.__new__(da.cyclic_4dvar)
+        b.device = "cpu"
+        b.da_win, b.obs_type, b.obs_coeff, b.Nit, b.use_eval = 1, "real", 1.0, 1, False
+        b.nchannel, b.nlev, b.nlat, b.nlon, b.current_time = 69, 13, 721, 1440, "G8"
+        b.metric = metrics.Metrics()
+        b.metrics_list = {"bg_wrmse": [], "bg_bias": [], "ana_wrmse": [], "ana_bias": []}
+        b.model_mean, b.model_std, b.model_mean_gpu, b.model_std_gpu = b.get_model_mean_std()
+        b.vae, b.obs_interp = vae, oi
+        prob = make_real_problem(Hs=721, Ws=1440, T=1, seed=20250622)
+        t = lambda k: torch.from_numpy(prob[k])
+        buf = io.StringIO()
+        t0 = time.time()
+        with CPUMode(), contextlib.redirect_stdout(buf):
+            xa = b.one_step_DA(t("gt"), t("xb"), t("yo"), t("H"), t("R"), "vae4dvar")
+    finally:
+        torch.Tensor.cuda = old_cuda
+    log = buf.getvalue()
+    J = [(float(m.group(1)), float(m.group(2))) for m in re.finditer(r"loss reg: ([-0-9.e+]+) loss obs: ([-0-9.e+]+)", log)]
+    xa = xa.detach().numpy().astype(np.float32)
+    idx = sample_idx(xa.size, 8192, 808)
+    flat = xa.reshape(-1).astype(np.float64)
+    print(f"G8 real-obs one_step_DA 721x1440 T=1 Nit=1: {time.time() - t0:.0f}s, J per pass {J}")
+    np.savez(os.path.join(GOLD, "g8_real_obs.npz"), interp=interp, interp_inv=interp_inv, r_aug=r_aug, J=np.array(J),
+             idx_xa=idx, xa_sample=xa.reshape(-1)[idx], xa_sum=flat.sum(),
+             dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also generate G3 (full decoder, ~1 min)")
     ap.add_argument("--only", default=None)
     ap.add_argument("--g6", action="store_true", help="also generate G6 (genuine one_step_DA at 721x1440, ~5 min)")
+    ap.add_argument("--g8", action="store_true", help="also generate G8 (genuine real-obs one_step_DA, ~3 min)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.set_num_threads(8)
@@ -319,6 +392,8 @@ def main():
         steps["g3"] = lambda: g3(tr)
     if a.g6:
         steps["g6"] = lambda: g6(tr)
+    if a.g8:
+        steps["g8"] = lambda: g8(tr)
     for k, f in steps.items():
         if a.only and k not in a.only.split(","):
             continue

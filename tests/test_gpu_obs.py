@@ -1,0 +1,104 @@
+"""Real-observation operator on the GPU (obs_interpolater da_4dvar.py:62-94, the loss's x_aug
+:1196-1206, get_R_matrix_from_gt :729-756) through the C-ABI, against the oracle restatement (oracle/da_ref.py,
+pinned to the genuine reference by G8 in tests/test_oracle_golden.py) and against the genuine one_step_DA (G8).
+Tolerances as tests/test_gpu_parity.py."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLD
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+@pytest.fixture(scope="module")
+def full_dec():
+    from vaevar import config as C
+    from vaevar.engine import LGUnet
+
+    return LGUnet(C.DECODER, 1, 1).load_synthetic()
+
+
+def test_obs_augment_kernel(full_dec):
+    """vv_obs_augment == F.linear over the level axis (x_aug_ref), ragged grid, T=2, and on R (R_aug)."""
+    from oracle.da_ref import obs_interp_ref, x_aug_ref
+    from vaevar.engine import obs_augment
+    from vaevar.synth import smooth_field
+
+    interp, _ = obs_interp_ref(13, 40)
+    x = torch.from_numpy(3.0 * smooth_field(71, (2, 69, 33, 47), sigma=2.0))
+    xa = obs_augment(full_dec.ctx, interp.cuda(), x.cuda()).cpu()
+    ref = x_aug_ref(x, interp)
+    assert xa.shape == (2, 204, 33, 47)
+    assert rel(xa, ref) < 1e-6
+    assert torch.equal(xa[:, :4], x[:, :4])
+    # a coarser operator (n_out = 7) through the same kernel
+    i7, _ = obs_interp_ref(13, 7)
+    assert rel(obs_augment(full_dec.ctx, i7.cuda(), x.cuda()).cpu(), x_aug_ref(x, i7)) < 1e-6
+
+
+@pytest.mark.parametrize("T", [1, 2])
+def test_real_obs_closure(full_dec, T):
+    """One closure (J + dJ/dz) with the real-observation operator at 128x256 (T=2 adds the flow stand-in, so the
+    operator's gradient also travels through the adjoint of integrate) vs the oracle on CPU."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.engine import DAProblem, LGUnet
+    from vaevar.problem import make_real_problem
+    from vaevar.synth import smooth_field
+
+    p = make_real_problem(Hs=128, Ws=256, T=T, seed=20250623, obs_frac=0.05)
+    flow = LGUnet(C.FLOW, 1, 1).load_synthetic() if T > 1 else None
+    prob = DAProblem(full_dec, p, flow=flow)
+    z = torch.from_numpy(0.3 * smooth_field(406, (1, 32, 128, 256)))
+    g = torch.empty(1, 32, 128, 256, device="cuda")
+    jb, jo = prob.closure(z.cuda(), g)
+    torch.set_num_threads(16)
+    ro = oracle_problem(p, synth_params(C.DECODER), C.DECODER, synth_params(C.FLOW) if T > 1 else None,
+                        C.FLOW if T > 1 else None)
+    zr = z.clone().requires_grad_(True)
+    rb, rob = ro.loss_terms(zr)
+    (rb + rob).backward()
+    e_j = abs(jo - float(rob)) / abs(float(rob))
+    e_g = rel(g.cpu(), zr.grad)
+    print(f"real-obs closure T={T}: J_o {jo:.6e} (oracle {float(rob):.6e}, rel {e_j:.2e}), grad rel {e_g:.2e}")
+    assert e_j < 1e-4 and e_g < 1e-4
+    # the identity operator still rejects observation-space fields
+    with pytest.raises(ValueError):
+        DAProblem(full_dec, dict(p, interp=None), flow=flow)
+
+
+def test_one_step_da_real_obs_g8(full_dec):
+    """obs_type 'real' end to end against the GENUINE reference (G8: cyclic_4dvar.one_step_DA on CPU at
+    721x1440, T=1, Nit=1, same synthetic weights/inputs): J per outer pass (4 printed digits) and xa."""
+    path = os.path.join(GOLD, "g8_real_obs.npz")
+    if not os.path.exists(path):
+        pytest.skip("G8 fixture not generated (oracle/make_golden.py --g8)")
+    from vaevar.da import one_step_da
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_real_problem
+
+    g = np.load(path)
+    prob_np = make_real_problem(Hs=721, Ws=1440, T=1, seed=20250622)
+    assert np.array_equal(prob_np["interp"], g["interp"])
+    prob = DAProblem(full_dec, prob_np)
+    res = one_step_da(prob, nit=1)
+    J = np.array(res["J"], np.float64)
+    eJ = float(np.abs(J - g["J"]).max() / np.abs(g["J"]).max())
+    xa = res["xa"].cpu().numpy().reshape(-1).astype(np.float64)
+    s = xa[g["idx_xa"]]
+    e_xa = float(np.linalg.norm(s - g["xa_sample"]) / np.linalg.norm(g["xa_sample"]))
+    dx = float(((xa - prob_np["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+    e_dx = abs(dx - float(g["dxa_sumsq"])) / float(g["dxa_sumsq"])
+    print(f"G8 real-obs one_step_DA: J per pass {J.tolist()} vs {g['J'].tolist()} (rel {eJ:.1e}); "
+          f"xa rel-L2 {e_xa:.1e}; |xa-xb|^2 rel {e_dx:.1e}; evals {res['n_eval']}")
+    assert eJ < 1e-3 and e_xa < 1e-3 and e_dx < 1e-2

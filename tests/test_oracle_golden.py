@@ -140,3 +140,39 @@ def test_g7_tiny_lgunet1_oracle():
     with torch.no_grad():
         y = lgunet1_forward(synth_params(cfg), cfg, x)
     assert rel(y, g["out"]) < 1e-6
+
+
+def _g8():
+    path = os.path.join(GOLD, "g8_real_obs.npz")
+    if not os.path.exists(path):
+        pytest.skip("G8 fixture not generated (oracle/make_golden.py --g8)")
+    return np.load(path)
+
+
+def test_g8_obs_interpolater_matrices():
+    """obs_interpolater(13, 40) (da_4dvar.py:62-94): the oracle's and the product host's restatements equal the
+    genuine reference's interp / interp_inv bit for bit."""
+    from oracle.da_ref import obs_interp_ref
+    from vaevar.problem import ObsInterpolater
+
+    g = _g8()
+    a, b = obs_interp_ref(13, 40)
+    o = ObsInterpolater(13, 40)
+    assert np.array_equal(a.numpy(), g["interp"]) and np.array_equal(b.numpy(), g["interp_inv"])
+    assert np.array_equal(o.interp, g["interp"]) and np.array_equal(o.interp_inv, g["interp_inv"])
+
+
+def test_g8_r_matrix_from_gt():
+    """get_R_matrix_from_gt (da_4dvar.py:729-756) on the G8 small R: oracle x_aug_ref (F.linear, as the reference)
+    bit-exact; the host generator's einsum within fp32 rounding."""
+    from oracle.da_ref import x_aug_ref
+    from vaevar.problem import make_problem, obs_augment_np
+    from vaevar.synth import smooth_field
+
+    g = _g8()
+    rs = make_problem(nch=69, Hs=4, Ws=8, T=2, seed=811)["R"]
+    rs = (rs * (1.0 + 0.5 * smooth_field(812, rs.shape, sigma=1.0) ** 2)).astype(np.float32)
+    ra = x_aug_ref(torch.from_numpy(rs), torch.from_numpy(g["interp"])).numpy()
+    assert np.array_equal(ra, g["r_aug"])
+    rn = obs_augment_np(g["interp"], rs)
+    assert np.abs(rn - g["r_aug"]).max() <= 1e-6 * np.abs(g["r_aug"]).max()

@@ -260,6 +260,11 @@ struct Problem {
   float *X, *dec_out, *gdec, *prod, *FI, *FO, *GFO, *GFI, *carry;
   double *partial, *dJ;
   int nblk = 1024;
+  // real-observation operator (vv_set_obs_operator): nout = 0 is the identity (synthetic observations)
+  int nin = 0, nout = 0;
+  std::unique_ptr<Arena> obs_arena;
+  float *Pobs = nullptr, *GOBS = nullptr;  // [nout][nin] ; (T,C,Hs,Ws) observation-term gradient
+  size_t obs_hw() const { return (size_t)(nout ? 4 + 5 * nout : C) * Hs * Ws; }  // floats per time of yo/Hm/R
 };
 
 }  // namespace
@@ -981,6 +986,27 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
 // ----------------------------------------------------------------------------
 // closure  (da_4dvar.py:1183-1208 loss(z) + backward)
 // ----------------------------------------------------------------------------
+// the observation term of time t under the real-observation operator (no-op for the identity operator):
+// J partials of slot t and the state-space gradient GOBS[t] (da_4dvar.py:1196-1207)
+hipError_t obs_term(const Problem& P, int t, hipStream_t st) {
+  if (!P.nout) return hipSuccess;
+  const size_t HW = (size_t)P.Hs * P.Ws, OHW = P.obs_hw();
+  ObsArgs oa;
+  oa.nin = P.nin;
+  oa.nout = P.nout;
+  oa.HW = (int)HW;
+  oa.P = P.Pobs;
+  oa.x = P.X + t * P.C * HW;
+  oa.yo = P.yo + t * OHW;
+  oa.Hm = P.Hm + t * OHW;
+  oa.R = P.R + t * OHW;
+  oa.coeff = P.obs_coeff;
+  oa.g_obs = P.GOBS + t * P.C * HW;
+  oa.partial = P.partial + (size_t)t * P.nblk;
+  oa.nblk = P.nblk;
+  return obs_misfit(oa, st);
+}
+
 void set_maps(const Problem& P, MisfitArgs& m) {
   m.Hl = P.Hl;
   m.Wl = P.Wl;
@@ -1017,7 +1043,10 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   ma.std_ = P.std_;
   ma.partial = P.partial;
   ma.nblk = P.nblk;
+  const size_t OHW = P.obs_hw();
+  if (P.nout) ma.Hm = nullptr;  // J from the observation operator below
   CK(misfit_fwd(ma, st));
+  CK(obs_term(P, 0, st));
   if (P.T > 1 && P.interp) CK(flow_input(P.X, P.FI, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
   for (int t = 1; t < P.T; ++t) {
     // x_t = integrate(x_{t-1}) = flow((x - mean)/std)[:C]*std + mean   (da_4dvar.py:666-681)
@@ -1028,13 +1057,14 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     mt.scale2 = nullptr;
     mt.xb = nullptr;
     mt.offset = P.mean;
-    mt.yo = P.yo + t * CHW;
-    mt.Hm = P.Hm + t * CHW;
-    mt.R = P.R + t * CHW;
+    mt.yo = P.yo + t * OHW;
+    mt.Hm = P.nout ? nullptr : P.Hm + t * OHW;
+    mt.R = P.R + t * OHW;
     mt.x_out = P.X + t * CHW;
     mt.flow_in = t < P.T - 1 ? P.FI + t * CHWl : nullptr;
     mt.partial = P.partial + (size_t)t * P.nblk;
     CK(misfit_fwd(mt, st));
+    CK(obs_term(P, t, st));
     if (t < P.T - 1 && P.interp)
       CK(flow_input(P.X + t * CHW, P.FI + t * CHWl, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
   }
@@ -1055,9 +1085,10 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     mb.ri0 = P.interp ? P.ri0 : nullptr;
     mb.rj0 = P.interp ? P.rj0 : nullptr;
     mb.x = P.X + t * CHW;
-    mb.yo = P.yo + t * CHW;
-    mb.Hm = P.Hm + t * CHW;
-    mb.R = P.R + t * CHW;
+    mb.yo = P.yo + t * OHW;
+    mb.Hm = P.Hm + t * OHW;
+    mb.R = P.R + t * OHW;
+    mb.g_obs = P.nout ? P.GOBS + t * CHW : nullptr;
     mb.g_carry = carry;
     mb.coeff = P.obs_coeff;
     mb.scale = P.std_;
@@ -1084,6 +1115,7 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   mb.yo = P.yo;
   mb.Hm = P.Hm;
   mb.R = P.R;
+  mb.g_obs = P.nout ? P.GOBS : nullptr;
   mb.g_carry = carry;
   mb.coeff = P.obs_coeff;
   mb.scale = P.prod;
@@ -1455,10 +1487,49 @@ int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream) {
   ma.yo = P.yo;
   ma.Hm = P.Hm;
   ma.R = P.R;
+  ma.Hm = nullptr;  // the analysis only: no misfit
   ma.x_out = xa;
   ma.partial = P.partial;
   ma.nblk = P.nblk;
   CK(misfit_fwd(ma, st));
+  return 0;
+}
+
+int vv_set_obs_operator(vv_ctx* ctx, int n_out, int n_in, const float* interp) {
+  if (!ctx) return fail(VV_E_ARG, "null context");
+  Problem& P = ctx->prob;
+  if (!P.bound) return fail(VV_E_STATE, "vv_bind_problem first");
+  int r = set_dev(ctx);
+  if (r) return r;
+  if (n_out == 0) {
+    P.nout = P.nin = 0;
+    return 0;
+  }
+  if (!interp) return fail(VV_E_ARG, "null interp");
+  if (n_in < 1 || n_in > vv::kObsMaxIn || n_out < 1 || n_out > vv::kObsMaxOut)
+    return fail(VV_E_ARG, "operator %dx%d outside 1..%d x 1..%d", n_out, n_in, vv::kObsMaxOut, vv::kObsMaxIn);
+  if (P.C != 4 + 5 * n_in) return fail(VV_E_ARG, "state has %d channels, the operator needs 4 + 5*%d", P.C, n_in);
+  const size_t CHW = (size_t)P.C * P.Hs * P.Ws;
+  const size_t nP = Arena::up((size_t)n_out * n_in * sizeof(float));
+  P.obs_arena = std::make_unique<Arena>();
+  P.obs_arena->cap = nP + CHW * P.T * sizeof(float);
+  if (hipMalloc(&P.obs_arena->base, P.obs_arena->cap) != hipSuccess) return fail(VV_E_ALLOC, "observation operator");
+  P.Pobs = reinterpret_cast<float*>(P.obs_arena->base);
+  P.GOBS = reinterpret_cast<float*>(P.obs_arena->base + nP);
+  VV_HIP(hipMemcpy(P.Pobs, interp, (size_t)n_out * n_in * sizeof(float), hipMemcpyDefault));
+  P.nin = n_in;
+  P.nout = n_out;
+  return 0;
+}
+
+int vv_obs_augment(vv_ctx* ctx, const float* interp, int n_out, int n_in, const float* x, float* x_aug, int T,
+                   int Hs, int Ws, void* stream) {
+  if (!ctx || !interp || !x || !x_aug) return fail(VV_E_ARG, "null argument");
+  if (n_in < 1 || n_in > vv::kObsMaxIn || n_out < 1 || n_out > vv::kObsMaxOut || T < 1 || Hs < 1 || Ws < 1)
+    return fail(VV_E_ARG, "bad operator / field shape");
+  int r = set_dev(ctx);
+  if (r) return r;
+  VV_HIP(vv::obs_augment(interp, n_in, n_out, x, x_aug, T, Hs * Ws, (hipStream_t)stream));
   return 0;
 }
 

@@ -199,6 +199,8 @@ struct MisfitBwdArgs {
   const int* ri0; const int* rj0; const int* mi; const int* mj;
   const float* x; const float* yo; const float* Hm; const float* R;
   const float* g_carry;   // null or (C,Hs,Ws) gradient arriving from later times
+  const float* g_obs;     // null, or (C,Hs,Ws) observation-term gradient already formed (real-obs operator);
+                          // then it replaces coeff*H*(x-yo)/R and yo/Hm/R are not read
   float coeff;
   const float* scale;     // [C]
   float* g_net;           // (C', Hl, Wl) first C channels written, the rest zero-filled
@@ -206,6 +208,25 @@ struct MisfitBwdArgs {
   float* g_state;         // scratch (C,Hs,Ws) (needed when maps are not identity)
 };
 hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s);
+// real-observation operator (da_4dvar.py:62-94 obs_interpolater, loss x_aug :1196-1206): the state (C,HW),
+// C = 4 + 5*nin, maps to Ca = 4 + 5*nout observation channels: channels 0..3 directly, and for each of the five
+// pressure-level variables i, x_aug[4 + nout*i + o] = sum_j P[o][j] x[4 + nin*i + j] (F.linear over the level axis)
+struct ObsArgs {
+  int nin, nout, HW;
+  const float* P;       // [nout][nin] (obs_interpolater.interp)
+  const float* x;       // (C, HW) state
+  const float* yo;      // (Ca, HW)
+  const float* Hm;
+  const float* R;
+  float coeff;
+  float* g_obs;         // (C, HW): coeff * Op^T (H (Op x - yo) / R)
+  double* partial;      // per-block partial sums of H (Op x - yo)^2 / R
+  int nblk;
+};
+constexpr int kObsMaxIn = 16, kObsMaxOut = 64;
+hipError_t obs_misfit(const ObsArgs& a, hipStream_t s);
+// x_aug (T, Ca, HW) = Op x (T, C, HW) for T fields (also get_R_matrix_from_gt, da_4dvar.py:729-756, on R)
+hipError_t obs_augment(const float* P, int nin, int nout, const float* x, float* x_aug, int T, int HW, hipStream_t s);
 // general (nearest-interpolated) grids, F.interpolate mode='nearest' (quirk Q3):
 //   flow_in[c][a][b] = (x[c][di[a]][dj[b]] - mean[c]) / std[c]          (integrate: down-sample, da_4dvar.py:668-671)
 hipError_t flow_input(const float* x, float* flow_in, const int* di, const int* dj, const float* mean,

@@ -759,8 +759,10 @@ __global__ __launch_bounds__(256) void k_misfit_fwd(MisfitArgs a) {
     if (a.offset) v = v + a.offset[c];
     a.x_out[id] = v;
     if (a.flow_in && !a.mi) a.flow_in[id] = (v - a.mean[c]) / a.std_[c];
-    const float d = v - a.yo[id];
-    acc += (double)((a.Hm[id] * (d * d)) / a.R[id]);
+    if (a.Hm) {
+      const float d = v - a.yo[id];
+      acc += (double)((a.Hm[id] * (d * d)) / a.R[id]);
+    }
   }
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[blockIdx.x] = t;
@@ -772,7 +774,7 @@ __global__ __launch_bounds__(256) void k_misfit_bwd(MisfitBwdArgs a) {
   for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
     const int c = id / HW;
     const int p = id - c * HW;
-    float g = a.coeff * ((a.Hm[id] * (a.x[id] - a.yo[id])) / a.R[id]);
+    float g = a.g_obs ? a.g_obs[id] : a.coeff * ((a.Hm[id] * (a.x[id] - a.yo[id])) / a.R[id]);
     if (a.g_carry) g += a.g_carry[id];
     a.g_net[(size_t)c * HW + p] = g * a.scale[c];
   }
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(256) void k_misfit_bwd_gather(MisfitBwdArgs a) {
     for (int i = a.ri0[ra]; i < a.ri0[ra + 1]; ++i)
       for (int j = a.rj0[cb]; j < a.rj0[cb + 1]; ++j) {
         const size_t e = (size_t)c * HW + (size_t)i * a.Ws + j;
-        float v = a.coeff * ((a.Hm[e] * (a.x[e] - a.yo[e])) / a.R[e]);
+        float v = a.g_obs ? a.g_obs[e] : a.coeff * ((a.Hm[e] * (a.x[e] - a.yo[e])) / a.R[e]);
         if (a.g_carry) v += a.g_carry[e];
         g += v;
       }
@@ -859,6 +861,95 @@ hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_misfit_bwd, dim3(1024), dim3(256), 0, s, a);
   }
   prof_end(ph, s, PC_MISFIT, 5.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * (a.g_carry ? 6 : 5));
+  return hipGetLastError();
+}
+
+// real-observation operator: one thread per pixel holds the pixel's 13-level column of each variable in
+// registers; every state and observation channel is read once, coalesced along the pixel axis. J partials in
+// fp64 (deterministic block order, as k_misfit_fwd), the gradient formed in the same pass.
+__global__ __launch_bounds__(256) void k_obs_misfit(ObsArgs a) {
+  __shared__ float Ps[kObsMaxOut * kObsMaxIn];
+  __shared__ double red[4];
+  const int nin = a.nin, nout = a.nout, HW = a.HW;
+  for (int i = threadIdx.x; i < nout * nin; i += 256) Ps[i] = a.P[i];
+  __syncthreads();
+  double acc = 0.0;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const size_t e = (size_t)c * HW + p;
+      const float d = a.x[e] - a.yo[e];
+      acc += (double)((a.Hm[e] * (d * d)) / a.R[e]);
+      a.g_obs[e] = a.coeff * ((a.Hm[e] * d) / a.R[e]);
+    }
+    for (int v = 0; v < 5; ++v) {
+      float xs[kObsMaxIn], gs[kObsMaxIn];
+#pragma unroll
+      for (int j = 0; j < kObsMaxIn; ++j) {
+        xs[j] = j < nin ? a.x[(size_t)(4 + nin * v + j) * HW + p] : 0.0f;
+        gs[j] = 0.0f;
+      }
+      for (int o = 0; o < nout; ++o) {
+        const float* pr = Ps + o * nin;
+        float y = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kObsMaxIn; ++j)
+          if (j < nin) y += pr[j] * xs[j];
+        const size_t e = (size_t)(4 + nout * v + o) * HW + p;
+        const float d = y - a.yo[e], h = a.Hm[e], r = a.R[e];
+        acc += (double)((h * (d * d)) / r);
+        const float g = a.coeff * ((h * d) / r);
+#pragma unroll
+        for (int j = 0; j < kObsMaxIn; ++j)
+          if (j < nin) gs[j] += pr[j] * g;
+      }
+#pragma unroll
+      for (int j = 0; j < kObsMaxIn; ++j)
+        if (j < nin) a.g_obs[(size_t)(4 + nin * v + j) * HW + p] = gs[j];
+    }
+  }
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) a.partial[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_obs_augment(const float* P, int nin, int nout, const float* x, float* xa,
+                                                     int HW) {
+  __shared__ float Ps[kObsMaxOut * kObsMaxIn];
+  for (int i = threadIdx.x; i < nout * nin; i += 256) Ps[i] = P[i];
+  __syncthreads();
+  const float* xt = x + (size_t)blockIdx.y * (4 + 5 * nin) * HW;
+  float* yt = xa + (size_t)blockIdx.y * (4 + 5 * nout) * HW;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) yt[(size_t)c * HW + p] = xt[(size_t)c * HW + p];
+    for (int v = 0; v < 5; ++v) {
+      float xs[kObsMaxIn];
+#pragma unroll
+      for (int j = 0; j < kObsMaxIn; ++j) xs[j] = j < nin ? xt[(size_t)(4 + nin * v + j) * HW + p] : 0.0f;
+      for (int o = 0; o < nout; ++o) {
+        float y = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kObsMaxIn; ++j)
+          if (j < nin) y += Ps[o * nin + j] * xs[j];
+        yt[(size_t)(4 + nout * v + o) * HW + p] = y;
+      }
+    }
+  }
+}
+
+hipError_t obs_misfit(const ObsArgs& a, hipStream_t s) {
+  if (a.nin < 1 || a.nin > kObsMaxIn || a.nout < 1 || a.nout > kObsMaxOut) return hipErrorInvalidValue;
+  const int ph = prof_begin(s);
+  hipLaunchKernelGGL(k_obs_misfit, dim3(a.nblk), dim3(256), 0, s, a);
+  const double ca = 4.0 + 5.0 * a.nout, cs = 4.0 + 5.0 * a.nin;
+  prof_end(ph, s, PC_MISFIT, (4.0 * 5 * a.nin * a.nout + 8.0 * ca) * a.HW, 4.0 * a.HW * (3 * ca + 2 * cs));
+  return hipGetLastError();
+}
+hipError_t obs_augment(const float* P, int nin, int nout, const float* x, float* x_aug, int T, int HW,
+                       hipStream_t s) {
+  if (nin < 1 || nin > kObsMaxIn || nout < 1 || nout > kObsMaxOut || T < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_obs_augment, dim3(std::min((HW + 255) / 256, 2048), T), dim3(256), 0, s, P, nin, nout, x, x_aug,
+                     HW);
   return hipGetLastError();
 }
 

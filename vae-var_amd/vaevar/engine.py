@@ -260,20 +260,35 @@ class VAE_lr:
 class DAProblem:
     """The vae4dvar closure (da_4dvar.py:1183-1208) bound to device buffers; evaluated by libvaevar."""
 
-    def __init__(self, dec: LGUnet, prob: dict, flow: LGUnet | None = None, obs_coeff: float = 1.0, device: int = 0):
+    def __init__(self, dec: LGUnet, prob: dict, flow: LGUnet | None = None, obs_coeff: float = 1.0, device: int = 0,
+                 obs_interp=None):
+        """obs_interp: None (synthetic observations of the state) or the (n_out, n_in) obs_interpolater.interp of
+        obs_type 'real*' (da_4dvar.py:1196-1206); `prob["interp"]` is used when present. yo, H, R then hold
+        4 + 5*n_out observation channels."""
         dev = torch.device("cuda", device)
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32).to(dev)
         self.xb, self.yo, self.H, self.R = t(prob["xb"]), t(prob["yo"]), t(prob["H"]), t(prob["R"])
         self.mean, self.std, self.std_tr = t(prob["mean"]), t(prob["std"]), t(prob["std_tr"])
-        self.T, self.C = self.yo.shape[0], self.yo.shape[1]
-        self.Hs, self.Ws = self.yo.shape[2:]
+        self.T, self.C = self.yo.shape[0], self.xb.shape[0]
+        self.Hs, self.Ws = self.xb.shape[1:]
         self.dec, self.flow, self.obs_coeff = dec, flow, float(obs_coeff)
         self.ctx = dec.ctx
         self.latent_shape = (1, dec.in_ch, dec.H, dec.W)
+        if obs_interp is None:
+            obs_interp = prob.get("interp")
+        self.interp = None if obs_interp is None else t(obs_interp)
+        if self.interp is not None:
+            n_out, n_in = self.interp.shape
+            if self.yo.shape[1] != 4 + 5 * n_out:
+                raise ValueError(f"yo has {self.yo.shape[1]} channels, the operator gives {4 + 5 * n_out}")
+        elif self.yo.shape[1] != self.C:
+            raise ValueError("yo/H/R channels differ from the state's: pass the observation operator (obs_interp)")
         fid = flow.id if flow is not None else -1
         check(lib.vv_bind_problem(self.ctx.h, dec.id, fid, self.T, self.C, self.Hs, self.Ws, _ptr(self.xb),
                                   _ptr(self.yo), _ptr(self.H), _ptr(self.R), _ptr(self.mean), _ptr(self.std),
                                   _ptr(self.std_tr), self.obs_coeff), "bind_problem")
+        if self.interp is not None:
+            check(lib.vv_set_obs_operator(self.ctx.h, n_out, n_in, _ptr(self.interp)), "set_obs_operator")
         self.n_evals = 0
 
     def closure(self, z: torch.Tensor, grad: torch.Tensor | None):
@@ -322,3 +337,18 @@ class _ClosureFn(torch.autograd.Function):
 def loss(prob: DAProblem, z: torch.Tensor) -> torch.Tensor:
     """Drop-in for the reference's `loss(z)` (da_4dvar.py:1183-1208)."""
     return _ClosureFn.apply(z, prob)
+
+
+def obs_augment(ctx: Context, interp: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """x_aug (da_4dvar.py:1196-1206) of (T, 4 + 5*n_in, H, W) device fields on the GPU; applied to R it is
+    get_R_matrix_from_gt (da_4dvar.py:729-756)."""
+    n_out, n_in = interp.shape
+    T, C, Hs, Ws = x.shape
+    if C != 4 + 5 * n_in:
+        raise ValueError(f"{C} channels, the operator expects {4 + 5 * n_in}")
+    interp = interp.to(device=x.device, dtype=torch.float32).contiguous()
+    x = x.contiguous()
+    out = torch.empty(T, 4 + 5 * n_out, Hs, Ws, device=x.device, dtype=torch.float32)
+    check(lib.vv_obs_augment(ctx.h, _ptr(interp), n_out, n_in, _ptr(x), _ptr(out), T, Hs, Ws, _stream()),
+          "obs_augment")
+    return out
