@@ -14,6 +14,7 @@
  *   vv_closure                    closure() -> loss(z); backward (da_4dvar.py:1183-1208, 1242-1246)
  *   vv_decode                     the analysis xa = decoder_hr(z)*stdTr*std + xb (da_4dvar.py:1301-1306)
  *   vv_set_obs_operator/_augment  the real-observation operator obs_interpolater (da_4dvar.py:62-94, :1196-1206)
+ *   vv_metrics                    WRMSE / Bias of the DA logging (utils/metrics.py, da_4dvar.py:1256-1262)
  *   vv_integrate                  integrate(x, model, 1) (da_4dvar.py:666-681): the outer-cycle forecast with
  *                                 the 0.25-degree LGUnet_all_1 (da_4dvar.py:1329, :652), forward only
  *   vv_dot/axpy/... , vv_adam     vector arithmetic of torch/optim/lbfgs.py:333-535 and adam.py
@@ -117,6 +118,12 @@ int vv_set_obs_operator(vv_ctx* ctx, int n_out, int n_in, const float* interp);
    Also get_R_matrix_from_gt (da_4dvar.py:729-756) when applied to R. */
 int vv_obs_augment(vv_ctx* ctx, const float* interp, int n_out, int n_in, const float* x, float* x_aug, int T,
                    int Hs, int Ws, void* stream);
+/* latitude-weighted WRMSE and Bias per channel as one_step_DA logs them (da_4dvar.py:1256-1262 with
+   utils/metrics.py Metrics.WRMSE / Metrics.Bias, weighted_rmse_torch_channels :282-289, type_weighted_bias_torch
+   'all' :65-82): both fields normalised by (x - mean)/std, then scaled by `scale` (the float64 model_std).
+   pred, gt (B,C,H,W); mean, std_ (C) fp32; scale (C) fp64; wrmse, bias (C) fp64 device. Synchronises `stream`. */
+int vv_metrics(vv_ctx* ctx, const float* pred, const float* gt, const float* mean, const float* std_,
+               const double* scale, int B, int C, int H, int W, double* wrmse, double* bias, void* stream);
 /* trajectory x_t (T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
 int vv_state_ptr(vv_ctx* ctx, const float** x);
 

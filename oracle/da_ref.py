@@ -141,3 +141,40 @@ def one_step_da_ref(rp: RefProblem, nit: int, latent_shape, history_size=10, max
     with torch.no_grad():
         xa = rp.analysis(z)
     return xa, z.detach(), js, n_eval[0], lbfgs.state[lbfgs._params[0]]["n_iter"]
+
+
+def lat_weights_ref(num_lat):
+    """utils/metrics.py:4-9 lat / latitude_weighting_factor_torch with s from :287-289 (fp32)."""
+    j = torch.arange(start=0, end=num_lat)
+    lat = 90.0 - j * 180.0 / float(num_lat - 1)
+    c = torch.cos(3.1416 / 180.0 * lat)
+    return num_lat * c / torch.sum(c)
+
+
+def wrmse_ref(pred_n, gt_n, data_std):
+    """Metrics.WRMSE (utils/metrics.py:526-545 -> weighted_rmse_torch :291-294, _channels :282-289); pred_n,
+    gt_n (N,C,H,W) normalised; data_std float64 numpy (the reference passes model_std)."""
+    w = lat_weights_ref(pred_n.shape[2]).reshape(1, 1, -1, 1)
+    r = torch.sqrt(torch.mean(w * (pred_n - gt_n) ** 2.0, dim=(-1, -2)))
+    return torch.mean(r, dim=0) * data_std
+
+
+def bias_ref(pred_n, gt_n, data_std):
+    """Metrics.Bias (utils/metrics.py:473-474 -> type_weighted_bias_torch 'all' :265-267, :65-82)."""
+    d = pred_n - gt_n
+    w = lat_weights_ref(d.shape[2]).reshape(1, 1, -1, 1)
+    return torch.mean(torch.mean(w * d, dim=(-1, -2)), dim=0) * data_std
+
+
+def run_cycles_ref(make_rp, xb0, forecast_fn, n_cycles, nit, latent_shape):
+    """run_assimilation (da_4dvar.py:1314-1342) restated: per cycle xa = one_step_DA(xb), xb <- integrate(xa,
+    forecast, 1); make_rp(cycle, xb) builds that cycle's RefProblem. Returns the analyses, backgrounds and J."""
+    xb = xb0
+    out = []
+    for k in range(n_cycles):
+        rp = make_rp(k, xb)
+        xa, _, js, _, _ = one_step_da_ref(rp, nit, latent_shape)
+        out.append({"xb": xb, "xa": xa.detach(), "J": js})
+        with torch.no_grad():
+            xb = forecast_fn(xa.detach())
+    return out

@@ -18,6 +18,8 @@ are stored):
   g8_real_obs.npz       G8 (--g8, ~3 min): the genuine obs_interpolater(13, 40) matrices, get_R_matrix_from_gt on a
                         small R, and cyclic_4dvar.one_step_DA(..., 'vae4dvar') with obs_type 'real' at 721x1440,
                         T=1, Nit=1 (J per outer pass, sampled xa)
+  g9_metrics.npz        G9: the genuine utils.metrics.Metrics WRMSE / Bias as one_step_DA calls them
+                        (da_4dvar.py:1256-1262) at 128x256 and 721x1440
   g7_tiny_lgunet1.npz   G7: tiny networks.LGUnet_all_1 (RoPE, -inf mask, global LG window, 3 levels): out
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
                         and one config-2 closure (J_b, J_o, sampled dJ/dz)
@@ -374,6 +376,34 @@ def g8(tr):
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
 
+def g9():
+    """G9: Metrics.WRMSE / Metrics.Bias (utils/metrics.py) exactly as one_step_DA's logging calls
+    them (da_4dvar.py:1256-1262): normalised by model_mean_gpu/model_std_gpu (fp32), scaled by model_std (f64)."""
+    import importlib
+
+    cwd = os.getcwd()
+    os.chdir(ref_harness.REF)
+    da = importlib.import_module("da_4dvar")
+    metrics = importlib.import_module("utils.metrics")
+    os.chdir(cwd)
+    a = object.__new__(da.cyclic_4dvar)
+    a.device = "cpu"
+    mean, std, mean_g, std_g = a.get_model_mean_std()
+    m = metrics.Metrics()
+    out = {}
+    for tag, (Hs, Ws, seed) in {"s": (128, 256, 901), "l": (721, 1440, 902)}.items():
+        p = make_problem(nch=69, Hs=Hs, Ws=Ws, T=1, seed=seed)
+        xhat, gt = torch.from_numpy(p["xb"]), torch.from_numpy(p["gt"][0])
+        xn = (xhat - mean_g.reshape(-1, 1, 1)) / std_g.reshape(-1, 1, 1)
+        gn = (gt - mean_g.reshape(-1, 1, 1)) / std_g.reshape(-1, 1, 1)
+        w = m.WRMSE(xn.unsqueeze(0), gn.unsqueeze(0), None, None, std)
+        b = m.Bias(xn.unsqueeze(0), gn.unsqueeze(0), None, None, std)
+        out["wrmse_" + tag] = w.numpy()
+        out["bias_" + tag] = b.numpy()
+        print(f"G9 {Hs}x{Ws}: wrmse dtype {w.dtype}, z500 {float(w[11]):.6g}, bias z500 {float(b[11]):.6g}")
+    np.savez(os.path.join(GOLD, "g9_metrics.npz"), model_std=std, **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also generate G3 (full decoder, ~1 min)")
@@ -387,7 +417,7 @@ def main():
     tr, sb = ref_harness.import_reference()
     os.chdir(cwd)
     steps = {"g1": lambda: g1(tr), "g2": lambda: g2(sb), "g4": g4, "g5": lambda: g5(tr), "g5b": lambda: g5b(tr),
-             "g7": g7}
+             "g7": g7, "g9": g9}
     if a.full:
         steps["g3"] = lambda: g3(tr)
     if a.g6:

@@ -115,3 +115,21 @@ def test_adam_mirror_matches_torch():
         opt.step()
         mir.step(closure_m)
     assert torch.allclose(zm, zt.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_state_files_layout(tmp_path):
+    """StateFiles writes/reads data_reader.get_state's file layout (da_4dvar.py:148-166) in CHANNELS order."""
+    import datetime as dt
+    import os
+
+    from vaevar.cycle import CHANNELS, StateFiles
+
+    t = dt.datetime(2018, 1, 1, 6)
+    sf = StateFiles(str(tmp_path), shape=(3, 5))
+    x = np.arange(69 * 15, dtype=np.float32).reshape(69, 3, 5)
+    sf.put_state(t, x)
+    assert os.path.exists(os.path.join(str(tmp_path), "single", "2018", "2018-01-01", "06:00:00-u10.npy"))
+    assert os.path.exists(os.path.join(str(tmp_path), "2018", "2018-01-01", "06:00:00-z-50.0.npy"))
+    assert os.path.exists(os.path.join(str(tmp_path), "2018", "2018-01-01", "06:00:00-t-1000.0.npy"))
+    assert np.array_equal(sf.get_state(t), x)
+    assert len(CHANNELS) == 69 and CHANNELS[11] == "z500" and CHANNELS[66] == "t850" and CHANNELS[24] == "q500"

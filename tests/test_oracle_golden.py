@@ -176,3 +176,22 @@ def test_g8_r_matrix_from_gt():
     assert np.array_equal(ra, g["r_aug"])
     rn = obs_augment_np(g["interp"], rs)
     assert np.abs(rn - g["r_aug"]).max() <= 1e-6 * np.abs(g["r_aug"]).max()
+
+
+@pytest.mark.parametrize("tag,Hs,Ws,seed", [("s", 128, 256, 901), ("l", 721, 1440, 902)])
+def test_g9_metrics_oracle(tag, Hs, Ws, seed):
+    """WRMSE / Bias restatement (oracle/da_ref.py) vs the genuine Metrics (G9)."""
+    from oracle.da_ref import bias_ref, wrmse_ref
+    from vaevar import config as C
+    from vaevar.problem import make_problem
+
+    g = gold("g9_metrics.npz")
+    p = make_problem(nch=69, Hs=Hs, Ws=Ws, T=1, seed=seed)
+    mean = torch.tensor(C.MODEL_MEAN, dtype=torch.float32).reshape(-1, 1, 1)
+    std = torch.tensor(C.MODEL_STD, dtype=torch.float32).reshape(-1, 1, 1)
+    xn = ((torch.from_numpy(p["xb"]) - mean) / std).unsqueeze(0)
+    gn = ((torch.from_numpy(p["gt"][0]) - mean) / std).unsqueeze(0)
+    assert np.array_equal(np.asarray(C.MODEL_STD, np.float64), g["model_std"])
+    w = wrmse_ref(xn, gn, g["model_std"]).numpy()
+    b = bias_ref(xn, gn, g["model_std"]).numpy()
+    assert rel(w, g["wrmse_" + tag]) < 1e-6 and rel(b, g["bias_" + tag]) < 1e-6

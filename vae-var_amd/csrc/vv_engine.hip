@@ -279,6 +279,8 @@ struct vv_ctx {
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
   float* twoloop = nullptr;  // L-BFGS two-loop scalars: al[kMaxHistory], coef
+  char* metric_ws = nullptr;  // vv_metrics partial sums + latitude weights
+  size_t metric_cap = 0;
   struct SplitW {
     const float* base;
     size_t n;
@@ -1242,6 +1244,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
 
   (void)hipFree(ctx->red);
   (void)hipFree(ctx->twoloop);
+  if (ctx->metric_ws) (void)hipFree(ctx->metric_ws);
   (void)hipFree(ctx->redf);
   (void)hipFree(ctx->dout);
   (void)hipFree(ctx->doutf);
@@ -1519,6 +1522,45 @@ int vv_set_obs_operator(vv_ctx* ctx, int n_out, int n_in, const float* interp) {
   VV_HIP(hipMemcpy(P.Pobs, interp, (size_t)n_out * n_in * sizeof(float), hipMemcpyDefault));
   P.nin = n_in;
   P.nout = n_out;
+  return 0;
+}
+
+int vv_metrics(vv_ctx* ctx, const float* pred, const float* gt, const float* mean, const float* std_,
+               const double* scale, int B, int C, int H, int W, double* wrmse, double* bias, void* stream) {
+  if (!ctx || !pred || !gt || !mean || !std_ || !scale || !wrmse || !bias) return fail(VV_E_ARG, "null argument");
+  if (B < 1 || C < 1 || H < 2 || W < 1) return fail(VV_E_ARG, "bad field shape");
+  int r = set_dev(ctx);
+  if (r) return r;
+  // latitude weights as utils/metrics.py:4-9 + :287-289 compute them in fp32:
+  // lat = 90 - j*180/(H-1); c = cos(3.1416/180 * lat); w = H * c / sum(c)
+  std::vector<float> cw(H);
+  float csum = 0.0f;
+  for (int j = 0; j < H; ++j) {
+    const float lat = 90.0f - ((float)j * 180.0f) / (float)(H - 1);
+    cw[j] = cosf((float)(3.1416 / 180.0) * lat);
+  }
+  // torch.sum of a float32 vector: pairwise; a double sum rounded once differs by < 1 ulp of the total
+  double cs = 0.0;
+  for (int j = 0; j < H; ++j) cs += cw[j];
+  csum = (float)cs;
+  for (int j = 0; j < H; ++j) cw[j] = ((float)H * cw[j]) / csum;
+  const int nchunk = std::max(1, std::min(64, H / 8));
+  const size_t need = (size_t)H * sizeof(float) + (size_t)B * C * nchunk * 2 * sizeof(double);
+  if (ctx->metric_cap < need) {
+    if (ctx->metric_ws) (void)hipFree(ctx->metric_ws);
+    ctx->metric_ws = nullptr;
+    ctx->metric_cap = 0;
+    if (hipMalloc(&ctx->metric_ws, need) != hipSuccess) return fail(VV_E_ALLOC, "metric workspace");
+    ctx->metric_cap = need;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(ctx->metric_ws);
+  float* wl = reinterpret_cast<float*>(ctx->metric_ws + (size_t)B * C * nchunk * 2 * sizeof(double));
+  VV_HIP(hipMemcpyAsync(wl, cw.data(), (size_t)H * sizeof(float), hipMemcpyHostToDevice, st));
+  vv::MetricArgs a{pred, gt, mean, std_, scale, wl, B, C, H, W, part, nchunk, wrmse, bias};
+  VV_HIP(vv::metrics(a, st));
+  // the host weight table must outlive the async copy
+  VV_HIP(hipStreamSynchronize(st));
   return 0;
 }
 

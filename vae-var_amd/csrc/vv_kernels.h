@@ -226,6 +226,23 @@ struct ObsArgs {
 constexpr int kObsMaxIn = 16, kObsMaxOut = 64;
 hipError_t obs_misfit(const ObsArgs& a, hipStream_t s);
 // x_aug (T, Ca, HW) = Op x (T, C, HW) for T fields (also get_R_matrix_from_gt, da_4dvar.py:729-756, on R)
+// latitude-weighted WRMSE / Bias of one_step_DA's logging (utils/metrics.py:282-296 weighted_rmse_torch_channels,
+// :65-82 type_weighted_bias_torch 'all'; da_4dvar.py:1256-1262), on normalised fields (x - mean)/std, scaled
+// back by std: wrmse[c] = mean_b sqrt(mean_hw w_h d^2) * std[c], bias[c] = mean_b mean_hw (w_h d) * std[c]
+struct MetricArgs {
+  const float* pred;    // (B, C, H, W) physical
+  const float* gt;      // (B, C, H, W)
+  const float* mean;    // [C]
+  const float* std_;    // [C] normalisation (fp32, as model_std_gpu)
+  const double* scale;  // [C] final multiply (the reference's float64 model_std)
+  const float* wlat;    // [H] latitude weights (fp32, as the reference computes them)
+  int B, C, H, W;
+  double* partial;      // [B*C][nchunk][2]
+  int nchunk;
+  double* wrmse;        // [C]
+  double* bias;         // [C]
+};
+hipError_t metrics(const MetricArgs& a, hipStream_t s);
 hipError_t obs_augment(const float* P, int nin, int nout, const float* x, float* x_aug, int T, int HW, hipStream_t s);
 // general (nearest-interpolated) grids, F.interpolate mode='nearest' (quirk Q3):
 //   flow_in[c][a][b] = (x[c][di[a]][dj[b]] - mean[c]) / std[c]          (integrate: down-sample, da_4dvar.py:668-671)

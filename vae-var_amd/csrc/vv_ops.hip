@@ -937,6 +937,58 @@ __global__ __launch_bounds__(256) void k_obs_augment(const float* P, int nin, in
   }
 }
 
+// metrics: grid (nchunk, B*C); rows of a plane split into nchunk contiguous chunks, fp64 block sums
+__global__ __launch_bounds__(256) void k_metric_partial(MetricArgs a) {
+  __shared__ double red[4], red1[4];
+  const int bc = blockIdx.y, c = bc % a.C, HW = a.H * a.W;
+  const int r0 = (int)(((long)blockIdx.x * a.H) / a.nchunk), r1 = (int)(((long)(blockIdx.x + 1) * a.H) / a.nchunk);
+  const float* p = a.pred + (size_t)bc * HW;
+  const float* g = a.gt + (size_t)bc * HW;
+  const float m = a.mean[c], sd = a.std_[c];
+  double s2 = 0.0, s1 = 0.0;
+  for (int i = r0 * a.W + threadIdx.x; i < r1 * a.W; i += 256) {
+    const float w = a.wlat[i / a.W];
+    const float d = (p[i] - m) / sd - (g[i] - m) / sd;
+    s2 += (double)(w * (d * d));
+    s1 += (double)(w * d);
+  }
+  s2 = block_sum(s2, red);
+  s1 = block_sum(s1, red1);
+  if (threadIdx.x == 0) {
+    a.partial[((size_t)bc * a.nchunk + blockIdx.x) * 2] = s2;
+    a.partial[((size_t)bc * a.nchunk + blockIdx.x) * 2 + 1] = s1;
+  }
+}
+__global__ __launch_bounds__(64) void k_metric_final(MetricArgs a) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const double n = (double)a.H * a.W;
+  double r = 0.0, b = 0.0;
+  for (int bb = 0; bb < a.B; ++bb) {
+    const double* q = a.partial + (size_t)(bb * a.C + c) * a.nchunk * 2;
+    double s2 = 0.0, s1 = 0.0;
+    for (int k = lane; k < a.nchunk; k += 64) {
+      s2 += q[2 * k];
+      s1 += q[2 * k + 1];
+    }
+    s2 = wave_sum_d(s2);
+    s1 = wave_sum_d(s1);
+    r += (double)sqrtf((float)(s2 / n));  // torch.sqrt(torch.mean(...)) of an fp32 tensor
+    b += (double)(float)(s1 / n);
+  }
+  if (lane == 0) {
+    a.wrmse[c] = (double)(float)(r / a.B) * a.scale[c];
+    a.bias[c] = (double)(float)(b / a.B) * a.scale[c];
+  }
+}
+hipError_t metrics(const MetricArgs& a, hipStream_t s) {
+  if (a.B < 1 || a.C < 1 || a.H < 1 || a.W < 1 || a.nchunk < 1) return hipErrorInvalidValue;
+  const int ph = prof_begin(s);
+  hipLaunchKernelGGL(k_metric_partial, dim3(a.nchunk, a.B * a.C), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_metric_final, dim3(a.C), dim3(64), 0, s, a);
+  prof_end(ph, s, PC_MISFIT, 8.0 * a.B * a.C * a.H * a.W, 8.0 * a.B * a.C * a.H * a.W);
+  return hipGetLastError();
+}
+
 hipError_t obs_misfit(const ObsArgs& a, hipStream_t s) {
   if (a.nin < 1 || a.nin > kObsMaxIn || a.nout < 1 || a.nout > kObsMaxOut) return hipErrorInvalidValue;
   const int ph = prof_begin(s);

@@ -84,6 +84,8 @@ _SIGS = {
     "vv_closure_async": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vv_decode": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vv_state_ptr": (c_int, [c_void_p, P(c_void_p)]),
+    "vv_metrics": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                           c_void_p, c_void_p, c_void_p]),
     "vv_set_obs_operator": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "vv_obs_augment": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "vv_dot": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, P(c_double), c_void_p]),

@@ -1,5 +1,6 @@
 """The vae4dvar analysis step on the HIP engine — mirror of cyclic_4dvar.one_step_DA(..., 'vae4dvar')
-(da_4dvar.py:1179-1306), without the CPU WRMSE/Bias logging of :1256-1269.
+(da_4dvar.py:1179-1306). The WRMSE/Bias logging of :1256-1269 runs on the device (vaevar.metrics) when a truth
+field and a Metrics object are given.
 
   z = zeros(1,32,128,256)                                  (:1238)
   LBFGS(history_size=10, max_iter=10, strong_wolfe)        (:1240)
@@ -17,8 +18,10 @@ from .lbfgs import LBFGS, Adam
 
 
 def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10, optimizer: str = "lbfgs",
-                lr: float | None = None, log_terms: bool = True, log=None):
-    """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, seconds)."""
+                lr: float | None = None, log_terms: bool = True, log=None, gt=None, metrics=None):
+    """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, seconds); with gt (T,C,Hs,Ws) and a
+    vaevar.metrics.Metrics also metrics=[(wrmse[C], bias[C]) per outer pass] of xhat against gt[0] — the
+    reference's bg_* (pass 0) and ana_* (pass Nit) entries of metrics_list (:1285-1291)."""
     dev = prob.xb.device
     z = torch.zeros(prob.latent_shape, device=dev, dtype=torch.float32)
     ctx = prob.ctx
@@ -34,13 +37,17 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
         jb, jo = prob.closure(zz, g)
         return prob.loss_f32(jb, jo)
 
-    js = []
+    js, ms = [], []
     n0 = prob.n_evals
     t0 = time.time()
     for kk in range(nit + 1):
         if log_terms:
             jb, jo = prob.closure(z, None)  # cal_loss (:1210-1236): no gradient
             js.append((jb, jo))
+            if gt is not None and metrics is not None:
+                xhat = prob.trajectory()[0]  # decoder_hr(z)*stdTr*std + xb of this pass (:1256-1258)
+                w, b = metrics.wrmse_bias(xhat, gt[0])
+                ms.append((w.cpu().numpy(), b.cpu().numpy()))
             if log is not None:
                 log(kk, jb, jo)
         if kk < nit:
@@ -50,4 +57,4 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
     n_log = (nit + 1) if log_terms else 0
     n_iter = opt.state["n_iter"] if optimizer == "lbfgs" else opt.t
     return {"xa": xa, "z": z, "J": js, "n_eval": prob.n_evals - n0 - n_log, "n_iter": n_iter,
-            "seconds": time.time() - t0}
+            "seconds": time.time() - t0, "metrics": ms}

@@ -266,7 +266,12 @@ class DAProblem:
         obs_type 'real*' (da_4dvar.py:1196-1206); `prob["interp"]` is used when present. yo, H, R then hold
         4 + 5*n_out observation channels."""
         dev = torch.device("cuda", device)
-        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32).to(dev)
+
+        def t(a):
+            if isinstance(a, torch.Tensor):
+                return a.to(device=dev, dtype=torch.float32).contiguous()
+            return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32).to(dev)
+
         self.xb, self.yo, self.H, self.R = t(prob["xb"]), t(prob["yo"]), t(prob["H"]), t(prob["R"])
         self.mean, self.std, self.std_tr = t(prob["mean"]), t(prob["std"]), t(prob["std_tr"])
         self.T, self.C = self.yo.shape[0], self.xb.shape[0]
