@@ -159,7 +159,7 @@ int vv_nearest_map(int in_size, int out_size, int* map);
    VV_GEMM_F32     = v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (torch fp32 matmul semantics);
    VV_GEMM_SPLIT   = each fp32 operand split exactly into three bf16 planes (x = h + m + l) and the six
                      products of order >= 2^-16 accumulated in fp32 by v_mfma_f32_32x32x16_bf16;
-   VV_GEMM_SPLIT16 = each fp32 operand scaled by a power of two (A per row and 32-wide k-chunk, B per row) and
+   VV_GEMM_SPLIT16 = each fp32 operand scaled by a power of two per row (its maximum to [2^14, 2^15)) and
                      split into two fp16 planes (x = h + l, 22 bits), three products (hh, hl, lh) accumulated
                      in fp32 by v_mfma_f32_32x32x16_f16.
    Both split modes have fp32-level error (measured vs fp64, tests/test_gpu_kernels.py). */

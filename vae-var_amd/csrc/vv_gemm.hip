@@ -1291,12 +1291,21 @@ __global__ __launch_bounds__(256) void k_rowscale(GemmArgs args, float* __restri
   const GemmGroup G = args.g[blockIdx.z];
   const int ar = args.arow ? args.arow[r] : r;
   const float* a = G.A + (size_t)ar * args.lda;
+  auto amax = [](const f4& v) {
+    return max(max(__float_as_uint(fabsf(v[0])), __float_as_uint(fabsf(v[1]))),
+               max(__float_as_uint(fabsf(v[2])), __float_as_uint(fabsf(v[3]))));
+  };
   unsigned mx = 0;
-  for (int k = lane * 4; k < args.ksplit; k += 256) {
-    const f4 v = *reinterpret_cast<const f4*>(a + k);
-    mx = max(mx, max(max(__float_as_uint(fabsf(v[0])), __float_as_uint(fabsf(v[1]))),
-                     max(__float_as_uint(fabsf(v[2])), __float_as_uint(fabsf(v[3])))));
+  int k = lane * 4;
+  // four independent row loads in flight per lane (K = 1152: 4.5 float4 per lane)
+  for (; k + 768 < args.ksplit; k += 1024) {
+    const f4 v0 = *reinterpret_cast<const f4*>(a + k);
+    const f4 v1 = *reinterpret_cast<const f4*>(a + k + 256);
+    const f4 v2 = *reinterpret_cast<const f4*>(a + k + 512);
+    const f4 v3 = *reinterpret_cast<const f4*>(a + k + 768);
+    mx = max(mx, max(max(amax(v0), amax(v1)), max(amax(v2), amax(v3))));
   }
+  for (; k < args.ksplit; k += 256) mx = max(mx, amax(*reinterpret_cast<const f4*>(a + k)));
   if (G.A2) {
     const float* a2 = G.A2 + (size_t)r * args.lda2;
     for (int k = lane * 4; k < args.K - args.ksplit; k += 256) {

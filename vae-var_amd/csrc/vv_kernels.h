@@ -58,7 +58,7 @@ size_t gemm_ws_floats();
 // GEMM arithmetic:
 //   GEMM_F32     v_mfma_f32_32x32x2_f32 (exact f32 fma chain)
 //   GEMM_SPLIT   fp32 operands split into three bf16 planes, six v_mfma_f32_32x32x16_bf16 products
-//   GEMM_SPLIT16 fp32 operands scaled by a power of two (A: per row and 32-wide k-chunk, B: per row) and split
+//   GEMM_SPLIT16 fp32 operands scaled by a power of two per row (A and B) and split
 //                into two fp16 planes, three v_mfma_f32_32x32x16_f16 products (both fp32-level error)
 enum GemmMath : int { GEMM_F32 = 0, GEMM_SPLIT = 1, GEMM_SPLIT16 = 2 };
 void set_gemm_math(int m);
