@@ -18,7 +18,7 @@ for (M, N, K) in shapes:
     ref = (A.double() @ B.double().T)
     row["err"] = float((ctx.gemm(A, B, tile=36).double() - ref).abs().max() / ref.abs().max())
     for t in tiles:
-        if t in (36, 40):
+        if t in (36, 40) and os.environ.get("ERR", "1") == "1":
             row[f"err{t}"] = float((ctx.gemm(A, B, tile=t).double() - ref).abs().max() / ref.abs().max())
         for _ in range(3):
             ctx.gemm(A, B, tile=t)
