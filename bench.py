@@ -180,6 +180,9 @@ def main():
         "ms_per_eval": 1e3 * t_max * size / max(evals, 1),
         "J_start": j_0[0] + j_0[1],
         "J_final": j_end[0] + j_end[1],
+        "timed_region": "the Nit outer lbfgs.step calls + the analysis decode (+ the gather at N>1); the "
+                        "per-outer-pass logging evaluation cal_loss and WRMSE/Bias (da_4dvar.py:1256-1269, SURVEY "
+                        "§8 a3) is not run in it: 1 forward per outer pass, reported here as excluded",
     }
     flops_eval = FLOPS_PER_EVAL.get(T)
     if prof:

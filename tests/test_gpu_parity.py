@@ -315,3 +315,28 @@ def test_one_step_da_config5_g6():
     print(f"G6 config 5 one_step_DA: J per pass {J.tolist()} vs {g['J'].tolist()} (rel {eJ:.1e}); "
           f"xa rel-L2 {e_xa:.1e}; |xa-xb|^2 rel {e_dx:.1e}; evals {res['n_eval']}")
     assert eJ < 1e-3 and e_xa < 1e-3 and e_dx < 1e-2
+
+
+def test_closure_edge_cases(tiny):
+    """Size-independent properties of the closure (tiny decoder, T=2 with the tiny flow): with no observations
+    J_o = 0 and dJ/dz = z exactly; J_o and the observation gradient are linear in obs_coeff."""
+    from vaevar import config as C
+    from vaevar.engine import DAProblem, LGUnet
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    flow = LGUnet(C.TINY_FLOW, 1, 1).load_synthetic()
+    p = make_problem(nch=4, Hs=32, Ws=64, T=2, seed=31, obs_frac=0.2)
+    z = torch.from_numpy(0.3 * smooth_field(32, (1, 4, 32, 64), sigma=2.0)).cuda()
+    g = torch.empty_like(z)
+    empty = dict(p, H=np.zeros_like(p["H"]))
+    jb, jo = DAProblem(tiny, empty, flow=flow).closure(z, g)
+    assert jo == 0.0 and torch.equal(g, z)
+    assert abs(jb - 0.5 * float((z.double() ** 2).sum())) <= 1e-12 * jb
+    g1, g2 = torch.empty_like(z), torch.empty_like(z)
+    _, jo1 = DAProblem(tiny, p, flow=flow, obs_coeff=1.0).closure(z, g1)
+    _, jo2 = DAProblem(tiny, p, flow=flow, obs_coeff=2.0).closure(z, g2)
+    assert jo1 == jo2  # J_o is returned without the coefficient
+    e = rel((g2 - z).cpu(), (2 * (g1 - z)).cpu())
+    print(f"obs_coeff linearity: grad rel {e:.1e}")
+    assert e < 1e-6
