@@ -245,6 +245,28 @@ def g7():
     np.savez(os.path.join(GOLD, "g7_tiny_lgunet1.npz"), out=y.numpy())
 
 
+class LineSearchRecorder:
+    """Records (t, ls_func_evals) of every torch.optim.lbfgs._strong_wolfe call the reference's LBFGS makes, for
+    the fixed-step replay comparison of SURVEY §8 c6 (vaevar.lbfgs.LBFGS.replay)."""
+
+    def __enter__(self):
+        import torch.optim.lbfgs as tl
+
+        self.tl, self.orig, self.steps = tl, tl._strong_wolfe, []
+
+        def rec(*a, **k):
+            out = self.orig(*a, **k)
+            self.steps.append((float(out[2]), int(out[3])))
+            return out
+
+        tl._strong_wolfe = rec
+        return self
+
+    def __exit__(self, *exc):
+        self.tl._strong_wolfe = self.orig
+        return False
+
+
 def g6(tr):
     """G6: run the reference's own one_step_DA vae4dvar branch (da_4dvar.py:1179-1306) on CPU at 721x1440 with
     T=2 (flow stand-in), Nit=1, synthetic weights and the make_problem(seed=20250620) inputs (SURVEY §8 c2 iv:
@@ -292,7 +314,7 @@ def g6(tr):
     buf = io.StringIO()
     t0 = time.time()
     try:
-        with CPUMode(), contextlib.redirect_stdout(buf):
+        with CPUMode(), contextlib.redirect_stdout(buf), LineSearchRecorder() as ls:
             xa = a.one_step_DA(t("gt"), t("xb"), t("yo"), t("H"), t("R"), "vae4dvar")
     finally:
         torch.Tensor.cuda = old_cuda
@@ -303,6 +325,7 @@ def g6(tr):
     flat = xa.reshape(-1).astype(np.float64)
     print(f"G6 one_step_DA 721x1440 T=2 Nit=1: {time.time() - t0:.0f}s, J per pass {J}")
     np.savez(os.path.join(GOLD, "g6_one_step_da_c5.npz"), J=np.array(J), idx_xa=idx, xa_sample=xa.reshape(-1)[idx],
+             ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]),
              xa_sum=flat.sum(), xa_sumsq=(flat * flat).sum(),
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
@@ -361,7 +384,7 @@ def g8(tr):
         t = lambda k: torch.from_numpy(prob[k])
         buf = io.StringIO()
         t0 = time.time()
-        with CPUMode(), contextlib.redirect_stdout(buf):
+        with CPUMode(), contextlib.redirect_stdout(buf), LineSearchRecorder() as ls:
             xa = b.one_step_DA(t("gt"), t("xb"), t("yo"), t("H"), t("R"), "vae4dvar")
     finally:
         torch.Tensor.cuda = old_cuda
@@ -372,6 +395,7 @@ def g8(tr):
     flat = xa.reshape(-1).astype(np.float64)
     print(f"G8 real-obs one_step_DA 721x1440 T=1 Nit=1: {time.time() - t0:.0f}s, J per pass {J}")
     np.savez(os.path.join(GOLD, "g8_real_obs.npz"), interp=interp, interp_inv=interp_inv, r_aug=r_aug, J=np.array(J),
+             ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]),
              idx_xa=idx, xa_sample=xa.reshape(-1)[idx], xa_sum=flat.sum(),
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 

@@ -290,12 +290,12 @@ def test_config5_grid_closure():
 def test_one_step_da_config5_g6():
     """BASELINE config 5 end to end against the GENUINE reference method (G6: cyclic_4dvar.one_step_DA run on
     CPU at 721x1440, T=2 flow stand-in, Nit=1, same synthetic weights/inputs): J per outer pass (the reference
-    prints 4 significant digits) and the analysis xa (J rel <= 1e-3, xa rel-L2 <= 1e-3)."""
+    prints 4 significant digits) and the analysis xa, free-running and as a fixed-step replay."""
     path = os.path.join(GOLD, "g6_one_step_da_c5.npz")
     if not os.path.exists(path):
         pytest.skip("G6 fixture not generated (oracle/make_golden.py --g6)")
+    from test_gpu_obs import one_step_vs_golden
     from vaevar import config as C
-    from vaevar.da import one_step_da
     from vaevar.engine import DAProblem, LGUnet
     from vaevar.problem import make_problem
 
@@ -303,19 +303,7 @@ def test_one_step_da_config5_g6():
     dec = LGUnet(C.DECODER, 1, 1).load_synthetic()
     flow = LGUnet(C.FLOW, 1, 1).load_synthetic()
     prob_np = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250620)
-    prob = DAProblem(dec, prob_np, flow=flow)
-    res = one_step_da(prob, nit=1)
-    J = np.array(res["J"], np.float64)
-    eJ = float(np.abs(J - g["J"]).max() / np.abs(g["J"]).max())
-    xa = res["xa"].cpu().numpy().reshape(-1).astype(np.float64)
-    s = xa[g["idx_xa"]]
-    e_xa = float(np.linalg.norm(s - g["xa_sample"]) / np.linalg.norm(g["xa_sample"]))
-    dx = float(((xa - prob_np["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
-    e_dx = abs(dx - float(g["dxa_sumsq"])) / float(g["dxa_sumsq"])
-    print(f"G6 config 5 one_step_DA: J per pass {J.tolist()} vs {g['J'].tolist()} (rel {eJ:.1e}); "
-          f"xa rel-L2 {e_xa:.1e}; |xa-xb|^2 rel {e_dx:.1e}; evals {res['n_eval']}")
-    assert eJ < 1e-3 and e_xa < 1e-3 and e_dx < 1e-2
-
+    one_step_vs_golden(DAProblem(dec, prob_np, flow=flow), prob_np, g, "G6 config 5 one_step_DA")
 
 def test_closure_edge_cases(tiny):
     """Size-independent properties of the closure (tiny decoder, T=2 with the tiny flow): with no observations

@@ -133,3 +133,54 @@ def test_state_files_layout(tmp_path):
     assert os.path.exists(os.path.join(str(tmp_path), "2018", "2018-01-01", "06:00:00-t-1000.0.npy"))
     assert np.array_equal(sf.get_state(t), x)
     assert len(CHANNELS) == 69 and CHANNELS[11] == "z500" and CHANNELS[66] == "t850" and CHANNELS[24] == "q500"
+
+
+def test_lbfgs_fixed_step_replay():
+    """Fixed-step replay: the (t, evals) that torch.optim.LBFGS's _strong_wolfe returned, fed to
+    the mirror, reproduce torch's iterates and eval counts without running the mirror's own line search."""
+    import torch.optim.lbfgs as tl
+
+    from vaevar.lbfgs import LBFGS
+
+    n = 2048
+    zt = torch.zeros(n, requires_grad=True)
+    opt = torch.optim.LBFGS([zt], history_size=10, max_iter=10, line_search_fn="strong_wolfe")
+    steps, orig = [], tl._strong_wolfe
+
+    def rec(*a, **k):
+        out = orig(*a, **k)
+        steps.append((float(out[2]), int(out[3])))
+        return out
+
+    def closure_t():
+        opt.zero_grad()
+        f = objective(zt)
+        f.backward()
+        return f
+
+    tl._strong_wolfe = rec
+    try:
+        for _ in range(2):
+            opt.step(closure_t)
+    finally:
+        tl._strong_wolfe = orig
+    zm = torch.zeros(n)
+    mir = LBFGS(CpuPrims(), zm, history_size=10, max_iter=10, line_search_fn="strong_wolfe")
+    mir.replay = list(steps)
+    calls = [0]
+
+    def closure_m(z, g):
+        zz = z.clone().requires_grad_(True)
+        f = objective(zz)
+        f.backward()
+        g.copy_(zz.grad)
+        calls[0] += 1
+        return float(f.detach())
+
+    for _ in range(2):
+        mir.step(closure_m)
+    st = opt.state[opt._params[0]]
+    assert not mir.replay and len(steps) == st["n_iter"]
+    assert mir.state["func_evals"] == st["func_evals"] and mir.state["n_iter"] == st["n_iter"]
+    assert calls[0] == 2 + len(steps)  # one evaluation per replayed line search (+ the initial one per step)
+    assert torch.allclose(zm, zt.detach(), rtol=1e-4, atol=1e-4)

@@ -1521,7 +1521,7 @@ static hipError_t launch_h3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   return hipGetLastError();
 }
 
-constexpr size_t kWsFloats = (size_t)1 << 21;      // 8 MB: tail partials of up to 512 chunks of a 64x64 tile
+constexpr size_t kWsFloats = (size_t)1 << 23;      // 32 MB: split-K partials (e.g. 3 x 144 tiles of 128x128)
 constexpr size_t kScaleFloats = (size_t)1 << 19;   // then the A row scales of GEMM_SPLIT16 (groups x M)
 
 // requires fp16 planes for every group's B (registered weights) and a workspace for the A row scales; the
@@ -1742,6 +1742,15 @@ static void variant_tile(int t, int& bm, int& bn, int& bk) {
   bk = tab[t][2];
 }
 
+static bool small_split_enabled() {
+  static int v = -1;  // VAEVAR_SMALL_SPLIT=0 disables the whole-grid split-K of sub-chip fp16x3 GEMMs
+  if (v < 0) {
+    const char* e = getenv("VAEVAR_SMALL_SPLIT");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
   GemmArgs a = a_in;
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
@@ -1788,6 +1797,19 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
         a.tdp = tdp;
         a.tsplit = S;
       }
+    } else if (tdp == 0 && (t == 36) && small_split_enabled()) {
+      // fewer fp16x3 tiles than CUs (N = 1152 at 2048 tokens: 144 tiles): every tile split along K so that
+      // two workgroups share most CUs (the co-resident pair overlaps one's staging with the other's MFMAs)
+      // chunks of >= 24 k-tiles (K >= 2304 at S = 3): at K = 1152 the fixup costs more than the split gains
+      static int min_kt = -1;  // VAEVAR_SMALL_SPLIT_MINKT: k-tiles per chunk at least (default 24)
+      if (min_kt < 0) {
+        const char* e = getenv("VAEVAR_SMALL_SPLIT_MINKT");
+        min_kt = e ? std::max(1, atoi(e)) : 24;
+      }
+      int S = std::min((2 * P) / T, nkt / min_kt);
+      const size_t tile_f = (size_t)bm * bn;
+      while (S > 1 && (size_t)T * S * tile_f > kWsFloats) --S;
+      if (S > 1) a.tsplit = S;
     }
   }
   const int ph = prof_begin(s);

@@ -18,7 +18,7 @@ from .lbfgs import LBFGS, Adam
 
 
 def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10, optimizer: str = "lbfgs",
-                lr: float | None = None, log_terms: bool = True, log=None, gt=None, metrics=None):
+                lr: float | None = None, log_terms: bool = True, log=None, gt=None, metrics=None, replay=None):
     """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, seconds); with gt (T,C,Hs,Ws) and a
     vaevar.metrics.Metrics also metrics=[(wrmse[C], bias[C]) per outer pass] of xhat against gt[0] — the
     reference's bg_* (pass 0) and ana_* (pass Nit) entries of metrics_list (:1285-1291)."""
@@ -28,6 +28,7 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
     if optimizer == "lbfgs":
         opt = LBFGS(ctx, z, lr=1 if lr is None else lr, history_size=history_size, max_iter=max_iter,
                     line_search_fn="strong_wolfe")
+        opt.replay = list(replay) if replay is not None else None  # fixed-step replay of a reference run
     elif optimizer == "adam":
         opt = Adam(ctx, z, lr=1e-3 if lr is None else lr)
     else:

@@ -50,6 +50,9 @@ class LBFGS:
         self.tolerance_grad, self.tolerance_change = tolerance_grad, tolerance_change
         self.history_size, self.line_search_fn = history_size, line_search_fn
         self.device_two_loop = device_two_loop  # False: the two loops with host scalars (one sync per dot)
+        # fixed-step replay: a list of (t, ls_func_evals) recorded from the reference's
+        # _strong_wolfe calls; each line search then takes the recorded step and eval count instead of searching
+        self.replay = None
         self.state = {"func_evals": 0, "n_iter": 0}
 
     # --- vector helpers ---------------------------------------------------
@@ -235,8 +238,12 @@ class LBFGS:
                 def obj_func(x, t, d):
                     return self._directional_evaluate(closure, x, t, d)
 
-                loss, flat_grad, t, ls_func_evals = self._strong_wolfe(obj_func, x_init, t, d, loss, flat_grad, gtd,
-                                                                       max_ls=max_eval - current_evals)
+                if self.replay:
+                    t, ls_func_evals = self.replay.pop(0)
+                    loss, flat_grad = obj_func(x_init, t, d)
+                else:
+                    loss, flat_grad, t, ls_func_evals = self._strong_wolfe(obj_func, x_init, t, d, loss, flat_grad,
+                                                                           gtd, max_ls=max_eval - current_evals)
                 self._add_grad(t, d)
                 opt_cond = self._absmax(flat_grad) <= tolerance_grad
             else:
