@@ -169,6 +169,101 @@ __global__ __launch_bounds__(256) void k_attn_flash(FlashArgs a) {
   }
 }
 
+// Small windows (N <= 96 tokens, hd <= 64; the [6, 12] = 72-token windows of every non-global stage): one
+// workgroup per (window, head) holds q, k, v of the window and the N x N scores in LDS. S in 4x4 register blocks
+// (8 float4 LDS reads per 64 FMAs), an exact row softmax (one wave per row, max then sum), O = P V in 4-row x
+// float4 blocks; each score's exp is evaluated once (the streaming kernel above recomputes every exp on the 8
+// lanes of a query and runs its online rescale per 32-key tile).
+constexpr int kWinMaxN = 96, kWinMaxHd = 64;  // LDS <= 116 KB
+__global__ __launch_bounds__(256) void k_attn_win(FlashArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smw[];
+  const int g = blockIdx.z, w = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int N = a.N, C = a.C, hd = C / a.heads, ld = hd + 4, ls = N + 1, nb = (N + 3) / 4;
+  float* q = smw;
+  float* k = q + N * ld;
+  float* v = k + N * ld;
+  float* S = v + N * ld;  // [N][N+1]
+  const float* base = a.qkv[g] + (size_t)w * N * 3 * C + h * hd;
+  const int q4 = hd / 4;
+  for (int e = tid; e < N * q4; e += 256) {
+    const int t = e / q4, c = (e - t * q4) * 4;
+    const float* src = base + (size_t)t * 3 * C + c;
+    *reinterpret_cast<f4*>(q + t * ld + c) = *reinterpret_cast<const f4*>(src);
+    *reinterpret_cast<f4*>(k + t * ld + c) = *reinterpret_cast<const f4*>(src + C);
+    *reinterpret_cast<f4*>(v + t * ld + c) = *reinterpret_cast<const f4*>(src + 2 * C);
+  }
+  __syncthreads();
+  const int wr = (w / a.nWw) % a.nWh;
+  for (int b = tid; b < nb * nb; b += 256) {
+    const int i0 = (b / nb) * 4, j0 = (b % nb) * 4;
+    float acc[4][4] = {};
+    for (int d = 0; d < hd; d += 4) {
+      f4 qa[4], ka[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        qa[r] = *reinterpret_cast<const f4*>(q + min(i0 + r, N - 1) * ld + d);
+        ka[r] = *reinterpret_cast<const f4*>(k + min(j0 + r, N - 1) * ld + d);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[r][c] += qa[r][0] * ka[c][0] + qa[r][1] * ka[c][1] + qa[r][2] * ka[c][2] + qa[r][3] * ka[c][3];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r;
+      if (i >= N) break;
+      const int li = a.masked ? row_label(wr * a.wh + i / a.ww, a.H, a.wh, a.sh) : 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = j0 + c;
+        if (j >= N) break;
+        const bool ok = !a.masked || row_label(wr * a.wh + j / a.ww, a.H, a.wh, a.sh) == li;
+        S[i * ls + j] = ok ? acc[r][c] : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+  // row softmax (Attention.py:563: softmax over keys; -inf entries give exact zeros)
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int i = wave; i < N; i += 4) {
+    float* row = S + i * ls;
+    float mx = -INFINITY;
+    for (int j = lane; j < N; j += 64) mx = fmaxf(mx, row[j]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+    for (int j = lane; j < N; j += 64) {
+      const float e = expf(row[j] - mx);
+      row[j] = e;
+      sum += e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.f / sum;
+    for (int j = lane; j < N; j += 64) row[j] *= inv;
+  }
+  __syncthreads();
+  float* ob = a.out[g] + (size_t)w * N * C + h * hd;
+  for (int b = tid; b < nb * q4; b += 256) {
+    const int i0 = (b / q4) * 4, c = (b % q4) * 4;
+    f4 acc[4] = {};
+    for (int j = 0; j < N; ++j) {
+      const f4 vv = *reinterpret_cast<const f4*>(v + j * ld + c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = S[min(i0 + r, N - 1) * ls + j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[r][e] += p * vv[e];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (i0 + r < N) *reinterpret_cast<f4*>(ob + (size_t)(i0 + r) * C + c) = acc[r];
+  }
+}
+
 struct ConvArgs {
   int B, Cimg, Himg, Wimg;  // image (B, Cimg, Himg, Wimg)
   int Ho, Wo, Ctok, kh, kw, sh, sw;
@@ -705,7 +800,28 @@ LnArgs lbase(int rows, int C, int G) {
   return a;
 }
 
+static bool win_attn_enabled() {
+  static int v = -1;  // VAEVAR_WIN_ATTN=0: the streaming kernel for small windows too
+  if (v < 0) {
+    const char* e = getenv("VAEVAR_WIN_ATTN");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st) {
+  if (a.N <= kWinMaxN && hd <= kWinMaxHd && hd % 4 == 0 && win_attn_enabled()) {
+    const size_t lds = (3 * (size_t)a.N * (hd + 4) + (size_t)a.N * (a.N + 1)) * sizeof(float);
+    static bool init = false;
+    if (!init) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_attn_win, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(3 * kWinMaxN * (kWinMaxHd + 4) + kWinMaxN * (kWinMaxN + 1)) * 4);
+      if (e != hipSuccess) return e;
+      init = true;
+    }
+    hipLaunchKernelGGL(k_attn_win, dim3(nwin, a.heads, G), dim3(256), lds, st, a);
+    return hipGetLastError();
+  }
   const int qblocks = (a.N + 31) / 32;
   dim3 grid(nwin, a.heads * qblocks, G);
   switch (hd / 8) {
