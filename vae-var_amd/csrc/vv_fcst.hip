@@ -403,6 +403,52 @@ __global__ void k_vt(const float* qkv, float* vt, int N, int Np, int C, int head
 }
 
 // row softmax of S [rows][Np] (first N columns), in place; pad columns set to 0 (they feed the P.V GEMM's K)
+// one row held in registers (Np <= 256 * 4 * RV): one read and one write of the row, each exp once
+constexpr int kSmRV = 16;
+__global__ __launch_bounds__(256) void k_softmax_rows_reg(float* S, int N, int Np) {
+  __shared__ float red[8];
+  float* row = S + (size_t)blockIdx.x * Np;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  f4 x[kSmRV];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kSmRV; ++i) {
+    const int j = (tid + 256 * i) * 4;
+    x[i] = j < Np ? *reinterpret_cast<const f4*>(row + j) : f4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (j + e >= N) x[i][e] = -INFINITY;  // padding columns [N, Np)
+      mx = fmaxf(mx, x[i][e]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) red[wv] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < kSmRV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[i][e] = expf(x[i][e] - mx);  // exp(-inf) = 0 for the padding
+      sum += x[i][e];
+    }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if (lane == 0) red[4 + wv] = sum;
+  __syncthreads();
+  const float inv = 1.f / ((red[4] + red[5]) + (red[6] + red[7]));
+#pragma unroll
+  for (int i = 0; i < kSmRV; ++i) {
+    const int j = (tid + 256 * i) * 4;
+    if (j < Np) {
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = x[i][e] * inv;
+      *reinterpret_cast<f4*>(row + j) = o;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_softmax_rows(float* S, int N, int Np) {
   __shared__ float red[8];
   float* row = S + (size_t)blockIdx.x * Np;
@@ -903,7 +949,10 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
                       nullptr};
         FH(gemm_nt(sq, st, -1, nullptr));
         ph = prof_begin(st);
-        hipLaunchKernelGGL(k_softmax_rows, dim3(S.heads * N), dim3(256), 0, st, m.att_s, N, Np);
+        if (Np % 4 == 0 && Np <= 256 * 4 * kSmRV)
+          hipLaunchKernelGGL(k_softmax_rows_reg, dim3(S.heads * N), dim3(256), 0, st, m.att_s, N, Np);
+        else
+          hipLaunchKernelGGL(k_softmax_rows, dim3(S.heads * N), dim3(256), 0, st, m.att_s, N, Np);
         FH(hipGetLastError());
         hipLaunchKernelGGL(k_vt, dim3(grid_for((size_t)C * Np)), dim3(256), 0, st, qkv, m.att_vt, N, Np, C, S.heads,
                            hd);
