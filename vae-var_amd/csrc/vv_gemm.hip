@@ -1340,9 +1340,12 @@ __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* 
   } else if ((int)blockIdx.x < args.tdp) {
     tile = xcd_remap(blockIdx.x, args.tdp);
   } else {
-    part = blockIdx.x - args.tdp;
-    const int S = args.tsplit, c = part % S;
-    tile = args.tdp + part / S;
+    // split items in chunk-major order, contiguous per XCD (xcd_remap): one XCD runs the same k-chunk of
+    // neighbouring tiles, so the A / B k-slices it shares stay in its L2; part = the item's partial slot
+    const int items = gridDim.x - args.tdp, S = args.tsplit, tt = items / S;
+    const int L = xcd_remap(blockIdx.x - args.tdp, items), c = L / tt, tl = L - c * tt;
+    part = tl * S + c;
+    tile = args.tdp + tl;
     kb = (c * nkt) / S;
     ke = ((c + 1) * nkt) / S;
   }
