@@ -340,6 +340,36 @@ __device__ __forceinline__ void attn_rows(const float* __restrict__ src, int ld,
   }
 }
 
+// NA such [16][n] blocks (n <= 192: at most 3 float4 per thread each), every global load issued before the
+// first LDS store so the workgroup waits for one memory round trip instead of one per block
+template <int NA>
+__device__ __forceinline__ void attn_rows_all(const float* const (&src)[NA], const int (&ld)[NA], float* const (&dst)[NA],
+                                              int st, int n) {
+  constexpr int IT = 3;
+  const int q4 = n >> 2, tot = WN_ * q4;
+  f4 r[NA][IT];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int idx = threadIdx.x + i * kAttnThreads;
+      if (idx < tot) {
+        const int t = idx / q4, d = (idx - t * q4) * 4;
+        r[a][i] = *reinterpret_cast<const f4*>(src[a] + (size_t)t * ld[a] + d);
+      }
+    }
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int idx = threadIdx.x + i * kAttnThreads;
+      if (idx < tot) {
+        const int t = idx / q4, d = (idx - t * q4) * 4;
+        *reinterpret_cast<f4*>(dst[a] + t * st + d) = r[a][i];
+      }
+    }
+}
+
 // sv[jj] = sum_d x[i][hl*hd + d] y[j0+jj][hl*hd + d] over this lane's d-part, then over the DP lanes
 __device__ __forceinline__ void attn_quad(const float* x, const float* y, const AttnShape& S, int hl, int i, int j0,
                                           int dpi, float sv[4]) {
@@ -371,9 +401,16 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_fwd(AttnArgs a) {
   float* v = k + WN_ * S.st;
   float* p = v + WN_ * S.st;  // [hpb][16][17]
   const float* base = G.qkv + (size_t)win * WN_ * ldq + h0 * S.hd;
-  attn_rows(base, ldq, q, S.st, W);
-  attn_rows(base + C, ldq, k, S.st, W);
-  attn_rows(base + 2 * C, ldq, v, S.st, W);
+  if (W <= 192) {
+    const float* const srcs[3] = {base, base + C, base + 2 * C};
+    const int lds_[3] = {ldq, ldq, ldq};
+    float* const dsts[3] = {q, k, v};
+    attn_rows_all<3>(srcs, lds_, dsts, S.st, W);
+  } else {
+    attn_rows(base, ldq, q, S.st, W);
+    attn_rows(base + C, ldq, k, S.st, W);
+    attn_rows(base + 2 * C, ldq, v, S.st, W);
+  }
   __syncthreads();
   // S = (q k^T) scale + bias + mask -> softmax (swinblock.py:151-168)
   const int dpi = tid % S.dp;
@@ -440,10 +477,18 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_bwd(AttnArgs a) {
   float* p = dO + WN_ * S.st;       // [hpb][16][17]
   float* ds = p + S.hpb * WN_ * 17;  // [hpb][16][17]
   const float* base = G.qkv + (size_t)win * WN_ * ldq + h0 * S.hd;
-  attn_rows(base, ldq, q, S.st, W);
-  attn_rows(base + C, ldq, k, S.st, W);
-  attn_rows(base + 2 * C, ldq, v, S.st, W);
-  attn_rows(G.dO + (size_t)win * WN_ * C + h0 * S.hd, C, dO, S.st, W);
+  const float* dOb = G.dO + (size_t)win * WN_ * C + h0 * S.hd;
+  if (W <= 192) {
+    const float* const srcs[4] = {base, base + C, base + 2 * C, dOb};
+    const int lds_[4] = {ldq, ldq, ldq, C};
+    float* const dsts[4] = {q, k, v, dO};
+    attn_rows_all<4>(srcs, lds_, dsts, S.st, W);
+  } else {
+    attn_rows(base, ldq, q, S.st, W);
+    attn_rows(base + C, ldq, k, S.st, W);
+    attn_rows(base + 2 * C, ldq, v, S.st, W);
+    attn_rows(dOb, C, dO, S.st, W);
+  }
   const float* Pg = G.P + ((size_t)win * a.heads + h0) * WN_ * WN_;
   for (int idx = tid; idx < S.hpb * WN_ * WN_; idx += kAttnThreads) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
   __syncthreads();
