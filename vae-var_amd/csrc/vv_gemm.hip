@@ -1717,7 +1717,12 @@ static int pick_tile(const GemmArgs& a) {
   if (g_math == GEMM_SPLIT16 || g_math == GEMM_SPLIT) {
     // GEMM_SPLIT16: fp16x3 128x128 for the deep-K GEMMs that give >= 128 tiles; the bf16x6 64x64 kernel for the
     // short-K / few-tile GEMMs of the Swin towers (its pipeline prologue and epilogue dominate there)
-    if (g_math == GEMM_SPLIT16 && a.K >= 768 && tiles_of(a, 128, 128) >= 128) return 36;
+    static int h3_mink = -1;  // VAEVAR_H3_MINK: smallest K sent to the fp16x3 kernel (default 768)
+    if (h3_mink < 0) {
+      const char* e = getenv("VAEVAR_H3_MINK");
+      h3_mink = e ? std::max(64, atoi(e)) : 768;
+    }
+    if (g_math == GEMM_SPLIT16 && a.K >= h3_mink && tiles_of(a, 128, 128) >= 128) return 36;
     // pipelined 128x128 (64x64 per wave, one barrier per k-tile) for the deep-K GEMMs that fill the chip with
     // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline)
     const long t128 = tiles_of(a, 128, 128);
