@@ -101,3 +101,21 @@ def test_fcst_param_enumeration_matches_reference_keys():
         assert set(got) == set(want)
         for k, v in want.items():
             assert tuple(got[k]) == tuple(v), k
+
+
+def test_new_entry_points_reject_bad_arguments():
+    """The observation-operator, metrics and two-loop entry points validate their arguments before any device
+    work: a null context or null buffers return VV_E_ARG (1001) with a message, never a crash (no GPU needed)."""
+    import ctypes
+
+    from vaevar import _lib
+
+    lib = _lib.lib
+    assert lib.vv_set_obs_operator(None, 40, 13, None) == 1001
+    assert lib.vv_obs_augment(None, None, 40, 13, None, None, 1, 8, 8, None) == 1001
+    assert lib.vv_metrics(None, None, None, None, None, None, 1, 69, 8, 8, None, None, None) == 1001
+    ro = (ctypes.c_float * 1)(1.0)
+    assert lib.vv_lbfgs_two_loop(None, None, None, None, ro, 1, 1.0, 16, None) == 1001
+    buf = ctypes.create_string_buffer(256)
+    lib.vv_last_error(buf, 256)
+    assert buf.value  # a message describes the failure
