@@ -116,3 +116,52 @@ def test_metrics_kernel_g9(tag, Hs, Ws, seed):
     eb = float(np.abs(b.cpu().numpy() - g["bias_" + tag]).max() / np.abs(g["bias_" + tag]).max())
     print(f"G9 {Hs}x{Ws}: WRMSE rel {ew:.1e}, Bias rel {eb:.1e}")
     assert ew < 1e-5 and eb < 1e-5
+
+
+def test_cycle_real_obs_matches_manual_composition(tmp_path):
+    """obs_type 'real_simu_nofiltering' through the cycle driver (full decoder, 69ch 128x256, the flow stand-in as
+    the forecast, 2 cycles, Nit=1) equals the same steps composed by hand from DAProblem / one_step_da / integrate
+    bit for bit; the observation-space fields have 4 + 5*40 channels."""
+    from vaevar import config as C
+    from vaevar.cycle import CyclicVAE4DVar, SyntheticRealObs
+    from vaevar.da import one_step_da
+    from vaevar.engine import DAProblem, LGUnet, integrate, obs_augment
+    from vaevar.problem import ObsInterpolater, make_problem
+    from vaevar.synth import smooth_field, splitmix_uniform
+
+    oi = ObsInterpolater(13, 40)
+    mean = np.asarray(C.MODEL_MEAN, np.float32)[:, None, None]
+    std = np.asarray(C.MODEL_STD, np.float32)[:, None, None]
+
+    def truth(t):
+        k = int((t - T0).total_seconds() // 3600)
+        return (mean + std * smooth_field(6000 + k, (69, 128, 256))).astype(np.float32)
+
+    p = make_problem(nch=69, Hs=128, Ws=256, T=1, seed=8080, obs_frac=0.03)
+    H = (splitmix_uniform(81, 204 * 128 * 256).reshape(1, 204, 128, 256) < 0.03).astype(np.float32)
+    dec = LGUnet(C.DECODER, 1, 1).load_synthetic()
+    fc = LGUnet(C.FLOW, 1, 1).load_synthetic()
+    obs = SyntheticRealObs(dec.ctx, truth, H, p["R"], oi.interp)
+    end = T0 + dt.timedelta(hours=12)
+    cyc = CyclicVAE4DVar(dec, fc, obs, T0, end, Nit=1, name="real", out_dir=str(tmp_path), xb0=p["xb"],
+                         obs_interp=oi.interp)
+    xas = []
+    cyc.run_assimilation(log=lambda t, res: xas.append(res["xa"].clone()))
+    assert len(xas) == 2
+    # by hand
+    interp = torch.from_numpy(oi.interp).cuda()
+    Rd = obs_augment(dec.ctx, interp, torch.from_numpy(p["R"]).cuda())
+    xb = torch.from_numpy(p["xb"]).cuda()
+    for k in range(2):
+        gt = torch.from_numpy(truth(T0 + dt.timedelta(hours=6 * k)))[None].cuda()
+        Hd = torch.from_numpy(H).cuda()
+        yo = obs_augment(dec.ctx, interp, gt) * Hd
+        assert yo.shape[1] == 204
+        prob = DAProblem(dec, {"xb": xb, "yo": yo, "H": Hd, "R": Rd, "mean": cyc.mean, "std": cyc.std,
+                               "std_tr": cyc.std_tr}, obs_interp=oi.interp)
+        xa = one_step_da(prob, nit=1)["xa"]
+        assert torch.equal(xa, xas[k]), k
+        xb = integrate(fc, xa, cyc.mean_d, cyc.std_d, 1)
+    assert torch.equal(xb, cyc.xb)
+    w = np.asarray(cyc.metrics_list["ana_wrmse"])
+    assert w.shape == (2, 69) and np.isfinite(w).all()

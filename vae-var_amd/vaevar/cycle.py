@@ -73,6 +73,30 @@ class SyntheticObs:
         return gt, self.H, self.R, gt  # yo, H, R, gt
 
 
+class SyntheticRealObs:
+    """get_obs_info for obs_type 'real_simu_nofiltering' (da_4dvar.py:764-792): the truth window gt, its level
+    interpolation gt_aug = x_aug(gt) (obs_interpolater, :770-776), yo = gt_aug * H (no filtering mask, :783-792),
+    R = get_R_matrix_from_gt (:729-756), all in the 4 + 5*n_out observation channels; x_aug runs on the GPU
+    (vv_obs_augment). H: (da_win, 4 + 5*n_out, Hs, Ws) station mask; R: the static (da_win, 69, Hs, Ws) R."""
+
+    def __init__(self, ctx, truth, H, R, interp, da_win: int = 1,
+                 step_int_time: _dt.timedelta = _dt.timedelta(hours=1), device: int = 0):
+        from .engine import obs_augment
+
+        self.dev = torch.device("cuda", device)
+        self.truth, self.da_win, self.step = truth, da_win, step_int_time
+        self.interp = torch.as_tensor(np.asarray(interp, np.float32)).to(self.dev)
+        self.H = torch.as_tensor(np.asarray(H, np.float32)).to(self.dev)
+        self._aug = lambda x: obs_augment(ctx, self.interp, x)
+        self.R = self._aug(torch.as_tensor(np.asarray(R, np.float32)).to(self.dev))
+
+    def get_obs_info(self, t: _dt.datetime):
+        gt = np.stack([self.truth(t + i * self.step) for i in range(self.da_win)], 0).astype(np.float32)
+        gt_d = torch.from_numpy(gt).to(self.dev)
+        yo = self._aug(gt_d) * self.H
+        return yo, self.H, self.R, gt_d
+
+
 class CyclicVAE4DVar:
     """cyclic_4dvar restricted to da_mode 'vae4dvar' (da_4dvar.py:1179-1306, 1314-1342)."""
 
