@@ -1173,42 +1173,47 @@ hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s) {
   return hipGetLastError();
 }
 // L-BFGS two-loop recursion (torch/optim/lbfgs.py:404-442) with its scalars kept on the device: per history
-// pair one dot (k_dot partials), one single-block kernel that finishes the dot exactly as k_final_d does and
-// forms the coefficient in fp32 as torch does on 0-d tensors, and one axpy that reads the coefficient; no host
-// round trip. First loop (mode 0): al[i] = f32(s_i . q) * ro[i], q += (-al[i]) y_i. Second loop (mode 1):
-// be = f32(y_i . r) * ro[i], r += (al[i] - be) s_i.
-__global__ __launch_bounds__(256) void k_twoloop_coef(const double* partial, int n, float ro, float* al, int i,
-                                                      int mode, float* coef) {
+// pair one dot (k_dot partials) and one axpy whose blocks each finish the dot exactly as k_final_d does and form
+// the coefficient in fp32 as torch does on 0-d tensors; no host round trip. First loop (mode 0):
+// al[i] = f32(s_i . q) * ro[i], q += (-al[i]) y_i. Second loop (mode 1): be = f32(y_i . r) * ro[i],
+// r += (al[i] - be) s_i.
+// the coefficient step fused into the axpy: every block finishes the dot from the same partials in the same order
+// as k_final_d (so every block holds the same fp32 coefficient) and block 0 records al[i]; 2 launches per
+// history pair instead of 3
+constexpr int kTwoLoopBlocks = 256;
+__global__ __launch_bounds__(256) void k_twoloop_axpy(float* y, const float* x, const double* partial, int nblk,
+                                                      float ro, float* al, int i, int mode, int64_t n) {
   __shared__ double red[4];
+  __shared__ float coef;
   double acc = 0.0;
-  for (int j = threadIdx.x; j < n; j += 256) acc += partial[j];
+  for (int j = threadIdx.x; j < nblk; j += 256) acc += partial[j];
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) {
     const float v = (float)t * ro;
     if (mode == 0) {
-      al[i] = v;
-      coef[0] = -v;
+      if (blockIdx.x == 0) al[i] = v;
+      coef = -v;
     } else {
-      coef[0] = al[i] - v;
+      coef = al[i] - v;
     }
   }
-}
-__global__ __launch_bounds__(256) void k_axpy_dev(float* y, const float* x, const float* coef, int64_t n) {
-  const float a = coef[0];
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] = y[i] + a * x[i];
+  __syncthreads();
+  const float a = coef;
+  for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) y[k] = y[k] + a * x[k];
 }
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,
                           int64_t n, double* partial, int nblk, float* al, float* coef, hipStream_t s) {
+  (void)coef;
   for (int i = m - 1; i >= 0; --i) {
     hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, S[i], q, n, partial);
-    hipLaunchKernelGGL(k_twoloop_coef, dim3(1), dim3(256), 0, s, partial, nblk, ro[i], al, i, 0, coef);
-    hipLaunchKernelGGL(k_axpy_dev, dim3(vgrid(n)), dim3(256), 0, s, q, Y[i], coef, n);
+    hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, Y[i], partial, nblk, ro[i], al, i, 0,
+                       n);
   }
   hipLaunchKernelGGL(k_scale, dim3(vgrid(n)), dim3(256), 0, s, q, H_diag, n);
   for (int i = 0; i < m; ++i) {
     hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, Y[i], q, n, partial);
-    hipLaunchKernelGGL(k_twoloop_coef, dim3(1), dim3(256), 0, s, partial, nblk, ro[i], al, i, 1, coef);
-    hipLaunchKernelGGL(k_axpy_dev, dim3(vgrid(n)), dim3(256), 0, s, q, S[i], coef, n);
+    hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, S[i], partial, nblk, ro[i], al, i, 1,
+                       n);
   }
   return hipGetLastError();
 }
