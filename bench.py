@@ -1,23 +1,29 @@
 #!/usr/bin/env python3
-"""Benchmark of the VAE-Var 4D-Var inner loop on MI355X (BASELINE.json metric).
+"""Benchmark of the VAE-Var 4D-Var inner loop on MI355X (BASELINE.json metric: inner-loop iterations/s and
+wall-clock to the converged analysis, 69ch 128x256 state).
 
-Workload (N=1): BASELINE config 2 — 3D-Var with the full VAE decoder (nf_model/parameters0_old.yaml,
-216M parameters), 69-channel 128x256 state, L-BFGS(history 10, max_iter 10, strong Wolfe) as in
-da_4dvar.py:1240, synthetic weights and observations (no checkpoints ship with the reference).
+Workload (default): BASELINE config 2 — 3D-Var with the full VAE decoder (nf_model/parameters0_old.yaml, 216M
+parameters), 69-channel 128x256 state, L-BFGS(history 10, max_iter 10, strong Wolfe) as da_4dvar.py:1240, Nit = 10
+outer passes (the reference's budget: <= 100 iterations), synthetic weights and observations (no checkpoints ship
+with the reference). `--config 3|4|5` selects the other BASELINE configs (Nit 10 / 10 / 5).
 
-  step   = one outer `lbfgs.step(closure)` (<= 10 L-BFGS iterations, <= 12 closure evaluations);
-           --steps 10 is the reference's converged budget for config 2 (Nit 10 x max_iter 10 = 100 iters).
-  value  = L-BFGS iterations per second over the whole job (sum over ranks / max time over ranks);
-           the analysis decode and the RCCL gather of all analyses to rank 0 are inside the timed region.
-  N > 1  = ensemble: rank r runs its own analysis (seed + r), weak scaling, no inner-loop communication.
+  step   = one converged analysis (one_step_DA 'vae4dvar', da_4dvar.py:1179-1306): z = 0, Nit outer lbfgs.step
+           calls, the analysis decode; at N > 1 plus the RCCL gather of every rank's analysis to rank 0
+  value  = L-BFGS iterations per second over the whole job (iterations summed over ranks / max time over ranks)
+  N > 1  = ensemble: rank r runs its own analysis (seed + r), weak scaling, no inner-loop
+           communication. `--gpus N` without WORLD_SIZE spawns the N ranks itself (before any GPU call); under
+           torch.distributed.run WORLD_SIZE must equal --gpus.
+  config4 = every line also carries BASELINE config 4 (T = 6 window, one analysis per GPU, the RCCL gather),
+           timed on its own after the main region, so its analyses/s can be compared across N as well.
 
-Prints ONE JSON line on rank 0. See DESIGN.md §Measurement.
+Prints ONE JSON line on rank 0. See DESIGN.md §6.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -25,213 +31,394 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "vae-var_amd"))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense peak (MI355X_MICROARCH.md, chip-level table)
-PEAK_BF16_TFLOPS = 2500.0  # MI355X bf16 MFMA dense peak; the split GEMM spends 6 bf16 products per fp32 product
-PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
-PEAK_SPLIT16_TFLOPS = 2500.0 / 3  # fp16 MFMA dense peak (= bf16); the fp16x3 split spends 3 products per fp32 one
-PEAK_HBM_GBS = 8000.0     # HBM3E spec
+PEAK_F32_TFLOPS = 157.3    # MI355X exact-f32 MFMA dense peak (MI355X_MICROARCH.md, chip-level table)
+PEAK_16_TFLOPS = 2500.0    # MI355X bf16 / fp16 MFMA dense peak
+PEAK_SPLIT16_TFLOPS = PEAK_16_TFLOPS / 3  # fp16x3 split: 3 fp16 MFMA products per fp32 product
+PEAK_SPLIT_TFLOPS = PEAK_16_TFLOPS / 6    # bf16x6 split: 6 bf16 MFMA products per fp32 product
 FLOPS_PER_EVAL = {1: 1787.8e9, 2: 3577.0e9, 6: 10733.7e9}  # SURVEY §8 d (input-grad only)
+METRIC = "4D-Var inner-loop iters/sec + wall-clock to convergence, 69ch 128×256 state"
 
 CONFIGS = {
-    2: dict(T=1, name="config 2: 3D-Var, full VAE decoder (parameters0_old), 69ch 128x256, 100 L-BFGS iters"),
-    3: dict(T=2, name="config 3: 4D-Var, 2-step window with LGUnet flow stand-in, 69ch 128x256, 100 iters"),
-    4: dict(T=6, name="config 4: 4D-Var, 6-step window, one analysis per GPU (ensemble)"),
-    5: dict(T=2, grid=(721, 1440), name="config 5: 4D-Var at 0.25 deg (69ch 721x1440 state, nearest-interpolated "
-                                          "to the 128x256 networks), T=2, 50 iters"),
+    2: dict(T=1, nit=10, name="config 2: 3D-Var, full VAE decoder (parameters0_old), 69ch 128x256, L-BFGS Nit 10 "
+                             "(<= 100 iterations) per analysis"),
+    3: dict(T=2, nit=10, name="config 3: 4D-Var, 2-step window with the LGUnet flow stand-in, 69ch 128x256, Nit 10"),
+    4: dict(T=6, nit=10, name="config 4: 4D-Var, 6-step window (5 flow steps), 69ch 128x256, Nit 10, one analysis "
+                             "per GPU + RCCL gather"),
+    5: dict(T=2, nit=5, grid=(721, 1440), name="config 5: 4D-Var at 0.25 deg (69ch 721x1440 state, nearest-"
+                                               "interpolated to the 128x256 networks), T=2, Nit 5 (<= 50 iterations)"),
 }
 
 
-def cpu_baseline(prob_np, evals_per_iter, n_evals, threads):
-    """Oracle torch-CPU restatement (oracle/) timed in both SURVEY §8 d modes: weight grads ON (the reference
-    computes them, quirk Q5; this is `value`) and OFF (input gradient only, like the HIP path)."""
+# ---------------------------------------------------------------------------------------------------------------
+# launch
+def spawn(n: int, argv) -> int:
+    """Start N ranks of this script (before this process touches the GPU) and return rank 0's exit code."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def physical_cores():
+    """(physical cores among the CPUs this process may run on, those CPUs, the OMP_NUM_THREADS share if set)."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", str(c)))
+    share = os.environ.get("OMP_NUM_THREADS")
+    return len(cores), len(cpus), int(share) if share and share.isdigit() else None
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle restatement (oracle/, a torch-CPU port of the reference path) on the host cores
+def cpu_baseline(prob_np, T, evals_per_iter, gpu_evals_per_analysis, evals, threads, cores_note):
+    import torch
+
     from oracle.da_ref import oracle_problem
     from oracle.lgunet_ref import synth_params
     from vaevar import config as C
 
     torch.set_num_threads(threads)
     p = synth_params(C.DECODER)
-    ro = oracle_problem(prob_np, p, C.DECODER)
+    fp = synth_params(C.FLOW) if T > 1 else None
+    ro = oracle_problem(prob_np, p, C.DECODER, fp, C.FLOW if T > 1 else None)
     z = torch.zeros(1, 32, 128, 256, requires_grad=True)
+    params = list(p.values()) + (list(fp.values()) if fp else [])
 
-    def timed(weight_grads):
-        for v in p.values():
+    def timed(weight_grads, n):
+        for v in params:
             v.requires_grad_(weight_grads)
             v.grad = None
 
         def ev():
-            for v in p.values():
+            for v in params:
                 v.grad = None
             z.grad = None
             ro.loss(z).backward()
 
         ev()  # warm-up
         t0 = time.time()
-        for _ in range(n_evals):
+        for _ in range(n):
             ev()
-        return (time.time() - t0) / n_evals
+        return (time.time() - t0) / n
 
-    per_eval = timed(True)
-    per_eval_off = timed(False)
-    return per_eval, {"value": 1.0 / (per_eval * evals_per_iter), "unit": "L-BFGS iters/s", "cores": threads,
-                      "kind": "port",
-                      "value_weight_grads_off": 1.0 / (per_eval_off * evals_per_iter),
-                      "sample": f"{n_evals} closure evaluations (J + dJ/dz) of config 2 at z=0 on {threads} host "
-                                f"threads after 1 warm-up, per mode: weight grads on (reference-faithful, `value`) "
-                                f"{per_eval:.3f} s/eval, off {per_eval_off:.3f} s/eval; iters/s = 1/(s_per_eval x "
-                                f"{evals_per_iter:.3f} evals per iteration of the GPU run)"}
+    per_eval = timed(True, evals)
+    out = {"value": 1.0 / (per_eval * evals_per_iter), "unit": "L-BFGS iters/s", "cores": threads, "kind": "port"}
+    sample = (f"{evals} closure evaluation(s) (J + dJ/dz) at z=0 after 1 warm-up on {threads} host threads "
+              f"({cores_note}), weight grads on as the reference computes them (quirk Q5): {per_eval:.3f} s/eval")
+    if T == 1:
+        per_off = timed(False, evals)
+        out["value_weight_grads_off"] = 1.0 / (per_off * evals_per_iter)
+        sample += f"; off: {per_off:.3f} s/eval"
+    out["sample"] = sample + (f"; iters/s = 1 / (s_per_eval x {evals_per_iter:.3f} evals per iteration of the GPU "
+                              f"run)")
+    return per_eval, out, per_eval * gpu_evals_per_analysis
 
 
 def gemm_traffic(kernel):
-    """HBM bytes per launch of `kernel` ("k_gemm_h3" or "all") from the committed rocprofv3 --pmc passes
-    (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections, tools/pmc_traffic.py) of `bench.py --config 2`; PMC counters
-    cannot be read live."""
-    path = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f)[kernel]["hbm_bytes_per_launch"]
-    except (OSError, KeyError, ValueError, TypeError):
-        return None
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes of `bench.py` (FETCH_SIZE x2 +
+    WRITE_SIZE with the gfx950 corrections, tools/pmc_traffic.py); PMC counters cannot be read live."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, "gemm_traffic.json")
+        try:
+            with open(path) as f:
+                return json.load(f)[kernel]["hbm_bytes_per_launch"], f"profiles/{rnd}/gemm_traffic.json"
+        except (OSError, KeyError, ValueError, TypeError):
+            continue
+    return None, None
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# per-rank workloads
+class GpuAnalyses:
+    """One rank's share: the HIP engine (libvaevar) on cuda:LOCAL_RANK."""
+
+    def __init__(self, cfg_id: int, rank: int, local: int):
+        import torch
+
+        from vaevar import config as C
+        from vaevar.engine import DAProblem, LGUnet
+        from vaevar.problem import make_problem
+
+        self.torch = torch
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.cfg = CONFIGS[cfg_id]
+        self.T, self.nit = self.cfg["T"], self.cfg["nit"]
+        self.dec = LGUnet(C.DECODER, 1, 1, device=local).load_synthetic()
+        self.flow = None
+        Hs, Ws = self.cfg.get("grid", (128, 256))
+        self.prob_np = make_problem(nch=69, Hs=Hs, Ws=Ws, T=self.T, seed=20250620 + rank)
+        if self.T > 1:
+            self.flow = LGUnet(C.FLOW, 1, self.T - 1, device=local).load_synthetic()
+        self.prob = DAProblem(self.dec, self.prob_np, flow=self.flow, device=local)
+        self.ctx = self.prob.ctx
+        self._C, self._DAProblem, self._LGUnet, self._make_problem = C, DAProblem, LGUnet, make_problem
+        self.rank, self.local = rank, local
+
+    def analysis(self):
+        from vaevar.da import one_step_da
+
+        res = one_step_da(self.prob, nit=self.nit, log_terms=False)
+        return res["xa"], res["n_iter"], res["n_eval"]
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def config4(self):
+        """Re-bind this rank to a config-4 problem (T = 6, five flow slots); returns the analysis runner."""
+        flow6 = self._LGUnet(self._C.FLOW, 1, 5, device=self.local).load_synthetic()
+        p6 = self._make_problem(nch=69, Hs=128, Ws=256, T=6, seed=20250620 + self.rank)
+        self.prob = self._DAProblem(self.dec, p6, flow=flow6, device=self.local)
+        self.flow, self.nit = flow6, CONFIGS[4]["nit"]
+        return self.analysis
+
+
+class SelftestAnalyses:
+    """--selftest: a stand-in analysis with known outputs (CPU, no GPU) that exercises the launch, the gloo/RCCL
+    collectives, the gather and the JSON aggregation of this script (tests/test_bench_launch.py)."""
+
+    def __init__(self, cfg_id: int, rank: int, local: int):
+        import torch
+
+        self.torch, self.rank = torch, rank
+        self.T, self.nit = CONFIGS[cfg_id]["T"], CONFIGS[cfg_id]["nit"]
+
+    def analysis(self):
+        time.sleep(0.01 * (1 + self.rank))
+        return self.torch.full((69, 128, 256), float(self.rank)), 97 + self.rank, 110 + self.rank
+
+    def sync(self):
+        pass
+
+    def config4(self):
+        return self.analysis
+
+
+def timed_analyses(w, ensemble, steps, dev):
+    """Barrier + sync, `steps` analyses (each gathered to rank 0 at N > 1), sync + barrier; max time over ranks."""
+    ensemble.barrier()
+    w.sync()
+    t0 = time.perf_counter()
+    iters = evals = 0
+    shapes = None
+    for _ in range(steps):
+        xa, it, ev = w.analysis()
+        xs = ensemble.gather_analyses(xa)
+        iters, evals = iters + it, evals + ev
+        shapes = [tuple(x.shape) for x in xs] if xs is not None else None
+    w.sync()
+    ensemble.barrier()
+    el = time.perf_counter() - t0
+    return (ensemble.reduce_scalar(el, "max", dev), ensemble.reduce_scalar(iters, "sum", dev),
+            ensemble.reduce_scalar(evals, "sum", dev), shapes)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10, help="outer L-BFGS steps (Nit)")
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed analyses per rank (each = Nit outer L-BFGS passes)")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed analyses per rank before the timed ones")
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-evals", type=int, default=3)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-evals", type=int, default=None, help="timed CPU closure evaluations (default by config)")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel-class profile")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (T=6) line section")
+    ap.add_argument("--no-exact-f32", action="store_true", help="skip the exact-f32 GEMM analysis")
+    ap.add_argument("--selftest", action="store_true", help="CPU stand-in analyses (tests the launch/aggregation)")
     args = ap.parse_args()
 
-    from vaevar import config as C
+    world = os.environ.get("WORLD_SIZE")
+    if world is None and args.gpus > 1:
+        sys.exit(spawn(args.gpus, sys.argv[1:]))
+    if world is not None and int(world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch  # noqa: F401  (after the spawn: the parent of N ranks never touches the GPU)
+
     from vaevar import ensemble
-    from vaevar.da import one_step_da
-    from vaevar.engine import DAProblem, LGUnet
-    from vaevar.lbfgs import LBFGS
-    from vaevar.problem import make_problem
 
-    rank, size, local = ensemble.init()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    T = CONFIGS[args.config]["T"]
-    dec = LGUnet(C.DECODER, 1, 1, device=local).load_synthetic()
-    flow = LGUnet(C.FLOW, 1, T - 1, device=local).load_synthetic() if T > 1 else None
-    Hs, Ws = CONFIGS[args.config].get("grid", (128, 256))
-    prob_np = make_problem(nch=69, Hs=Hs, Ws=Ws, T=T, seed=20250620 + rank)
-    prob = DAProblem(dec, prob_np, flow=flow, device=local)
+    rank, size, local = ensemble.init("gloo" if args.selftest else None)
+    Runner = SelftestAnalyses if args.selftest else GpuAnalyses
+    w = Runner(args.config, rank, local)
+    dev = None if args.selftest else w.dev
 
-    # warm-up: W outer steps of a throw-away analysis (same path, same shapes)
-    if args.warmup > 0:
-        one_step_da(prob, nit=args.warmup, log_terms=False)
-    torch.cuda.synchronize()
-    prof = (rank == 0) and not args.no_profile
+    for _ in range(args.warmup):
+        w.analysis()
+    t_max, iters, evals, shapes = timed_analyses(w, ensemble, args.steps, dev)
 
-    ensemble.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = one_step_da(prob, nit=args.steps, log_terms=False)
-    xs = ensemble.gather_analyses(res["xa"])
-    torch.cuda.synchronize()
-    ensemble.barrier()
-    elapsed = time.perf_counter() - t0
-    if prof:
-        # per-kernel-class HIP-event profile of the same work (a second pass of the same analysis, so the
-        # event records do not perturb the timed region above)
-        prob.ctx.profile_start()
-        res_p = one_step_da(prob, nit=args.steps, log_terms=False)
-        torch.cuda.synchronize()
-        pr = prob.ctx.profile_stop()
-        prof_elapsed = res_p["seconds"]
-    t_max = ensemble.reduce_scalar(elapsed, "max", dev)
-    iters = ensemble.reduce_scalar(res["n_iter"], "sum", dev)
-    evals = ensemble.reduce_scalar(res["n_eval"], "sum", dev)
+    prof = None
+    exact = None
+    if not args.selftest:
+        w.sync()
+        if rank == 0 and not args.no_profile:
+            # per-kernel-class HIP-event profile of one more analysis of the same problem (outside the timed region,
+            # so the event records do not perturb it; the closure launches eagerly while events are recorded)
+            w.ctx.profile_start()
+            t0 = time.perf_counter()
+            w.analysis()
+            w.sync()
+            prof = (w.ctx.profile_stop(), time.perf_counter() - t0)
+        if rank == 0 and not args.no_exact_f32:
+            old = w.ctx.gemm_math
+            w.ctx.gemm_math = "f32"
+            w.analysis()  # warm-up (graph capture) in this arithmetic
+            t0 = time.perf_counter()
+            _, it_f, ev_f = w.analysis()
+            w.sync()
+            exact = (it_f / (time.perf_counter() - t0), it_f, ev_f)
+            w.ctx.gemm_math = old
 
-    # J before / after (not timed)
-    j_end = prob.closure(res["z"], None)
-    z0 = torch.zeros_like(res["z"])
-    j_0 = prob.closure(z0, None)
+    # J before / after of the main problem (not timed)
+    j_info = None
+    if not args.selftest:
+        from vaevar.da import one_step_da
+
+        res = one_step_da(w.prob, nit=w.nit, log_terms=False)
+        j_end = w.prob.closure(res["z"], None)
+        j_0 = w.prob.closure(torch.zeros_like(res["z"]), None)
+        j_info = (j_0[0] + j_0[1], j_end[0] + j_end[1])
+
+    c4 = None
+    if not args.no_config4 and args.config != 4:
+        run4 = w.config4()
+        w.sync()
+        run4()  # warm-up / graph capture
+        ensemble.barrier()
+        w.sync()
+        t0 = time.perf_counter()
+        xa4, it4, ev4 = run4()
+        xs4 = ensemble.gather_analyses(xa4)
+        w.sync()
+        ensemble.barrier()
+        t4 = ensemble.reduce_scalar(time.perf_counter() - t0, "max", dev)
+        it4 = ensemble.reduce_scalar(it4, "sum", dev)
+        ev4 = ensemble.reduce_scalar(ev4, "sum", dev)
+        c4 = {"workload": CONFIGS[4]["name"], "n_gpus": size, "analyses": size, "analyses_per_s": size / t4,
+              "iters_per_s": it4 / t4, "wall_clock_s": t4, "iters": it4, "evals": ev4,
+              "gathered": [list(x.shape) for x in xs4] if xs4 is not None else None,
+              "timed_region": "barrier + sync, one config-4 analysis per rank, RCCL gather of the analyses to rank 0, "
+                              "sync + barrier; max over ranks"}
 
     if rank != 0:
+        ensemble.barrier()
         return
+    cfg = CONFIGS[args.config]
+    per_analysis = t_max / max(args.steps, 1)
     out = {
-        "metric": "4D-Var inner-loop iters/sec + wall-clock to convergence, 69ch 128×256 state",
+        "metric": METRIC,
         "value": iters / t_max,
         "unit": "L-BFGS iters/s",
         "n_gpus": size,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * t_max / args.steps,
+        "ms_per_step": 1e3 * per_analysis,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic",
-        "config": {"workload": CONFIGS[args.config]["name"], "analyses": size, "T": T, "outer_steps": args.steps,
-                   "parallelism": "ensemble: 1 independent analysis per GPU, RCCL gather of xa at the end"},
-        "wall_clock_to_convergence_s": t_max,
+        "dtype": "f32 (GEMMs: fp16x3 split, fp32-level error)",
+        "data": "synthetic (counter-hash RNG weights and observations; the reference ships no checkpoints)",
+        "config": {"workload": cfg["name"], "analyses_per_gpu": 1, "T": cfg["T"], "nit": cfg["nit"],
+                   "parallelism": f"ensemble: {size} independent analyses, 1 per GPU, RCCL gather of xa per step"},
+        "wall_clock_to_convergence_s": per_analysis,
         "iters": iters,
         "evals": evals,
+        "iters_per_analysis": iters / (size * args.steps),
         "evals_per_s": evals / t_max,
         "ms_per_eval": 1e3 * t_max * size / max(evals, 1),
-        "J_start": j_0[0] + j_0[1],
-        "J_final": j_end[0] + j_end[1],
-        "timed_region": "the Nit outer lbfgs.step calls + the analysis decode (+ the gather at N>1); the "
-                        "per-outer-pass logging evaluation cal_loss and WRMSE/Bias (da_4dvar.py:1256-1269, SURVEY "
-                        "§8 a3) is not run in it: 1 forward per outer pass, reported here as excluded",
+        "analyses_per_s": size * args.steps / t_max,
+        "gathered": [list(s) for s in shapes] if shapes else None,
+        "timed_region": f"barrier + sync, {args.steps} analyses per rank (z = 0, Nit = {cfg['nit']} outer lbfgs.step "
+                        "calls, the analysis decode, at N > 1 the RCCL gather of every analysis to rank 0), sync + "
+                        "barrier; max over ranks. The per-outer-pass logging evaluation cal_loss and WRMSE/Bias "
+                        "(da_4dvar.py:1256-1269, SURVEY §8 a3; 1 forward per pass) is not run in it",
     }
-    flops_eval = FLOPS_PER_EVAL.get(T)
-    if prof:
-        math = prob.ctx.gemm_math
+    if j_info:
+        out["J_start"], out["J_final"] = j_info
+    if exact:
+        out["exact_f32"] = {"value": exact[0], "unit": "L-BFGS iters/s", "iters": exact[1], "evals": exact[2],
+                            "note": "one analysis with every GEMM on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32), "
+                                    "rank 0, timed on its own"}
+    if c4:
+        out["config4"] = c4
+    if prof is not None:
+        pr, prof_s = prof
+        math = w.ctx.gemm_math
         g16, g6 = pr["gemm16"], pr["gemm"]
         allg = {k: g16[k] + g6[k] for k in ("ms", "flops", "bytes", "launches")}
         if math == "split16":
             dom, peak, tkey = g16, PEAK_SPLIT16_TFLOPS, "k_gemm_h3"
-            kname = ("k_rowscale + k_gemm_h3 (+ split-K fixup): every GEMM launch that ran the fp16x3 kernel in a "
-                     "HIP-event-profiled repeat of the timed analysis")
+            kname = ("k_gemm_h3 (+ its split-K fixup and the A row scaling): every GEMM launch that ran the fp16x3 "
+                     "kernel in a HIP-event-profiled repeat of one timed analysis")
             desc = ("fp16x3 split: fp32 operands scaled per row by 2^e and split into 2 fp16 planes, 3 "
                     "v_mfma_f32_32x32x16_f16 products per fp32 product; peak = 2.5 PF fp16 dense / 3")
         elif math == "split":
             dom, peak, tkey = allg, PEAK_SPLIT_TFLOPS, "all"
-            kname = "every GEMM launch (k_gemm_bs*) of a HIP-event-profiled repeat of the timed analysis"
-            desc = "bf16x6 split (fp32 operands as 3 bf16 planes, 6 v_mfma_f32_32x32x16_bf16 products; peak = 2.5 PF / 6)"
+            kname = "every GEMM launch of a HIP-event-profiled repeat of one timed analysis"
+            desc = "bf16x6 split (6 v_mfma_f32_32x32x16_bf16 products per fp32 product; peak = 2.5 PF / 6)"
         else:
             dom, peak, tkey = allg, PEAK_F32_TFLOPS, "all"
-            kname = "every GEMM launch (k_gemm_nt) of a HIP-event-profiled repeat of the timed analysis"
+            kname = "every GEMM launch (k_gemm_nt) of a HIP-event-profiled repeat of one timed analysis"
             desc = "exact f32 MFMA (v_mfma_f32_32x32x2_f32; peak 157.3 TF)"
         ach = dom["flops"] / max(dom["ms"] * 1e-3, 1e-12) / 1e12
         n = max(dom["launches"], 1)
-        all_ach = allg["flops"] / max(allg["ms"] * 1e-3, 1e-12) / 1e12
-        out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                           "frac": ach / peak, "traffic": gemm_traffic(tkey),
-                           "kernel": kname, "gemm_math": desc,
-                           "frac_of_f32_mfma_peak": ach / PEAK_F32_TFLOPS,
+        traffic, tsrc = gemm_traffic(tkey)
+        out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+                           "traffic": traffic, "kernel": kname, "gemm_math": desc,
                            "launches": dom["launches"], "avg_launch_us": 1e3 * dom["ms"] / n,
-                           "flops_per_launch": dom["flops"] / n,
-                           "algorithmic_bytes_per_launch": dom["bytes"] / n,
+                           "flops_per_launch": dom["flops"] / n, "algorithmic_bytes_per_launch": dom["bytes"] / n,
                            "share_of_gemm_time": dom["ms"] / max(allg["ms"], 1e-12),
-                           "all_gemm": {"achieved": all_ach, "launches": allg["launches"],
-                                        "avg_launch_us": 1e3 * allg["ms"] / max(allg["launches"], 1),
-                                        "frac_of_f32_mfma_peak": all_ach / PEAK_F32_TFLOPS},
-                           "traffic_source": "profiles/r01/gemm_traffic.json: rocprofv3 --pmc FETCH_SIZE / "
-                                             "WRITE_SIZE passes of bench.py (tools/pmc_traffic.py)"}
+                           "traffic_source": (f"{tsrc}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py "
+                                              "(tools/pmc_traffic.py)") if tsrc else None}
+        if math == "split16":
+            # the other GEMM class (bf16x6, short-K Swin-tower linears) against its own peak
+            g6a = g6["flops"] / max(g6["ms"] * 1e-3, 1e-12) / 1e12
+            out["roofline"]["bf16x6_class"] = {"achieved": g6a, "peak": PEAK_SPLIT_TFLOPS,
+                                               "frac": g6a / PEAK_SPLIT_TFLOPS, "launches": g6["launches"]}
         busy = sum(v["ms"] for v in pr.values())
         out["kernel_time_ms"] = {k: round(v["ms"], 3) for k, v in pr.items()}
         out["kernel_launches"] = {k: v["launches"] for k, v in pr.items()}
-        out["gpu_busy_frac"] = busy / (1e3 * prof_elapsed)
-        if flops_eval:
-            out["eval_roofline_frac"] = (flops_eval / (PEAK_F32_TFLOPS * 1e12)) / (t_max * size / max(evals, 1))
-    if size == 1 and not args.no_cpu_baseline and args.config == 2:
+        out["profiled_analysis_s"] = prof_s
+        # busy time of the (eager, event-profiled) repeat against the timed (graph-replayed) analysis
+        out["gpu_busy_frac"] = busy / (1e3 * per_analysis)
+        fe = FLOPS_PER_EVAL.get(cfg["T"])
+        if fe:
+            # whole-evaluation roofline (SURVEY §8 d) against the peak of the arithmetic actually used
+            ms_eval = 1e3 * t_max * size / max(evals, 1)
+            pk = {"split16": PEAK_SPLIT16_TFLOPS, "split": PEAK_SPLIT_TFLOPS}.get(math, PEAK_F32_TFLOPS)
+            out["eval_roofline"] = {"achieved_tflops": fe / (ms_eval * 1e-3) / 1e12, "peak": pk,
+                                    "frac": fe / (ms_eval * 1e-3) / 1e12 / pk}
+    if size == 1 and not args.no_cpu_baseline and not args.selftest and cfg["T"] <= 2 and "grid" not in cfg:
+        pc, ncpu, share = physical_cores()
+        threads = min(pc, share) if share else pc
+        note = (f"{pc} physical cores on the {ncpu} CPUs of this process's affinity"
+                + (f", OMP_NUM_THREADS share {share}" if share else ""))
         evals_per_iter = evals / max(iters, 1)
-        per_eval, cb = cpu_baseline(prob_np, evals_per_iter, args.cpu_evals, args.cpu_threads)
+        n_cpu = args.cpu_evals or (3 if cfg["T"] == 1 else 2)
+        per_eval, cb, cpu_conv = cpu_baseline(w.prob_np, cfg["T"], evals_per_iter, evals / max(args.steps, 1),
+                                              n_cpu, threads, note)
         out["cpu_baseline"] = cb
-        out["cpu_wall_clock_to_convergence_s_extrapolated"] = per_eval * evals
+        out["cpu_wall_clock_to_convergence_s_extrapolated"] = cpu_conv
         out["speedup_vs_cpu"] = out["value"] / cb["value"]
     print(json.dumps(out), flush=True)
+    ensemble.barrier()
 
 
 if __name__ == "__main__":

@@ -101,6 +101,10 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
 int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream);
 /* same, leaving {J_b, J_o} in device memory d_J[2]; no synchronisation */
 int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, void* stream);
+/* replay the closure from a hipGraph (default on; VAEVAR_GRAPH=0 at vv_ctx_create turns it off): the evaluation's
+   ~540 kernel launches are captured once per kind (J only / J + gradient) and replayed as one graph launch, with z
+   and grad_z copied through problem-owned buffers; results are bit-identical to the eager launches */
+int vv_set_closure_graph(vv_ctx* ctx, int enable);
 /* analysis state xa (C,Hs,Ws) */
 int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
 /* out = integrate(x, model, steps) (da_4dvar.py:666-681): z = (x - mean)/std (nearest to the model grid when
@@ -154,7 +158,7 @@ int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* 
    decoder_hr (nf_model/vae.py:90) and integrate (da_4dvar.py:671, 679); map has out_size entries (host) */
 int vv_nearest_map(int in_size, int out_size, int* map);
 
-/* GEMM arithmetic for every nn.Linear of the engine (process-wide; default VV_GEMM_SPLIT16, or the
+/* GEMM arithmetic for every nn.Linear of the context's models (per context; default VV_GEMM_SPLIT16, or the
    VAEVAR_GEMM_MATH=f32|split|split16 environment variable at vv_ctx_create):
    VV_GEMM_F32     = v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (torch fp32 matmul semantics);
    VV_GEMM_SPLIT   = each fp32 operand split exactly into three bf16 planes (x = h + m + l) and the six
@@ -174,7 +178,9 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    vv_ctx_destroy (which frees the planes) */
 int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K);
 
-/* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), epi as vv::Epi */
+/* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), K a multiple of 32. tile = -1 picks the
+   kernel as the engine does; otherwise one of the library kernels: 0 / 2 / 4 exact-f32 MFMA 128x128 / 64x64 /
+   32x64, 24 / 34 bf16x6 split 64x64 / pipelined 128x128, 36 fp16x3 split 128x128. Any other tile: VV_E_ARG. */
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
             int tile, void* stream);
 

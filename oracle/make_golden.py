@@ -428,12 +428,97 @@ def g9():
     np.savez(os.path.join(GOLD, "g9_metrics.npz"), model_std=std, **out)
 
 
+def g10(tr):
+    """G10 (BASELINE config 2 at its full budget): the reference's networks_old.LGUnet_all decoder
+    with torch.optim.LBFGS(history 10, max_iter 10, strong Wolfe) on the restated vae4dvar closure
+    (da_4dvar.py:1183-1246; the genuine one_step_DA hard-codes 721x1440, so the 128x256-state case is restated,
+    exactly as G5), Nit = 10 outer passes: J per pass, every line search's (t, evals), sampled xa. The decoder
+    parameters are frozen (requires_grad False): the latent gradient is the same computation, the unused
+    weight gradients (quirk Q5) only cost time."""
+    cfg = C.DECODER
+    m, p = build_ref(tr, cfg)
+    for v in m.parameters():
+        v.requires_grad_(False)
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620)
+    rp = RefProblem(prob, m, cfg["img_size"])
+    t0 = time.time()
+    with LineSearchRecorder() as ls:
+        xa, z, js, nev, nit = one_step_da_ref(rp, 10, (32, 128, 256),
+                                              log=lambda k, j: print(f"G10 pass {k}: J_b {j[0]:.6e} J_o {j[1]:.6e} "
+                                                                     f"({time.time() - t0:.0f}s)", flush=True))
+    xa = xa.numpy().astype(np.float32)
+    idx = sample_idx(xa.size, 8192, 1010)
+    flat = xa.reshape(-1).astype(np.float64)
+    print(f"G10 config-2 trajectory: {time.time() - t0:.0f}s, evals {nev}, iters {nit}, J {js}")
+    np.savez(os.path.join(GOLD, "g10_config2_trajectory.npz"), J=np.array(js, np.float64), n_eval=nev, n_iter=nit,
+             ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]),
+             idx_xa=idx, xa_sample=xa.reshape(-1)[idx], xa_sum=flat.sum(),
+             dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+
+
+def g11():
+    """G11: the reference's networks.LGUnet_all.LGUnet_all_1 at the full 0.25-degree
+    configuration (training_options.yaml:64-119: 69ch 721x1440, 16,200-token global LG window), synthetic weights,
+    one forward on a smooth input: sampled outputs + sums."""
+    import importlib
+
+    from oracle.lgunet1_ref import synth_params as synth1
+
+    L1 = importlib.import_module("networks.LGUnet_all")
+    cfg = C.FCST
+    torch.manual_seed(0)
+    t0 = time.time()
+    m = L1.LGUnet_all_1(**ref_cfg_l1(cfg))
+    p = synth1(cfg)
+    m.load_state_dict(p, strict=True)
+    m.eval()
+    del p
+    x = torch.from_numpy(smooth_field(1101, (1, C.in_channels(cfg)) + tuple(cfg["img_size"])))
+    with torch.no_grad():
+        y = m(x)
+    y = y.numpy()
+    idx = sample_idx(y.size, 16384, 1111)
+    flat = y.reshape(-1).astype(np.float64)
+    print(f"G11 LGUnet_all_1 0.25deg forward {tuple(y.shape)}: {time.time() - t0:.0f}s, sumsq {(flat * flat).sum():.6e}")
+    np.savez(os.path.join(GOLD, "g11_fcst_025deg.npz"), idx=idx, out_sample=y.reshape(-1)[idx], out_sum=flat.sum(),
+             out_sumsq=(flat * flat).sum(), out_abssum=np.abs(flat).sum(), shape=np.array(y.shape))
+
+
+def g12(tr):
+    """G12 (BASELINE config 4's 6-step window): the reference's networks_old.LGUnet_all
+    tiny decoder and tiny flow model, T = 6 (five integrate steps in the loss, da_4dvar.py:1190-1194): one closure
+    (J_b, J_o, dJ/dz) at a non-zero latent, and one outer pass of torch.optim.LBFGS (Nit = 1) with every line
+    search's (t, evals) recorded."""
+    cfg, fcfg = C.TINY, C.TINY_FLOW
+    m, p = build_ref(tr, cfg)
+    fm, fp = build_ref(tr, fcfg)
+    prob = make_problem(nch=4, Hs=32, Ws=64, T=6, seed=779, obs_frac=0.1)
+    rp = RefProblem(prob, m, cfg["img_size"], fm)
+    z = torch.from_numpy(0.3 * smooth_field(1201, (1, 4, 32, 64), sigma=2.0)).requires_grad_(True)
+    r, o = rp.loss_terms(z)
+    (r + o).backward()
+    ro = oracle_problem(prob, p, cfg, fp, fcfg)
+    z2 = z.detach().clone().requires_grad_(True)
+    r2, o2 = ro.loss_terms(z2)
+    (r2 + o2).backward()
+    print(f"G12 tiny 4D-Var T=6: J_b {float(r):.6e} J_o {float(o):.6e}; oracle rel J_o "
+          f"{abs(float(o2) - float(o)) / abs(float(o)):.2e} grad {rel(z2.grad, z.grad):.2e}")
+    with LineSearchRecorder() as ls:
+        xa, zf, js, nev, nit = one_step_da_ref(rp, 1, (4, 32, 64))
+    print(f"G12 L-BFGS Nit=1: J {js} evals {nev} iters {nit}")
+    np.savez(os.path.join(GOLD, "g12_tiny_4dvar_t6.npz"), z=z.detach().numpy(), J_b=float(r), J_o=float(o),
+             grad=z.grad.numpy(), J=np.array(js, np.float64), n_eval=nev, n_iter=nit, xa=xa.numpy(),
+             ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also generate G3 (full decoder, ~1 min)")
     ap.add_argument("--only", default=None)
     ap.add_argument("--g6", action="store_true", help="also generate G6 (genuine one_step_DA at 721x1440, ~5 min)")
     ap.add_argument("--g8", action="store_true", help="also generate G8 (genuine real-obs one_step_DA, ~3 min)")
+    ap.add_argument("--g10", action="store_true", help="also generate G10 (config-2 trajectory, Nit 10, ~10 min)")
+    ap.add_argument("--g11", action="store_true", help="also generate G11 (0.25-deg LGUnet_all_1 forward, ~3 min)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.set_num_threads(8)
@@ -441,13 +526,17 @@ def main():
     tr, sb = ref_harness.import_reference()
     os.chdir(cwd)
     steps = {"g1": lambda: g1(tr), "g2": lambda: g2(sb), "g4": g4, "g5": lambda: g5(tr), "g5b": lambda: g5b(tr),
-             "g7": g7, "g9": g9}
+             "g7": g7, "g9": g9, "g12": lambda: g12(tr)}
     if a.full:
         steps["g3"] = lambda: g3(tr)
     if a.g6:
         steps["g6"] = lambda: g6(tr)
     if a.g8:
         steps["g8"] = lambda: g8(tr)
+    if a.g10:
+        steps["g10"] = lambda: g10(tr)
+    if a.g11:
+        steps["g11"] = g11
     for k, f in steps.items():
         if a.only and k not in a.only.split(","):
             continue

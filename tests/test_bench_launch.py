@@ -1,0 +1,41 @@
+"""CPU: bench.py's multi-rank path as the driver runs it — `bench.py --gpus 2` spawns its own two ranks (no
+WORLD_SIZE), they meet over gloo, every rank's analysis is gathered to rank 0, time is the max over ranks and
+iterations the sum — with the --selftest stand-in analysis (known outputs) in place of the GPU engine."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def _run(*extra, env=None):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + list(extra)
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=e)
+    return p
+
+
+def test_bench_spawns_its_ranks():
+    p = _run("--gpus", "2", "--selftest", "--steps", "2", "--warmup", "1")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # one JSON line, from rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    # stand-in analysis of rank r: 97 + r iterations, 110 + r evaluations; 2 steps each
+    assert out["iters"] == 2 * (97 + 98) and out["evals"] == 2 * (110 + 111)
+    assert out["gathered"] == [[69, 128, 256], [69, 128, 256]]
+    assert out["value"] == out["iters"] / (out["ms_per_step"] * 1e-3 * out["steps"])
+    c4 = out["config4"]
+    assert c4["n_gpus"] == 2 and c4["gathered"] == [[69, 128, 256], [69, 128, 256]] and c4["iters"] == 97 + 98
+    for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+
+
+def test_bench_world_size_must_match():
+    p = _run("--gpus", "2", "--selftest", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr

@@ -39,6 +39,27 @@ def test_fcst_tiny_g7():
     assert e < 1e-5
 
 
+def test_fcst_025deg_g11():
+    """G11: the full 0.25-degree forecast network (training_options.yaml:64-119: 69ch 721x1440, 427M parameters,
+    LG layer 0 one 16,200-token global window) against the reference's own LGUnet_all_1 forward on CPU: 16,384
+    sampled outputs and the sums over all 143M outputs."""
+    path = os.path.join(GOLD, "g11_fcst_025deg.npz")
+    from vaevar import config as C
+    from vaevar.synth import smooth_field
+
+    g = np.load(path)
+    cfg = C.FCST
+    x = torch.from_numpy(smooth_field(1101, (1, C.in_channels(cfg)) + tuple(cfg["img_size"]))).cuda()
+    out = _model(cfg).forward_raw(x)
+    assert tuple(out.shape) == tuple(g["shape"])
+    o = out.cpu().numpy().reshape(-1).astype(np.float64)
+    e = rel(o[g["idx"]], g["out_sample"])
+    e_ss = abs((o * o).sum() - float(g["out_sumsq"])) / float(g["out_sumsq"])
+    e_as = abs(np.abs(o).sum() - float(g["out_abssum"])) / float(g["out_abssum"])
+    print(f"G11 LGUnet_all_1 0.25deg: sampled out rel {e:.2e}, sumsq rel {e_ss:.1e}, abssum rel {e_as:.1e}")
+    assert e < 1e-4 and e_ss < 1e-5 and e_as < 1e-5
+
+
 @pytest.mark.parametrize("name", ["MID_FCST", "BIG_FCST"])
 def test_fcst_mid_vs_oracle(name):
     """Real FCST widths/heads/window on a 97x192 image: head_dim 32/32/64/192, [6,12] windows with the -inf

@@ -22,10 +22,10 @@ def _ref_gemm(A, B, bias):
 
 
 @pytest.mark.parametrize("M,N,K,tile", [
-    (256, 96, 96, -1), (2048, 1152, 1152, 0), (2048, 1152, 1152, 1), (2048, 1152, 1152, 2),
+    (256, 96, 96, -1), (2048, 1152, 1152, 0), (2048, 1152, 1152, 4), (2048, 1152, 1152, 2),
     (2048, 3456, 1152, -1), (2048, 1152, 4608, -1), (8192, 288, 96, -1), (100, 70, 64, 2), (130, 200, 32, 0),
-    (2048, 1152, 1152, 21), (2048, 1152, 1152, 24), (100, 70, 64, 21), (130, 200, 32, 24), (300, 96, 384, 23),
-    (2048, 4608, 1152, 26), (130, 200, 64, 25), (130, 200, 64, 22),
+    (2048, 1152, 1152, 34), (2048, 1152, 1152, 24), (100, 70, 64, 34), (130, 200, 32, 24), (300, 96, 384, 24),
+    (2048, 4608, 1152, 34), (130, 200, 64, 4), (130, 200, 64, 34),
 ])
 def test_gemm_nt(ctx, M, N, K, tile):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
@@ -34,7 +34,7 @@ def test_gemm_nt(ctx, M, N, K, tile):
     bias = torch.rand(N, generator=g) - 0.5
     C = ctx.gemm(A.cuda(), B.cuda(), bias.cuda(), tile=tile).cpu().double()
     ref = _ref_gemm(A, B, bias)
-    # exact-f32 MFMA (tiles < 21) and the bf16x6 split (tiles >= 21): error ~1e-7 * sum|a*b| per element
+    # exact-f32 MFMA (tiles 0/2/4) and the bf16x6 split (24/34): error ~1e-7 * sum|a*b| per element
     scale = (A.abs().double() @ B.abs().double().t()).max()
     err = (C - ref).abs().max() / scale
     assert err < 2e-6, float(err)
@@ -42,7 +42,7 @@ def test_gemm_nt(ctx, M, N, K, tile):
 
 @pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 1152, 4608), (8192, 96, 384), (777, 300, 96)])
 def test_gemm_split_accuracy(ctx, M, N, K):
-    """bf16x6 split GEMM (tiles >= 21) vs fp64: element error / sum|a*b| no larger than the exact-f32
+    """bf16x6 split GEMM (tiles 24, 34) vs fp64: element error / sum|a*b| no larger than the exact-f32
     MFMA's on the same operands (x1.5 margin) and below 1e-6; randn operands, weight-like B scale."""
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
@@ -51,7 +51,7 @@ def test_gemm_split_accuracy(ctx, M, N, K):
     scale = A.double().abs() @ B.double().abs().t()
     A, B = A.cuda(), B.cuda()
     e32 = float(((ctx.gemm(A, B, tile=2).cpu().double() - ref).abs() / scale).max())
-    for t in (21, 24):
+    for t in (24, 34):
         es = float(((ctx.gemm(A, B, tile=t).cpu().double() - ref).abs() / scale).max())
         print(f"gemm {M}x{N}x{K}: f32 {e32:.2e} split t{t} {es:.2e}")
         assert es < 1e-6 and es < 1.5 * e32, (t, es, e32)
@@ -60,7 +60,7 @@ def test_gemm_split_accuracy(ctx, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 1152, 4608), (300, 200, 96), (4096, 384, 1152),
                                    (2048, 3456, 1152)])
 def test_gemm_pipelined_registered(ctx, M, N, K):
-    """Pipelined 128x128 split kernels (tile 34/35 bf16x6, 36 fp16x3) on a registered weight (pre-split planes),
+    """Pipelined 128x128 split kernels (tile 34 bf16x6, 36 fp16x3) and the 64x64 bf16x6 kernel (24) on a registered weight (pre-split planes),
     incl. ragged edges and the split-K tail: same fp32-level error bound as the other variants."""
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
     A = torch.randn(M, K, generator=g)
@@ -69,7 +69,7 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
     scale = A.double().abs() @ B.double().abs().t()
     Bd = B.cuda()
     ctx.gemm_register_weight(Bd)
-    for t in (36, 35, 34, 31, 24):
+    for t in (36, 34, 24):
         C = ctx.gemm(A.cuda(), Bd, tile=t).cpu().double()
         es = float(((C - ref).abs() / scale).max())
         print(f"registered gemm {M}x{N}x{K} t{t}: {es:.2e}")
@@ -104,6 +104,22 @@ def test_gemm_split16_dynamic_range(ctx, M, N, K):
     assert es < 1e-6 and es < 2.0 * e32, (es, e32)
     assert torch.all(C[5] == 0)
     _keep.append(Bd)
+
+
+def test_gemm_rejects_non_library_tiles(ctx):
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36): any other hint, e.g. the r01
+    timing experiments 37-39, returns VV_E_ARG instead of running something."""
+    from vaevar._lib import VVError
+
+    A = torch.rand(64, 64, device="cuda")
+    B = torch.rand(64, 64, device="cuda")
+    for t in (1, 3, 21, 35, 37, 38, 39, 40, 1000):
+        with pytest.raises(VVError, match="1001"):
+            ctx.gemm(A, B, tile=t)
+    ref = A.double().cpu() @ B.double().cpu().t()
+    for t in (0, 2, 4, 24, 34, 36):
+        C = ctx.gemm(A, B, tile=t).cpu().double()
+        assert float((C - ref).abs().max()) < 1e-4
 
 
 def test_gemm_math_switch(ctx):

@@ -29,7 +29,7 @@ class CpuPrims:
         dst.copy_(src)
 
     def lbfgs_two_loop(self, q, stps, dirs, ro, H_diag):
-        # k_twoloop_coef's arithmetic: fp64-accumulated dot rounded to fp32, times ro[i] in fp32
+        # k_twoloop_axpy's arithmetic: fp64-accumulated dot rounded to fp32, times ro[i] in fp32
         f32 = np.float32
         al = [None] * len(stps)
         for i in range(len(stps) - 1, -1, -1):

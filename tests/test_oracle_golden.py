@@ -96,6 +96,38 @@ def test_g5b_tiny_4dvar_closure():
     assert rel(z.grad, g["grad"]) < 1e-6
 
 
+def test_g12_tiny_4dvar_t6():
+    """G12: the T = 6 window (five integrate steps) — closure and one outer L-BFGS pass of the reference modules."""
+    from oracle.da_ref import one_step_da_ref, oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.problem import make_problem
+
+    g = gold("g12_tiny_4dvar_t6.npz")
+    p = make_problem(nch=4, Hs=32, Ws=64, T=6, seed=779, obs_frac=0.1)
+    ro = oracle_problem(p, synth_params(C.TINY), C.TINY, synth_params(C.TINY_FLOW), C.TINY_FLOW)
+    z = torch.from_numpy(g["z"]).requires_grad_(True)
+    r, o = ro.loss_terms(z)
+    (r + o).backward()
+    assert abs(float(r) - g["J_b"]) / g["J_b"] < 1e-6 and abs(float(o) - g["J_o"]) / g["J_o"] < 1e-6
+    assert rel(z.grad, g["grad"]) < 1e-6
+    xa, _, js, nev, nit = one_step_da_ref(ro, 1, (4, 32, 64))
+    assert np.allclose(np.array(js), g["J"], rtol=1e-5)
+    assert nev == int(g["n_eval"]) and nit == int(g["n_iter"])
+    assert rel(xa, g["xa"]) < 1e-5
+
+
+def test_g10_g11_fixtures_consistent():
+    """G10 / G11 are outputs of the reference itself (too long to re-run here); check they are self-consistent."""
+    g = gold("g10_config2_trajectory.npz")
+    J = g["J"].sum(1)
+    assert len(J) == 11 and np.all(np.diff(J) < 0)  # monotone decrease over the 10 outer passes
+    assert int(g["n_iter"]) <= 100 and len(g["ls_t"]) == int(g["n_iter"]) and int(g["ls_evals"].sum()) + 10 == int(g["n_eval"])
+    f = gold("g11_fcst_025deg.npz")
+    assert tuple(f["shape"]) == (1, 138, 721, 1440) and np.isfinite(f["out_sample"]).all()
+    assert float(f["out_sumsq"]) > 0 and len(f["idx"]) == len(f["out_sample"])
+
+
 def test_g5_tiny_lbfgs_trajectory():
     from oracle.da_ref import one_step_da_ref, oracle_problem
     from oracle.lgunet_ref import synth_params

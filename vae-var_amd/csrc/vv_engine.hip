@@ -218,6 +218,7 @@ struct StageSave {
 struct Scratch {
   float *t1, *t2, *h, *dqkv;
   float* ws;  // GEMM tail-split partials (vv::gemm_ws_floats())
+  int math = vv::GEMM_SPLIT16;  // GEMM arithmetic (the context's vv_set_gemm_math)
 };
 
 struct Save {
@@ -258,6 +259,8 @@ struct Problem {
   float obs_coeff = 1.f;
   std::unique_ptr<Arena> arena;
   float *X, *dec_out, *gdec, *prod, *FI, *FO, *GFO, *GFI, *carry;
+  float *Z = nullptr, *GZ = nullptr;  // the closure graph's latent input / gradient output
+  size_t zn = 0;                      // floats of the latent
   double *partial, *dJ;
   int nblk = 1024;
   // real-observation operator (vv_set_obs_operator): nout = 0 is the identity (synthetic observations)
@@ -271,6 +274,7 @@ struct Problem {
 
 struct vv_ctx {
   int device = 0;
+  int math = vv::GEMM_SPLIT16;  // GEMM arithmetic of every model of this context (vv_set_gemm_math)
   std::vector<std::unique_ptr<Model>> models;
   Problem prob;
   double* red = nullptr;   // reduction scratch
@@ -278,7 +282,7 @@ struct vv_ctx {
   float* redf = nullptr;
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
-  float* twoloop = nullptr;  // L-BFGS two-loop scalars: al[kMaxHistory], coef
+  float* twoloop = nullptr;  // L-BFGS two-loop scalars: al[kMaxHistory]
   char* metric_ws = nullptr;  // vv_metrics partial sums + latitude weights
   size_t metric_cap = 0;
   struct SplitW {
@@ -287,6 +291,15 @@ struct vv_ctx {
     unsigned short* planes;
   };
   std::vector<SplitW> split_owned;  // vv_gemm_register_weight planes
+  // hipGraph of the closure: the ~540 launches of one evaluation replayed as one graph launch. One graph per kind
+  // (J only / J + gradient), captured at the second evaluation of that kind, against the problem-owned latent and
+  // gradient buffers (Problem::Z / GZ), so it does not depend on the caller's pointers. VAEVAR_GRAPH=0 disables.
+  struct ClosureGraph {
+    hipGraphExec_t exec = nullptr;
+    int eager_runs = 0;
+  } graphs[2];
+  hipStream_t cap_stream = nullptr;
+  bool use_graphs = true;  // vv_set_closure_graph / VAEVAR_GRAPH
 };
 
 namespace {
@@ -421,9 +434,10 @@ int bind_weights(Model& m) {
 // ----------------------------------------------------------------------------
 // forward / backward of one Swin stage (BasicLayer / BasicLayer_up / Layer: blocks only)
 // ----------------------------------------------------------------------------
-GemmArgs gemm_base(int M, int N, int K, int G, int epi) {
+GemmArgs gemm_base(int M, int N, int K, int G, int epi, int math) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
+  a.math = math;
   a.M = M;
   a.N = N;
   a.K = K;
@@ -487,7 +501,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                  nullptr, nullptr};
     CK(layernorm_fwd(ln, st));
     // qkv
-    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE);
+    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc.math);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
     CK(gemm_nt(q, st, -1, sc.ws));
@@ -509,7 +523,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                  sv.P[b] + (size_t)g * nwin * S.heads * 256, nullptr, nullptr};
     CK(attn_fwd(at, st));
     // proj + window reverse + residual
-    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID);
+    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID, sc.math);
     p.crow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
@@ -522,13 +536,13 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                   nullptr, nullptr};
     CK(layernorm_fwd(ln2, st));
     // fc1 + GELU
-    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU);
+    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc.math);
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, sc.h + g * MC * 4, nullptr,
                  sv.h1[b] + g * MC * 4};
     CK(gemm_nt(f1, st, -1, sc.ws));
     // fc2 + residual
-    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID);
+    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc.math);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, sv.x[b + 1] + g * MC, sv.x1[b] + g * MC,
                  nullptr};
@@ -545,11 +559,11 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
   for (int b = S.depth - 1; b >= 0; --b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
-    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU);
+    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc.math);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
     CK(gemm_nt(f2, st, -1, sc.ws));
-    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE);
+    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc.math);
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     CK(gemm_nt(f1, st, -1, sc.ws));
@@ -558,7 +572,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
                   sc.t1 + g * MC, gx + g * MC};
     CK(layernorm_bwd(ln2, st));
-    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE);
+    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc.math);
     p.arow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {gx + g * MC, nullptr, S.w[b][g].projWT, nullptr, sc.t2 + g * MC, nullptr, nullptr};
@@ -579,7 +593,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, nullptr, sv.P[b] + (size_t)g * nwin * S.heads * 256,
                  sc.t2 + g * MC, sc.dqkv + g * MC * 3};
     CK(attn_bwd(at, st));
-    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE);
+    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE, sc.math);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     CK(gemm_nt(q, st, -1, sc.ws));
@@ -755,7 +769,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
                w(eg(g) + ".layers.1.downsample.norm.bias"), m.xm + (size_t)g * M1 * 4 * C0,
                sv.st_m + (size_t)g * M1 * 2, nullptr, nullptr};
   CK(layernorm_fwd(lm, st));
-  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE);
+  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE, m.sc.math);
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.xm + (size_t)g * M1 * 4 * C0, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight"), nullptr,
                 sv.enc1.x[0] + g * M1C1, nullptr, nullptr};
@@ -771,7 +785,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   CK(layernorm_fwd(le, st));
   // Enc_net.proj (+ LG_net.pos_embed, transformer.py:704)
   float* lg_in = m.lg.empty() ? sv.dec1.x[0] : sv.lg[0].x[0];
-  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID);
+  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID, m.sc.math);
   ep.rmod = c.H1 * c.W1;
   ep.ldr = E;
   ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
@@ -781,11 +795,11 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
     if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st))) return r;
   const float* lg_out = m.lg.empty() ? lg_in : sv.lg.back().x.back();
   // ---- Dec_net.proj (transformer.py:600)
-  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE);
+  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math);
   dp.g[0] = {lg_out, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m.dp, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
   // concat_back_dim[0]: cat(x, skip1) (transformer.py:468-469)
-  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE);
+  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math);
   c0.lda = G * C1;
   c0.ksplit = C1;
   c0.lda2 = C1;
@@ -795,7 +809,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   CK(gemm_nt(c0, st, -1, m.sc.ws));
   if ((r = stage_fwd(m.dec1, sv.dec1, m.sc, c.ws, st))) return r;
   // PatchExpand: expand (no bias) + rearrange + LN(C0, eps 1e-6) (transformer.py:106-118)
-  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE);
+  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE, m.sc.math);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {sv.dec1.x.back() + g * M1C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight"), nullptr,
                sv.ex + (size_t)g * M1 * 2 * C1, nullptr, nullptr};
@@ -811,7 +825,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
                nullptr};
   CK(layernorm_fwd(lx, st));
   // concat_back_dim[1]: cat(x, skip0)
-  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE);
+  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE, m.sc.math);
   c1.lda = C0;
   c1.ksplit = C0;
   c1.lda2 = C0;
@@ -896,7 +910,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   if ((r = stage_bwd(m.dec0, sv.dec0, m.sc, c.ws, m.gd0, st))) return r;
   // concat_back_dim[1] backward: left -> PatchExpand output, right -> skip0
   for (int half = 0; half < 2; ++half) {
-    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE);
+    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE, m.sc.math);
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd0 + g * M0C0, nullptr, w(dg(g) + ".concat_back_dim.1.weight^T") + (size_t)half * C0 * C0,
                  nullptr, (half ? m.gsk0 : m.gxe) + g * M0C0, nullptr, nullptr};
@@ -912,7 +926,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
     lx.g[g] = {sv.ex + (size_t)g * M1 * 2 * C1, w(dg(g) + ".layers_up.0.upsample.norm.weight"), nullptr,
                m.gex + (size_t)g * M1 * 2 * C1, sv.st_ex + (size_t)g * M0 * 2, m.gxe + g * M0C0, nullptr};
   CK(layernorm_bwd(lx, st));
-  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE);
+  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {m.gex + (size_t)g * M1 * 2 * C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight^T"), nullptr,
                m.gd1 + g * M1C1, nullptr, nullptr};
@@ -920,7 +934,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   if ((r = stage_bwd(m.dec1, sv.dec1, m.sc, c.ws, m.gd1, st))) return r;
   // concat_back_dim[0] backward: left -> Dec_net.proj output slice g, right -> skip1
   for (int half = 0; half < 2; ++half) {
-    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE);
+    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE, m.sc.math);
     if (!half) cb.ldc = G * C1;
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd1 + g * M1C1, nullptr, w(dg(g) + ".concat_back_dim.0.weight^T") + (size_t)half * C1 * C1,
@@ -929,13 +943,13 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   }
   // Dec_net.proj backward
   float* glg = m.glg;
-  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE);
+  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE, m.sc.math);
   dp.g[0] = {m.gdp, nullptr, w("dec.proj.weight^T"), nullptr, glg, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
   for (int l = (int)m.lg.size() - 1; l >= 0; --l)
     if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st))) return r;
   // pos_embed: identity ; Enc_net.proj backward
-  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE);
+  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math);
   ep.g[0] = {glg, nullptr, w("enc.proj.weight^T"), nullptr, m.gcat, nullptr, nullptr};
   CK(gemm_nt(ep, st, -1, m.sc.ws));
   // encoder norm backward (+ skip1 gradient), in place on gsk1
@@ -948,7 +962,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   CK(layernorm_bwd(le, st));
   if ((r = stage_bwd(m.enc1, sv.enc1, m.sc, c.ws, m.gsk1, st))) return r;
   // PatchMerging backward: reduction^T, then LN (merge mode) scattered onto level-0 tokens (+ skip0 grad)
-  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE);
+  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE, m.sc.math);
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.gsk1 + g * M1C1, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight^T"), nullptr,
                 m.gxm + (size_t)g * M1 * 4 * C0, nullptr, nullptr};
@@ -1152,6 +1166,51 @@ int closure_enqueue(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hip
   return 0;
 }
 
+
+void drop_graphs(vv_ctx* ctx) {
+  for (auto& g : ctx->graphs) {
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    g = vv_ctx::ClosureGraph{};
+  }
+}
+
+// the closure through its cached graph: z -> Problem::Z, replay (J and, with grad_z, Problem::GZ), GZ -> grad_z
+int closure_graphed(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hipStream_t st) {
+  Problem& P = ctx->prob;
+  auto& g = ctx->graphs[grad_z ? 1 : 0];
+  float* gz = grad_z ? P.GZ : nullptr;
+  VV_HIP(hipMemcpyAsync(P.Z, z, P.zn * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (!g.exec && g.eager_runs == 0) {
+    // the first evaluation of each kind runs eagerly (it also performs the one-time kernel attribute set-up)
+    g.eager_runs = 1;
+    int r = closure_enqueue(ctx, P.Z, gz, nullptr, st);
+    if (r) return r;
+  } else {
+    if (!g.exec) {
+      if (!ctx->cap_stream) VV_HIP(hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking));
+      VV_HIP(hipStreamBeginCapture(ctx->cap_stream, hipStreamCaptureModeRelaxed));
+      const int r = closure_enqueue(ctx, P.Z, gz, nullptr, ctx->cap_stream);
+      hipGraph_t graph = nullptr;
+      const hipError_t ec = hipStreamEndCapture(ctx->cap_stream, &graph);
+      if (r) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return r;
+      }
+      VV_HIP(ec);
+      const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (ei != hipSuccess) {
+        g.exec = nullptr;
+        return fail((int)ei, "closure graph instantiate: %s", hipGetErrorString(ei));
+      }
+    }
+    VV_HIP(hipGraphLaunch(g.exec, st));
+  }
+  if (grad_z) VV_HIP(hipMemcpyAsync(grad_z, P.GZ, P.zn * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (d_J) VV_HIP(hipMemcpyAsync(d_J, P.dJ, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1219,12 +1278,13 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipSetDevice(device));
   VV_HIP(hipMalloc(&c->red, kRedBlocks * sizeof(double)));
   VV_HIP(hipMalloc(&c->redf, kRedBlocks * sizeof(float)));
-  VV_HIP(hipMalloc(&c->twoloop, (kMaxHistory + 1) * sizeof(float)));
+  VV_HIP(hipMalloc(&c->twoloop, kMaxHistory * sizeof(float)));
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
+  if (const char* e = getenv("VAEVAR_GRAPH")) c->use_graphs = e[0] != '0';
   if (const char* e = getenv("VAEVAR_GEMM_MATH"))
-    vv::set_gemm_math(strcmp(e, "f32") == 0 ? vv::GEMM_F32 : strcmp(e, "split") == 0 ? vv::GEMM_SPLIT : vv::GEMM_SPLIT16);
+    c->math = strcmp(e, "f32") == 0 ? vv::GEMM_F32 : strcmp(e, "split") == 0 ? vv::GEMM_SPLIT : vv::GEMM_SPLIT16;
   *out = c;
   return 0;
 }
@@ -1242,6 +1302,8 @@ int vv_ctx_destroy(vv_ctx* ctx) {
     (void)hipFree(w.planes);
   }
 
+  drop_graphs(ctx);
+  if (ctx->cap_stream) (void)hipStreamDestroy(ctx->cap_stream);
   (void)hipFree(ctx->red);
   (void)hipFree(ctx->twoloop);
   if (ctx->metric_ws) (void)hipFree(ctx->metric_ws);
@@ -1261,6 +1323,7 @@ int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_s
     auto m = std::make_unique<Model>();
     std::string err;
     if ((r = vvf::create(cfg, batch, &m->fm, err))) return fail(r, "%s", err.c_str());
+    vvf::set_math(m->fm, ctx->math);
     m->B = batch;
     m->nslots = 1;
     m->workspace = vvf::workspace_bytes(m->fm);
@@ -1274,12 +1337,15 @@ int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_s
     return 0;
   }
   if (cfg->arch != VV_ARCH_LGUNET) return fail(VV_E_ARG, "unknown arch %d", cfg->arch);
-  return create_model(ctx, cfg, batch, n_slots, model_id);
+  if ((r = create_model(ctx, cfg, batch, n_slots, model_id))) return r;
+  ctx->models[*model_id]->sc.math = ctx->math;
+  return 0;
 }
 
 int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
   Model* m = get_model(ctx, model_id);
   if (!m || !ptrs) return fail(VV_E_ARG, "bad model or ptrs");
+  drop_graphs(ctx);
   if (m->fm) {
     int r = set_dev(ctx);
     if (r) return r;
@@ -1371,6 +1437,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   if (!xb || !yo || !Hmask || !R || !mean || !std_ || !std_tr) return fail(VV_E_ARG, "null problem buffer");
   int r = set_dev(ctx);
   if (r) return r;
+  drop_graphs(ctx);
   Problem& P = ctx->prob;
   P = Problem();
   P.dec = dec_model_id;
@@ -1406,6 +1473,9 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     P.GFO = pl.f((size_t)fcout * HWl + 1);
     P.GFI = pl.f(CHWl);
     P.carry = pl.f(CHW);
+    P.zn = (size_t)D->B * D->cfg.Cin * D->cfg.Himg * D->cfg.Wimg;
+    P.Z = pl.f(P.zn);
+    P.GZ = pl.f(P.zn);
     float* maps = pl.f((size_t)Hs + Ws + 2 * (P.Hl + 1) + 2 * (P.Wl + 1));
     double* pd = reinterpret_cast<double*>(pl.f((size_t)2 * P.nblk * (T + 1) + 8));
     if (pass) {
@@ -1453,7 +1523,10 @@ int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, vo
   if (!ctx || !z) return fail(VV_E_ARG, "null argument");
   int r = set_dev(ctx);
   if (r) return r;
-  return closure_enqueue(ctx, z, grad_z, d_J, (hipStream_t)stream);
+  if (!ctx->prob.bound) return fail(VV_E_STATE, "vv_bind_problem first");
+  hipStream_t st = (hipStream_t)stream;
+  if (!ctx->use_graphs || vv::prof_enabled() || sync_check()) return closure_enqueue(ctx, z, grad_z, d_J, st);
+  return closure_graphed(ctx, z, grad_z, d_J, st);
 }
 
 int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream) {
@@ -1504,6 +1577,7 @@ int vv_set_obs_operator(vv_ctx* ctx, int n_out, int n_in, const float* interp) {
   if (!P.bound) return fail(VV_E_STATE, "vv_bind_problem first");
   int r = set_dev(ctx);
   if (r) return r;
+  drop_graphs(ctx);
   if (n_out == 0) {
     P.nout = P.nin = 0;
     return 0;
@@ -1626,7 +1700,7 @@ int vv_lbfgs_two_loop(vv_ctx* ctx, float* q, const float* const* S, const float*
   if (m < 0 || m > kMaxHistory) return fail(VV_E_ARG, "history size out of range");
   for (int i = 0; i < m; ++i)
     if (!S[i] || !Y[i]) return fail(VV_E_ARG, "null history vector");
-  VV_HIP(vv::lbfgs_two_loop(q, S, Y, ro, m, H_diag, n, ctx->red, kRedBlocks, ctx->twoloop, ctx->twoloop + kMaxHistory,
+  VV_HIP(vv::lbfgs_two_loop(q, S, Y, ro, m, H_diag, n, ctx->red, kRedBlocks, ctx->twoloop,
                             (hipStream_t)stream));
   return 0;
 }
@@ -1667,13 +1741,27 @@ int vv_nearest_map(int in_size, int out_size, int* map) {
 int vv_set_gemm_math(vv_ctx* ctx, int math) {
   if (!ctx || (math != VV_GEMM_F32 && math != VV_GEMM_SPLIT && math != VV_GEMM_SPLIT16))
     return fail(VV_E_ARG, "bad gemm math %d", math);
-  vv::set_gemm_math(math);
+  if (math != ctx->math) drop_graphs(ctx);
+  ctx->math = math;
+  for (auto& m : ctx->models) {
+    m->sc.math = math;
+    if (m->fm) vvf::set_math(m->fm, math);
+  }
+  return 0;
+}
+
+int vv_set_closure_graph(vv_ctx* ctx, int enable) {
+  if (!ctx) return fail(VV_E_ARG, "null context");
+  int r = set_dev(ctx);
+  if (r) return r;
+  drop_graphs(ctx);
+  ctx->use_graphs = enable != 0;
   return 0;
 }
 
 int vv_get_gemm_math(vv_ctx* ctx, int* math) {
   if (!ctx || !math) return fail(VV_E_ARG, "null argument");
-  *math = vv::gemm_math();
+  *math = ctx->math;
   return 0;
 }
 
@@ -1764,7 +1852,11 @@ int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K) {
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C, int tile,
             void* stream) {
   if (!ctx || !A || !B || !C) return fail(VV_E_ARG, "null argument");
-  GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE);
+  if (tile >= 0 && !vv::valid_tile(tile)) return fail(VV_E_ARG, "tile hint %d is not a library kernel", tile);
+  if (M <= 0 || N <= 0 || K <= 0 || K % 32) return fail(VV_E_ARG, "bad GEMM shape %dx%dx%d (K a multiple of 32)", M, N, K);
+  int r = set_dev(ctx);
+  if (r) return r;
+  GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE, ctx->math);
   a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
   VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
   return 0;

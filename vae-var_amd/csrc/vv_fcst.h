@@ -26,6 +26,8 @@ int load(FModel* m, const void* const* ptrs, int n, std::string& err);
 // out (batch, sum(outchans), H, W), channels < climit (0 = all)
 int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, std::string& err);
 int64_t workspace_bytes(const FModel* m);
+// GEMM arithmetic (vv::GemmMath) of the model's forward
+void set_math(FModel* m, int math);
 int in_channels(const FModel* m);
 int out_channels(const FModel* m);
 int img_h(const FModel* m);

@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 namespace vv {
@@ -29,6 +31,35 @@ __device__ __forceinline__ float dgelu_f(float x) {
 }
 
 constexpr int KALIGN = 32;  // K, ksplit granularity accepted by gemm_nt (covers every BK variant)
+
+// dynamic-LDS limit of a kernel, set once per (kernel, device): hipFuncSetAttribute acts on the current device
+static hipError_t set_lds_limit(const void* k, size_t lds) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, int>> done;
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& d : done)
+    if (d.first == k && d.second == dev) return hipSuccess;
+  if (hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) return e;
+  done.emplace_back(k, dev);
+  return hipSuccess;
+}
+
+// compute units of the current device (cached per device)
+static int device_cus() {
+  static std::mutex mu;
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!cus[dev]) {
+    hipDeviceProp_t p;
+    cus[dev] = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ? p.multiProcessorCount : 256;
+  }
+  return cus[dev];
+}
+
 
 // GEMM epilogue. 32x32: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31; 16x16: row 4h + r,
 // col lane&15 (h = lane>>4). Everything an element needs (bias, output row, residual, pre-activation) is
@@ -113,7 +144,7 @@ __device__ __forceinline__ void tile_mn(int t, int ntm, int ntn, int& mb, int& n
   nb = r / gm;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int EPI, bool XCD, int MF, int DEPTH>
+template <int BM, int BN, int BK, int WM, int WN, int EPI, int MF>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
   constexpr int NT = 64 * WM * WN;
   constexpr int LS = BK + 4;        // LDS row stride (floats): rows land on distinct 16-B slots
@@ -140,7 +171,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
   const int nkt = K / BK;
   int tile, kb = 0, ke = nkt, part = -1;
   if ((int)blockIdx.x < args.tdp || args.tsplit <= 1) {
-    tile = XCD ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
+    tile = blockIdx.x;
   } else {
     part = blockIdx.x - args.tdp;  // tail item: tile tdp + part / S, k-chunk part % S
     const int S = args.tsplit, c = part % S;
@@ -167,9 +198,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
     bp[i] = G.B + (size_t)n * (args.ldb ? args.ldb : K) + lc;
   }
 
-  // register staging sets (named, statically indexed): DEPTH 1 = tile t+1 in flight during tile t,
-  // DEPTH 2 = tiles t+1 (landed, written to LDS after the compute) and t+2 (in flight)
-  f4 ra0[AI], rb0[BI], ra1[AI], rb1[BI];
+  // register staging: tile t+1 is in flight during the MFMAs of tile t
+  f4 ra0[AI], rb0[BI];
   auto gload = [&](int k0, f4 (&ra)[AI], f4 (&rb)[BI]) {
     if (k0 < ksplit) {
 #pragma unroll
@@ -226,38 +256,15 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(GemmArgs args) {
   };
 
   const int nk = ke - kb;
-  if constexpr (DEPTH == 1) {
-    gload(kb * BK, ra0, rb0);
-    sstore(0, ra0, rb0);
+  gload(kb * BK, ra0, rb0);
+  sstore(0, ra0, rb0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kb + kt + 1) * BK, ra0, rb0);
+    compute(cur);
+    if (kt + 1 < nk) sstore(cur ^ 1, ra0, rb0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) gload((kb + kt + 1) * BK, ra0, rb0);
-      compute(cur);
-      if (kt + 1 < nk) sstore(cur ^ 1, ra0, rb0);
-      __syncthreads();
-    }
-  } else {
-    static_assert(DEPTH == 1 || DEPTH == 2, "depth");
-    // prologue: tile 0 -> LDS buffer 0, tile 1 -> registers set 1
-    gload(kb * BK, ra0, rb0);
-    if (nk > 1) gload((kb + 1) * BK, ra1, rb1);
-    sstore(0, ra0, rb0);
-    __syncthreads();
-    // steady state, unrolled by two so each register set is named statically
-    for (int kt = 0; kt < nk; kt += 2) {
-      // even step: compute buf 0 (tile kt); set 1 holds tile kt+1; load tile kt+2 into set 0
-      if (kt + 2 < nk) gload((kb + kt + 2) * BK, ra0, rb0);
-      compute(0);
-      if (kt + 1 < nk) sstore(1, ra1, rb1);
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      // odd step: compute buf 1 (tile kt+1); set 0 holds tile kt+2; load tile kt+3 into set 1
-      if (kt + 3 < nk) gload((kb + kt + 3) * BK, ra1, rb1);
-      compute(1);
-      if (kt + 2 < nk) sstore(0, ra0, rb0);
-      __syncthreads();
-    }
   }
 
   // epilogue: 32x32: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31;
@@ -422,7 +429,7 @@ hipError_t split_planes(const float* src, unsigned short* dst, size_t n, int K, 
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool BPRE, int DEPTH, int NBUF, bool APRE = false>
+template <int BM, int BN, int WM, int WN, int EPI, bool BPRE, int NBUF, bool APRE = false>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
   constexpr int BK = 32;
   constexpr int NT = 64 * WM * WN;
@@ -621,30 +628,19 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
   };
 
   const int nk = ke - kb;
+  Stg s0;
+  gload(kb * BK, s0);
   if constexpr (NBUF == 1) {
     // one LDS buffer (several workgroups per CU): store -> barrier -> compute -> barrier; the next tile's
-    // global loads (DEPTH tiles ahead) are in flight during the compute
-    Stg s0, s1;
-    gload(kb * BK, s0);
-    if (DEPTH == 2 && nk > 1) gload((kb + 1) * BK, s1);
-    for (int kt = 0; kt < nk; kt += DEPTH) {
+    // global loads are in flight during the compute
+    for (int kt = 0; kt < nk; ++kt) {
       sstore(0, s0);
       __syncthreads();
-      if (kt + DEPTH < nk) gload((kb + kt + DEPTH) * BK, s0);
+      if (kt + 1 < nk) gload((kb + kt + 1) * BK, s0);
       compute(0);
       __syncthreads();
-      if constexpr (DEPTH == 2) {
-        if (kt + 1 >= nk) break;
-        sstore(0, s1);
-        __syncthreads();
-        if (kt + 3 < nk) gload((kb + kt + 3) * BK, s1);
-        compute(0);
-        __syncthreads();
-      }
     }
-  } else if constexpr (DEPTH == 1) {
-    Stg s0;
-    gload(kb * BK, s0);
+  } else {
     sstore(0, s0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
@@ -652,24 +648,6 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
       if (kt + 1 < nk) gload((kb + kt + 1) * BK, s0);
       compute(cur);
       if (kt + 1 < nk) sstore(cur ^ 1, s0);
-      __syncthreads();
-    }
-  } else {
-    // two LDS buffers, two register sets: tile t+1's loads were issued two computes before its store
-    Stg s0, s1;
-    gload(kb * BK, s0);
-    if (nk > 1) gload((kb + 1) * BK, s1);
-    sstore(0, s0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-      if (kt + 2 < nk) gload((kb + kt + 2) * BK, s0);
-      compute(0);
-      if (kt + 1 < nk) sstore(1, s1);
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      if (kt + 3 < nk) gload((kb + kt + 3) * BK, s1);
-      compute(1);
-      if (kt + 2 < nk) sstore(0, s0);
       __syncthreads();
     }
   }
@@ -690,23 +668,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
     epilogue<BM, BN, WM, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool BPRE, int DEPTH, int NBUF, bool APRE = false>
+template <int BM, int BN, int WM, int WN, int EPI, bool BPRE, int NBUF, bool APRE = false>
 static hipError_t launch_bs_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail) {
-  static bool init = false;
-  if (!init) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_gemm_bs<BM, BN, WM, WN, EPI, BPRE, DEPTH, NBUF, APRE>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    init = true;
-  }
-  hipLaunchKernelGGL((k_gemm_bs<BM, BN, WM, WN, EPI, BPRE, DEPTH, NBUF, APRE>), grid, dim3(64 * WM * WN), lds, s, a);
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_bs<BM, BN, WM, WN, EPI, BPRE, NBUF, APRE>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_bs<BM, BN, WM, WN, EPI, BPRE, NBUF, APRE>), grid, dim3(64 * WM * WN), lds, s, a);
   if (tail)
     hipLaunchKernelGGL((k_gemm_fixup_sub<BM, BN, WM, WN, EPI>),
                        dim3(tail, (BM / WM / 32) * (BN / WN / 32), a.ngroups), dim3(64 * WM * WN), 0, s, a);
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int DEPTH = 1, int NBUF = 2>
+template <int BM, int BN, int WM, int WN, int NBUF = 2>
 static hipError_t launch_bs(const GemmArgs& a, hipStream_t s) {
   constexpr int BK = 32;
   if (a.K % BK || a.ksplit % BK) return hipErrorInvalidValue;
@@ -719,11 +691,11 @@ static hipError_t launch_bs(const GemmArgs& a, hipStream_t s) {
     pre = pre && a.g[g].Bp;
     apre = apre && a.g[g].Ap;
   }
-  if (pre && apre && a.epi == EPI_STORE) return launch_bs_k<BM, BN, WM, WN, EPI_STORE, true, DEPTH, NBUF, true>(a, s, grid, lds, tail);
+  if (pre && apre && a.epi == EPI_STORE) return launch_bs_k<BM, BN, WM, WN, EPI_STORE, true, NBUF, true>(a, s, grid, lds, tail);
   switch (a.epi * 2 + (pre ? 1 : 0)) {
 #define VV_EPI(E)                                                                    \
-  case 2 * E: return launch_bs_k<BM, BN, WM, WN, E, false, DEPTH, NBUF>(a, s, grid, lds, tail); \
-  case 2 * E + 1: return launch_bs_k<BM, BN, WM, WN, E, true, DEPTH, NBUF>(a, s, grid, lds, tail);
+  case 2 * E: return launch_bs_k<BM, BN, WM, WN, E, false, NBUF>(a, s, grid, lds, tail); \
+  case 2 * E + 1: return launch_bs_k<BM, BN, WM, WN, E, true, NBUF>(a, s, grid, lds, tail);
     VV_EPI(EPI_STORE)
     VV_EPI(EPI_GELU)
     VV_EPI(EPI_RESID)
@@ -734,7 +706,15 @@ static hipError_t launch_bs(const GemmArgs& a, hipStream_t s) {
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool XCD = false, int MF = 32, int DEPTH = 1>
+template <int BM, int BN, int BK, int WM, int WN, int EPI>
+static hipError_t launch_tile_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail) {
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_nt<BM, BN, BK, WM, WN, EPI, 32>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_nt<BM, BN, BK, WM, WN, EPI, 32>), grid, dim3(64 * WM * WN), lds, s, a);
+  if (tail) hipLaunchKernelGGL((k_gemm_fixup<BM, BN, WM, WN, EPI, 32>), dim3(tail, 1, a.ngroups), dim3(64 * WM * WN), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int BK, int WM, int WN>
 static hipError_t launch_tile(const GemmArgs& a, hipStream_t s) {
   constexpr int LS = BK + 4;
   if (a.K % BK || a.ksplit % BK) return hipErrorInvalidValue;
@@ -743,28 +723,11 @@ static hipError_t launch_tile(const GemmArgs& a, hipStream_t s) {
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
   dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
   switch (a.epi) {
-#define VV_EPI(E)                                                                                   \
-  case E: {                                                                                         \
-    static bool init = false;                                                                       \
-    if (!init) {                                                                                    \
-      hipError_t e = hipFuncSetAttribute((const void*)k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF, DEPTH>,             \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
-      if (e != hipSuccess) return e;                                                                \
-      init = true;                                                                                  \
-    }                                                                                               \
-    hipLaunchKernelGGL((k_gemm_nt<BM, BN, BK, WM, WN, E, XCD, MF, DEPTH>), grid, dim3(64 * WM * WN), lds, s, a);   \
-    if (tail)                                                                                       \
-      hipLaunchKernelGGL((k_gemm_fixup<BM, BN, WM, WN, E, MF>), dim3(tail, 1, a.ngroups), dim3(64 * WM * WN), 0, \
-                         s, a);                                                                     \
-    return hipGetLastError();                                                                       \
-  }
-    VV_EPI(EPI_STORE)
-    VV_EPI(EPI_GELU)
-    VV_EPI(EPI_RESID)
-    VV_EPI(EPI_DGELU)
-#undef VV_EPI
-    default:
-      return hipErrorInvalidValue;
+    case EPI_STORE: return launch_tile_k<BM, BN, BK, WM, WN, EPI_STORE>(a, s, grid, lds, tail);
+    case EPI_GELU: return launch_tile_k<BM, BN, BK, WM, WN, EPI_GELU>(a, s, grid, lds, tail);
+    case EPI_RESID: return launch_tile_k<BM, BN, BK, WM, WN, EPI_RESID>(a, s, grid, lds, tail);
+    case EPI_DGELU: return launch_tile_k<BM, BN, BK, WM, WN, EPI_DGELU>(a, s, grid, lds, tail);
+    default: return hipErrorInvalidValue;
   }
 }
 
@@ -1002,13 +965,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bs2(GemmArgs args) {
 
 template <int EPI, bool APRE>
 static hipError_t launch_bs2_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail) {
-  static bool init = false;
-  if (!init) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_gemm_bs2<EPI, APRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (e != hipSuccess) return e;
-    init = true;
-  }
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_bs2<EPI, APRE>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_bs2<EPI, APRE>), grid, dim3(256), lds, s, a);
   if (tail)
     hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
@@ -1023,7 +980,7 @@ static hipError_t launch_bs2(const GemmArgs& a, hipStream_t s) {
     pre = pre && a.g[g].Bp;
     apre = apre && a.g[g].Ap;
   }
-  if (!pre) return launch_bs<128, 128, 2, 2, 1, 1>(a, s);
+  if (!pre) return launch_bs<128, 128, 2, 2, 1>(a, s);
   const size_t lds = 2 * 3 * 256 * 32 * sizeof(unsigned short);
   const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
@@ -1034,235 +991,6 @@ static hipError_t launch_bs2(const GemmArgs& a, hipStream_t s) {
     case EPI_GELU: return launch_bs2_k<EPI_GELU, false>(a, s, grid, lds, tail);
     case EPI_RESID: return launch_bs2_k<EPI_RESID, false>(a, s, grid, lds, tail);
     case EPI_DGELU: return launch_bs2_k<EPI_DGELU, false>(a, s, grid, lds, tail);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Split GEMM with a 3-buffer LDS ring and half-step fragment prefetch: 128x128x32 tile, 4 waves of 64x64.
-// Tile kt is consumed from ring slot kt%3 while tile kt+2 is split/written into slot (kt+2)%3 and tile kt+3 is
-// loaded into registers. The MFMAs of each half k-tile (16-deep step) run on fragments read during the previous
-// half, so the ONE barrier per k-tile is the only point where a wave waits on LDS; the staging work is
-// hand-interleaved between the MFMAs (sched_barrier keeps the source order).
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void k_gemm_bs3(GemmArgs args) {
-  constexpr int BM = 128, BN = 128, BK = 32, NT = 256, WN = 2, TM = 2, TN = 2;
-  constexpr int LSB = BK, PLANE = (BM + BN) * LSB, RING = 3 * PLANE;
-  constexpr int TPR = BK / 4, RPP = NT / TPR, AI = BM / RPP, BQ = BN * 4 / NT;
-  typedef float accv __attribute__((ext_vector_type(16)));
-  extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const GemmGroup G = args.g[blockIdx.z];
-  const int M = args.M, N = args.N, K = args.K, ksplit = args.ksplit;
-  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int nkt = K / BK;
-  int tile, kb = 0, ke = nkt, part = -1;
-  if (args.tsplit <= 1) {
-    tile = xcd_remap(blockIdx.x, ntm * ntn);
-  } else if ((int)blockIdx.x < args.tdp) {
-    tile = xcd_remap(blockIdx.x, args.tdp);
-  } else {
-    part = blockIdx.x - args.tdp;
-    const int S = args.tsplit, c = part % S;
-    tile = args.tdp + part / S;
-    kb = (c * nkt) / S;
-    ke = ((c + 1) * nkt) / S;
-  }
-  int mb, nb;
-  tile_mn(tile, ntm, ntn, mb, nb);
-  const int m0 = mb * BM, n0 = nb * BN;
-  const int lr = tid / TPR, lc = (tid % TPR) * 4;
-  auto swz = [](int row, int k) { return row * LSB + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); };
-
-  const float* a1p[AI];
-  const float* a2p[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int r = min(m0 + lr + RPP * i, M - 1);
-    const int ar = args.arow ? args.arow[r] : r;
-    a1p[i] = G.A + (size_t)ar * args.lda + lc;
-    a2p[i] = G.A2 ? G.A2 + (size_t)r * args.lda2 + lc - ksplit : a1p[i];
-  }
-  const unsigned short* bq[BQ];
-#pragma unroll
-  for (int i = 0; i < BQ; ++i) {
-    const int c = tid + NT * i;
-    const int n = min(n0 + c / 4, N - 1);
-    bq[i] = G.Bp + (size_t)n * 3 * K + (c % 4) * 8;
-  }
-
-  f4 ra[AI];
-  u4v rq[BQ][3];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < AI; ++i) ra[i] = *reinterpret_cast<const f4*>((k0 < ksplit ? a1p[i] : a2p[i]) + k0);
-#pragma unroll
-    for (int i = 0; i < BQ; ++i)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) rq[i][p] = *reinterpret_cast<const u4v*>(bq[i] + p * K + k0);
-  };
-  auto sstore = [&](unsigned short* P) {
-    u2v h, m, l;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      split3t(ra[i], h, m, l);
-      const int o = swz(lr + RPP * i, lc);
-      *reinterpret_cast<u2v*>(P + o) = h;
-      *reinterpret_cast<u2v*>(P + PLANE + o) = m;
-      *reinterpret_cast<u2v*>(P + 2 * PLANE + o) = l;
-    }
-#pragma unroll
-    for (int i = 0; i < BQ; ++i) {
-      const int c = tid + NT * i;
-      const int o = swz(BM + c / 4, (c % 4) * 8);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<u4v*>(P + p * PLANE + o) = rq[i][p];
-    }
-  };
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int rin = lane & 31, hh = lane >> 5;
-  // fragments of one 16-deep step: A [TM][3 planes], B [TN][3 planes]
-  auto frags = [&](const unsigned short* P, int s, bf8v (&fa)[TM][3], bf8v (&fb)[TN][3]) {
-    const unsigned short* As = P + (wm * TM * 32 + rin) * LSB;
-    const unsigned short* Bs = P + (BM + wn * TN * 32 + rin) * LSB;
-    const int ck = ((2 * s + hh) ^ ((rin >> 2) & 3)) * 8;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fa[a][p] = *reinterpret_cast<const bf8v*>(As + p * PLANE + a * 32 * LSB + ck);
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fb[b][p] = *reinterpret_cast<const bf8v*>(Bs + p * PLANE + b * 32 * LSB + ck);
-  };
-  accv acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
-
-  // 24 MFMA slots of one half-step; slot j of half `half` also does staging piece q = 24*half + j:
-  //   q 0-19: A chunk c = q/5: elements 0-3 split (q%5 < 4), then pack + write the 3 planes (q%5 == 4)
-  //   q 20-25: B plane writes; q 26-29: A loads of tile kt+3; q 36-41: B loads of tile kt+3
-  unsigned xs[4], ms[4], ls[4];
-  auto half_step = [&](const bf8v (&fa)[TM][3], const bf8v (&fb)[TN][3], int half, unsigned short* Pw, int k3) {
-#pragma unroll
-    for (int j = 0; j < 24; ++j) {
-      const int pr = j / 4, a = (j % 4) / 2, b = j % 2;
-      const int pa = pr == 0 ? 2 : (pr == 2 || pr == 3) ? 1 : 0;
-      const int pb = pr == 1 ? 2 : (pr == 2 || pr == 4) ? 1 : 0;
-      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][pa], fb[b][pb], acc[a][b], 0, 0, 0);
-      const int q = 24 * half + j;
-      if (q < 20) {
-        const int c = q / 5, e = q % 5;
-        if (e < 4) {
-          const unsigned xv = __float_as_uint(ra[c][e]);
-          const float r1 = ra[c][e] - __uint_as_float(xv & 0xffff0000u);
-          xs[e] = xv;
-          ms[e] = __float_as_uint(r1);
-          ls[e] = __float_as_uint(r1 - __uint_as_float(ms[e] & 0xffff0000u));
-        } else {
-          u2v h, m, l;
-          h[0] = __builtin_amdgcn_perm(xs[1], xs[0], 0x07060302u);
-          h[1] = __builtin_amdgcn_perm(xs[3], xs[2], 0x07060302u);
-          m[0] = __builtin_amdgcn_perm(ms[1], ms[0], 0x07060302u);
-          m[1] = __builtin_amdgcn_perm(ms[3], ms[2], 0x07060302u);
-          l[0] = __builtin_amdgcn_perm(ls[1], ls[0], 0x07060302u);
-          l[1] = __builtin_amdgcn_perm(ls[3], ls[2], 0x07060302u);
-          const int o = swz(lr + RPP * c, lc);
-          *reinterpret_cast<u2v*>(Pw + o) = h;
-          *reinterpret_cast<u2v*>(Pw + PLANE + o) = m;
-          *reinterpret_cast<u2v*>(Pw + 2 * PLANE + o) = l;
-        }
-      } else if (q < 26) {
-        const int i = (q - 20) / 3, p = (q - 20) % 3;
-        const int c = tid + NT * i;
-        *reinterpret_cast<u4v*>(Pw + p * PLANE + swz(BM + c / 4, (c % 4) * 8)) = rq[i][p];
-      } else if (q < 30) {
-        const int i = q - 26;
-        ra[i] = *reinterpret_cast<const f4*>((k3 < ksplit ? a1p[i] : a2p[i]) + k3);
-      } else if (q >= 36 && q < 42) {
-        const int i = (q - 36) / 3, p = (q - 36) % 3;
-        rq[i][p] = *reinterpret_cast<const u4v*>(bq[i] + p * K + k3);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  const int nk = ke - kb;
-  gload(kb * BK);
-  sstore(lds16);
-  gload(min(kb + 1, ke - 1) * BK);
-  sstore(lds16 + RING);
-  gload(min(kb + 2, ke - 1) * BK);
-  __syncthreads();
-  bf8v x0a[TM][3], x0b[TN][3], x1a[TM][3], x1b[TN][3];
-  frags(lds16, 0, x0a, x0b);
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int nxt = cur == 2 ? 0 : cur + 1, wr = nxt == 2 ? 0 : nxt + 1;
-    unsigned short* Pc = lds16 + cur * RING;
-    unsigned short* Pw = lds16 + wr * RING;
-    const int k3 = min(kb + kt + 3, ke - 1) * BK;
-    frags(Pc, 1, x1a, x1b);
-    __builtin_amdgcn_sched_barrier(0);
-    half_step(x0a, x0b, 0, Pw, k3);
-    frags(lds16 + nxt * RING, 0, x0a, x0b);
-    __builtin_amdgcn_sched_barrier(0);
-    half_step(x1a, x1b, 1, Pw, k3);
-    __syncthreads();
-    cur = nxt;
-  }
-
-  if (part >= 0) {
-    float* w = args.ws + ((size_t)blockIdx.z * (gridDim.x - args.tdp) + part) * (size_t)(TM * TN * 16 * NT);
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) w[(size_t)((a * TN + b) * 16 + r) * NT + tid] = acc[a][b][r];
-    return;
-  }
-  if (m0 + BM <= M && n0 + BN <= N)
-    epilogue<BM, BN, 2, WN, EPI, 32, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
-  else
-    epilogue<BM, BN, 2, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
-}
-
-template <int EPI>
-static hipError_t launch_bs3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail) {
-  static bool init = false;
-  if (!init) {
-    hipError_t e =
-        hipFuncSetAttribute((const void*)k_gemm_bs3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    init = true;
-  }
-  hipLaunchKernelGGL((k_gemm_bs3<EPI>), grid, dim3(256), lds, s, a);
-  if (tail)
-    hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-static hipError_t launch_bs3(const GemmArgs& a, hipStream_t s) {
-  if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
-  bool pre = true;
-  for (int g = 0; g < a.ngroups; ++g) pre = pre && a.g[g].Bp;
-  if (!pre) return launch_bs<128, 128, 2, 2, 1, 1>(a, s);
-  const size_t lds = 3 * 3 * 256 * 32 * sizeof(unsigned short);
-  const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
-  const int tail = a.tsplit > 1 ? T - a.tdp : 0;
-  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
-  switch (a.epi) {
-    case EPI_STORE: return launch_bs3_k<EPI_STORE>(a, s, grid, lds, tail);
-    case EPI_GELU: return launch_bs3_k<EPI_GELU>(a, s, grid, lds, tail);
-    case EPI_RESID: return launch_bs3_k<EPI_RESID>(a, s, grid, lds, tail);
-    case EPI_DGELU: return launch_bs3_k<EPI_DGELU>(a, s, grid, lds, tail);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1318,9 +1046,7 @@ __global__ __launch_bounds__(256) void k_rowscale(GemmArgs args, float* __restri
   if (lane == 0) out[(size_t)blockIdx.z * args.M + r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
 }
 
-// XP != 0: timing experiments only (wrong results): 1 no global loads in the k loop, 2 no MFMAs, 3 no A split
-// arithmetic
-template <int EPI, int XP = 0>
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* __restrict__ ascale) {
   constexpr int BM = 128, BN = 128, BK = 32, NT = 256, WN = 2, TM = 2, TN = 2;
   constexpr int LSB = BK, PLANE = (BM + BN) * LSB;  // unsigned shorts
@@ -1381,11 +1107,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* 
   auto bload = [&](int q, int p, int k0) { rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + p * K + k0); };
   auto asplit = [&](unsigned short* P, int i) {
     const int o = swz(lr + RPP * i, lc);
-    if constexpr (XP == 3) {
-      *reinterpret_cast<u2v*>(P + o) = u2v{__float_as_uint(ra[i][0]), __float_as_uint(ra[i][1])};
-      *reinterpret_cast<u2v*>(P + PLANE + o) = u2v{__float_as_uint(ra[i][2]), __float_as_uint(ra[i][3])};
-      return;
-    }
     h4v hv, lv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1462,15 +1183,11 @@ __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* 
       const int st = i / 12, pr = (i % 12) / 4, a = (i % 4) / 2, b = i % 2;
       const h8v& xa = fa[st][a][pr == 0 ? 1 : 0];
       const h8v& xb = fb[st][b][pr == 1 ? 1 : 0];
-      if constexpr (XP == 2) {
-        if (i < 4) acc[a][b][0] += (float)xa[0] + (float)xb[1];
-      } else {
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa, xb, acc[a][b], 0, 0, 0);
-      }
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa, xb, acc[a][b], 0, 0, 0);
       if (i < 2 * AI && (i & 1)) asplit(Pn, i / 2);
       if (i >= 8 && i < 12) bstore(Pn, (i - 8) / 2, (i - 8) % 2);
-      if (XP != 1 && i >= 12 && i < 12 + AI) aload(i - 12, k2);
-      if (XP != 1 && i >= 16 && i < 20) bload((i - 16) / 2, (i - 16) % 2, k2);
+      if (i >= 12 && i < 12 + AI) aload(i - 12, k2);
+      if (i >= 16 && i < 20) bload((i - 16) / 2, (i - 16) % 2, k2);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
@@ -1509,16 +1226,10 @@ __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* 
     epilogue<BM, BN, 2, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
-template <int EPI, int XP = 0>
+template <int EPI>
 static hipError_t launch_h3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc) {
-  static bool init = false;
-  if (!init) {
-    hipError_t e =
-        hipFuncSetAttribute((const void*)k_gemm_h3<EPI, XP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    init = true;
-  }
-  hipLaunchKernelGGL((k_gemm_h3<EPI, XP>), grid, dim3(256), lds, s, a, sc);
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_h3<EPI>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_h3<EPI>), grid, dim3(256), lds, s, a, sc);
   if (tail)
     hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -1535,7 +1246,7 @@ static bool h3_ready(const GemmArgs& a) {
   return pre;
 }
 
-static hipError_t launch_h3(const GemmArgs& a, hipStream_t s, int xp = 0) {
+static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
   if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
   if (!h3_ready(a)) return launch_bs2(a, s);
   float* sc = a.ws + kWsFloats;
@@ -1544,14 +1255,6 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s, int xp = 0) {
   const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
   dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
-  if (xp && a.epi == EPI_STORE) {
-    switch (xp) {
-      case 1: return launch_h3_k<EPI_STORE, 1>(a, s, grid, lds, tail, sc);
-      case 2: return launch_h3_k<EPI_STORE, 2>(a, s, grid, lds, tail, sc);
-      case 3: return launch_h3_k<EPI_STORE, 3>(a, s, grid, lds, tail, sc);
-      default: return hipErrorInvalidValue;
-    }
-  }
   switch (a.epi) {
     case EPI_STORE: return launch_h3_k<EPI_STORE>(a, s, grid, lds, tail, sc);
     case EPI_GELU: return launch_h3_k<EPI_GELU>(a, s, grid, lds, tail, sc);
@@ -1561,49 +1264,20 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s, int xp = 0) {
   }
 }
 
-// tile variants (index = tile hint)
+// the GEMM kernels of the library, by tile hint (vv_gemm's `tile`; gemm_nt rejects every other value):
+//   exact f32 MFMA   0: 128x128   2: 64x64   4: 32x64            (GEMM_F32)
+//   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
+//   fp16x3 split    36: 128x128 (deep-K GEMMs of GEMM_SPLIT16)
+bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || t == 36; }
+
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
     case 0: return launch_tile<128, 128, 32, 2, 2>(a, s);
-    case 1: return launch_tile<128, 64, 32, 2, 2>(a, s);
     case 2: return launch_tile<64, 64, 32, 2, 2>(a, s);
-    case 3: return launch_tile<64, 64, 16, 2, 2>(a, s);
     case 4: return launch_tile<32, 64, 32, 1, 2>(a, s);
-    case 5: return launch_tile<64, 32, 32, 2, 1>(a, s);
-    case 6: return launch_tile<64, 128, 32, 2, 2>(a, s);
-    case 7: return launch_tile<32, 64, 16, 1, 2>(a, s);
-    case 8: return launch_tile<64, 64, 64, 2, 2>(a, s);
-    case 9: return launch_tile<64, 64, 32, 2, 2, true>(a, s);     // 2 with the XCD remap
-    case 10: return launch_tile<64, 64, 32, 2, 2, false, 16>(a, s);   // 16x16x4 MFMA
-    case 11: return launch_tile<128, 64, 32, 2, 2, false, 16>(a, s);
-    case 12: return launch_tile<64, 128, 32, 2, 2, false, 16>(a, s);
-    case 13: return launch_tile<128, 128, 32, 2, 2, false, 16>(a, s);
-    case 14: return launch_tile<64, 64, 16, 2, 2, false, 16>(a, s);
-    case 15: return launch_tile<32, 64, 32, 1, 2, false, 16>(a, s);
-    case 16: return launch_tile<64, 64, 32, 2, 2, false, 32, 2>(a, s);    // 2-deep register prefetch
-    case 17: return launch_tile<64, 128, 32, 2, 2, false, 32, 2>(a, s);
-    case 18: return launch_tile<32, 64, 32, 1, 2, false, 32, 2>(a, s);
-    case 19: return launch_tile<64, 64, 64, 2, 2, false, 32, 2>(a, s);
-    case 20: return launch_tile<64, 64, 16, 2, 2, false, 32, 2>(a, s);
-    // bf16x6 split (fp32-accurate) variants
-    case 21: return launch_bs<128, 128, 2, 4>(a, s);
-    case 22: return launch_bs<128, 128, 2, 2>(a, s);
-    case 23: return launch_bs<128, 64, 2, 2>(a, s);
     case 24: return launch_bs<64, 64, 2, 2>(a, s);
-    case 25: return launch_bs<64, 128, 2, 2>(a, s);
-    case 26: return launch_bs<128, 64, 2, 1>(a, s);
-    case 27: return launch_bs<128, 128, 2, 4, 2, 2>(a, s);   // 2-deep register prefetch
-    case 28: return launch_bs<128, 128, 2, 4, 1, 1>(a, s);   // one LDS buffer: 2 WGs / CU
-    case 29: return launch_bs<64, 64, 2, 2, 2, 2>(a, s);
-    case 30: return launch_bs<128, 64, 2, 2, 2, 2>(a, s);
-    case 31: return launch_bs<128, 128, 2, 2, 1, 1>(a, s);
-    case 32: return launch_bs<128, 128, 2, 4, 2, 1>(a, s);
-    case 33: return launch_bs<64, 128, 2, 2, 2, 2>(a, s);
-    case 34: return launch_bs2(a, s);   // pipelined 128x128, one barrier per k-tile
-    case 35: return launch_bs3(a, s);   // 3-buffer ring + half-step fragment prefetch
-    // fp16x3 split (fp32-accurate)
+    case 34: return launch_bs2(a, s);
     case 36: return launch_h3(a, s);
-    case 37: case 38: case 39: return launch_h3(a, s, t - 36);   // timing experiments (wrong results)
     default: return hipErrorInvalidValue;
   }
 }
@@ -1615,11 +1289,6 @@ static long tiles_of(const GemmArgs& a, int bm, int bn) {
 // tile choice (measured on MI355X, tools/gemm_bench.py; 4 WGs/CU resident): high-occupancy 64x64 tiles beat
 // larger tiles on every decoder shape at M = 2048 / 8192; 32x64 when 64x64 leaves CUs idle
 
-static int g_num_cu = 0;
-static int g_math = GEMM_SPLIT16;
-static int g_tail_occ = -1;  // VAEVAR_TAIL_OCC=1: size the split-K tail by workgroups per CU (measured slower)
-void set_gemm_math(int m) { g_math = m; }
-int gemm_math() { return g_math; }
 
 struct SplitArena {
   const float* base;
@@ -1714,7 +1383,7 @@ size_t gemm_ws_floats() { return kWsFloats + kScaleFloats; }
 
 // tile choice (measured on MI355X, tools/gemm_bench.py, tools/gemm_split_check.py)
 static int pick_tile(const GemmArgs& a) {
-  if (g_math == GEMM_SPLIT16 || g_math == GEMM_SPLIT) {
+  if (a.math == GEMM_SPLIT16 || a.math == GEMM_SPLIT) {
     // GEMM_SPLIT16: fp16x3 128x128 for the deep-K GEMMs that give >= 128 tiles; the bf16x6 64x64 kernel for the
     // short-K / few-tile GEMMs of the Swin towers (its pipeline prologue and epilogue dominate there)
     static int h3_mink = -1;  // VAEVAR_H3_MINK: smallest K sent to the fp16x3 kernel (default 768)
@@ -1722,7 +1391,7 @@ static int pick_tile(const GemmArgs& a) {
       const char* e = getenv("VAEVAR_H3_MINK");
       h3_mink = e ? std::max(64, atoi(e)) : 768;
     }
-    if (g_math == GEMM_SPLIT16 && a.K >= h3_mink && tiles_of(a, 128, 128) >= 128) return 36;
+    if (a.math == GEMM_SPLIT16 && a.K >= h3_mink && tiles_of(a, 128, 128) >= 128) return 36;
     // pipelined 128x128 (64x64 per wave, one barrier per k-tile) for the deep-K GEMMs that fill the chip with
     // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline)
     const long t128 = tiles_of(a, 128, 128);
@@ -1737,17 +1406,9 @@ static int pick_tile(const GemmArgs& a) {
 
 // tile edge of each variant (for the tail split)
 static void variant_tile(int t, int& bm, int& bn, int& bk) {
-  static const int tab[][3] = {{128, 128, 32}, {128, 64, 32}, {64, 64, 32}, {64, 64, 16}, {32, 64, 32}, {64, 32, 32},
-                               {64, 128, 32}, {32, 64, 16}, {64, 64, 64}, {64, 64, 32}, {64, 64, 32}, {128, 64, 32},
-                               {64, 128, 32}, {128, 128, 32}, {64, 64, 16}, {32, 64, 32}, {64, 64, 32}, {64, 128, 32},
-                               {32, 64, 32}, {64, 64, 64}, {64, 64, 16}, {128, 128, 32}, {128, 128, 32},
-                               {128, 64, 32}, {64, 64, 32}, {64, 128, 32}, {128, 64, 32}, {128, 128, 32},
-                               {128, 128, 32}, {64, 64, 32}, {128, 64, 32}, {128, 128, 32}, {128, 128, 32},
-                               {64, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32},
-                               {128, 128, 32}, {128, 128, 32}};
-  bm = tab[t][0];
-  bn = tab[t][1];
-  bk = tab[t][2];
+  bk = 32;
+  bm = t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
+  bn = t == 0 || t >= 34 ? 128 : 64;
 }
 
 static bool small_split_enabled() {
@@ -1765,25 +1426,16 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
   const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
-  if (t < 0 || t > 39) return hipErrorInvalidValue;
+  if (!valid_tile(t)) return hipErrorInvalidValue;
   // data-parallel rounds of whole tiles + the remaining tiles split along K over the idle CUs
-  if (g_tail_occ < 0) {
-    const char* e = getenv("VAEVAR_TAIL_OCC");
-    g_tail_occ = (e && e[0] == '1') ? 1 : 0;
-  }
-  if (!g_num_cu) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) g_num_cu = p.multiProcessorCount;
-    if (g_num_cu <= 0) g_num_cu = 256;
-  }
+  const int num_cu = device_cus();
   a.tdp = 0;
   a.tsplit = 1;
   a.ws = ws;
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start
-    a.g[g].Ap = (t >= 21 && t <= 35 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_exact(a.g[g].A) : a.g[g].Ap;
+    a.g[g].Ap = (t >= 21 && t < 36 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_exact(a.g[g].A) : a.g[g].Ap;
     a.g[g].Bh = nullptr;
     a.g[g].Bs = nullptr;
     if (t >= 36 && (!a.ldb || a.ldb == a.K)) split16_of(a.g[g].B, a.K, a.g[g].Bh, a.g[g].Bs);
@@ -1792,9 +1444,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
     int bm, bn, bk;
     variant_tile(t, bm, bn, bk);
     const int T = ((a.N + bn - 1) / bn) * ((a.M + bm - 1) / bm);
-    // concurrent workgroups per CU of the split variants (LDS-limited): 64x64 3, 128x128 single-buffer 2
-    const int occ = g_tail_occ ? (t == 24 || t == 29 ? 3 : (t == 31 || t == 28 ? 2 : 1)) : 1;
-    const int P = g_num_cu * occ, nkt = a.K / bk;
+    const int P = num_cu, nkt = a.K / bk;
     const int tdp = (T / P) * P, tail = T - tdp;
     if (tdp > 0 && tail > 0 && tail <= P / 2) {
       // chunks of >= 12 k-tiles: below that the fixup launch and partial traffic cost more than the tail

@@ -48,6 +48,7 @@ struct GemmArgs {
   // tsplit k-chunks whose fp32 partials go to ws and are summed (in chunk order) by the fixup kernel
   int tdp, tsplit;
   float* ws;
+  int math;  // GemmMath of this GEMM (the context's setting)
   GemmGroup g[kMaxGroups];
 };
 
@@ -61,8 +62,8 @@ size_t gemm_ws_floats();
 //   GEMM_SPLIT16 fp32 operands scaled by a power of two per row (A and B) and split
 //                into two fp16 planes, three v_mfma_f32_32x32x16_f16 products (both fp32-level error)
 enum GemmMath : int { GEMM_F32 = 0, GEMM_SPLIT = 1, GEMM_SPLIT16 = 2 };
-void set_gemm_math(int m);
-int gemm_math();
+// tile hints gemm_nt accepts (the product kernels; see vv_gemm.hip)
+bool valid_tile(int t);
 // Weight arenas with precomputed split planes. The planes buffer of an arena of n floats holds, at these
 // offsets (split_arena_bytes(n) bytes in all):
 //   bf16: [0, 3n) unsigned shorts; row r of the [N][K] operand at float offset o = B - base: 3*(o + r*K) = h[K], m[K], l[K]
@@ -265,9 +266,9 @@ hipError_t vec_axpby(float* out, const float* x, float a, const float* y, float 
 hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s);
 hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float* out, hipStream_t s);
 hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
-// q (= -g on entry) -> L-BFGS direction d (two-loop recursion, device scalars); al, coef: >= m + 1 device floats
+// q (= -g on entry) -> L-BFGS direction d (two-loop recursion, device scalars); al: >= m device floats
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,
-                          int64_t n, double* partial, int nblk, float* al, float* coef, hipStream_t s);
+                          int64_t n, double* partial, int nblk, float* al, hipStream_t s);
 hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                      float eps, float bc1, float bc2_sqrt, hipStream_t s);
 // ---------------------------------------------------------------------------

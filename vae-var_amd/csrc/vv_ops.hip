@@ -858,6 +858,10 @@ __global__ __launch_bounds__(256) void k_flow_input(const float* x, float* fi, c
   }
 }
 
+__global__ __launch_bounds__(256) void k_zero(float* __restrict__ p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) p[i] = 0.f;
+}
+
 __global__ __launch_bounds__(256) void k_flow_input_adj(const float* gfi, float* carry, const int* di, const int* dj,
                                                         const float* std_, int C, int Hs, int Ws, int Hl, int Wl) {
   const int HWl = Hl * Wl;
@@ -881,9 +885,11 @@ hipError_t flow_input(const float* x, float* fi, const int* di, const int* dj, c
 hipError_t flow_input_adjoint(const float* gfi, float* carry, const int* di, const int* dj, const float* std_, int C,
                               int Hs, int Ws, int Hl, int Wl, hipStream_t s) {
   if (Hs < Hl || Ws < Wl) return hipErrorNotSupported;
-  hipError_t e = hipMemsetAsync(carry, 0, (size_t)C * Hs * Ws * sizeof(float), s);
-  if (e != hipSuccess) return e;
+  // zero the whole carry with a kernel, not hipMemsetAsync: a memset node captured into the closure's hipGraph was
+  // not ordered before the scatter below on replay (config 5's wrong gradients in r01)
   const int ph = prof_begin(s);
+  const size_t n = (size_t)C * Hs * Ws;
+  hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, s, carry, n);
   hipLaunchKernelGGL(k_flow_input_adj, dim3(1024), dim3(256), 0, s, gfi, carry, di, dj, std_, C, Hs, Ws, Hl, Wl);
   prof_end(ph, s, PC_MISFIT, 1.0 * C * Hl * Wl, 8.0 * C * Hl * Wl);
   return hipGetLastError();
@@ -1202,8 +1208,7 @@ __global__ __launch_bounds__(256) void k_twoloop_axpy(float* y, const float* x, 
   for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) y[k] = y[k] + a * x[k];
 }
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,
-                          int64_t n, double* partial, int nblk, float* al, float* coef, hipStream_t s) {
-  (void)coef;
+                          int64_t n, double* partial, int nblk, float* al, hipStream_t s) {
   for (int i = m - 1; i >= 0; --i) {
     hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, S[i], q, n, partial);
     hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, Y[i], partial, nblk, ro[i], al, i, 0,

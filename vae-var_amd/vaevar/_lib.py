@@ -103,6 +103,7 @@ _SIGS = {
     "vv_profile_stop": (c_int, [c_void_p, P(c_double), P(c_double), P(c_double), P(c_int), c_int]),
     "vv_nearest_map": (c_int, [c_int, c_int, P(c_int)]),
     "vv_set_gemm_math": (c_int, [c_void_p, c_int]),
+    "vv_set_closure_graph": (c_int, [c_void_p, c_int]),
     "vv_integrate": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                              c_int, c_void_p]),
     "vv_get_gemm_math": (c_int, [c_void_p, P(c_int)]),

@@ -117,7 +117,11 @@ class CyclicVAE4DVar:
         self.mean_d = torch.from_numpy(self.mean).to(dev)
         self.std_d = torch.from_numpy(self.std).to(dev)
         self.metric = Metrics(decoder.ctx, self.mean, C.MODEL_STD[:nch] if std is None else std, device)
-        self.metrics_list = {"bg_wrmse": [], "bg_bias": [], "ana_wrmse": [], "ana_bias": []}
+        # the reference's full key set (da_4dvar.py:511), so da_cycle_results/<name>/*.npy match file for file; the
+        # vae4dvar branch fills bg_/ana_ wrmse and bias (:1285-1291), the others stay empty (mse: other modes,
+        # error_obs: use_eval only)
+        self.metrics_list = {"bg_wrmse": [], "ana_wrmse": [], "bg_mse": [], "ana_mse": [], "bg_bias": [],
+                             "ana_bias": [], "error_obs": []}
         self.dev = dev
         os.makedirs(self.dir, exist_ok=True)  # init_file_dir (:605-606)
         self._xb0 = xb0
@@ -163,11 +167,14 @@ class CyclicVAE4DVar:
         p = DAProblem(self.dec, prob, flow=self.flow, obs_coeff=self.obs_coeff, obs_interp=self.obs_interp)
         gt_d = torch.as_tensor(np.asarray(gt, np.float32)).to(self.dev) if not isinstance(gt, torch.Tensor) else gt
         res = one_step_da(p, self.Nit, gt=gt_d, metrics=self.metric)
-        (w0, b0), (w1, b1) = res["metrics"][0], res["metrics"][-1]
+        # da_4dvar.py:1285-1291: pass kk == 0 -> bg_*, `elif kk == Nit` -> ana_* (so Nit = 0 records only bg_*)
+        w0, b0 = res["metrics"][0]
         self.metrics_list["bg_wrmse"].append(w0)
         self.metrics_list["bg_bias"].append(b0)
-        self.metrics_list["ana_wrmse"].append(w1)
-        self.metrics_list["ana_bias"].append(b1)
+        if self.Nit > 0:
+            w1, b1 = res["metrics"][self.Nit]
+            self.metrics_list["ana_wrmse"].append(w1)
+            self.metrics_list["ana_bias"].append(b1)
         self.last = res
         return res["xa"]
 

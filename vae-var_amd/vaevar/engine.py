@@ -117,6 +117,10 @@ class Context:
     def gemm_math(self, name: str):
         check(lib.vv_set_gemm_math(self.h, self.GEMM_MATH[name]), "set_gemm_math")
 
+    def set_closure_graph(self, enable: bool):
+        """Replay the closure from a captured hipGraph (default) or launch its kernels eagerly."""
+        check(lib.vv_set_closure_graph(self.h, 1 if enable else 0), "set_closure_graph")
+
     def gemm_register_weight(self, B):
         """Precompute B's split planes (bf16 and fp16; B must outlive the context and stay unchanged)."""
         check(lib.vv_gemm_register_weight(self.h, _ptr(B), B.shape[0], B.shape[1]), "gemm_register_weight")
