@@ -1,0 +1,106 @@
+"""ORACLE tool (survey container only): how far does the config-2 trajectory of G10 move when only the
+floating-point summation order changes? The reference's own decoder modules (oracle/ref_harness.py) are run again
+with a different torch thread count (so the CPU GEMMs block and sum differently), (a) free-running with
+torch.optim.LBFGS and (b) as a fixed-step replay of G10's recorded line-search steps through the product's L-BFGS
+mirror (vaevar.lbfgs.LBFGS with torch-CPU vector primitives). The relative J difference per outer pass against G10
+is the intrinsic sensitivity of the problem; tests/test_gpu_parity.py::test_config2_trajectory_g10 takes its
+tolerance from it (written to tests/golden/g10_sensitivity.npz).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python -B oracle/g10_sensitivity.py [--threads 4]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "vae-var_amd"))
+
+from oracle import ref_harness  # noqa: E402
+from oracle.da_ref import RefProblem, one_step_da_ref  # noqa: E402
+from oracle.make_golden import build_ref  # noqa: E402
+from vaevar import config as C  # noqa: E402
+from vaevar.lbfgs import LBFGS  # noqa: E402
+from vaevar.problem import make_problem  # noqa: E402
+
+GOLD = os.path.join(REPO, "tests", "golden")
+
+
+class CpuPrims:
+    """The vector-primitive contract of vaevar.engine.Context on torch-CPU tensors (double-accumulated dots)."""
+
+    def dot(self, a, b):
+        return float((a.double() * b.double()).sum())
+
+    def abssum(self, a):
+        return float(a.double().abs().sum())
+
+    def absmax(self, a):
+        return float(a.abs().max())
+
+    def axpy(self, y, x, alpha):
+        y.add_(x, alpha=alpha)
+
+    def axpby(self, out, x, a, y, b):
+        out.copy_(a * x + (b * y if y is not None else 0))
+
+    def scale(self, y, alpha):
+        y.mul_(alpha)
+
+    def copy(self, dst, src):
+        dst.copy_(src)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=4)
+    a = ap.parse_args()
+    g = np.load(os.path.join(GOLD, "g10_config2_trajectory.npz"))
+    Jr = g["J"].sum(1)
+    torch.set_num_threads(a.threads)
+    cwd = os.getcwd()
+    tr, _ = ref_harness.import_reference()
+    os.chdir(cwd)
+    m, _ = build_ref(tr, C.DECODER)
+    for v in m.parameters():
+        v.requires_grad_(False)
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620)
+    rp = RefProblem(prob, m, C.DECODER["img_size"])
+    t0 = time.time()
+    _, _, js, _, _ = one_step_da_ref(rp, 10, (32, 128, 256))
+    free = np.abs(np.array(js).sum(1) - Jr) / np.abs(Jr)
+    print(f"free-running, {a.threads} threads ({time.time() - t0:.0f}s): J rel per pass {free.tolist()}", flush=True)
+
+    # fixed-step replay of G10's line searches through the product's L-BFGS mirror
+    z = torch.zeros(1, 32, 128, 256)
+    opt = LBFGS(CpuPrims(), z, history_size=10, max_iter=10, line_search_fn="strong_wolfe", device_two_loop=False)
+    opt.replay = [(float(t), int(n)) for t, n in zip(g["ls_t"], g["ls_evals"])]
+
+    def closure(zz, gr):
+        x = zz.detach().clone().requires_grad_(True)
+        r, o = rp.loss_terms(x)
+        (r + o).backward()
+        gr.copy_(x.grad)
+        return float(np.float32(float(r)) + np.float32(float(o)))
+
+    jr = []
+    for kk in range(11):
+        with torch.no_grad():
+            r, o = rp.loss_terms(z)
+        jr.append(float(r) + float(o))
+        if kk < 10:
+            opt.step(closure)
+    rep = np.abs(np.array(jr) - Jr) / np.abs(Jr)
+    print(f"replay, {a.threads} threads ({time.time() - t0:.0f}s): J rel per pass {rep.tolist()}", flush=True)
+    np.savez(os.path.join(GOLD, "g10_sensitivity.npz"), threads=a.threads, free_rel=free, replay_rel=rep)
+
+
+if __name__ == "__main__":
+    main()

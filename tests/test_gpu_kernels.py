@@ -113,13 +113,31 @@ def test_gemm_rejects_non_library_tiles(ctx):
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 35, 37, 38, 39, 40, 1000):
+    for t in (1, 3, 21, 35, 37, 38, 39, 40, 41, 42, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
     for t in (0, 2, 4, 24, 34, 36):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 1152, 4608), (2048, 4608, 1152), (2048, 1152, 3456)])
+def test_gemm_splitk_deterministic(ctx, M, N, K):
+    """fp16x3 GEMMs whose tiles are split along K (every tile at N = 1152, the tail at N = 4608): the fixup sums
+    the partials in chunk order, so 30 back-to-back launches give bit-identical results at fp32-level error."""
+    g = torch.Generator().manual_seed(M + N + K + 7)
+    A = torch.randn(M, K, generator=g).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.03).cuda()
+    ctx.gemm_register_weight(B)
+    _keep.append(B)
+    first = ctx.gemm(A, B, tile=36)
+    outs = [ctx.gemm(A, B, tile=36) for _ in range(30)]
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, first) for o in outs)
+    ref = A.double().cpu() @ B.double().cpu().t()
+    scale = A.double().abs().cpu() @ B.double().abs().cpu().t()
+    assert float(((first.cpu().double() - ref).abs() / scale).max()) < 1e-6
 
 
 def test_gemm_math_switch(ctx):

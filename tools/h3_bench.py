@@ -1,5 +1,7 @@
-"""fp16x3 GEMM microbenchmark over the LG-stage shapes (registered weights), incl. the timing-experiment
-variants 37-39 (no loads / no MFMA / no A-split arithmetic; wrong results). Development tool."""
+"""fp16x3 GEMM microbenchmark over the LG-stage shapes at 2048 tokens per analysis (registered weights, the
+engine's tile choice incl. split-K). Development tool: run once per VAEVAR_H3_APRE setting to A/B the in-loop A
+split against k_split_rows. Times one GEMM call (the whole launch sequence: scaling/split pass, main kernel,
+fixup) with HIP events on the current stream."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vae-var_amd"))
@@ -7,29 +9,51 @@ import torch
 from vaevar.engine import Context
 
 ctx = Context.get(0)
-shapes = [(2048, 3456, 1152), (2048, 1152, 1152), (2048, 4608, 1152), (2048, 1152, 4608), (2048, 1152, 3456),
-          (8192, 1152, 1152), (4096, 4608, 1152)]
-tiles = [int(t) for t in os.environ.get("TILES", "36,37,38,39").split(",")]
+mult = int(os.environ.get("MROWS", "1"))
+shapes = [(2048 * mult, n, k) for n, k in ((3456, 1152), (1152, 1152), (4608, 1152), (1152, 4608), (1152, 3456))]
+tot = 0.0
 for (M, N, K) in shapes:
-    A = torch.rand(M, K, device="cuda") * 2 - 1
-    B = torch.rand(N, K, device="cuda") * 2 - 1
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(N, K, device="cuda", generator=g) * 0.03
     ctx.gemm_register_weight(B)
+    ref = A.double() @ B.double().T
+    scale = A.double().abs() @ B.double().abs().T
+    tiles = [int(t) for t in os.environ.get("TILES", "-1").split(",")]
     row = {"M": M, "N": N, "K": K}
-    ref = (A.double() @ B.double().T)
-    row["err"] = float((ctx.gemm(A, B, tile=36).double() - ref).abs().max() / ref.abs().max())
     for t in tiles:
-        if t in (36, 40) and os.environ.get("ERR", "1") == "1":
-            row[f"err{t}"] = float((ctx.gemm(A, B, tile=t).double() - ref).abs().max() / ref.abs().max())
+        C = ctx.gemm(A, B, tile=t)
+        err = float(((C.double() - ref).abs() / scale).max())
         for _ in range(3):
             ctx.gemm(A, B, tile=t)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        n = 30
+        n = 50
         e0.record()
         for _ in range(n):
             ctx.gemm(A, B, tile=t)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / n
-        row[f"t{t}"] = f"{us:.1f}us {2 * M * N * K / us / 1e6:.0f}TF"
+        row[f"t{t}"] = [round(us, 1), round(2 * M * N * K / us / 1e6 / 833.3, 3), float('%.2g' % err)]
     print(json.dumps(row), flush=True)
+    del A, B
+    continue
+    C = ctx.gemm(A, B)
+    err = float(((C.double() - ref).abs() / scale).max())
+    for _ in range(3):
+        ctx.gemm(A, B)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 50
+    e0.record()
+    for _ in range(n):
+        ctx.gemm(A, B)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / n
+    tot += us
+    print(json.dumps({"M": M, "N": N, "K": K, "us": round(us, 2), "tflops": round(2 * M * N * K / us / 1e6, 1),
+                      "frac_833": round(2 * M * N * K / us / 1e6 / 833.3, 3), "err": err}), flush=True)
+    del A, B
+print(json.dumps({"total_us": round(tot, 1), "apre": os.environ.get("VAEVAR_H3_APRE", "1")}), flush=True)
