@@ -15,6 +15,8 @@ with the reference). `--config 3|4|5` selects the other BASELINE configs (Nit 10
            torch.distributed.run WORLD_SIZE must equal --gpus.
   config4 = every line also carries BASELINE config 4 (T = 6 window, one analysis per GPU, the RCCL gather),
            timed on its own after the main region, so its analyses/s can be compared across N as well.
+  --batch B = B independent analyses per GPU advanced in lockstep over ONE batched closure per evaluation (the
+           decoder / flow GEMMs on B x 2048 rows, vaevar.da.one_step_da_batch); value counts every analysis.
 
 Prints ONE JSON line on rank 0. See DESIGN.md §6.
 """
@@ -148,9 +150,10 @@ def gemm_traffic(kernel):
 # ---------------------------------------------------------------------------------------------------------------
 # per-rank workloads
 class GpuAnalyses:
-    """One rank's share: the HIP engine (libvaevar) on cuda:LOCAL_RANK."""
+    """One rank's share: the HIP engine (libvaevar) on cuda:LOCAL_RANK; `batch` analyses per GPU run in lockstep
+    over one batched closure (vaevar.da.one_step_da_batch) when batch > 1."""
 
-    def __init__(self, cfg_id: int, rank: int, local: int):
+    def __init__(self, cfg_id: int, rank: int, local: int, batch: int = 1):
         import torch
 
         from vaevar import config as C
@@ -161,32 +164,38 @@ class GpuAnalyses:
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
         self.cfg = CONFIGS[cfg_id]
-        self.T, self.nit = self.cfg["T"], self.cfg["nit"]
-        self.dec = LGUnet(C.DECODER, 1, 1, device=local).load_synthetic()
+        self.T, self.nit, self.batch = self.cfg["T"], self.cfg["nit"], batch
+        self.dec = LGUnet(C.DECODER, batch, 1, device=local).load_synthetic()
         self.flow = None
         Hs, Ws = self.cfg.get("grid", (128, 256))
-        self.prob_np = make_problem(nch=69, Hs=Hs, Ws=Ws, T=self.T, seed=20250620 + rank)
+        probs = [make_problem(nch=69, Hs=Hs, Ws=Ws, T=self.T, seed=20250620 + rank * batch + b) for b in range(batch)]
+        self.prob_np = probs[0]
         if self.T > 1:
-            self.flow = LGUnet(C.FLOW, 1, self.T - 1, device=local).load_synthetic()
-        self.prob = DAProblem(self.dec, self.prob_np, flow=self.flow, device=local)
+            self.flow = LGUnet(C.FLOW, batch, self.T - 1, device=local).load_synthetic()
+        self.prob = DAProblem(self.dec, probs if batch > 1 else probs[0], flow=self.flow, device=local)
         self.ctx = self.prob.ctx
         self._C, self._DAProblem, self._LGUnet, self._make_problem = C, DAProblem, LGUnet, make_problem
         self.rank, self.local = rank, local
 
     def analysis(self):
-        from vaevar.da import one_step_da
+        """One step: the rank's `batch` analyses to convergence; (xa of every analysis, iterations, evaluations)."""
+        from vaevar.da import one_step_da, one_step_da_batch
 
-        res = one_step_da(self.prob, nit=self.nit, log_terms=False)
-        return res["xa"], res["n_iter"], res["n_eval"]
+        if self.batch == 1:
+            res = one_step_da(self.prob, nit=self.nit, log_terms=False)
+            return res["xa"], res["n_iter"], res["n_eval"]
+        res = one_step_da_batch(self.prob, nit=self.nit)
+        return res["xa"], sum(res["n_iter"]), sum(res["n_eval"])
 
     def sync(self):
         self.torch.cuda.synchronize()
 
     def config4(self):
-        """Re-bind this rank to a config-4 problem (T = 6, five flow slots); returns the analysis runner."""
-        flow6 = self._LGUnet(self._C.FLOW, 1, 5, device=self.local).load_synthetic()
-        p6 = self._make_problem(nch=69, Hs=128, Ws=256, T=6, seed=20250620 + self.rank)
-        self.prob = self._DAProblem(self.dec, p6, flow=flow6, device=self.local)
+        """Re-bind this rank to config-4 problems (T = 6, five flow slots); returns the analysis runner."""
+        flow6 = self._LGUnet(self._C.FLOW, self.batch, 5, device=self.local).load_synthetic()
+        p6 = [self._make_problem(nch=69, Hs=128, Ws=256, T=6, seed=20250620 + self.rank * self.batch + b)
+              for b in range(self.batch)]
+        self.prob = self._DAProblem(self.dec, p6 if self.batch > 1 else p6[0], flow=flow6, device=self.local)
         self.flow, self.nit = flow6, CONFIGS[4]["nit"]
         return self.analysis
 
@@ -195,15 +204,16 @@ class SelftestAnalyses:
     """--selftest: a stand-in analysis with known outputs (CPU, no GPU) that exercises the launch, the gloo/RCCL
     collectives, the gather and the JSON aggregation of this script (tests/test_bench_launch.py)."""
 
-    def __init__(self, cfg_id: int, rank: int, local: int):
+    def __init__(self, cfg_id: int, rank: int, local: int, batch: int = 1):
         import torch
 
-        self.torch, self.rank = torch, rank
+        self.torch, self.rank, self.batch = torch, rank, batch
         self.T, self.nit = CONFIGS[cfg_id]["T"], CONFIGS[cfg_id]["nit"]
 
     def analysis(self):
         time.sleep(0.01 * (1 + self.rank))
-        return self.torch.full((69, 128, 256), float(self.rank)), 97 + self.rank, 110 + self.rank
+        shape = (69, 128, 256) if self.batch == 1 else (self.batch, 69, 128, 256)
+        return self.torch.full(shape, float(self.rank)), self.batch * (97 + self.rank), self.batch * (110 + self.rank)
 
     def sync(self):
         pass
@@ -242,6 +252,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel-class profile")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (T=6) line section")
     ap.add_argument("--no-exact-f32", action="store_true", help="skip the exact-f32 GEMM analysis")
+    ap.add_argument("--batch", type=int, default=1, help="independent analyses per GPU, evaluated in one batched "
+                                                         "closure (B x 2048-row GEMMs)")
     ap.add_argument("--selftest", action="store_true", help="CPU stand-in analyses (tests the launch/aggregation)")
     args = ap.parse_args()
 
@@ -257,7 +269,7 @@ def main():
 
     rank, size, local = ensemble.init("gloo" if args.selftest else None)
     Runner = SelftestAnalyses if args.selftest else GpuAnalyses
-    w = Runner(args.config, rank, local)
+    w = Runner(args.config, rank, local, args.batch)
     dev = None if args.selftest else w.dev
 
     for _ in range(args.warmup):
@@ -289,12 +301,16 @@ def main():
     # J before / after of the main problem (not timed)
     j_info = None
     if not args.selftest:
-        from vaevar.da import one_step_da
+        from vaevar.da import one_step_da, one_step_da_batch
 
-        res = one_step_da(w.prob, nit=w.nit, log_terms=False)
-        j_end = w.prob.closure(res["z"], None)
-        j_0 = w.prob.closure(torch.zeros_like(res["z"]), None)
-        j_info = (j_0[0] + j_0[1], j_end[0] + j_end[1])
+        # analysis 0 of this rank
+        if w.batch == 1:
+            res = one_step_da(w.prob, nit=w.nit, log_terms=False)
+        else:
+            res = one_step_da_batch(w.prob, nit=w.nit)
+        j_end = w.prob.closure_batch(res["z"], None)
+        j_0 = w.prob.closure_batch(torch.zeros_like(res["z"]), None)
+        j_info = (float(j_0[0][0] + j_0[1][0]), float(j_end[0][0] + j_end[1][0]))
 
     c4 = None
     if not args.no_config4 and args.config != 4:
@@ -311,7 +327,8 @@ def main():
         t4 = ensemble.reduce_scalar(time.perf_counter() - t0, "max", dev)
         it4 = ensemble.reduce_scalar(it4, "sum", dev)
         ev4 = ensemble.reduce_scalar(ev4, "sum", dev)
-        c4 = {"workload": CONFIGS[4]["name"], "n_gpus": size, "analyses": size, "analyses_per_s": size / t4,
+        c4 = {"workload": CONFIGS[4]["name"], "n_gpus": size, "analyses_per_gpu": args.batch,
+              "analyses": size * args.batch, "analyses_per_s": size * args.batch / t4,
               "iters_per_s": it4 / t4, "wall_clock_s": t4, "iters": it4, "evals": ev4,
               "gathered": [list(x.shape) for x in xs4] if xs4 is not None else None,
               "timed_region": "barrier + sync, one config-4 analysis per rank, RCCL gather of the analyses to rank 0, "
@@ -335,17 +352,19 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 (GEMMs: fp16x3 split, fp32-level error)",
         "data": "synthetic (counter-hash RNG weights and observations; the reference ships no checkpoints)",
-        "config": {"workload": cfg["name"], "analyses_per_gpu": 1, "T": cfg["T"], "nit": cfg["nit"],
-                   "parallelism": f"ensemble: {size} independent analyses, 1 per GPU, RCCL gather of xa per step"},
+        "config": {"workload": cfg["name"], "analyses_per_gpu": args.batch, "T": cfg["T"], "nit": cfg["nit"],
+                   "parallelism": f"ensemble: {size * args.batch} independent analyses, {args.batch} per GPU "
+                                  f"({'one batched closure' if args.batch > 1 else 'one closure each'}), RCCL gather "
+                                  "of xa per step"},
         "wall_clock_to_convergence_s": per_analysis,
         "iters": iters,
         "evals": evals,
-        "iters_per_analysis": iters / (size * args.steps),
+        "iters_per_analysis": iters / (size * args.steps * args.batch),
         "evals_per_s": evals / t_max,
         "ms_per_eval": 1e3 * t_max * size / max(evals, 1),
-        "analyses_per_s": size * args.steps / t_max,
+        "analyses_per_s": size * args.batch * args.steps / t_max,
         "gathered": [list(s) for s in shapes] if shapes else None,
-        "timed_region": f"barrier + sync, {args.steps} analyses per rank (z = 0, Nit = {cfg['nit']} outer lbfgs.step "
+        "timed_region": f"barrier + sync, {args.steps} step(s) of {args.batch} analyses per rank (z = 0, Nit = {cfg['nit']} outer lbfgs.step "
                         "calls, the analysis decode, at N > 1 the RCCL gather of every analysis to rank 0), sync + "
                         "barrier; max over ranks. The per-outer-pass logging evaluation cal_loss and WRMSE/Bias "
                         "(da_4dvar.py:1256-1269, SURVEY §8 a3; 1 forward per pass) is not run in it",
@@ -412,7 +431,7 @@ def main():
                 + (f", OMP_NUM_THREADS share {share}" if share else ""))
         evals_per_iter = evals / max(iters, 1)
         n_cpu = args.cpu_evals or (3 if cfg["T"] == 1 else 2)
-        per_eval, cb, cpu_conv = cpu_baseline(w.prob_np, cfg["T"], evals_per_iter, evals / max(args.steps, 1),
+        per_eval, cb, cpu_conv = cpu_baseline(w.prob_np, cfg["T"], evals_per_iter, evals / max(args.steps * args.batch, 1),
                                               n_cpu, threads, note)
         out["cpu_baseline"] = cb
         out["cpu_wall_clock_to_convergence_s_extrapolated"] = cpu_conv

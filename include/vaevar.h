@@ -93,19 +93,23 @@ int vv_model_workspace_bytes(vv_ctx* ctx, int model_id, int64_t* bytes);
 /* one_step_DA 'vae4dvar' problem: state (C,Hs,Ws), window of T times; flow_model_id < 0 when T == 1.
    When (Hs,Ws) differs from the network grid (e.g. 721x1440 vs 128x256) the decoder output and each forecast are
    nearest-up-sampled to the state grid and the forecast input nearest-down-sampled, as decoder_hr / integrate do.
-   xb (C,Hs,Ws); yo, Hmask, R (T,C,Hs,Ws); mean, std, std_tr (C). Buffers stay owned by the caller. */
+   B independent analyses (ensemble members / windows) are bound at once when the decoder model (and the flow model)
+   were created with batch B: every evaluation then runs ONE decoder launch sequence over the B latents (GEMMs of
+   B x 2048 rows) and one flow sequence per forecast step; each analysis keeps its own J.
+   xb (B,C,Hs,Ws); yo, Hmask, R (B,T,C,Hs,Ws); mean, std, std_tr (C). Buffers stay owned by the caller. */
 int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int C, int Hs, int Ws,
                     const float* xb, const float* yo, const float* Hmask, const float* R, const float* mean,
                     const float* std_, const float* std_tr, float obs_coeff);
-/* J = J_b + obs_coeff * J_o at latent z (1,32,128,256); grad_z = dJ/dz. Synchronises `stream`. */
+/* J = J_b + obs_coeff * J_o at latent z (B,32,128,256); grad_z = dJ/dz (B,32,128,256); J_b, J_o: B doubles each
+   (host), one per analysis. Synchronises `stream`. */
 int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream);
-/* same, leaving {J_b, J_o} in device memory d_J[2]; no synchronisation */
+/* same, leaving {J_b, J_o} per analysis in device memory d_J[2B]; no synchronisation */
 int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, void* stream);
 /* replay the closure from a hipGraph (default on; VAEVAR_GRAPH=0 at vv_ctx_create turns it off): the evaluation's
    ~540 kernel launches are captured once per kind (J only / J + gradient) and replayed as one graph launch, with z
    and grad_z copied through problem-owned buffers; results are bit-identical to the eager launches */
 int vv_set_closure_graph(vv_ctx* ctx, int enable);
-/* analysis state xa (C,Hs,Ws) */
+/* analysis states xa (B,C,Hs,Ws) */
 int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
 /* out = integrate(x, model, steps) (da_4dvar.py:666-681): z = (x - mean)/std (nearest to the model grid when
    (Hs,Ws) differs, interpolation=True); `steps` times z = model(z)[:, :C]; nearest back to (Hs,Ws); *std + mean.
@@ -128,7 +132,7 @@ int vv_obs_augment(vv_ctx* ctx, const float* interp, int n_out, int n_in, const 
    pred, gt (B,C,H,W); mean, std_ (C) fp32; scale (C) fp64; wrmse, bias (C) fp64 device. Synchronises `stream`. */
 int vv_metrics(vv_ctx* ctx, const float* pred, const float* gt, const float* mean, const float* std_,
                const double* scale, int B, int C, int H, int W, double* wrmse, double* bias, void* stream);
-/* trajectory x_t (T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
+/* trajectories x_t (B,T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
 int vv_state_ptr(vv_ctx* ctx, const float** x);
 
 /* vector primitives (n floats). Host-returning ones synchronise `stream`. */

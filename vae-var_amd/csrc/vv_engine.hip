@@ -250,7 +250,7 @@ struct Model {
 
 struct Problem {
   bool bound = false;
-  int dec = -1, flow = -1, T = 1, C = 0, Hs = 0, Ws = 0, Hl = 0, Wl = 0;
+  int dec = -1, flow = -1, B = 1, T = 1, C = 0, Hs = 0, Ws = 0, Hl = 0, Wl = 0;  // B analyses (the decoder's batch)
   bool interp = false;                 // state grid != network grid: nearest maps (quirk Q3)
   int *mi = nullptr, *mj = nullptr;    // state -> net (decoder_hr / integrate up-sampling)
   int *ri0 = nullptr, *rj0 = nullptr;  // net -> first state row/col mapping onto it (adjoint ranges)
@@ -266,7 +266,7 @@ struct Problem {
   // real-observation operator (vv_set_obs_operator): nout = 0 is the identity (synthetic observations)
   int nin = 0, nout = 0;
   std::unique_ptr<Arena> obs_arena;
-  float *Pobs = nullptr, *GOBS = nullptr;  // [nout][nin] ; (T,C,Hs,Ws) observation-term gradient
+  float *Pobs = nullptr, *GOBS = nullptr;  // [nout][nin] ; (B,T,C,Hs,Ws) observation-term gradient
   size_t obs_hw() const { return (size_t)(nout ? 4 + 5 * nout : C) * Hs * Ws; }  // floats per time of yo/Hm/R
 };
 
@@ -1004,21 +1004,21 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
 // ----------------------------------------------------------------------------
 // the observation term of time t under the real-observation operator (no-op for the identity operator):
 // J partials of slot t and the state-space gradient GOBS[t] (da_4dvar.py:1196-1207)
-hipError_t obs_term(const Problem& P, int t, hipStream_t st) {
+hipError_t obs_term(const Problem& P, int b, int t, hipStream_t st) {
   if (!P.nout) return hipSuccess;
-  const size_t HW = (size_t)P.Hs * P.Ws, OHW = P.obs_hw();
+  const size_t HW = (size_t)P.Hs * P.Ws, OHW = P.obs_hw(), bt = (size_t)b * P.T + t;
   ObsArgs oa;
   oa.nin = P.nin;
   oa.nout = P.nout;
   oa.HW = (int)HW;
   oa.P = P.Pobs;
-  oa.x = P.X + t * P.C * HW;
-  oa.yo = P.yo + t * OHW;
-  oa.Hm = P.Hm + t * OHW;
-  oa.R = P.R + t * OHW;
+  oa.x = P.X + bt * P.C * HW;
+  oa.yo = P.yo + bt * OHW;
+  oa.Hm = P.Hm + bt * OHW;
+  oa.R = P.R + bt * OHW;
   oa.coeff = P.obs_coeff;
-  oa.g_obs = P.GOBS + t * P.C * HW;
-  oa.partial = P.partial + (size_t)t * P.nblk;
+  oa.g_obs = P.GOBS + bt * P.C * HW;
+  oa.partial = P.partial + ((size_t)b * (P.T + 1) + t) * P.nblk;
   oa.nblk = P.nblk;
   return obs_misfit(oa, st);
 }
@@ -1030,13 +1030,22 @@ void set_maps(const Problem& P, MisfitArgs& m) {
   m.mj = P.interp ? P.mj : nullptr;
 }
 
+// B analyses per evaluation (the decoder's batch): one decoder launch sequence over all B, one flow launch
+// sequence per forecast step; the misfit / adjoint kernels run per analysis (each has its own J partials).
+// Layouts: X (B, T, C, Hs, Ws); decoder output / gradient (B, Cout, Hl, Wl); flow input FI[t] (B, C, Hl, Wl), flow
+// output FO[t] (B, Fcout, Hl, Wl); carry (B, C, Hs, Ws); J partials [b][t + J_b][nblk]; dJ[b] = {J_b, J_o}.
 int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   Problem& P = ctx->prob;
   if (!P.bound) return fail(VV_E_STATE, "vv_bind_problem first");
   Model& D = *ctx->models[P.dec];
   Model* F = P.flow >= 0 ? ctx->models[P.flow].get() : nullptr;
-  const int C = P.C, HW = P.Hs * P.Ws, HWl = P.Hl * P.Wl;
-  const size_t CHW = (size_t)C * HW, CHWl = (size_t)C * HWl;
+  const int C = P.C, HW = P.Hs * P.Ws, HWl = P.Hl * P.Wl, B = P.B, T = P.T;
+  const size_t CHW = (size_t)C * HW, CHWl = (size_t)C * HWl, OHW = P.obs_hw();
+  const size_t DO = (size_t)D.cfg.Cout * HWl, FO = F ? (size_t)F->cfg.Cout * HWl : 0;
+  const size_t zper = (size_t)D.cfg.Cin * D.cfg.Himg * D.cfg.Wimg;
+  auto part = [&](int b, int t) { return P.partial + ((size_t)b * (T + 1) + t) * P.nblk; };
+  auto X = [&](int b, int t) { return P.X + ((size_t)b * T + t) * CHW; };
+  auto FI = [&](int t, int b) { return P.FI + ((size_t)t * B + b) * CHWl; };
   int r;
   // forward: x_0 = decoder(z)*stdTr*std + xb
   if ((r = model_fwd(D, 0, z, P.dec_out, C, st))) return r;
@@ -1046,98 +1055,102 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   ma.Hs = P.Hs;
   ma.Ws = P.Ws;
   set_maps(P, ma);
-  ma.net = P.dec_out;
   ma.scale = P.std_tr;
   ma.scale2 = P.std_;
-  ma.xb = P.xb;
-  ma.yo = P.yo;
-  ma.Hm = P.Hm;
-  ma.R = P.R;
-  ma.x_out = P.X;
-  ma.flow_in = P.T > 1 ? P.FI : nullptr;
   ma.mean = P.mean;
   ma.std_ = P.std_;
-  ma.partial = P.partial;
   ma.nblk = P.nblk;
-  const size_t OHW = P.obs_hw();
-  if (P.nout) ma.Hm = nullptr;  // J from the observation operator below
-  CK(misfit_fwd(ma, st));
-  CK(obs_term(P, 0, st));
-  if (P.T > 1 && P.interp) CK(flow_input(P.X, P.FI, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
-  for (int t = 1; t < P.T; ++t) {
-    // x_t = integrate(x_{t-1}) = flow((x - mean)/std)[:C]*std + mean   (da_4dvar.py:666-681)
-    if ((r = model_fwd(*F, t - 1, P.FI + (t - 1) * CHWl, P.FO + (size_t)(t - 1) * F->cfg.Cout * HWl, C, st))) return r;
-    MisfitArgs mt = ma;
-    mt.net = P.FO + (size_t)(t - 1) * F->cfg.Cout * HWl;
-    mt.scale = P.std_;
-    mt.scale2 = nullptr;
-    mt.xb = nullptr;
-    mt.offset = P.mean;
-    mt.yo = P.yo + t * OHW;
-    mt.Hm = P.nout ? nullptr : P.Hm + t * OHW;
-    mt.R = P.R + t * OHW;
-    mt.x_out = P.X + t * CHW;
-    mt.flow_in = t < P.T - 1 ? P.FI + t * CHWl : nullptr;
-    mt.partial = P.partial + (size_t)t * P.nblk;
-    CK(misfit_fwd(mt, st));
-    CK(obs_term(P, t, st));
-    if (t < P.T - 1 && P.interp)
-      CK(flow_input(P.X + t * CHW, P.FI + t * CHWl, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
+  for (int b = 0; b < B; ++b) {
+    MisfitArgs m0 = ma;
+    m0.net = P.dec_out + b * DO;
+    m0.xb = P.xb + b * CHW;
+    m0.yo = P.yo + (size_t)b * T * OHW;
+    m0.Hm = P.nout ? nullptr : P.Hm + (size_t)b * T * OHW;  // J from the observation operator when set
+    m0.R = P.R + (size_t)b * T * OHW;
+    m0.x_out = X(b, 0);
+    m0.flow_in = T > 1 ? FI(0, b) : nullptr;
+    m0.partial = part(b, 0);
+    CK(misfit_fwd(m0, st));
+    CK(obs_term(P, b, 0, st));
+    if (T > 1 && P.interp)
+      CK(flow_input(X(b, 0), FI(0, b), P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
   }
-  CK(reduce_final(P.partial, P.nblk * P.T, P.dJ + 1, st));
-  CK(reduce_sumsq(z, (int64_t)D.B * D.cfg.Cin * D.cfg.Himg * D.cfg.Wimg, P.partial + (size_t)P.T * P.nblk, P.nblk, st));
-  CK(reduce_final(P.partial + (size_t)P.T * P.nblk, P.nblk, P.dJ, st));
+  for (int t = 1; t < T; ++t) {
+    // x_t = integrate(x_{t-1}) = flow((x - mean)/std)[:C]*std + mean   (da_4dvar.py:666-681)
+    float* fo = P.FO + (size_t)(t - 1) * B * FO;
+    if ((r = model_fwd(*F, t - 1, FI(t - 1, 0), fo, C, st))) return r;
+    for (int b = 0; b < B; ++b) {
+      MisfitArgs mt = ma;
+      mt.net = fo + b * FO;
+      mt.scale = P.std_;
+      mt.scale2 = nullptr;
+      mt.offset = P.mean;
+      mt.yo = P.yo + ((size_t)b * T + t) * OHW;
+      mt.Hm = P.nout ? nullptr : P.Hm + ((size_t)b * T + t) * OHW;
+      mt.R = P.R + ((size_t)b * T + t) * OHW;
+      mt.x_out = X(b, t);
+      mt.flow_in = t < T - 1 ? FI(t, b) : nullptr;
+      mt.partial = part(b, t);
+      CK(misfit_fwd(mt, st));
+      CK(obs_term(P, b, t, st));
+      if (t < T - 1 && P.interp)
+        CK(flow_input(X(b, t), FI(t, b), P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
+    }
+  }
+  for (int b = 0; b < B; ++b) {
+    CK(reduce_final(part(b, 0), P.nblk * T, P.dJ + 2 * b + 1, st));
+    CK(reduce_sumsq(z + b * zper, (int64_t)zper, part(b, T), P.nblk, st));
+    CK(reduce_final(part(b, T), P.nblk, P.dJ + 2 * b, st));
+  }
   if (!grad) return 0;
   // backward
-  const float* carry = nullptr;
-  for (int t = P.T - 1; t >= 1; --t) {
-    MisfitBwdArgs mb;
-    memset(&mb, 0, sizeof(mb));
-    mb.C = C;
-    mb.Hs = P.Hs;
-    mb.Ws = P.Ws;
-    mb.Hl = P.Hl;
-    mb.Wl = P.Wl;
-    mb.ri0 = P.interp ? P.ri0 : nullptr;
-    mb.rj0 = P.interp ? P.rj0 : nullptr;
-    mb.x = P.X + t * CHW;
-    mb.yo = P.yo + t * OHW;
-    mb.Hm = P.Hm + t * OHW;
-    mb.R = P.R + t * OHW;
-    mb.g_obs = P.nout ? P.GOBS + t * CHW : nullptr;
-    mb.g_carry = carry;
-    mb.coeff = P.obs_coeff;
-    mb.scale = P.std_;
-    mb.g_net = P.GFO;
-    mb.net_cstride = F->cfg.Cout;
-    CK(misfit_bwd(mb, st));
+  MisfitBwdArgs mb0;
+  memset(&mb0, 0, sizeof(mb0));
+  mb0.C = C;
+  mb0.Hs = P.Hs;
+  mb0.Ws = P.Ws;
+  mb0.Hl = P.Hl;
+  mb0.Wl = P.Wl;
+  mb0.ri0 = P.interp ? P.ri0 : nullptr;
+  mb0.rj0 = P.interp ? P.rj0 : nullptr;
+  mb0.coeff = P.obs_coeff;
+  bool carry = false;
+  for (int t = T - 1; t >= 1; --t) {
+    for (int b = 0; b < B; ++b) {
+      MisfitBwdArgs mb = mb0;
+      mb.x = X(b, t);
+      mb.yo = P.yo + ((size_t)b * T + t) * OHW;
+      mb.Hm = P.Hm + ((size_t)b * T + t) * OHW;
+      mb.R = P.R + ((size_t)b * T + t) * OHW;
+      mb.g_obs = P.nout ? P.GOBS + ((size_t)b * T + t) * CHW : nullptr;
+      mb.g_carry = carry ? P.carry + b * CHW : nullptr;
+      mb.scale = P.std_;
+      mb.g_net = P.GFO + b * FO;
+      mb.net_cstride = F->cfg.Cout;
+      CK(misfit_bwd(mb, st));
+    }
     if ((r = model_bwd(*F, t - 1, P.GFO, P.GFI, nullptr, C, st))) return r;
-    if (P.interp)
-      CK(flow_input_adjoint(P.GFI, P.carry, P.di, P.dj, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
-    else
-      CK(scale_channels(P.GFI, P.carry, P.std_, C, HW, nullptr, st));
-    carry = P.carry;
+    for (int b = 0; b < B; ++b) {
+      if (P.interp)
+        CK(flow_input_adjoint(P.GFI + b * CHWl, P.carry + b * CHW, P.di, P.dj, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
+      else
+        CK(scale_channels(P.GFI + b * CHWl, P.carry + b * CHW, P.std_, C, HW, nullptr, st));
+    }
+    carry = true;
   }
-  MisfitBwdArgs mb;
-  memset(&mb, 0, sizeof(mb));
-  mb.C = C;
-  mb.Hs = P.Hs;
-  mb.Ws = P.Ws;
-  mb.Hl = P.Hl;
-  mb.Wl = P.Wl;
-  mb.ri0 = P.interp ? P.ri0 : nullptr;
-  mb.rj0 = P.interp ? P.rj0 : nullptr;
-  mb.x = P.X;
-  mb.yo = P.yo;
-  mb.Hm = P.Hm;
-  mb.R = P.R;
-  mb.g_obs = P.nout ? P.GOBS : nullptr;
-  mb.g_carry = carry;
-  mb.coeff = P.obs_coeff;
-  mb.scale = P.prod;
-  mb.g_net = P.gdec;
-  mb.net_cstride = D.cfg.Cout;
-  CK(misfit_bwd(mb, st));
+  for (int b = 0; b < B; ++b) {
+    MisfitBwdArgs mb = mb0;
+    mb.x = X(b, 0);
+    mb.yo = P.yo + (size_t)b * T * OHW;
+    mb.Hm = P.Hm + (size_t)b * T * OHW;
+    mb.R = P.R + (size_t)b * T * OHW;
+    mb.g_obs = P.nout ? P.GOBS + (size_t)b * T * CHW : nullptr;
+    mb.g_carry = carry ? P.carry + b * CHW : nullptr;
+    mb.scale = P.prod;
+    mb.g_net = P.gdec + b * DO;
+    mb.net_cstride = D.cfg.Cout;
+    CK(misfit_bwd(mb, st));
+  }
   // grad_z = z + decoder^T(g)   (d/dz of sum(z^2)/2 is z)
   if ((r = model_bwd(D, 0, P.gdec, grad, z, C, st))) return r;
   return 0;
@@ -1147,11 +1160,8 @@ __global__ void k_prod(const float* a, const float* b, float* o, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) o[i] = a[i] * b[i];
 }
-__global__ void k_half(double* d) {
-  if (threadIdx.x == 0) {
-    d[0] *= 0.5;
-    d[1] *= 0.5;
-  }
+__global__ void k_half(double* d, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] *= 0.5;
 }
 
 }  // namespace
@@ -1160,9 +1170,9 @@ namespace {
 int closure_enqueue(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hipStream_t st) {
   int r;
   if ((r = closure_impl(ctx, z, grad_z, st))) return r;
-  hipLaunchKernelGGL(k_half, dim3(1), dim3(64), 0, st, ctx->prob.dJ);
+  hipLaunchKernelGGL(k_half, dim3(1), dim3(64), 0, st, ctx->prob.dJ, 2 * ctx->prob.B);
   VV_HIP(hipGetLastError());
-  if (d_J) VV_HIP(hipMemcpyAsync(d_J, ctx->prob.dJ, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
+  if (d_J) VV_HIP(hipMemcpyAsync(d_J, ctx->prob.dJ, 2 * ctx->prob.B * sizeof(double), hipMemcpyDeviceToDevice, st));
   return 0;
 }
 
@@ -1207,7 +1217,7 @@ int closure_graphed(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hip
     VV_HIP(hipGraphLaunch(g.exec, st));
   }
   if (grad_z) VV_HIP(hipMemcpyAsync(grad_z, P.GZ, P.zn * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if (d_J) VV_HIP(hipMemcpyAsync(d_J, P.dJ, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
+  if (d_J) VV_HIP(hipMemcpyAsync(d_J, P.dJ, 2 * P.B * sizeof(double), hipMemcpyDeviceToDevice, st));
   return 0;
 }
 
@@ -1421,7 +1431,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   if (D->fm || (flow_model_id >= 0 && get_model(ctx, flow_model_id) && get_model(ctx, flow_model_id)->fm))
     return fail(VV_E_ARG, "the closure needs differentiable networks_old LGUnet_all models");
   if (T < 1 || C < 1) return fail(VV_E_ARG, "bad T/C");
-  if (D->B != 1) return fail(VV_E_ARG, "closure needs a batch-1 decoder");
+
   if (D->cfg.Cout < C) return fail(VV_E_ARG, "decoder produces %d channels < C=%d", D->cfg.Cout, C);
   if (Hs < D->cfg.Himg || Ws < D->cfg.Wimg)
     return fail(VV_E_ARG, "state grid %dx%d coarser than the network grid %dx%d", Hs, Ws, D->cfg.Himg, D->cfg.Wimg);
@@ -1429,9 +1439,9 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   if (T > 1) {
     F = get_model(ctx, flow_model_id);
     if (!F) return fail(VV_E_ARG, "T > 1 needs a flow model");
-    if (F->cfg.Cin != C || F->cfg.Cout < C || F->nslots < T - 1 || F->B != 1)
-      return fail(VV_E_ARG, "flow model shape/slots incompatible (Cin %d Cout %d slots %d)", F->cfg.Cin, F->cfg.Cout,
-                  F->nslots);
+    if (F->cfg.Cin != C || F->cfg.Cout < C || F->nslots < T - 1 || F->B != D->B)
+      return fail(VV_E_ARG, "flow model shape/slots/batch incompatible (Cin %d Cout %d slots %d batch %d vs %d)",
+                  F->cfg.Cin, F->cfg.Cout, F->nslots, F->B, D->B);
     if (F->cfg.Himg != D->cfg.Himg || F->cfg.Wimg != D->cfg.Wimg) return fail(VV_E_ARG, "flow grid mismatch");
   }
   if (!xb || !yo || !Hmask || !R || !mean || !std_ || !std_tr) return fail(VV_E_ARG, "null problem buffer");
@@ -1442,6 +1452,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   P = Problem();
   P.dec = dec_model_id;
   P.flow = T > 1 ? flow_model_id : -1;
+  P.B = D->B;
   P.T = T;
   P.C = C;
   P.Hs = Hs;
@@ -1461,26 +1472,27 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   const size_t HWl = (size_t)P.Hl * P.Wl;
   const size_t CHWl = (size_t)C * HWl;
   const int fcout = F ? F->cfg.Cout : 0;
+  const size_t B = (size_t)P.B;
   for (int pass = 0; pass < 2; ++pass) {
     Planner pl;
     if (pass) pl.base = P.arena->base;
-    P.X = pl.f(CHW * T);
-    P.dec_out = pl.f((size_t)D->cfg.Cout * HWl);
-    P.gdec = pl.f((size_t)D->cfg.Cout * HWl);
+    P.X = pl.f(B * CHW * T);
+    P.dec_out = pl.f(B * D->cfg.Cout * HWl);
+    P.gdec = pl.f(B * D->cfg.Cout * HWl);
     P.prod = pl.f(C);
-    P.FI = pl.f(CHWl * std::max(T - 1, 1));
-    P.FO = pl.f((size_t)fcout * HWl * std::max(T - 1, 1) + 1);
-    P.GFO = pl.f((size_t)fcout * HWl + 1);
-    P.GFI = pl.f(CHWl);
-    P.carry = pl.f(CHW);
-    P.zn = (size_t)D->B * D->cfg.Cin * D->cfg.Himg * D->cfg.Wimg;
+    P.FI = pl.f(B * CHWl * std::max(T - 1, 1));
+    P.FO = pl.f(B * fcout * HWl * std::max(T - 1, 1) + 1);
+    P.GFO = pl.f(B * fcout * HWl + 1);
+    P.GFI = pl.f(B * CHWl);
+    P.carry = pl.f(B * CHW);
+    P.zn = B * D->cfg.Cin * D->cfg.Himg * D->cfg.Wimg;
     P.Z = pl.f(P.zn);
     P.GZ = pl.f(P.zn);
     float* maps = pl.f((size_t)Hs + Ws + 2 * (P.Hl + 1) + 2 * (P.Wl + 1));
-    double* pd = reinterpret_cast<double*>(pl.f((size_t)2 * P.nblk * (T + 1) + 8));
+    double* pd = reinterpret_cast<double*>(pl.f(2 * (B * P.nblk * (T + 1) + 2 * B + 8)));
     if (pass) {
       P.partial = pd;
-      P.dJ = pd + (size_t)P.nblk * (T + 1) + 2;
+      P.dJ = pd + B * P.nblk * (T + 1) + 2;
       int* mp = reinterpret_cast<int*>(maps);
       P.mi = mp;
       P.mj = P.mi + Hs;
@@ -1532,12 +1544,15 @@ int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, vo
 int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream) {
   int r = vv_closure_async(ctx, z, grad_z, nullptr, stream);
   if (r) return r;
-  double h[2];
+  const int B = ctx->prob.B;
+  std::vector<double> h(2 * B);
   hipStream_t st = (hipStream_t)stream;
-  VV_HIP(hipMemcpyAsync(h, ctx->prob.dJ, sizeof(h), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipMemcpyAsync(h.data(), ctx->prob.dJ, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
   VV_HIP(hipStreamSynchronize(st));
-  if (J_b) *J_b = h[0];
-  if (J_o) *J_o = h[1];
+  for (int b = 0; b < B; ++b) {
+    if (J_b) J_b[b] = h[2 * b];
+    if (J_o) J_o[b] = h[2 * b + 1];
+  }
   return 0;
 }
 
@@ -1556,18 +1571,20 @@ int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream) {
   ma.Hs = P.Hs;
   ma.Ws = P.Ws;
   set_maps(P, ma);
-  ma.net = P.dec_out;
   ma.scale = P.std_tr;
   ma.scale2 = P.std_;
-  ma.xb = P.xb;
   ma.yo = P.yo;
-  ma.Hm = P.Hm;
   ma.R = P.R;
   ma.Hm = nullptr;  // the analysis only: no misfit
-  ma.x_out = xa;
   ma.partial = P.partial;
   ma.nblk = P.nblk;
-  CK(misfit_fwd(ma, st));
+  const size_t CHW = (size_t)P.C * P.Hs * P.Ws;
+  for (int b = 0; b < P.B; ++b) {
+    ma.net = P.dec_out + (size_t)b * D.cfg.Cout * P.Hl * P.Wl;
+    ma.xb = P.xb + b * CHW;
+    ma.x_out = xa + b * CHW;
+    CK(misfit_fwd(ma, st));
+  }
   return 0;
 }
 
@@ -1589,7 +1606,7 @@ int vv_set_obs_operator(vv_ctx* ctx, int n_out, int n_in, const float* interp) {
   const size_t CHW = (size_t)P.C * P.Hs * P.Ws;
   const size_t nP = Arena::up((size_t)n_out * n_in * sizeof(float));
   P.obs_arena = std::make_unique<Arena>();
-  P.obs_arena->cap = nP + CHW * P.T * sizeof(float);
+  P.obs_arena->cap = nP + CHW * P.T * P.B * sizeof(float);
   if (hipMalloc(&P.obs_arena->base, P.obs_arena->cap) != hipSuccess) return fail(VV_E_ALLOC, "observation operator");
   P.Pobs = reinterpret_cast<float*>(P.obs_arena->base);
   P.GOBS = reinterpret_cast<float*>(P.obs_arena->base + nP);

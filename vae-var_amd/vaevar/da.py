@@ -59,3 +59,53 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
     n_iter = opt.state["n_iter"] if optimizer == "lbfgs" else opt.t
     return {"xa": xa, "z": z, "J": js, "n_eval": prob.n_evals - n0 - n_log, "n_iter": n_iter,
             "seconds": time.time() - t0, "metrics": ms}
+
+
+def one_step_da_batch(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10):
+    """B independent one_step_DA analyses (da_4dvar.py:1179-1306) in lockstep over one batched closure: each
+    analysis b runs its own L-BFGS mirror on its latent z[b]; whenever every unfinished analysis has requested an
+    evaluation, ONE vv_closure evaluates all B latents (the GEMMs of the decoder / flow run on B x 2048 rows) and
+    each optimiser resumes with its own J and gradient. Analyses that have finished keep their final latent in
+    the batch (their results are not used). Returns dict(xa (B,C,Hs,Ws), z, n_eval per analysis, n_iter per
+    analysis, batched_evals, seconds)."""
+    dev = prob.xb.device
+    B = prob.B
+    Z = torch.zeros(prob.latent_shape, device=dev, dtype=torch.float32)
+    G = torch.empty_like(Z)
+    ctx = prob.ctx
+    opts = [LBFGS(ctx, Z[b], lr=1, history_size=history_size, max_iter=max_iter, line_search_fn="strong_wolfe")
+            for b in range(B)]
+
+    def run(opt):
+        for _ in range(nit):
+            yield from opt.step_gen()
+
+    t0 = time.time()
+    gens = [run(o) for o in opts]
+    pending = [None] * B
+    active = [True] * B
+    n_eval = [0] * B
+    for b in range(B):
+        try:
+            pending[b] = next(gens[b])
+        except StopIteration:
+            active[b] = False
+    batched = 0
+    while any(active):
+        jb, jo = prob.closure_batch(Z, G)
+        batched += 1
+        for b in range(B):
+            if not active[b]:
+                continue
+            zb, gb = pending[b]
+            ctx.copy(gb, G[b])
+            n_eval[b] += 1
+            try:
+                pending[b] = gens[b].send(prob.loss_f32(jb[b], jo[b]))
+            except StopIteration:
+                active[b] = False
+    xa = prob.analysis(Z)
+    torch.cuda.synchronize()
+    return {"xa": xa, "z": Z, "n_eval": n_eval, "n_iter": [o.state["n_iter"] for o in opts],
+            "batched_evals": batched, "seconds": time.time() - t0}
+

@@ -262,14 +262,26 @@ class VAE_lr:
 
 
 class DAProblem:
-    """The vae4dvar closure (da_4dvar.py:1183-1208) bound to device buffers; evaluated by libvaevar."""
+    """The vae4dvar closure (da_4dvar.py:1183-1208) bound to device buffers; evaluated by libvaevar.
 
-    def __init__(self, dec: LGUnet, prob: dict, flow: LGUnet | None = None, obs_coeff: float = 1.0, device: int = 0,
+    With a decoder (and flow model) of batch B > 1 the problem holds B independent analyses: xb (B,C,Hs,Ws) and
+    yo, H, R (B,T,C,Hs,Ws) — or pass a list of B single-analysis problem dicts — and one evaluation runs all B
+    (closure_batch: J per analysis)."""
+
+    def __init__(self, dec: LGUnet, prob, flow: LGUnet | None = None, obs_coeff: float = 1.0, device: int = 0,
                  obs_interp=None):
         """obs_interp: None (synthetic observations of the state) or the (n_out, n_in) obs_interpolater.interp of
         obs_type 'real*' (da_4dvar.py:1196-1206); `prob["interp"]` is used when present. yo, H, R then hold
         4 + 5*n_out observation channels."""
         dev = torch.device("cuda", device)
+        self.B = dec.batch
+        if isinstance(prob, (list, tuple)):
+            if len(prob) != self.B:
+                raise ValueError(f"{len(prob)} problems for a decoder of batch {self.B}")
+            stacked = {k: np.stack([np.asarray(p[k], np.float32) for p in prob]) for k in ("xb", "yo", "H", "R")}
+            prob = dict(prob[0], **stacked)
+        elif self.B > 1 and np.ndim(prob["xb"]) != 4:
+            raise ValueError("a batched problem needs xb (B,C,Hs,Ws) and yo/H/R (B,T,C,Hs,Ws)")
 
         def t(a):
             if isinstance(a, torch.Tensor):
@@ -278,19 +290,25 @@ class DAProblem:
 
         self.xb, self.yo, self.H, self.R = t(prob["xb"]), t(prob["yo"]), t(prob["H"]), t(prob["R"])
         self.mean, self.std, self.std_tr = t(prob["mean"]), t(prob["std"]), t(prob["std_tr"])
-        self.T, self.C = self.yo.shape[0], self.xb.shape[0]
-        self.Hs, self.Ws = self.xb.shape[1:]
+        if self.B > 1:
+            if self.xb.shape[0] != self.B or self.yo.shape[0] != self.B:
+                raise ValueError(f"leading dimension of xb/yo must be the batch {self.B}")
+            self.T, self.C = self.yo.shape[1], self.xb.shape[1]
+        else:
+            self.T, self.C = self.yo.shape[0], self.xb.shape[0]
+        self.Hs, self.Ws = self.xb.shape[-2:]
         self.dec, self.flow, self.obs_coeff = dec, flow, float(obs_coeff)
         self.ctx = dec.ctx
-        self.latent_shape = (1, dec.in_ch, dec.H, dec.W)
+        self.latent_shape = (self.B, dec.in_ch, dec.H, dec.W)
         if obs_interp is None:
             obs_interp = prob.get("interp")
         self.interp = None if obs_interp is None else t(obs_interp)
+        ych = self.yo.shape[-3]
         if self.interp is not None:
             n_out, n_in = self.interp.shape
-            if self.yo.shape[1] != 4 + 5 * n_out:
-                raise ValueError(f"yo has {self.yo.shape[1]} channels, the operator gives {4 + 5 * n_out}")
-        elif self.yo.shape[1] != self.C:
+            if ych != 4 + 5 * n_out:
+                raise ValueError(f"yo has {ych} channels, the operator gives {4 + 5 * n_out}")
+        elif ych != self.C:
             raise ValueError("yo/H/R channels differ from the state's: pass the observation operator (obs_interp)")
         fid = flow.id if flow is not None else -1
         check(lib.vv_bind_problem(self.ctx.h, dec.id, fid, self.T, self.C, self.Hs, self.Ws, _ptr(self.xb),
@@ -300,31 +318,41 @@ class DAProblem:
             check(lib.vv_set_obs_operator(self.ctx.h, n_out, n_in, _ptr(self.interp)), "set_obs_operator")
         self.n_evals = 0
 
-    def closure(self, z: torch.Tensor, grad: torch.Tensor | None):
-        """Returns (J_b, J_o) as Python floats (double sums); grad <- dJ/dz if given."""
-        jb, jo = ctypes.c_double(), ctypes.c_double()
+    def closure_batch(self, z: torch.Tensor, grad: torch.Tensor | None):
+        """One evaluation of all B analyses: (J_b[B], J_o[B]) as float64 arrays; grad <- dJ/dz (B,...) if given."""
+        jb, jo = (ctypes.c_double * self.B)(), (ctypes.c_double * self.B)()
         gp = _ptr(grad) if grad is not None else None
-        check(lib.vv_closure(self.ctx.h, _ptr(z), gp, ctypes.byref(jb), ctypes.byref(jo), _stream()), "closure")
+        check(lib.vv_closure(self.ctx.h, _ptr(z), gp, jb, jo, _stream()), "closure")
         self.n_evals += 1
-        return jb.value, jo.value
+        return np.array(jb[:], np.float64), np.array(jo[:], np.float64)
+
+    def closure(self, z: torch.Tensor, grad: torch.Tensor | None):
+        """Returns (J_b, J_o) as Python floats (double sums); grad <- dJ/dz if given. Single analysis (B = 1)."""
+        if self.B != 1:
+            raise ValueError("batched problem: use closure_batch")
+        jb, jo = self.closure_batch(z, grad)
+        return float(jb[0]), float(jo[0])
 
     def loss_f32(self, jb: float, jo: float) -> float:
         """loss_reg + obs_coeff * loss_obs with the reference's fp32 scalar arithmetic (quirk Q7)."""
         return float(np.float32(jb) + np.float32(np.float32(self.obs_coeff) * np.float32(jo)))
 
     def analysis(self, z: torch.Tensor) -> torch.Tensor:
-        xa = torch.empty(self.C, self.Hs, self.Ws, device=z.device, dtype=torch.float32)
-        check(lib.vv_decode(self.ctx.h, _ptr(z), _ptr(xa), _stream()), "decode")
+        """xa (C,Hs,Ws), or (B,C,Hs,Ws) for a batched problem."""
+        shape = (self.C, self.Hs, self.Ws) if self.B == 1 else (self.B, self.C, self.Hs, self.Ws)
+        xa = torch.empty(shape, device=z.device, dtype=torch.float32)
+        check(lib.vv_decode(self.ctx.h, _ptr(z.contiguous()), _ptr(xa), _stream()), "decode")
         return xa
 
     def trajectory(self) -> torch.Tensor:
-        """x_t (T,C,Hs,Ws) of the last closure (a copy)."""
+        """x_t (T,C,Hs,Ws) of the last closure (a copy); (B,T,C,Hs,Ws) for a batched problem."""
         p = ctypes.c_void_p()
         check(lib.vv_state_ptr(self.ctx.h, ctypes.byref(p)), "state_ptr")
-        n = self.T * self.C * self.Hs * self.Ws
+        n = self.B * self.T * self.C * self.Hs * self.Ws
         out = torch.empty(n, device=self.xb.device, dtype=torch.float32)
         check(lib.vv_copy(self.ctx.h, _ptr(out), p, n, _stream()), "copy")
-        return out.view(self.T, self.C, self.Hs, self.Ws)
+        shape = (self.T, self.C, self.Hs, self.Ws) if self.B == 1 else (self.B, self.T, self.C, self.Hs, self.Ws)
+        return out.view(shape)
 
 
 class _ClosureFn(torch.autograd.Function):

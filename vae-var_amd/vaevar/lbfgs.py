@@ -8,6 +8,10 @@ Vectors (1,048,576 floats for the 32x128x256 latent) stay in HBM and every vecto
 Scalar types follow torch's promotion rules (quirk Q7): quantities that are 0-d fp32 tensors in
 torch (dot products, ys, ro, H_diag, al, be, gtd, ...) are numpy float32 here (numpy 2 treats
 Python floats as weak scalars exactly like torch), the loss is a Python float.
+
+Every closure evaluation is a `yield (z, grad_out)` of the generator `step_gen()` that receives the loss, so B
+independent optimisers can be advanced in lockstep over one batched closure (vaevar.da.one_step_da_batch);
+`step(closure)` drives the same generator with a plain closure.
 """
 from __future__ import annotations
 
@@ -71,19 +75,19 @@ class LBFGS:
     def _add_grad(self, step_size, update):
         self.ctx.axpy(self.z, update, float(step_size))
 
-    def _directional_evaluate(self, closure, x, t, d):
-        # lbfgs.py:325-331
+    def _directional_evaluate(self, x, t, d):
+        # lbfgs.py:325-331 (a generator: the evaluation is a yield)
         self._add_grad(t, d)
         g = self._new()
-        loss = float(closure(self.z, g))
+        loss = float((yield self.z, g))
         self.ctx.copy(self.z, x)
         return loss, g
 
-    def _strong_wolfe(self, obj_func, x, t, d, f, g, gtd, c1=1e-4, c2=0.9, tolerance_change=1e-9, max_ls=25):
+    def _strong_wolfe(self, x, t, d, f, g, gtd, c1=1e-4, c2=0.9, tolerance_change=1e-9, max_ls=25):
         # lbfgs.py:40-209
         d_norm = self._absmax(d)
         g = g.clone()
-        f_new, g_new = obj_func(x, t, d)
+        f_new, g_new = yield from self._directional_evaluate(x, t, d)
         ls_func_evals = 1
         gtd_new = self._dot(g_new, d)
         t_prev, f_prev, g_prev, gtd_prev = 0, f, g, gtd
@@ -107,7 +111,7 @@ class LBFGS:
             tmp = t
             t = _cubic_interpolate(t_prev, f_prev, gtd_prev, t, f_new, gtd_new, bounds=(min_step, max_step))
             t_prev, f_prev, g_prev, gtd_prev = tmp, f_new, g_new.clone(), gtd_new
-            f_new, g_new = obj_func(x, t, d)
+            f_new, g_new = yield from self._directional_evaluate(x, t, d)
             ls_func_evals += 1
             gtd_new = self._dot(g_new, d)
             ls_iter += 1
@@ -133,7 +137,7 @@ class LBFGS:
                     insuf_progress = True
             else:
                 insuf_progress = False
-            f_new, g_new = obj_func(x, t, d)
+            f_new, g_new = yield from self._directional_evaluate(x, t, d)
             ls_func_evals += 1
             gtd_new = self._dot(g_new, d)
             ls_iter += 1
@@ -159,12 +163,22 @@ class LBFGS:
         return bracket_f[low_pos], bracket_g[low_pos], t, ls_func_evals
 
     def step(self, closure):
-        # lbfgs.py:333-535
+        """One optimizer step (lbfgs.py:333-535); closure(z, grad_out) -> loss."""
+        gen = self.step_gen()
+        try:
+            req = next(gen)
+            while True:
+                req = gen.send(closure(*req))
+        except StopIteration as e:
+            return e.value
+
+    def step_gen(self):
+        # lbfgs.py:333-535; every closure evaluation is `loss = yield (z, grad_out)`
         lr, max_iter, max_eval = self.lr, self.max_iter, self.max_eval
         tolerance_grad, tolerance_change = self.tolerance_grad, self.tolerance_change
         state = self.state
         flat_grad = self._new()
-        orig_loss = closure(self.z, flat_grad)
+        orig_loss = yield self.z, flat_grad
         loss = float(orig_loss)
         current_evals = 1
         state["func_evals"] += 1
@@ -234,23 +248,19 @@ class LBFGS:
                 if self.line_search_fn != "strong_wolfe":
                     raise RuntimeError("only 'strong_wolfe' is supported")
                 x_init = self.z.clone()
-
-                def obj_func(x, t, d):
-                    return self._directional_evaluate(closure, x, t, d)
-
                 if self.replay:
                     t, ls_func_evals = self.replay.pop(0)
-                    loss, flat_grad = obj_func(x_init, t, d)
+                    loss, flat_grad = yield from self._directional_evaluate(x_init, t, d)
                 else:
-                    loss, flat_grad, t, ls_func_evals = self._strong_wolfe(obj_func, x_init, t, d, loss, flat_grad,
-                                                                           gtd, max_ls=max_eval - current_evals)
+                    loss, flat_grad, t, ls_func_evals = yield from self._strong_wolfe(
+                        x_init, t, d, loss, flat_grad, gtd, max_ls=max_eval - current_evals)
                 self._add_grad(t, d)
                 opt_cond = self._absmax(flat_grad) <= tolerance_grad
             else:
                 self._add_grad(t, d)
                 if n_iter != max_iter:
                     flat_grad = self._new()
-                    loss = float(closure(self.z, flat_grad))
+                    loss = float((yield self.z, flat_grad))
                     opt_cond = self._absmax(flat_grad) <= tolerance_grad
                     ls_func_evals = 1
             current_evals += ls_func_evals
