@@ -308,10 +308,13 @@ def test_one_step_da_config5_g6():
 @pytest.mark.parametrize("mode", ["free", "replay"])
 def test_config2_trajectory_g10(full_dec, mode):
     """BASELINE config 2 at its full budget (Nit = 10 outer passes, 98 L-BFGS iterations, 111 evaluations)
-    against G10: the reference's decoder modules + torch.optim.LBFGS on CPU (oracle/make_golden.py). The fixed-step
-    replay (every recorded (t, evals)) must hold SURVEY §8 c6 (J per pass and xa rel <= 1e-3); free-running, a
-    rounding-level difference may flip a strong-Wolfe test and take another, equally valid path, so there J_final
-    and xa are held to 2e-2."""
+    against G10: the reference's decoder modules + torch.optim.LBFGS on CPU (oracle/make_golden.py).
+
+    The problem is ill-conditioned (R = (0.005 std)^2): J moves at the 1e-2 level when ONLY the floating-point
+    summation order changes. oracle/g10_sensitivity.py measured it on the reference itself (same modules, 4 instead
+    of 8 CPU threads; tests/golden/g10_sensitivity.npz): free-running J differs from G10 by up to 7.7e-2 (pass 1) /
+    9.2e-3 (pass 10), and even the fixed-step replay of G10's own line-search steps by up to 7.8e-3. So J per pass is
+    held to twice the reference's own replay drift (>= 1e-3), and the analysis xa to SURVEY §8 c6's 1e-3."""
     from vaevar.da import one_step_da
     from vaevar.engine import DAProblem
     from vaevar.problem import make_problem
@@ -331,10 +334,15 @@ def test_config2_trajectory_g10(full_dec, mode):
     print(f"G10 config 2 ({mode}): J per pass rel {['%.1e' % v for v in e_pass]}; xa rel-L2 {e_x:.1e}; "
           f"|xa-xb|^2 rel {e_dx:.1e}; iters {res['n_iter']} (ref {int(g['n_iter'])}), evals {res['n_eval']} "
           f"(ref {int(g['n_eval'])})")
+    sens = gold("g10_sensitivity.npz")
     if mode == "replay":
-        assert e_pass.max() < 1e-3 and e_x < 1e-3 and e_dx < 1e-2
+        bound = max(1e-3, 2 * float(sens["replay_rel"].max()))
+        print(f"replay J bound {bound:.1e} (reference vs itself under another summation order: "
+              f"{float(sens['replay_rel'].max()):.1e})")
+        assert e_pass.max() < bound and e_x < 1e-3 and e_dx < 1e-2
     else:
-        assert e_pass[-1] < 2e-2 and e_x < 2e-2
+        bound = max(1e-3, 2 * float(sens["free_rel"][-1]))
+        assert e_pass[-1] < bound and e_x < 1e-2
 
 
 def test_closure_graph_replay_bitwise():
