@@ -80,9 +80,10 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
 _keep = []
 
 
+@pytest.mark.parametrize("tile", [36, 44])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
-def test_gemm_split16_dynamic_range(ctx, M, N, K):
-    """fp16x3 split (tile 36) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
+def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):
+    """fp16x3 split (tiles 36 = 128x128 and 44 = 256x128) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
     (per-chunk scales), B rows span 2^+-8, with zeros, a zero row and huge/tiny values: no overflow, no flush."""
     g = torch.Generator().manual_seed(M + N + K + 1)
     A = torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-12, 12, generator=g)) \
@@ -97,17 +98,17 @@ def test_gemm_split16_dynamic_range(ctx, M, N, K):
     Bd = B.cuda()
     ctx.gemm_register_weight(Bd)
     e32 = float(((ctx.gemm(A.cuda(), Bd, tile=2).cpu().double() - ref).abs() / scale).max())
-    C = ctx.gemm(A.cuda(), Bd, tile=36).cpu().double()
+    C = ctx.gemm(A.cuda(), Bd, tile=tile).cpu().double()
     assert torch.isfinite(C).all()
     es = float(((C - ref).abs() / scale).max())
-    print(f"split16 dynamic range {M}x{N}x{K}: f32 {e32:.2e} split16 {es:.2e}")
+    print(f"split16 (tile {tile}) dynamic range {M}x{N}x{K}: f32 {e32:.2e} split16 {es:.2e}")
     assert es < 1e-6 and es < 2.0 * e32, (es, e32)
     assert torch.all(C[5] == 0)
     _keep.append(Bd)
 
 
 def test_gemm_rejects_non_library_tiles(ctx):
-    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36): any other hint, e.g. the r01
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44): any other hint, e.g. the r01
     timing experiments 37-39, returns VV_E_ARG instead of running something."""
     from vaevar._lib import VVError
 
@@ -117,13 +118,14 @@ def test_gemm_rejects_non_library_tiles(ctx):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
-    for t in (0, 2, 4, 24, 34, 36):
+    for t in (0, 2, 4, 24, 34, 36, 44):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
 
 
+@pytest.mark.parametrize("tile", [36, 44])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 4608), (2048, 4608, 1152), (2048, 1152, 3456)])
-def test_gemm_splitk_deterministic(ctx, M, N, K):
+def test_gemm_splitk_deterministic(ctx, M, N, K, tile):
     """fp16x3 GEMMs whose tiles are split along K (every tile at N = 1152, the tail at N = 4608): the fixup sums
     the partials in chunk order, so 30 back-to-back launches give bit-identical results at fp32-level error."""
     g = torch.Generator().manual_seed(M + N + K + 7)
@@ -131,8 +133,8 @@ def test_gemm_splitk_deterministic(ctx, M, N, K):
     B = (torch.randn(N, K, generator=g) * 0.03).cuda()
     ctx.gemm_register_weight(B)
     _keep.append(B)
-    first = ctx.gemm(A, B, tile=36)
-    outs = [ctx.gemm(A, B, tile=36) for _ in range(30)]
+    first = ctx.gemm(A, B, tile=tile)
+    outs = [ctx.gemm(A, B, tile=tile) for _ in range(30)]
     torch.cuda.synchronize()
     assert all(torch.equal(o, first) for o in outs)
     ref = A.double().cpu() @ B.double().cpu().t()

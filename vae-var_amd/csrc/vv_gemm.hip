@@ -1046,9 +1046,12 @@ __global__ __launch_bounds__(256) void k_rowscale(GemmArgs args, float* __restri
   if (lane == 0) out[(size_t)blockIdx.z * args.M + r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
 }
 
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* __restrict__ ascale) {
-  constexpr int BM = 128, BN = 128, BK = 32, NT = 256, WN = 2, TM = 2, TN = 2;
+// BM = 128: 4 waves (2 x 2 of 64x64), 64 KB of LDS, two workgroups per CU. BM = 256: 8 waves (4 x 2 of 64x64),
+// 96 KB, one workgroup per CU: the same two waves per SIMD, but each B k-tile feeds 256 rows, so a CU stages 48 KB
+// (global loads and LDS stores) per 2 x 24 MFMAs per SIMD instead of 64 KB.
+template <int EPI, int BM>
+__global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3(GemmArgs args, const float* __restrict__ ascale) {
+  constexpr int BN = 128, BK = 32, NT = 2 * BM, WN = 2, WM = BM / 64, TM = 2, TN = 2;
   constexpr int LSB = BK, PLANE = (BM + BN) * LSB;  // unsigned shorts
   constexpr int BUF = 2 * PLANE;                    // fp16 planes h, l of the A and B rows
   constexpr int TPR = BK / 4, RPP = NT / TPR, AI = BM / RPP, BQ = BN * 4 / NT;  // 8, 32, 4, 2
@@ -1185,9 +1188,9 @@ __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* 
       const h8v& xb = fb[st][b][pr == 1 ? 1 : 0];
       acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa, xb, acc[a][b], 0, 0, 0);
       if (i < 2 * AI && (i & 1)) asplit(Pn, i / 2);
-      if (i >= 8 && i < 12) bstore(Pn, (i - 8) / 2, (i - 8) % 2);
+      if (i >= 8 && i < 8 + 2 * BQ) bstore(Pn, (i - 8) / 2, (i - 8) % 2);
       if (i >= 12 && i < 12 + AI) aload(i - 12, k2);
-      if (i >= 16 && i < 20) bload((i - 16) / 2, (i - 16) % 2, k2);
+      if (i >= 16 && i < 16 + 2 * BQ) bload((i - 16) / 2, (i - 16) % 2, k2);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
@@ -1221,17 +1224,18 @@ __global__ __launch_bounds__(256, 1) void k_gemm_h3(GemmArgs args, const float* 
     return;
   }
   if (m0 + BM <= M && n0 + BN <= N)
-    epilogue<BM, BN, 2, WN, EPI, 32, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+    epilogue<BM, BN, WM, WN, EPI, 32, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
   else
-    epilogue<BM, BN, 2, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+    epilogue<BM, BN, WM, WN, EPI, 32, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
-template <int EPI>
+template <int EPI, int BM>
 static hipError_t launch_h3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc) {
-  if (hipError_t e = set_lds_limit((const void*)k_gemm_h3<EPI>, lds)) return e;
-  hipLaunchKernelGGL((k_gemm_h3<EPI>), grid, dim3(256), lds, s, a, sc);
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_h3<EPI, BM>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_h3<EPI, BM>), grid, dim3(2 * BM), lds, s, a, sc);
   if (tail)
-    hipLaunchKernelGGL((k_gemm_fixup_sub<128, 128, 2, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_gemm_fixup_sub<BM, 128, BM / 64, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(2 * BM), 0, s,
+                       a);  // y: the 2 x 2 32x32 sub-blocks of each wave
   return hipGetLastError();
 }
 
@@ -1246,20 +1250,21 @@ static bool h3_ready(const GemmArgs& a) {
   return pre;
 }
 
+template <int BM>
 static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
   if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
   if (!h3_ready(a)) return launch_bs2(a, s);
   float* sc = a.ws + kWsFloats;
   hipLaunchKernelGGL(k_rowscale, dim3((a.M + 3) / 4, 1, a.ngroups), dim3(256), 0, s, a, sc);
-  const size_t lds = 2 * (2 * 256 * 32) * sizeof(unsigned short);
-  const int T = ((a.N + 127) / 128) * ((a.M + 127) / 128);
+  const size_t lds = 2 * (2 * (BM + 128) * 32) * sizeof(unsigned short);
+  const int T = ((a.N + 127) / 128) * ((a.M + BM - 1) / BM);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
   dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
   switch (a.epi) {
-    case EPI_STORE: return launch_h3_k<EPI_STORE>(a, s, grid, lds, tail, sc);
-    case EPI_GELU: return launch_h3_k<EPI_GELU>(a, s, grid, lds, tail, sc);
-    case EPI_RESID: return launch_h3_k<EPI_RESID>(a, s, grid, lds, tail, sc);
-    case EPI_DGELU: return launch_h3_k<EPI_DGELU>(a, s, grid, lds, tail, sc);
+    case EPI_STORE: return launch_h3_k<EPI_STORE, BM>(a, s, grid, lds, tail, sc);
+    case EPI_GELU: return launch_h3_k<EPI_GELU, BM>(a, s, grid, lds, tail, sc);
+    case EPI_RESID: return launch_h3_k<EPI_RESID, BM>(a, s, grid, lds, tail, sc);
+    case EPI_DGELU: return launch_h3_k<EPI_DGELU, BM>(a, s, grid, lds, tail, sc);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1267,8 +1272,8 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
 // the GEMM kernels of the library, by tile hint (vv_gemm's `tile`; gemm_nt rejects every other value):
 //   exact f32 MFMA   0: 128x128   2: 64x64   4: 32x64            (GEMM_F32)
 //   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
-//   fp16x3 split    36: 128x128 (deep-K GEMMs of GEMM_SPLIT16)
-bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || t == 36; }
+//   fp16x3 split    36: 128x128, 44: 256x128 (deep-K GEMMs of GEMM_SPLIT16)
+bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || t == 36 || t == 44; }
 
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
@@ -1277,7 +1282,8 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 4: return launch_tile<32, 64, 32, 1, 2>(a, s);
     case 24: return launch_bs<64, 64, 2, 2>(a, s);
     case 34: return launch_bs2(a, s);
-    case 36: return launch_h3(a, s);
+    case 36: return launch_h3<128>(a, s);
+    case 44: return launch_h3<256>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1391,6 +1397,17 @@ static int pick_tile(const GemmArgs& a) {
       const char* e = getenv("VAEVAR_H3_MINK");
       h3_mink = e ? std::max(64, atoi(e)) : 768;
     }
+    // 256x128 tiles where they measured faster than 128x128 (profiles/r02/h3big: 2048 rows x (N 3456, K 1152):
+    // 69.0 vs 73.4 us, (1152, 4608): 93.1 vs 98.5, (1152, 3456): 76.1 vs 79.3; slower at N 4608 x K 1152 and far
+    // slower at 1152 x 1152, where 72 tiles leave most CUs idle); VAEVAR_H3_BIG=0 keeps 128x128 everywhere
+    static int h3_big = -1;
+    if (h3_big < 0) {
+      const char* e = getenv("VAEVAR_H3_BIG");
+      h3_big = e ? atoi(e) : 1;
+    }
+    if (a.math == GEMM_SPLIT16 && a.K >= h3_mink && h3_big && tiles_of(a, 256, 128) >= 64 &&
+        (a.K >= 3456 || (a.N >= 2048 && a.N < 4096)))
+      return 44;
     if (a.math == GEMM_SPLIT16 && a.K >= h3_mink && tiles_of(a, 128, 128) >= 128) return 36;
     // pipelined 128x128 (64x64 per wave, one barrier per k-tile) for the deep-K GEMMs that fill the chip with
     // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline)
@@ -1407,7 +1424,7 @@ static int pick_tile(const GemmArgs& a) {
 // tile edge of each variant (for the tail split)
 static void variant_tile(int t, int& bm, int& bn, int& bk) {
   bk = 32;
-  bm = t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
+  bm = t == 44 ? 256 : t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
   bn = t == 0 || t >= 34 ? 128 : 64;
 }
 
@@ -1455,7 +1472,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
         a.tdp = tdp;
         a.tsplit = S;
       }
-    } else if (tdp == 0 && (t == 36) && small_split_enabled()) {
+    } else if (tdp == 0 && (t == 36 || t == 44) && small_split_enabled()) {
       // fewer fp16x3 tiles than CUs (N = 1152 at 2048 tokens: 144 tiles): every tile split along K so that
       // two workgroups share most CUs (the co-resident pair overlaps one's staging with the other's MFMAs)
       // chunks of >= 24 k-tiles (K >= 2304 at S = 3): at K = 1152 the fixup costs more than the split gains
@@ -1464,7 +1481,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
         const char* e = getenv("VAEVAR_SMALL_SPLIT_MINKT");
         min_kt = e ? std::max(1, atoi(e)) : 24;
       }
-      int S = std::min((2 * P) / T, nkt / min_kt);
+      int S = std::min(((t == 44 ? 1 : 2) * P) / T, nkt / min_kt);  // resident workgroups per CU: 2 / 1
       const size_t tile_f = (size_t)bm * bn;
       while (S > 1 && (size_t)T * S * tile_f > kWsFloats) --S;
       if (S > 1) a.tsplit = S;
@@ -1476,7 +1493,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   const double G = a.ngroups;
   double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);
   if (a.epi == EPI_RESID || a.epi == EPI_GELU || a.epi == EPI_DGELU) bytes += 4.0 * G * (double)a.M * a.N;
-  prof_end(ph, s, t == 36 && h3_ready(a) ? PC_GEMM16 : PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
+  prof_end(ph, s, (t == 36 || t == 44) && h3_ready(a) ? PC_GEMM16 : PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
   return e;
 }
 
