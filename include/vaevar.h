@@ -116,6 +116,27 @@ int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
    x, out (C,Hs,Ws); mean, std (C). The model (either arch, batch 1) must map C channels to >= C. */
 int vv_integrate(vv_ctx* ctx, int model_id, const float* x, float* out, int C, int Hs, int Ws, const float* mean,
                  const float* std_, int steps, void* stream);
+/* sc4dvar (da_4dvar.py:1064-1177): the B-matrix control-variable transform of the static 3D/4D-Var mode.
+   Replaces init_b_matrix (:520-526), get_static_info (:608-628: RealSHT/InverseRealSHT of torch_harmonics on the
+   equiangular 128x256 grid, the zonal Gaussian kernel of the first hpad = 112 rows, sph_scale) and binds the
+   loss of :1071-1101. B-matrix tables as the reference loads them from dataset/bq_info_lr (one .npy per table, float64, host):
+   len_scale[69] (multiplied by scale_factor, :521), reg_coeff[69][n_reg] (n_reg 13 or 26, :890-893),
+   std_sur[4], vert_eig_value[5][13], vert_eig_vec[5][13][13]. Problem buffers (device, caller-owned) as in
+   vv_bind_problem: xb (69,Hs,Ws), yo/Hmask/R (T, C_obs, Hs, Ws), mean/std (69) for the flow steps; C = 69 and
+   (Hs,Ws) >= (128,256). interp: null for observations of the state (C_obs = 69), else the (n_out, 13)
+   obs_interpolater.interp of obs_type 'real*' (C_obs = 4 + 5*n_out, host or device, copied). T > 1 needs a
+   networks_old LGUnet_all flow model (69 -> >= 69 channels, 128x256, batch 1): x_t = integrate(x_{t-1}) is
+   detached in the reference (:1080), so those terms enter J but not dJ/dw. */
+int vv_sc4dvar_bind(vv_ctx* ctx, int flow_model_id, int T, int C, int Hs, int Ws, const float* xb, const float* yo,
+                    const float* Hmask, const float* R, const float* mean, const float* std_, float obs_coeff,
+                    const float* interp, int n_out, const double* len_scale, const double* reg_coeff, int n_reg,
+                    const double* std_sur, const double* vert_eig_value, const double* vert_eig_vec,
+                    double scale_factor, int hpad);
+/* loss(w) = J_b + obs_coeff * J_o (:1099-1101) at w (69,128,256); grad_w (may be null) = its gradient with the
+   reference's detach; J_b, J_o to the host. Synchronises `stream`. */
+int vv_sc4dvar_closure(vv_ctx* ctx, const float* w, float* grad_w, double* J_b, double* J_o, void* stream);
+/* xhat (69,Hs,Ws) = transform(w, xb) (:878-931) */
+int vv_sc4dvar_transform(vv_ctx* ctx, const float* w, float* xhat, void* stream);
 /* real-observation operator (da_4dvar.py:62-94 obs_interpolater; the loss's x_aug, :1196-1206): after
    vv_bind_problem, the bound yo, Hmask, R become (T, 4 + 5*n_out, Hs, Ws) observation-space fields. Channels 0..3
    are observed directly; for each of the five 13-level variables i (z, q, u, v, t) x_aug[4 + n_out*i + o] =

@@ -270,6 +270,27 @@ struct Problem {
   size_t obs_hw() const { return (size_t)(nout ? 4 + 5 * nout : C) * Hs * Ws; }  // floats per time of yo/Hm/R
 };
 
+// sc4dvar (da_4dvar.py:1064-1177): control variable w (C, 128, 256), x_0 = transform(w, xb) on the state grid,
+// x_t = integrate(x_{t-1}) with the flow model detached (:1080: integrate(..., interpolation=True, detach=True)),
+// so the forecasts add to J_o but not to dJ/dw
+struct Sc4Problem {
+  bool bound = false;
+  int flow = -1, T = 1, C = 0, Hs = 0, Ws = 0, Hl = 128, Wl = 256;
+  bool interp = false;
+  const float *xb = nullptr, *yo = nullptr, *Hm = nullptr, *R = nullptr, *mean = nullptr, *std_ = nullptr;
+  float obs_coeff = 1.f;
+  int nin = 0, nout = 0;
+  vv::Sc4dvarB* bm = nullptr;
+  std::unique_ptr<Arena> arena;
+  float *t1, *t2, *recon, *grec, *X, *FI, *FO, *ones, *Pobs, *GOBS;
+  int *mi, *mj, *ri0, *rj0, *di, *dj;
+  double *partial, *dJ;
+  int nblk = 1024;
+  size_t wn = 0;  // floats of w
+  ~Sc4Problem() { vv::sc4dvar_destroy(bm); }
+  size_t obs_hw() const { return (size_t)(nout ? 4 + 5 * nout : C) * Hs * Ws; }
+};
+
 }  // namespace
 
 struct vv_ctx {
@@ -277,6 +298,7 @@ struct vv_ctx {
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic of every model of this context (vv_set_gemm_math)
   std::vector<std::unique_ptr<Model>> models;
   Problem prob;
+  std::unique_ptr<Sc4Problem> sc4;  // vv_sc4dvar_bind
   double* red = nullptr;   // reduction scratch
   float* gemm_ws = nullptr;
   float* redf = nullptr;
@@ -1156,6 +1178,108 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   return 0;
 }
 
+// sc4dvar loss(w) (da_4dvar.py:1099-1101) and, with grad, its gradient: J_b = sum(w^2)/2, J_o = sum_t H (x_t - yo_t)^2
+// / R / 2 (x_aug of the real-observation operator when set, :1085-1097); dJ/dw = w + obs_coeff * core^T(adjoint of
+// the nearest interpolation of H (x_0 - yo_0) / R) — the detached forecasts contribute no gradient
+int sc4_closure_impl(vv_ctx* ctx, const float* w, float* grad, hipStream_t st) {
+  Sc4Problem& P = *ctx->sc4;
+  const int C = P.C, T = P.T;
+  const size_t HW = (size_t)P.Hs * P.Ws, CHW = (size_t)C * HW, OHW = P.obs_hw();
+  auto part = [&](int t) { return P.partial + (size_t)t * P.nblk; };
+  auto X = [&](int t) { return P.X + (size_t)t * CHW; };
+  Model* F = P.flow >= 0 ? ctx->models[P.flow].get() : nullptr;
+  CK(vv::sc4dvar_fwd(P.bm, w, P.recon, P.t1, P.t2, ctx->gemm_ws, st));
+  MisfitArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  ma.C = C;
+  ma.Hs = P.Hs;
+  ma.Ws = P.Ws;
+  ma.Hl = P.Hl;
+  ma.Wl = P.Wl;
+  ma.mi = P.interp ? P.mi : nullptr;
+  ma.mj = P.interp ? P.mj : nullptr;
+  ma.mean = P.mean;
+  ma.std_ = P.std_;
+  ma.nblk = P.nblk;
+  auto obs = [&](int t) -> hipError_t {  // real-observation operator: J partials + (t = 0) the state gradient
+    if (!P.nout) return hipSuccess;
+    ObsArgs oa;
+    oa.nin = P.nin;
+    oa.nout = P.nout;
+    oa.HW = (int)HW;
+    oa.P = P.Pobs;
+    oa.x = X(t);
+    oa.yo = P.yo + t * OHW;
+    oa.Hm = P.Hm + t * OHW;
+    oa.R = P.R + t * OHW;
+    oa.coeff = P.obs_coeff;
+    oa.g_obs = t == 0 ? P.GOBS : P.GOBS + CHW;  // the gradient of t = 0 is kept; later times: scratch
+    oa.partial = part(t);
+    oa.nblk = P.nblk;
+    return obs_misfit(oa, st);
+  };
+  // x_0 = interpolate(recon) + xb   (:928)
+  {
+    MisfitArgs m0 = ma;
+    m0.net = P.recon;
+    m0.net_cstride = C;
+    m0.scale = P.ones;
+    m0.xb = P.xb;
+    m0.yo = P.yo;
+    m0.Hm = P.nout ? nullptr : P.Hm;
+    m0.R = P.R;
+    m0.x_out = X(0);
+    m0.flow_in = (T > 1 && !P.interp) ? P.FI : nullptr;
+    m0.partial = part(0);
+    CK(misfit_fwd(m0, st));
+    CK(obs(0));
+  }
+  for (int t = 1; t < T; ++t) {
+    // x_t = integrate(x_{t-1}, flow, 1, True)[:69]   (:1079-1081, detached)
+    if (P.interp) CK(flow_input(X(t - 1), P.FI, P.di, P.dj, P.mean, P.std_, C, P.Hs, P.Ws, P.Hl, P.Wl, st));
+    int r = model_fwd(*F, 0, P.FI, P.FO, C, st);
+    if (r) return r;
+    MisfitArgs mt = ma;
+    mt.net = P.FO;
+    mt.net_cstride = F->cfg.Cout;
+    mt.scale = P.std_;
+    mt.offset = P.mean;
+    mt.yo = P.yo + t * OHW;
+    mt.Hm = P.nout ? nullptr : P.Hm + t * OHW;
+    mt.R = P.R + t * OHW;
+    mt.x_out = X(t);
+    mt.flow_in = (t < T - 1 && !P.interp) ? P.FI : nullptr;
+    mt.partial = part(t);
+    CK(misfit_fwd(mt, st));
+    CK(obs(t));
+  }
+  CK(reduce_final(part(0), P.nblk * T, P.dJ + 1, st));
+  CK(reduce_sumsq(w, (int64_t)P.wn, part(T), P.nblk, st));
+  CK(reduce_final(part(T), P.nblk, P.dJ, st));
+  if (!grad) return 0;
+  MisfitBwdArgs mb;
+  memset(&mb, 0, sizeof(mb));
+  mb.C = C;
+  mb.Hs = P.Hs;
+  mb.Ws = P.Ws;
+  mb.Hl = P.Hl;
+  mb.Wl = P.Wl;
+  mb.ri0 = P.interp ? P.ri0 : nullptr;
+  mb.rj0 = P.interp ? P.rj0 : nullptr;
+  mb.coeff = P.obs_coeff;
+  mb.x = X(0);
+  mb.yo = P.yo;
+  mb.Hm = P.Hm;
+  mb.R = P.R;
+  mb.g_obs = P.nout ? P.GOBS : nullptr;
+  mb.scale = P.ones;
+  mb.g_net = P.grec;
+  mb.net_cstride = C;
+  CK(misfit_bwd(mb, st));
+  CK(vv::sc4dvar_adj(P.bm, P.grec, w, grad, P.t1, P.t2, ctx->gemm_ws, st));
+  return 0;
+}
+
 __global__ void k_prod(const float* a, const float* b, float* o, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) o[i] = a[i] * b[i];
@@ -1876,6 +2000,148 @@ int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, co
   GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE, ctx->math);
   a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
   VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
+  return 0;
+}
+
+int vv_sc4dvar_bind(vv_ctx* ctx, int flow_model_id, int T, int C, int Hs, int Ws, const float* xb, const float* yo,
+                    const float* Hmask, const float* R, const float* mean, const float* std_, float obs_coeff,
+                    const float* interp, int n_out, const double* len_scale, const double* reg_coeff, int n_reg,
+                    const double* std_sur, const double* vert_eig_value, const double* vert_eig_vec,
+                    double scale_factor, int hpad) {
+  if (!ctx) return fail(VV_E_ARG, "null context");
+  if (T < 1 || C != 69) return fail(VV_E_ARG, "sc4dvar needs T >= 1 and the 69-channel state (C = %d)", C);
+  if (Hs < 128 || Ws < 256) return fail(VV_E_ARG, "state grid %dx%d coarser than the 128x256 transform grid", Hs, Ws);
+  if (!xb || !yo || !Hmask || !R || !mean || !std_) return fail(VV_E_ARG, "null problem buffer");
+  if (!len_scale || !reg_coeff || !std_sur || !vert_eig_value || !vert_eig_vec) return fail(VV_E_ARG, "null B-matrix table");
+  if (interp && (n_out < 1 || n_out > kObsMaxOut)) return fail(VV_E_ARG, "n_out %d out of range", n_out);
+  Model* F = nullptr;
+  if (T > 1) {
+    F = get_model(ctx, flow_model_id);
+    if (!F || F->fm) return fail(VV_E_ARG, "T > 1 needs a networks_old LGUnet_all flow model");
+    if (!F->loaded) return fail(VV_E_STATE, "flow weights not loaded");
+    if (F->cfg.Cin != C || F->cfg.Cout < C || F->B != 1 || F->cfg.Himg != 128 || F->cfg.Wimg != 256)
+      return fail(VV_E_ARG, "flow model must map 69 channels on the 128x256 grid at batch 1");
+  }
+  int r = set_dev(ctx);
+  if (r) return r;
+  auto P = std::make_unique<Sc4Problem>();
+  std::string err;
+  if ((r = vv::sc4dvar_create(&P->bm, C, len_scale, reg_coeff, n_reg, std_sur, vert_eig_value, vert_eig_vec,
+                              scale_factor, hpad, err)))
+    return fail(r < 0 ? (r == -2 ? VV_E_ALLOC : VV_E_ARG) : r, "%s", err.c_str());
+  P->flow = T > 1 ? flow_model_id : -1;
+  P->T = T;
+  P->C = C;
+  P->Hs = Hs;
+  P->Ws = Ws;
+  P->interp = Hs != P->Hl || Ws != P->Wl;
+  P->xb = xb;
+  P->yo = yo;
+  P->Hm = Hmask;
+  P->R = R;
+  P->mean = mean;
+  P->std_ = std_;
+  P->obs_coeff = obs_coeff;
+  P->nin = interp ? 13 : 0;
+  P->nout = interp ? n_out : 0;
+  const size_t CHW = (size_t)C * Hs * Ws, fld = vv::sc4dvar_field_floats(P->bm), HWl = (size_t)P->Hl * P->Wl;
+  P->wn = fld;
+  for (int pass = 0; pass < 2; ++pass) {
+    Planner pl;
+    if (pass) pl.base = P->arena->base;
+    P->t1 = pl.f(fld);
+    P->t2 = pl.f(fld);
+    P->recon = pl.f(fld);
+    P->grec = pl.f(fld);
+    P->X = pl.f(CHW * T);
+    P->FI = pl.f((size_t)C * HWl);
+    P->FO = pl.f((F ? (size_t)F->cfg.Cout : 1) * HWl);
+    P->ones = pl.f(C);
+    P->Pobs = pl.f((size_t)std::max(P->nout, 1) * 13);
+    P->GOBS = pl.f(P->nout ? 2 * CHW : 1);
+    int* mp = reinterpret_cast<int*>(pl.f((size_t)Hs + Ws + 2 * (P->Hl + 1) + 2 * (P->Wl + 1)));
+    double* pd = reinterpret_cast<double*>(pl.f(2 * ((size_t)P->nblk * (T + 1) + 8)));
+    if (pass) {
+      P->partial = pd;
+      P->dJ = pd + (size_t)P->nblk * (T + 1) + 2;
+      P->mi = mp;
+      P->mj = P->mi + Hs;
+      P->ri0 = P->mj + Ws;
+      P->rj0 = P->ri0 + P->Hl + 1;
+      P->di = P->rj0 + P->Wl + 1;
+      P->dj = P->di + P->Hl;
+    } else {
+      P->arena = std::make_unique<Arena>();
+      if (hipMalloc(&P->arena->base, pl.bytes) != hipSuccess) return fail(VV_E_ALLOC, "sc4dvar arena");
+      P->arena->cap = pl.bytes;
+    }
+  }
+  {
+    // nearest maps (quirk Q3): transform output 128x256 -> state grid (:928), integrate's down/up-sampling
+    std::vector<int> mi = nearest_map(P->Hl, Hs), mj = nearest_map(P->Wl, Ws);
+    std::vector<int> di = nearest_map(Hs, P->Hl), dj = nearest_map(Ws, P->Wl);
+    auto ranges = [](const std::vector<int>& m, int n) {
+      std::vector<int> rr(n + 1, (int)m.size());
+      for (int k = (int)m.size() - 1; k >= 0; --k) rr[m[k]] = k;
+      for (int a = n - 1; a >= 0; --a) rr[a] = std::min(rr[a], rr[a + 1]);
+      return rr;
+    };
+    std::vector<int> ri0 = ranges(mi, P->Hl), rj0 = ranges(mj, P->Wl);
+    std::vector<int> all;
+    for (auto* v : {&mi, &mj, &ri0, &rj0, &di, &dj}) all.insert(all.end(), v->begin(), v->end());
+    VV_HIP(hipMemcpy(P->mi, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice));
+    std::vector<float> ones(C, 1.0f);
+    VV_HIP(hipMemcpy(P->ones, ones.data(), C * sizeof(float), hipMemcpyHostToDevice));
+    if (interp) VV_HIP(hipMemcpy(P->Pobs, interp, (size_t)n_out * 13 * sizeof(float), hipMemcpyDefault));
+  }
+  VV_HIP(hipDeviceSynchronize());
+  P->bound = true;
+  ctx->sc4 = std::move(P);
+  return 0;
+}
+
+int vv_sc4dvar_closure(vv_ctx* ctx, const float* w, float* grad_w, double* J_b, double* J_o, void* stream) {
+  if (!ctx || !w) return fail(VV_E_ARG, "null argument");
+  if (!ctx->sc4 || !ctx->sc4->bound) return fail(VV_E_STATE, "vv_sc4dvar_bind first");
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  if ((r = sc4_closure_impl(ctx, w, grad_w, st))) return r;
+  hipLaunchKernelGGL(k_half, dim3(1), dim3(64), 0, st, ctx->sc4->dJ, 2);
+  VV_HIP(hipGetLastError());
+  double h[2];
+  VV_HIP(hipMemcpyAsync(h, ctx->sc4->dJ, sizeof(h), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipStreamSynchronize(st));
+  if (J_b) *J_b = h[0];
+  if (J_o) *J_o = h[1];
+  return 0;
+}
+
+int vv_sc4dvar_transform(vv_ctx* ctx, const float* w, float* xhat, void* stream) {
+  if (!ctx || !w || !xhat) return fail(VV_E_ARG, "null argument");
+  if (!ctx->sc4 || !ctx->sc4->bound) return fail(VV_E_STATE, "vv_sc4dvar_bind first");
+  int r = set_dev(ctx);
+  if (r) return r;
+  Sc4Problem& P = *ctx->sc4;
+  hipStream_t st = (hipStream_t)stream;
+  VV_HIP(vv::sc4dvar_fwd(P.bm, w, P.recon, P.t1, P.t2, ctx->gemm_ws, st));
+  MisfitArgs m;
+  memset(&m, 0, sizeof(m));
+  m.C = P.C;
+  m.Hs = P.Hs;
+  m.Ws = P.Ws;
+  m.Hl = P.Hl;
+  m.Wl = P.Wl;
+  m.mi = P.interp ? P.mi : nullptr;
+  m.mj = P.interp ? P.mj : nullptr;
+  m.net = P.recon;
+  m.net_cstride = P.C;
+  m.scale = P.ones;
+  m.xb = P.xb;
+  m.x_out = xhat;  // Hm null: no misfit partials
+  m.partial = P.partial;
+  m.nblk = P.nblk;
+  VV_HIP(misfit_fwd(m, st));
   return 0;
 }
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <string>
 
 namespace vv {
 
@@ -285,6 +286,24 @@ bool prof_enabled();
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 
 hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// sc4dvar B-matrix transform (da_4dvar.py:878-931; vv_sc4dvar.hip) on the fixed 128 x 256 grid
+// ---------------------------------------------------------------------------
+struct Sc4dvarB;
+// tables from the B-matrix statistics (init_b_matrix :520-526, float64 as in dataset/bq_info_lr/*.npy):
+// len_scale[C], reg[C][nreg] (nreg 13 or 26), std_sur[4], eigval[5][13], eigvec[5][13][13]; 0 or nonzero + err
+int sc4dvar_create(Sc4dvarB** out, int C, const double* len_scale, const double* reg, int nreg,
+                   const double* std_sur, const double* eigval, const double* eigvec, double scale_factor, int hpad,
+                   std::string& err);
+void sc4dvar_destroy(Sc4dvarB* b);
+size_t sc4dvar_field_floats(const Sc4dvarB* b);  // C * 128 * 256
+// recon = transform core of w (before the interpolation and + xb); t1, t2: field-sized scratch
+hipError_t sc4dvar_fwd(const Sc4dvarB* b, const float* w, float* recon, float* t1, float* t2, float* gemm_ws,
+                       hipStream_t s);
+// g_w = core^T g_recon (+ add)
+hipError_t sc4dvar_adj(const Sc4dvarB* b, const float* g_recon, const float* add, float* g_w, float* t1, float* t2,
+                       float* gemm_ws, hipStream_t s);
 hipError_t fill(float* p, float v, int64_t n, hipStream_t s);
 
 }  // namespace vv

@@ -109,6 +109,11 @@ _SIGS = {
     "vv_get_gemm_math": (c_int, [c_void_p, P(c_int)]),
     "vv_gemm_register_weight": (c_int, [c_void_p, c_void_p, c_int, c_int]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "vv_sc4dvar_bind": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_float, c_void_p, c_int, P(c_double), P(c_double), c_int,
+                                P(c_double), P(c_double), P(c_double), c_double, c_int]),
+    "vv_sc4dvar_closure": (c_int, [c_void_p, c_void_p, c_void_p, P(c_double), P(c_double), c_void_p]),
+    "vv_sc4dvar_transform": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 EXPORTED = sorted(_SIGS)
