@@ -45,8 +45,9 @@ namespace {
 __global__ __launch_bounds__(256) void k_sht_filter(const float* __restrict__ in, float* __restrict__ out,
                                                     const float* __restrict__ A1, const float* __restrict__ A2,
                                                     const float* __restrict__ F, int C) {
-  __shared__ float v[2][kCPB][kLat];
-  __shared__ float u[2][kCPB][kLat];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float v[2][kCPB][kLat];
+  __shared__ __attribute__((aligned(16))) float u[2][kCPB][kLat];
   const int m = blockIdx.x, c0 = blockIdx.y * kCPB, tid = threadIdx.x;
   const int nc = min(kCPB, C - c0);
   const size_t NR = (size_t)C * kLat;
@@ -54,16 +55,22 @@ __global__ __launch_bounds__(256) void k_sht_filter(const float* __restrict__ in
   const float* src = in + (size_t)(ri * kM + m) * NR + (size_t)c0 * kLat;
   for (int ch = 0; ch < kCPB; ++ch) v[ri][ch][i] = ch < nc ? src[(size_t)ch * kLat + i] : 0.f;
   __syncthreads();
+  // k / l run in steps of 4: four independent matrix loads, float4 reads of the LDS columns (broadcast)
+  const int m4 = m & ~3;
   {
     float acc[kCPB];
 #pragma unroll
     for (int ch = 0; ch < kCPB; ++ch) acc[ch] = 0.f;
     const float* a = A1 + (size_t)m * kLat * kLat + i;  // A1[m][k][l = i]
     if (i >= m) {
-      for (int k = 0; k < kLat; ++k) {
-        const float w = a[(size_t)k * kLat];
+      for (int k = 0; k < kLat; k += 4) {
+        const float w0 = a[(size_t)k * kLat], w1 = a[(size_t)(k + 1) * kLat], w2 = a[(size_t)(k + 2) * kLat],
+                    w3 = a[(size_t)(k + 3) * kLat];
 #pragma unroll
-        for (int ch = 0; ch < kCPB; ++ch) acc[ch] = fmaf(w, v[ri][ch][k], acc[ch]);
+        for (int ch = 0; ch < kCPB; ++ch) {
+          const f4 x = *reinterpret_cast<const f4*>(&v[ri][ch][k]);
+          acc[ch] = fmaf(w3, x[3], fmaf(w2, x[2], fmaf(w1, x[1], fmaf(w0, x[0], acc[ch]))));
+        }
       }
     }
 #pragma unroll
@@ -73,34 +80,50 @@ __global__ __launch_bounds__(256) void k_sht_filter(const float* __restrict__ in
   float acc[kCPB];
 #pragma unroll
   for (int ch = 0; ch < kCPB; ++ch) acc[ch] = 0.f;
-  const float* a = A2 + (size_t)m * kLat * kLat + i;  // A2[m][l][k = i]
-  for (int l = m; l < kLat; ++l) {
-    const float w = a[(size_t)l * kLat];
+  const float* a = A2 + (size_t)m * kLat * kLat + i;  // A2[m][l][k = i]; rows l < m are zero
+  for (int l = m4; l < kLat; l += 4) {
+    const float w0 = a[(size_t)l * kLat], w1 = a[(size_t)(l + 1) * kLat], w2 = a[(size_t)(l + 2) * kLat],
+                w3 = a[(size_t)(l + 3) * kLat];
 #pragma unroll
-    for (int ch = 0; ch < kCPB; ++ch) acc[ch] = fmaf(w, u[ri][ch][l], acc[ch]);
+    for (int ch = 0; ch < kCPB; ++ch) {
+      const f4 x = *reinterpret_cast<const f4*>(&u[ri][ch][l]);
+      acc[ch] = fmaf(w3, x[3], fmaf(w2, x[2], fmaf(w1, x[1], fmaf(w0, x[0], acc[ch]))));
+    }
   }
   float* dst = out + (size_t)(ri * kM + m) * NR + (size_t)c0 * kLat;
   for (int ch = 0; ch < nc; ++ch) dst[(size_t)ch * kLat + i] = acc[ch];
 }
 
-// out[i][p] = sum_j A[i][j] in[j][p] over the C channels of one pixel p (one thread per pixel)
+// out[i][p] = sum_j A[i][j] in[j][p] over the C channels of one pixel p. 256 threads = 64 pixels x 4 output
+// groups; each thread keeps its pixel's column in registers and forms every fourth output from float4 broadcasts of
+// A's rows (zero-padded to kMaxC in LDS), four independent partial sums per output
 constexpr int kMaxC = 72;
-__global__ __launch_bounds__(64) void k_colmix(const float* __restrict__ in, float* __restrict__ out,
-                                               const float* __restrict__ A, int C, int HW) {
-  __shared__ float As[kMaxC * kMaxC];
-  for (int e = threadIdx.x; e < C * C; e += blockDim.x) As[e] = A[e];
+__global__ __launch_bounds__(256) void k_colmix(const float* __restrict__ in, float* __restrict__ out,
+                                                const float* __restrict__ A, int C, int HW) {
+  __shared__ __attribute__((aligned(16))) float As[kMaxC * kMaxC];
+  for (int e = threadIdx.x; e < kMaxC * kMaxC; e += blockDim.x) {
+    const int i = e / kMaxC, j = e % kMaxC;
+    As[e] = (i < C && j < C) ? A[i * C + j] : 0.f;
+  }
   __syncthreads();
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.x * 64 + (threadIdx.x & 63), og = threadIdx.x >> 6;
   if (p >= HW) return;
   float x[kMaxC];
 #pragma unroll
   for (int j = 0; j < kMaxC; ++j) x[j] = j < C ? in[(size_t)j * HW + p] : 0.f;
-  for (int i = 0; i < C; ++i) {
-    float s = 0.f;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  for (int i = og; i < C; i += 4) {
+    const f4* a = reinterpret_cast<const f4*>(As + i * kMaxC);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
-    for (int j = 0; j < kMaxC; ++j)
-      if (j < C) s = fmaf(As[i * C + j], x[j], s);
-    out[(size_t)i * HW + p] = s;
+    for (int q = 0; q < kMaxC / 4; ++q) {
+      const f4 v = a[q];
+      s0 = fmaf(v[0], x[4 * q], s0);
+      s1 = fmaf(v[1], x[4 * q + 1], s1);
+      s2 = fmaf(v[2], x[4 * q + 2], s2);
+      s3 = fmaf(v[3], x[4 * q + 3], s3);
+    }
+    out[(size_t)i * HW + p] = (s0 + s1) + (s2 + s3);
   }
 }
 
@@ -378,7 +401,7 @@ hipError_t sc4dvar_fwd(const Sc4dvarB* b, const float* w, float* recon, float* t
   hipLaunchKernelGGL(k_sht_filter, dim3(kM, (C + kCPB - 1) / kCPB), dim3(256), 0, s, t1, t2, b->WaT, b->P, b->F, C);
   if ((e = transpose2d(t2, t1, kQ, NR, s))) return e;           // t1 = Y [(c,k)][q]
   if ((e = gemm_f32(t1, b->Di, t2, nullptr, NR, kLon, kQ, gemm_ws, s))) return e;  // t2 = inc_static
-  hipLaunchKernelGGL(k_colmix, dim3((HW + 63) / 64), dim3(64), 0, s, t2, t1, b->A, C, HW);  // t1 = sfvp
+  hipLaunchKernelGGL(k_colmix, dim3((HW + 63) / 64), dim3(256), 0, s, t2, t1, b->A, C, HW);  // t1 = sfvp
   const size_t n = (size_t)C * HW;
   hipLaunchKernelGGL(k_winds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, t1, recon, b->stc, C, 4 + 2 * 13,
                      4 + 3 * 13, 13, 0);
@@ -393,7 +416,7 @@ hipError_t sc4dvar_adj(const Sc4dvarB* b, const float* g_recon, const float* add
   hipError_t e;
   hipLaunchKernelGGL(k_winds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g_recon, t1, b->stc, C,
                      4 + 2 * 13, 4 + 3 * 13, 13, 1);                                  // t1 = g_sfvp
-  hipLaunchKernelGGL(k_colmix, dim3((HW + 63) / 64), dim3(64), 0, s, t1, t2, b->AT, C, HW);  // t2 = g_static
+  hipLaunchKernelGGL(k_colmix, dim3((HW + 63) / 64), dim3(256), 0, s, t1, t2, b->AT, C, HW);  // t2 = g_static
   if ((e = gemm_f32(b->DiT, t2, t1, nullptr, kQ, NR, kLon, gemm_ws, s))) return e;  // t1 = g_Y^T [q][(c,k)]
   hipLaunchKernelGGL(k_sht_filter, dim3(kM, (C + kCPB - 1) / kCPB), dim3(256), 0, s, t1, t2, b->PT, b->Wa, b->F, C);
   if ((e = transpose2d(t2, t1, kQ, NR, s))) return e;                                  // t1 = g_X [(c,k)][q]
