@@ -137,6 +137,12 @@ int vv_sc4dvar_bind(vv_ctx* ctx, int flow_model_id, int T, int C, int Hs, int Ws
 int vv_sc4dvar_closure(vv_ctx* ctx, const float* w, float* grad_w, double* J_b, double* J_o, void* stream);
 /* xhat (69,Hs,Ws) = transform(w, xb) (:878-931) */
 int vv_sc4dvar_transform(vv_ctx* ctx, const float* w, float* xhat, void* stream);
+/* F.interpolate(x, (Ho, Wo)) with the default mode 'nearest' (quirk Q3; nf_model/vae.py:90 decoder_hr,
+   da_4dvar.py:671/679/928) on (BC, Hi, Wi) device fields -> out (BC, Ho, Wo); with adjoint != 0 the transposed
+   map: in (BC, Ho, Wo) -> out (BC, Hi, Wi), each source pixel the sum over its nearest preimage (deterministic).
+   Synchronises `stream`. */
+int vv_resample_nearest(vv_ctx* ctx, const float* in, float* out, int BC, int Hi, int Wi, int Ho, int Wo, int adjoint,
+                        void* stream);
 /* real-observation operator (da_4dvar.py:62-94 obs_interpolater; the loss's x_aug, :1196-1206): after
    vv_bind_problem, the bound yo, Hmask, R become (T, 4 + 5*n_out, Hs, Ws) observation-space fields. Channels 0..3
    are observed directly; for each of the five 13-level variables i (z, q, u, v, t) x_aug[4 + n_out*i + o] =

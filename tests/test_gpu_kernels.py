@@ -83,7 +83,7 @@ _keep = []
 @pytest.mark.parametrize("tile", [36, 44])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
 def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):
-    """fp16x3 split (tiles 36 = 128x128 and 44 = 256x128) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
+    """fp16x3 split (tiles 36 = 128x128, 44 = 256x128 of 8 waves) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
     (per-chunk scales), B rows span 2^+-8, with zeros, a zero row and huge/tiny values: no overflow, no flush."""
     g = torch.Generator().manual_seed(M + N + K + 1)
     A = torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-12, 12, generator=g)) \
@@ -114,7 +114,7 @@ def test_gemm_rejects_non_library_tiles(ctx):
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 35, 37, 38, 39, 40, 41, 42, 1000):
+    for t in (1, 3, 21, 35, 37, 38, 39, 40, 41, 42, 45, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
@@ -196,3 +196,23 @@ def test_adam_matches_torch(ctx):
         opt.step()
         ctx.adam(p, gr.cuda(), m, v, 0.1, 0.9, 0.999, 1e-8, i + 1)
     assert torch.allclose(p.cpu(), pt.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("src,dst", [((128, 256), (721, 1440)), ((721, 1440), (128, 256)), ((32, 64), (45, 90)),
+                                     ((64, 128), (64, 128))])
+def test_resample_nearest_matches_interpolate(ctx, src, dst):
+    """vv_resample_nearest == F.interpolate(mode='nearest') bit for bit (quirk Q3), and its adjoint == the autograd
+    backward of F.interpolate (sums over each source pixel's preimage)."""
+    from vaevar.engine import resample_nearest
+
+    g = torch.Generator().manual_seed(sum(src) + sum(dst))
+    x = torch.randn(2, 3, *src, generator=g)
+    ref = torch.nn.functional.interpolate(x, dst)
+    xd = x.cuda().requires_grad_(True)
+    out = resample_nearest(ctx, xd, dst)
+    assert torch.equal(out.detach().cpu(), ref)
+    cot = torch.randn(2, 3, *dst, generator=g)
+    out.backward(cot.cuda())
+    xr = x.clone().requires_grad_(True)
+    torch.nn.functional.interpolate(xr, dst).backward(cot)
+    assert float((xd.grad.cpu() - xr.grad).abs().max()) <= 1e-5 * float(xr.grad.abs().max())

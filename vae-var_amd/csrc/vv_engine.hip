@@ -2145,4 +2145,40 @@ int vv_sc4dvar_transform(vv_ctx* ctx, const float* w, float* xhat, void* stream)
   return 0;
 }
 
+int vv_resample_nearest(vv_ctx* ctx, const float* in, float* out, int BC, int Hi, int Wi, int Ho, int Wo, int adjoint,
+                        void* stream) {
+  if (!ctx || !in || !out) return fail(VV_E_ARG, "null argument");
+  if (BC < 1 || Hi < 1 || Wi < 1 || Ho < 1 || Wo < 1) return fail(VV_E_ARG, "bad shape");
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<int> maps;
+  std::vector<int> mi = nearest_map(Hi, Ho), mj = nearest_map(Wi, Wo);
+  if (adjoint) {
+    auto ranges = [](const std::vector<int>& m, int n) {
+      std::vector<int> rr(n + 1, (int)m.size());
+      for (int k = (int)m.size() - 1; k >= 0; --k) rr[m[k]] = k;
+      for (int a = n - 1; a >= 0; --a) rr[a] = std::min(rr[a], rr[a + 1]);
+      return rr;
+    };
+    for (size_t k = 1; k < mi.size(); ++k)
+      if (mi[k] < mi[k - 1]) return fail(VV_E_ARG, "non-monotone nearest map");
+    for (size_t k = 1; k < mj.size(); ++k)
+      if (mj[k] < mj[k - 1]) return fail(VV_E_ARG, "non-monotone nearest map");
+    for (auto& v : {ranges(mi, Hi), ranges(mj, Wi)}) maps.insert(maps.end(), v.begin(), v.end());
+  } else {
+    maps = mi;
+    maps.insert(maps.end(), mj.begin(), mj.end());
+  }
+  int* dm = nullptr;
+  VV_HIP(hipMallocAsync((void**)&dm, maps.size() * sizeof(int), st));
+  VV_HIP(hipMemcpyAsync(dm, maps.data(), maps.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  const hipError_t e = vv::resample_nearest(in, out, dm, BC, Hi, Wi, Ho, Wo, adjoint != 0, st);
+  // the host vector must outlive the async copy
+  VV_HIP(hipStreamSynchronize(st));
+  (void)hipFreeAsync(dm, st);
+  VV_HIP(e);
+  return 0;
+}
+
 }  // extern "C"

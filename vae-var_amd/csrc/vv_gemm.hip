@@ -1272,7 +1272,7 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
 // the GEMM kernels of the library, by tile hint (vv_gemm's `tile`; gemm_nt rejects every other value):
 //   exact f32 MFMA   0: 128x128   2: 64x64   4: 32x64            (GEMM_F32)
 //   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
-//   fp16x3 split    36: 128x128, 44: 256x128 (deep-K GEMMs of GEMM_SPLIT16)
+//   fp16x3 split    36: 128x128, 44: 256x128 (8 waves of 64x64)
 bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || t == 36 || t == 44; }
 
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
@@ -1481,7 +1481,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
         const char* e = getenv("VAEVAR_SMALL_SPLIT_MINKT");
         min_kt = e ? std::max(1, atoi(e)) : 24;
       }
-      int S = std::min(((t == 44 ? 1 : 2) * P) / T, nkt / min_kt);  // resident workgroups per CU: 2 / 1
+      int S = std::min(((t == 36 ? 2 : 1) * P) / T, nkt / min_kt);  // resident workgroups per CU: 2 / 1
       const size_t tile_f = (size_t)bm * bn;
       while (S > 1 && (size_t)T * S * tile_f > kWsFloats) --S;
       if (S > 1) a.tsplit = S;

@@ -257,6 +257,10 @@ hipError_t flow_input_adjoint(const float* gfi, float* carry, const int* di, con
 hipError_t scale_channels(const float* in, float* out, const float* inv_std, int C, int HW, const float* add,
                           hipStream_t s);
 
+// nearest resampling (BC, Hi, Wi) -> (BC, Ho, Wo); maps: mi[Ho], mj[Wo] (forward) or the preimage ranges
+// ri0[Hi + 1], rj0[Wi + 1] (adjoint: in = gout (BC, Ho, Wo), out = gin (BC, Hi, Wi))
+hipError_t resample_nearest(const float* in, float* out, const int* maps, int BC, int Hi, int Wi, int Ho, int Wo,
+                            bool adjoint, hipStream_t s);
 hipError_t reduce_sumsq(const float* x, int64_t n, double* partial, int nblk, hipStream_t s);
 hipError_t reduce_final(const double* partial, int n, double* out, hipStream_t s);
 

@@ -895,6 +895,43 @@ hipError_t flow_input_adjoint(const float* gfi, float* carry, const int* di, con
   return hipGetLastError();
 }
 
+// F.interpolate(mode='nearest') of (BC, Hi, Wi) fields to (Ho, Wo) with the source maps mi[Ho], mj[Wo] (quirk Q3),
+// and its adjoint: gin[i][j] = sum of gout over the rows y in [ri0[i], ri0[i+1]) and columns x in [rj0[j], rj0[j+1])
+// (the maps are monotone, so every preimage is a contiguous range; a deterministic gather, no atomics)
+__global__ __launch_bounds__(256) void k_resample(const float* __restrict__ in, float* __restrict__ out,
+                                                  const int* __restrict__ mi, const int* __restrict__ mj, int BC,
+                                                  int Hi, int Wi, int Ho, int Wo) {
+  const size_t n = (size_t)BC * Ho * Wo;
+  for (size_t id = (size_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (size_t)gridDim.x * 256) {
+    const size_t c = id / ((size_t)Ho * Wo);
+    const int q = (int)(id - c * Ho * Wo), y = q / Wo, x = q - y * Wo;
+    out[id] = in[(c * Hi + mi[y]) * Wi + mj[x]];
+  }
+}
+__global__ __launch_bounds__(256) void k_resample_adj(const float* __restrict__ gout, float* __restrict__ gin,
+                                                      const int* __restrict__ ri0, const int* __restrict__ rj0, int BC,
+                                                      int Hi, int Wi, int Ho, int Wo) {
+  const size_t n = (size_t)BC * Hi * Wi;
+  for (size_t id = (size_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (size_t)gridDim.x * 256) {
+    const size_t c = id / ((size_t)Hi * Wi);
+    const int q = (int)(id - c * Hi * Wi), i = q / Wi, j = q - i * Wi;
+    float s = 0.f;
+    for (int y = ri0[i]; y < ri0[i + 1]; ++y)
+      for (int x = rj0[j]; x < rj0[j + 1]; ++x) s += gout[(c * Ho + y) * Wo + x];
+    gin[id] = s;
+  }
+}
+hipError_t resample_nearest(const float* in, float* out, const int* maps, int BC, int Hi, int Wi, int Ho, int Wo,
+                            bool adjoint, hipStream_t s) {
+  const size_t n = (size_t)BC * (adjoint ? (size_t)Hi * Wi : (size_t)Ho * Wo);
+  const unsigned g = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+  if (adjoint)
+    hipLaunchKernelGGL(k_resample_adj, dim3(g), dim3(256), 0, s, in, out, maps, maps + Hi + 1, BC, Hi, Wi, Ho, Wo);
+  else
+    hipLaunchKernelGGL(k_resample, dim3(g), dim3(256), 0, s, in, out, maps, maps + Ho, BC, Hi, Wi, Ho, Wo);
+  return hipGetLastError();
+}
+
 hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
   if ((a.mi == nullptr) != (a.mj == nullptr)) return hipErrorInvalidValue;
   if (!a.mi && (a.Hs != a.Hl || a.Ws != a.Wl)) return hipErrorInvalidValue;

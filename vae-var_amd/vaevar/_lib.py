@@ -114,6 +114,7 @@ _SIGS = {
                                 P(c_double), P(c_double), P(c_double), c_double, c_int]),
     "vv_sc4dvar_closure": (c_int, [c_void_p, c_void_p, c_void_p, P(c_double), P(c_double), c_void_p]),
     "vv_sc4dvar_transform": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vv_resample_nearest": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
 }
 
 EXPORTED = sorted(_SIGS)

@@ -256,9 +256,34 @@ class VAE_lr:
     def decoder_hr(self, z):
         x = self.dec(z)
         if self.state_grid != tuple(x.shape[-2:]):
-            # nearest interpolation to the state grid (vae.py:90); the maps run in torch for now
-            x = torch.nn.functional.interpolate(x, self.state_grid)
+            # nearest interpolation to the state grid (vae.py:90) on the GPU (vv_resample_nearest), differentiable
+            x = resample_nearest(self.dec.ctx, x, self.state_grid)
         return x
+
+
+class _Resample(torch.autograd.Function):
+    @staticmethod
+    def forward(actx, x, ctx, size):
+        B, C, Hi, Wi = x.shape
+        out = torch.empty(B, C, size[0], size[1], device=x.device, dtype=torch.float32)
+        check(lib.vv_resample_nearest(ctx.h, _ptr(x.contiguous()), _ptr(out), B * C, Hi, Wi, size[0], size[1], 0,
+                                      _stream()), "resample_nearest")
+        actx.ctx, actx.shape = ctx, x.shape
+        return out
+
+    @staticmethod
+    def backward(actx, g):
+        B, C, Hi, Wi = actx.shape
+        gin = torch.empty(actx.shape, device=g.device, dtype=torch.float32)
+        check(lib.vv_resample_nearest(actx.ctx.h, _ptr(g.contiguous()), _ptr(gin), B * C, Hi, Wi, g.shape[2],
+                                      g.shape[3], 1, _stream()), "resample_nearest")
+        return gin, None, None
+
+
+def resample_nearest(ctx: Context, x: torch.Tensor, size) -> torch.Tensor:
+    """F.interpolate(x, size) (mode 'nearest', quirk Q3) of a (B, C, H, W) device tensor on libvaevar, with its
+    adjoint as the backward."""
+    return _Resample.apply(x, ctx, tuple(int(v) for v in size))
 
 
 class DAProblem:
