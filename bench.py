@@ -134,6 +134,41 @@ def cpu_baseline(prob_np, T, evals_per_iter, gpu_evals_per_analysis, evals, thre
     return per_eval, out, per_eval * gpu_evals_per_analysis
 
 
+def cpu_convergence_measured():
+    """The measured full CPU convergence of config 2 (tools/cpu_convergence.py on the GPU box's host cores: the
+    oracle restatement + torch.optim.LBFGS, Nit 10, weight grads on), committed under profiles/ (SURVEY §8 d)."""
+    for rnd in ("r02",):
+        try:
+            with open(os.path.join(ROOT, "profiles", rnd, "cpu_convergence_c2.jsonl")) as f:
+                rows = [json.loads(l) for l in f if l.strip().startswith("{")]
+            r = [x for x in rows if x.get("cpu_convergence")][-1]
+            return {"wall_clock_s": r["wall_clock_s"], "iters": r["iters"], "evals": r["evals"],
+                    "threads": r["threads"], "source": f"profiles/{rnd}/cpu_convergence_c2.jsonl (tools/cpu_convergence.py)"}
+        except (OSError, ValueError, KeyError, IndexError):
+            continue
+    return None
+
+
+def sc4dvar_line(dev_index: int):
+    """the sc4dvar mode (da_4dvar.py:1064-1177) on the same state (69ch 128x256): one Nit = 10 analysis
+    of LBFGS(10, max_iter 5) over the B-matrix transform closure, timed after a warm-up analysis."""
+    import torch
+
+    from vaevar.problem import make_problem
+    from vaevar.sc4dvar import BMatrix, Sc4dvarProblem, one_step_sc4dvar
+
+    bm = BMatrix.from_npz(os.path.join(ROOT, "tests", "golden", "bq_info_lr.npz"))
+    prob = Sc4dvarProblem(bm, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620), device=dev_index)
+    one_step_sc4dvar(prob, nit=10, log_terms=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = one_step_sc4dvar(prob, nit=10, log_terms=False)
+    dt = time.perf_counter() - t0
+    return {"workload": "sc4dvar (static B: SHT correlation, balance, vertical EOFs, winds), 69ch 128x256, T=1, "
+                        "Nit 10 x LBFGS max_iter 5", "iters_per_s": res["n_iter"] / dt, "wall_clock_s": dt,
+            "iters": res["n_iter"], "evals": res["n_eval"], "ms_per_eval": 1e3 * dt / max(res["n_eval"], 1)}
+
+
 def gemm_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes of `bench.py` (FETCH_SIZE x2 +
     WRITE_SIZE with the gfx950 corrections, tools/pmc_traffic.py); PMC counters cannot be read live."""
@@ -252,6 +287,7 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel-class profile")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (T=6) line section")
     ap.add_argument("--no-exact-f32", action="store_true", help="skip the exact-f32 GEMM analysis")
+    ap.add_argument("--no-sc4dvar", action="store_true", help="skip the sc4dvar (SURVEY §8 f4) section")
     ap.add_argument("--batch", type=int, default=1, help="independent analyses per GPU, evaluated in one batched "
                                                          "closure (B x 2048-row GEMMs)")
     ap.add_argument("--selftest", action="store_true", help="CPU stand-in analyses (tests the launch/aggregation)")
@@ -334,6 +370,10 @@ def main():
               "timed_region": "barrier + sync, one config-4 analysis per rank, RCCL gather of the analyses to rank 0, "
                               "sync + barrier; max over ranks"}
 
+    sc4 = None
+    if rank == 0 and not args.selftest and not args.no_sc4dvar:
+        sc4 = sc4dvar_line(w.local)
+
     if rank != 0:
         ensemble.barrier()
         return
@@ -377,6 +417,8 @@ def main():
                                     "rank 0, timed on its own"}
     if c4:
         out["config4"] = c4
+    if sc4:
+        out["sc4dvar"] = sc4
     if prof is not None:
         pr, prof_s = prof
         math = w.ctx.gemm_math
@@ -436,6 +478,10 @@ def main():
         out["cpu_baseline"] = cb
         out["cpu_wall_clock_to_convergence_s_extrapolated"] = cpu_conv
         out["speedup_vs_cpu"] = out["value"] / cb["value"]
+        meas = cpu_convergence_measured() if args.config == 2 and args.batch == 1 else None
+        if meas:
+            out["cpu_convergence_measured"] = meas
+            out["wall_clock_speedup_vs_cpu_measured"] = meas["wall_clock_s"] / per_analysis
     print(json.dumps(out), flush=True)
     ensemble.barrier()
 
