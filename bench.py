@@ -196,6 +196,7 @@ class GpuAnalyses:
         from vaevar.problem import make_problem
 
         self.torch = torch
+        local = local % max(torch.cuda.device_count(), 1)  # ranks beyond the visible GPUs share them (tests)
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
         self.cfg = CONFIGS[cfg_id]

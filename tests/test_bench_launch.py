@@ -1,10 +1,13 @@
 """CPU: bench.py's multi-rank path as the driver runs it — `bench.py --gpus 2` spawns its own two ranks (no
 WORLD_SIZE), they meet over gloo, every rank's analysis is gathered to rank 0, time is the max over ranks and
-iterations the sum — with the --selftest stand-in analysis (known outputs) in place of the GPU engine."""
+iterations the sum — with the --selftest stand-in analysis (known outputs) in place of the GPU engine; and (GPU)
+the same launch over the real engine."""
 import json
 import os
 import subprocess
 import sys
+
+import pytest
 
 from conftest import ROOT
 
@@ -39,3 +42,17 @@ def test_bench_spawns_its_ranks():
 def test_bench_world_size_must_match():
     p = _run("--gpus", "2", "--selftest", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_product_path():
+    """The product path with two ranks: `bench.py --gpus 2` spawns two processes that each run a full config-2
+    analysis on libvaevar (here both on the box's one GPU, over gloo since RCCL refuses two ranks per device), gather
+    both analyses to rank 0, take the max time and sum the iterations."""
+    p = _run("--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-profile", "--no-exact-f32",
+             "--no-config4", "--no-sc4dvar", env={"VAEVAR_DIST_BACKEND": "gloo"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    print({k: out[k] for k in ("n_gpus", "iters", "evals", "value", "gathered", "J_start", "J_final")})
+    assert out["n_gpus"] == 2 and out["gathered"] == [[69, 128, 256], [69, 128, 256]]
+    assert 150 <= out["iters"] <= 200 and out["J_final"] < 0.1 * out["J_start"]

@@ -17,10 +17,12 @@ def world():
 
 
 def init(backend: str | None = None):
+    """Process group of this rank; backend: "nccl" (RCCL) with a GPU, else "gloo" (VAEVAR_DIST_BACKEND overrides,
+    e.g. gloo for several ranks sharing one GPU in a test: RCCL refuses two ranks on one device)."""
     rank, size, local = world()
     if size > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("VAEVAR_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local)
@@ -44,10 +46,14 @@ def barrier():
         dist.barrier()
 
 
+def _cpu_backend() -> bool:
+    return dist.get_backend() == "gloo"
+
+
 def reduce_scalar(x: float, op: str, device=None) -> float:
     if not dist.is_initialized():
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=None if _cpu_backend() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -57,6 +63,7 @@ def gather_analyses(xa: torch.Tensor, dst: int = 0):
     if not dist.is_initialized():
         return [xa]
     rank, size = dist.get_rank(), dist.get_world_size()
-    out = [torch.empty_like(xa) for _ in range(size)] if rank == dst else None
-    dist.gather(xa.contiguous(), out, dst=dst)
+    x = xa.contiguous().cpu() if _cpu_backend() else xa.contiguous()
+    out = [torch.empty_like(x) for _ in range(size)] if rank == dst else None
+    dist.gather(x, out, dst=dst)
     return out
