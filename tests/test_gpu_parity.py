@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLD
+from conftest import GOLD, ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -416,3 +416,32 @@ def test_closure_edge_cases(tiny):
     e = rel((g2 - z).cpu(), (2 * (g1 - z)).cpu())
     print(f"obs_coeff linearity: grad rel {e:.1e}")
     assert e < 1e-6
+
+
+def test_ln_row_scales_bitwise(tmp_path):
+    """The fp16x3 GEMMs fed by a LayerNorm (qkv, fc1 forward; the proj and fc2 input gradients backward) take the row
+    scales the LayerNorm kernel wrote instead of a k_rowscale pass: the config-2 closure (J and dJ/dz) must be
+    bit-identical to the k_rowscale path (VAEVAR_LN_SCALES=0), run in two fresh processes."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys, numpy as np, torch; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "from vaevar import config as C\nfrom vaevar.engine import DAProblem, LGUnet\n"
+        "from vaevar.problem import make_problem\nfrom vaevar.synth import smooth_field\n"
+        "dec = LGUnet(C.DECODER, 1, 1).load_synthetic()\n"
+        "prob = DAProblem(dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))\n"
+        "z = torch.from_numpy(0.3 * smooth_field(11, (1, 32, 128, 256), sigma=2.0)).cuda()\n"
+        "g = torch.empty_like(z)\njb, jo = prob.closure(z, g)\n"
+        "np.save(sys.argv[1], np.concatenate([[jb, jo], g.cpu().numpy().ravel().astype(np.float64)]))\n"
+    ) % (os.path.join(ROOT, "vae-var_amd"), ROOT)
+    outs = []
+    for flag in ("1", "0"):
+        f = str(tmp_path / f"o{flag}.npy")
+        env = dict(os.environ, VAEVAR_LN_SCALES=flag)
+        p = subprocess.run([sys.executable, "-c", code, f], env=env, capture_output=True, text=True, timeout=280)
+        assert p.returncode == 0, p.stderr[-2000:]
+        outs.append(np.load(f))
+    print(f"LN row scales vs k_rowscale: J {outs[0][:2]} vs {outs[1][:2]}, grad max diff "
+          f"{np.abs(outs[0][2:] - outs[1][2:]).max():.1e}")
+    assert np.array_equal(outs[0], outs[1])

@@ -217,6 +217,7 @@ struct StageSave {
 
 struct Scratch {
   float *t1, *t2, *h, *dqkv;
+  float* rs;  // fp16x3 row scales of a LayerNorm output / input gradient, consumed by the GEMM that follows
   float* ws;  // GEMM tail-split partials (vv::gemm_ws_floats())
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic (the context's vv_set_gemm_math)
 };
@@ -520,10 +521,11 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     ln.map = idx;
     for (int g = 0; g < G; ++g)
       ln.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, sc.t1 + g * MC, sv.st1[b] + (size_t)g * M * 2,
-                 nullptr, nullptr};
+                 nullptr, nullptr, sc.rs + (size_t)g * M};
     CK(layernorm_fwd(ln, st));
-    // qkv
+    // qkv (A's fp16x3 row scales from LN1)
     GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc.math);
+    q.ascale = sc.rs;
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
     CK(gemm_nt(q, st, -1, sc.ws));
@@ -555,10 +557,11 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     LnArgs ln2 = ln_base(M, C, G, 1e-5f);
     for (int g = 0; g < G; ++g)
       ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, sc.t1 + g * MC, sv.st2[b] + (size_t)g * M * 2,
-                  nullptr, nullptr};
+                  nullptr, nullptr, sc.rs + (size_t)g * M};
     CK(layernorm_fwd(ln2, st));
-    // fc1 + GELU
+    // fc1 + GELU (row scales from LN2)
     GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc.math);
+    f1.ascale = sc.rs;
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, sc.h + g * MC * 4, nullptr,
                  sv.h1[b] + g * MC * 4};
@@ -582,6 +585,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
     GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc.math);
+    if (b < S.depth - 1) f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
     for (int g = 0; g < G; ++g)
       f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
     CK(gemm_nt(f2, st, -1, sc.ws));
@@ -592,10 +596,11 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     LnArgs ln2 = ln_base(M, C, G, 1e-5f);
     for (int g = 0; g < G; ++g)
       ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
-                  sc.t1 + g * MC, gx + g * MC};
+                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M};
     CK(layernorm_bwd(ln2, st));
     GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc.math);
     p.arow = idx;
+    p.ascale = sc.rs;  // per physical row of gx (the gather is applied to the scales too)
     for (int g = 0; g < G; ++g)
       p.g[g] = {gx + g * MC, nullptr, S.w[b][g].projWT, nullptr, sc.t2 + g * MC, nullptr, nullptr};
     CK(gemm_nt(p, st, -1, sc.ws));
@@ -623,7 +628,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     ln1.map = idx;
     for (int g = 0; g < G; ++g)
       ln1.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, nullptr, gx + g * MC, sv.st1[b] + (size_t)g * M * 2,
-                  sc.t1 + g * MC, gx + g * MC};
+                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M};
     CK(layernorm_bwd(ln1, st));
   }
   return 0;
@@ -694,6 +699,10 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
     m->sc.t2 = P.f(mx);
     m->sc.h = P.f(mx * 4);
     m->sc.dqkv = P.f(mx * 3);
+    size_t mrows = 0;
+    for (auto* st : {&m->enc0, &m->enc1, &m->dec1, &m->dec0}) mrows = std::max(mrows, (size_t)st->G * st->M);
+    for (auto& st : m->lg) mrows = std::max(mrows, (size_t)st.G * st.M);
+    m->sc.rs = P.f(mrows);
     m->sc.ws = P.f(vv::gemm_ws_floats());
     m->xm = P.f(G * M1 * 4 * c.C0);
     m->cat = P.f(M1 * G * c.C1);

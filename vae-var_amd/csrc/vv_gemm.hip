@@ -1046,6 +1046,13 @@ __global__ __launch_bounds__(256) void k_rowscale(GemmArgs args, float* __restri
   if (lane == 0) out[(size_t)blockIdx.z * args.M + r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
 }
 
+// out[z][r] = scales[z][arow[r]]: the producer's per-physical-row scales in the gathered GEMM's row order
+__global__ __launch_bounds__(256) void k_gather_scales(const float* __restrict__ scales, const int* __restrict__ arow,
+                                                       float* __restrict__ out, int M) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < M) out[(size_t)blockIdx.z * M + r] = scales[(size_t)blockIdx.z * M + arow[r]];
+}
+
 // BM = 128: 4 waves (2 x 2 of 64x64), 64 KB of LDS, two workgroups per CU. BM = 256: 8 waves (4 x 2 of 64x64),
 // 96 KB, one workgroup per CU: the same two waves per SIMD, but each B k-tile feeds 256 rows, so a CU stages 48 KB
 // (global loads and LDS stores) per 2 x 24 MFMAs per SIMD instead of 64 KB.
@@ -1254,8 +1261,15 @@ template <int BM>
 static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
   if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
   if (!h3_ready(a)) return launch_bs2(a, s);
-  float* sc = a.ws + kWsFloats;
-  hipLaunchKernelGGL(k_rowscale, dim3((a.M + 3) / 4, 1, a.ngroups), dim3(256), 0, s, a, sc);
+  const float* sc = a.ws + kWsFloats;
+  if (a.ascale_phys && !a.arow)
+    sc = a.ascale;  // row scales written by the producer of A (LayerNorm), already in GEMM row order
+  else if (a.ascale_phys)  // gathered A: the producer's scales permuted into GEMM row order (no pass over A)
+    hipLaunchKernelGGL(k_gather_scales, dim3((a.M + 255) / 256, 1, a.ngroups), dim3(256), 0, s, a.ascale, a.arow,
+                       const_cast<float*>(sc), a.M);
+  else
+    hipLaunchKernelGGL(k_rowscale, dim3((a.M + 3) / 4, 1, a.ngroups), dim3(256), 0, s, a,
+                       const_cast<float*>(sc));
   const size_t lds = 2 * (2 * (BM + 128) * 32) * sizeof(unsigned short);
   const int T = ((a.N + 127) / 128) * ((a.M + BM - 1) / BM);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
@@ -1449,6 +1463,17 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   a.tdp = 0;
   a.tsplit = 1;
   a.ws = ws;
+  a.ascale_phys = 0;
+  static int ln_scales = -1;  // VAEVAR_LN_SCALES=0: ignore producer scales, run k_rowscale for every fp16x3 GEMM
+  if (ln_scales < 0) {
+    const char* e = getenv("VAEVAR_LN_SCALES");
+    ln_scales = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (a.ascale && ln_scales) {
+    bool ok = true;
+    for (int g = 0; g < a.ngroups; ++g) ok = ok && !a.g[g].A2;
+    a.ascale_phys = ok ? 1 : 0;
+  }
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start

@@ -50,6 +50,10 @@ struct GemmArgs {
   int tdp, tsplit;
   float* ws;
   int math;  // GemmMath of this GEMM (the context's setting)
+  // GEMM_SPLIT16: null, or the row scales of A as its producer wrote them (LayerNorm rs), indexed by the physical A
+  // row (arow[r] when gathered), z * M + row; the fp16x3 kernels then skip k_rowscale (no concat A2 allowed)
+  const float* ascale;
+  int ascale_phys;  // set by gemm_nt: the kernel indexes its row scales by physical row
   GemmGroup g[kMaxGroups];
 };
 
@@ -97,6 +101,8 @@ struct LnGroup {
   float* stats;       // [rows][2] mean, rstd
   const float* dy;    // bwd: gradient wrt LN output
   const float* res;   // bwd: added to dx (may alias y), may be null
+  float* rs;          // null, or the fp16x3 GEMM row scale of every row written (k_rowscale's value, indexed by
+                      // the physical output row: fwd r, bwd map[r]); LN_ROWMAP only
 };
 
 struct LnArgs {

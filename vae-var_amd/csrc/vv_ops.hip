@@ -89,6 +89,18 @@ __device__ __forceinline__ float sub_sum(float v) {
   for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
+template <int L>
+__device__ __forceinline__ unsigned sub_max(unsigned v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
+  return v;
+}
+// the fp16x3 GEMM row scale of a row whose largest |value| has bit pattern mx (k_rowscale's formula, bit-identical)
+__device__ __forceinline__ float row_scale_of(unsigned mx) { return __uint_as_float((268u - max(mx >> 23, 15u)) << 23); }
+__device__ __forceinline__ unsigned absmax4(unsigned m, const f4& o) {
+  return max(max(m, max(__float_as_uint(fabsf(o[0])), __float_as_uint(fabsf(o[1])))),
+             max(__float_as_uint(fabsf(o[2])), __float_as_uint(fabsf(o[3]))));
+}
 
 // element offsets (relative to the input base, row stride ld) of this lane's float4s of output row r
 template <int L, int NV>
@@ -159,6 +171,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
   }
   const float rstd = 1.0f / sqrtf(sub_sum<L>(q) / (float)C + a.eps);
   float* y = G.y + (size_t)r * a.ldy;
+  unsigned mx = 0;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int j = sl + v * L;
@@ -169,7 +182,12 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (xv[v][e] - mean) * rstd * g[e] + b[e];
       *reinterpret_cast<f4*>(y + 4 * j) = o;
+      mx = absmax4(mx, o);
     }
+  }
+  if (G.rs) {
+    mx = sub_max<L>(mx);
+    if (sl == 0) G.rs[r] = row_scale_of(mx);
   }
   if (sl == 0 && G.stats) {
     G.stats[2 * r] = mean;
@@ -210,6 +228,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
   const float m1 = sub_sum<L>(s1) / (float)C;
   const float m2 = sub_sum<L>(s2) / (float)C;
   // second pass re-reads the row (L1/L2-resident) instead of holding it in registers
+  unsigned mx = 0;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int j = sl + v * L;
@@ -226,7 +245,12 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
         for (int e = 0; e < 4; ++e) o[e] += rr[e];
       }
       *reinterpret_cast<f4*>(G.y + eo[v]) = o;
+      mx = absmax4(mx, o);
     }
+  }
+  if (G.rs) {  // LN_ROWMAP: the row written is map[r]
+    mx = sub_max<L>(mx);
+    if (sl == 0) G.rs[a.map ? a.map[r] : r] = row_scale_of(mx);
   }
 }
 
@@ -246,6 +270,8 @@ static hipError_t ln_launch(const LnArgs& a, hipStream_t s) {
   if ((a.ldx & 3) || (a.ldy & 3) || (a.lddy & 3) || (a.ldres & 3)) return hipErrorInvalidValue;
   if (a.mode == LN_MERGE && ((a.C / 4) & 3)) return hipErrorInvalidValue;
   if (!FWD && (a.ldy != a.ldx || (a.g[0].res && a.ldres != a.ldx))) return hipErrorInvalidValue;
+  for (int g = 0; g < a.ngroups; ++g)
+    if (a.g[g].rs && a.mode != LN_ROWMAP) return hipErrorInvalidValue;
   const int L = ln_lanes(a.C);
   const int need = (a.C / 4 + L - 1) / L;
   const int NV = need <= 1 ? 1 : need <= 2 ? 2 : need <= 3 ? 3 : need <= 5 ? 5 : 8;
