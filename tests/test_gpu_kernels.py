@@ -80,10 +80,10 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
 _keep = []
 
 
-@pytest.mark.parametrize("tile", [36, 44])
+@pytest.mark.parametrize("tile", [36, 44, 46, 47])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
 def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):
-    """fp16x3 split (tiles 36 = 128x128, 44 = 256x128 of 8 waves) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
+    """fp16x3 split (tiles 36 = 128x128, 44 = 256x128 of 8 waves, 46 / 47 the same on 16x16x32 MFMAs) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
     (per-chunk scales), B rows span 2^+-8, with zeros, a zero row and huge/tiny values: no overflow, no flush."""
     g = torch.Generator().manual_seed(M + N + K + 1)
     A = torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-12, 12, generator=g)) \
@@ -108,22 +108,22 @@ def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):
 
 
 def test_gemm_rejects_non_library_tiles(ctx):
-    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44): any other hint, e.g. the r01
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47): any other hint, e.g. the r01
     timing experiments 37-39, returns VV_E_ARG instead of running something."""
     from vaevar._lib import VVError
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 35, 37, 38, 39, 40, 41, 42, 45, 1000):
+    for t in (1, 3, 21, 35, 37, 38, 39, 40, 41, 42, 45, 48, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
-    for t in (0, 2, 4, 24, 34, 36, 44):
+    for t in (0, 2, 4, 24, 34, 36, 44, 46, 47):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [36, 44])
+@pytest.mark.parametrize("tile", [36, 44, 46, 47])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 4608), (2048, 4608, 1152), (2048, 1152, 3456)])
 def test_gemm_splitk_deterministic(ctx, M, N, K, tile):
     """fp16x3 GEMMs whose tiles are split along K (every tile at N = 1152, the tail at N = 4608): the fixup sums

@@ -69,8 +69,16 @@ class Sc4dvarProblem:
 
         self.xb, self.yo, self.H, self.R = t(prob["xb"]), t(prob["yo"]), t(prob["H"]), t(prob["R"])
         self.mean, self.std = t(prob["mean"]), t(prob["std"])
+        if self.xb.dim() != 3 or self.xb.shape[0] != 69:
+            raise ValueError(f"xb must be (69, Hs, Ws), got {tuple(self.xb.shape)}")
         self.C, self.Hs, self.Ws = self.xb.shape
+        if self.yo.dim() != 4 or self.yo.shape[-2:] != self.xb.shape[-2:]:
+            raise ValueError(f"yo must be (T, C_obs, {self.Hs}, {self.Ws}), got {tuple(self.yo.shape)}")
+        if self.H.shape != self.yo.shape or self.R.shape[-2:] != self.yo.shape[-2:] or self.R.shape[0] != self.yo.shape[0]:
+            raise ValueError("H must match yo; R must be (T, C_obs, Hs, Ws)")
         self.T = self.yo.shape[0]
+        if self.T > 1 and flow is None:
+            raise ValueError("a window of T > 1 needs the flow model")
         self.ctx = flow.ctx if flow is not None else Context.get(device)
         self.obs_coeff = float(obs_coeff)
         self.bmat, self.flow = bmat, flow
@@ -78,6 +86,9 @@ class Sc4dvarProblem:
             obs_interp = prob.get("interp")
         self.interp = None if obs_interp is None else t(obs_interp)
         n_out = self.interp.shape[0] if self.interp is not None else 0
+        c_obs = 4 + 5 * n_out if n_out else self.C
+        if self.yo.shape[1] != c_obs or self.R.shape[1] != c_obs:
+            raise ValueError(f"yo / R have {self.yo.shape[1]} / {self.R.shape[1]} channels, expected {c_obs}")
         self.w_shape = (self.C, 128, 256)
         b = bmat
         check(lib.vv_sc4dvar_bind(self.ctx.h, flow.id if flow is not None else -1, self.T, self.C, self.Hs, self.Ws,
