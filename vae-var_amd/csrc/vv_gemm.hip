@@ -309,18 +309,29 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup(GemmArgs args) {
   const int m0 = mb * BM, n0 = nb * BN;
   const size_t items = (size_t)gridDim.x * S;
   const float* w = args.ws + ((size_t)blockIdx.z * items + (size_t)blockIdx.x * S) * (size_t)(NREG * NT);
+  // all NREG loads of one chunk in flight together, chunks summed in order (bit-identical to a per-register
+  // chain, one memory latency per chunk instead of one per register and chunk)
   accv acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const size_t j = (size_t)((a * TN + b) * NR + r) * NT + tid;
-        float v = w[j];
-        for (int c = 1; c < S; ++c) v += w[(size_t)c * NREG * NT + j];
-        acc[a][b][r] = v;
-      }
+      for (int r = 0; r < NR; ++r) acc[a][b][r] = w[(size_t)((a * TN + b) * NR + r) * NT + tid];
+  for (int c = 1; c < S; ++c) {
+    const float* wc = w + (size_t)c * NREG * NT;
+    accv t[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) t[a][b][r] = wc[(size_t)((a * TN + b) * NR + r) * NT + tid];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] += t[a][b];
+  }
   const int wm = wave / WN, wn = wave % WN;
   const int rin = lane & (MF - 1), hh = lane / MF;
   if (m0 + BM <= M && n0 + BN <= N)
@@ -349,12 +360,15 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup_sub(GemmArgs args) 
   const size_t items = (size_t)gridDim.x * S;
   const float* w = args.ws + ((size_t)blockIdx.z * items + (size_t)blockIdx.x * S) * (size_t)(NREG * NT);
   accv acc[1][1];
+  const size_t j0 = (size_t)((a * TN + b) * 16) * NT + tid;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const size_t j = (size_t)((a * TN + b) * 16 + r) * NT + tid;
-    float v = w[j];
-    for (int c = 1; c < S; ++c) v += w[(size_t)c * NREG * NT + j];
-    acc[0][0][r] = v;
+  for (int r = 0; r < 16; ++r) acc[0][0][r] = w[j0 + (size_t)r * NT];
+  for (int c = 1; c < S; ++c) {  // one chunk's 16 loads in flight together, chunks summed in order
+    const float* wc = w + (size_t)c * NREG * NT + j0;
+    accv t;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = wc[(size_t)r * NT];
+    acc[0][0] += t;
   }
   const int m0 = mb * BM + wm * TM * 32 + a * 32, n0 = nb * BN + wn * TN * 32 + b * 32;
   const int rin = lane & 31, hh = lane >> 5;
