@@ -64,7 +64,10 @@ static int device_cus() {
 // GEMM epilogue. 32x32: acc[a][b][r] -> row (r&3) + 8(r>>2) + 4h, col lane&31; 16x16: row 4h + r,
 // col lane&15 (h = lane>>4). Everything an element needs (bias, output row, residual, pre-activation) is
 // loaded for the whole fragment first, so the stores are not serialised behind one dependent load each;
-// FULL tiles skip all bounds checks.
+// FULL tiles skip all bounds checks. The optional bias and row-map loads are issued unconditionally (from a
+// dummy address, G.A, when the pointer is null) and selected afterwards: a load under a branch leaves the
+// compiler unable to count outstanding memory operations, and it then waits for ALL of them (vmcnt(0)) --
+// the next tile's prefetched A in a persistent kernel, and in partial tiles every previous store.
 template <int BM, int BN, int WM, int WN, int EPI, int MF, bool FULL, typename ACC>
 __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& G, ACC& acc, int m0, int n0, int wm,
                                          int wn, int rin, int hh) {
@@ -78,7 +81,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& 
   for (int b = 0; b < TN; ++b) {
     colv[b] = n0 + wn * TN * MF + b * MF + rin;
     const int cc = FULL ? colv[b] : min(colv[b], N - 1);
-    bv[b] = G.bias ? G.bias[cc] : 0.0f;
+    const float t = *(G.bias ? G.bias + cc : G.A);
+    bv[b] = G.bias ? t : 0.0f;
   }
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
@@ -87,7 +91,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& 
     for (int r = 0; r < NR; ++r) {
       const int row = m0 + wm * TM * MF + a * MF + (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * hh : 4 * hh + r);
       const int rc = FULL ? row : min(row, M - 1);
-      ov[r] = args.crow ? args.crow[rc] : rc;
+      const int t = *(args.crow ? args.crow + rc : reinterpret_cast<const int*>(G.A));
+      ov[r] = args.crow ? t : rc;
     }
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
