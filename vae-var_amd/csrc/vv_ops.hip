@@ -102,14 +102,15 @@ __device__ __forceinline__ unsigned absmax4(unsigned m, const f4& o) {
              max(__float_as_uint(fabsf(o[2])), __float_as_uint(fabsf(o[3]))));
 }
 
-// element offsets (relative to the input base, row stride ld) of this lane's float4s of output row r
+// element offsets (relative to the input base, row stride ld) of this lane's float4s of output row r; float4
+// indices past the row end are clamped to its last float4 (always a valid address)
 template <int L, int NV>
 __device__ __forceinline__ void ln_offsets(const LnArgs& a, int r, int sl, int ld, size_t (&eo)[NV]) {
   const int C = a.C, f4n = C >> 2;
   if (a.mode == LN_ROWMAP) {
     const size_t base = (size_t)(a.map ? a.map[r] : r) * ld;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) eo[v] = base + 4 * (sl + v * L);
+    for (int v = 0; v < NV; ++v) eo[v] = base + 4 * min(sl + v * L, f4n - 1);
   } else if (a.mode == LN_MERGE) {
     const int Hh = a.Hin >> 1, Wh = a.Win >> 1;
     const int b = r / (Hh * Wh);
@@ -122,7 +123,7 @@ __device__ __forceinline__ void ln_offsets(const LnArgs& a, int r, int sl, int l
       tb[q] = (size_t)((b * a.Hin + 2 * h + (q & 1)) * a.Win + 2 * w + (q >> 1)) * ld;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int c = 4 * (sl + v * L);
+      const int c = 4 * min(sl + v * L, f4n - 1);
       const int q = min(c / Cs, 3);
       eo[v] = tb[q] + (c - q * Cs);
     }
@@ -133,11 +134,13 @@ __device__ __forceinline__ void ln_offsets(const LnArgs& a, int r, int sl, int l
     const int y = rem / Wo, x = rem - y * Wo;
     const size_t base = (size_t)((b * a.Hin + (y >> 1)) * a.Win + (x >> 1)) * ld + ((y & 1) * 2 + (x & 1)) * C;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) eo[v] = base + 4 * (sl + v * L);
+    for (int v = 0; v < NV; ++v) eo[v] = base + 4 * min(sl + v * L, f4n - 1);
   }
-  (void)f4n;
 }
 
+// Every global load of a row (x, gamma, beta; dy, res) is issued up front and unconditionally (lanes past the
+// row end re-read its last float4 and contribute 0): one memory round trip per row instead of one per pass, and
+// no loads under branches (which make the compiler wait for all outstanding memory operations).
 template <int L, int NV>
 __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
   constexpr int RPB = 256 / L;
@@ -148,25 +151,33 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
   const int C = a.C, f4n = C >> 2;
   size_t eo[NV];
   ln_offsets<L, NV>(a, r, sl, a.ldx, eo);
-  f4 xv[NV];
+  f4 xv[NV], gv[NV], bv[NV];
+  bool ok[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int j = sl + v * L;
+    ok[v] = j < f4n;
+    const int jj = ok[v] ? j : f4n - 1;
+    xv[v] = *reinterpret_cast<const f4*>(G.x + eo[v]);
+    gv[v] = *reinterpret_cast<const f4*>(G.gamma + 4 * jj);
+    bv[v] = *reinterpret_cast<const f4*>(G.beta + 4 * jj);
+  }
+  // masked operands, not masked sums: the accumulations keep the exact form (and FMA contraction) of the
+  // per-element branches they replace, so the results are bit-identical
   float s = 0.f;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    if (sl + v * L < f4n) {
-      xv[v] = *reinterpret_cast<const f4*>(G.x + eo[v]);
-      s += (xv[v][0] + xv[v][1]) + (xv[v][2] + xv[v][3]);
-    }
+    const f4 x = ok[v] ? xv[v] : f4{0.f, 0.f, 0.f, 0.f};
+    s += (x[0] + x[1]) + (x[2] + x[3]);
   }
   const float mean = sub_sum<L>(s) / (float)C;
   float q = 0.f;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    if (sl + v * L < f4n) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = xv[v][e] - mean;
-        q += d * d;
-      }
+    for (int e = 0; e < 4; ++e) {
+      const float d = ok[v] ? xv[v][e] - mean : 0.f;
+      q += d * d;
     }
   }
   const float rstd = 1.0f / sqrtf(sub_sum<L>(q) / (float)C + a.eps);
@@ -175,12 +186,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int j = sl + v * L;
-    if (j < f4n) {
-      const f4 g = *reinterpret_cast<const f4*>(G.gamma + 4 * j);
-      const f4 b = *reinterpret_cast<const f4*>(G.beta + 4 * j);
-      f4 o;
+    f4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (xv[v][e] - mean) * rstd * g[e] + b[e];
+    for (int e = 0; e < 4; ++e) o[e] = (xv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
+    if (ok[v]) {
       *reinterpret_cast<f4*>(y + 4 * j) = o;
       mx = absmax4(mx, o);
     }
@@ -196,7 +205,8 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
 }
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)), written back at the input position (+ res);
-// x, dx and res share the input layout (ldx == ldy == ldres, checked on the host)
+// x, dx and res share the input layout (ldx == ldy == ldres, checked on the host). The row (x, dy, gamma, res)
+// stays in registers between the two reductions and the write.
 template <int L, int NV>
 __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
   constexpr int RPB = 256 / L;
@@ -209,41 +219,43 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
   ln_offsets<L, NV>(a, r, sl, a.ldx, eo);
   const float mean = G.stats[2 * r], rstd = G.stats[2 * r + 1];
   const float* dy = G.dy + (size_t)r * a.lddy;
-  float s1 = 0.f, s2 = 0.f;
+  const float* res = G.res ? G.res : G.x;  // dummy source when there is no residual (never added)
+  f4 xv[NV], dv[NV], gv[NV], rv[NV];
+  bool ok[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int j = sl + v * L;
-    if (j < f4n) {
-      const f4 x = *reinterpret_cast<const f4*>(G.x + eo[v]);
-      const f4 d = *reinterpret_cast<const f4*>(dy + 4 * j);
-      const f4 g = *reinterpret_cast<const f4*>(G.gamma + 4 * j);
+    ok[v] = j < f4n;
+    const int jj = ok[v] ? j : f4n - 1;
+    xv[v] = *reinterpret_cast<const f4*>(G.x + eo[v]);
+    dv[v] = *reinterpret_cast<const f4*>(dy + 4 * jj);
+    gv[v] = *reinterpret_cast<const f4*>(G.gamma + 4 * jj);
+    rv[v] = *reinterpret_cast<const f4*>(res + eo[v]);
+  }
+  float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float gd = g[e] * d[e];
-        s1 += gd;
-        s2 += gd * ((x[e] - mean) * rstd);
-      }
+  for (int v = 0; v < NV; ++v) {
+    const f4 d = ok[v] ? dv[v] : f4{0.f, 0.f, 0.f, 0.f};  // masked operand (see k_ln_fwd): gd = 0 adds nothing
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gd = gv[v][e] * d[e];
+      s1 += gd;
+      s2 += gd * ((xv[v][e] - mean) * rstd);
     }
   }
   const float m1 = sub_sum<L>(s1) / (float)C;
   const float m2 = sub_sum<L>(s2) / (float)C;
-  // second pass re-reads the row (L1/L2-resident) instead of holding it in registers
   unsigned mx = 0;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    const int j = sl + v * L;
-    if (j < f4n) {
-      const f4 x = *reinterpret_cast<const f4*>(G.x + eo[v]);
-      const f4 d = *reinterpret_cast<const f4*>(dy + 4 * j);
-      const f4 g = *reinterpret_cast<const f4*>(G.gamma + 4 * j);
-      f4 o;
+    f4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = rstd * (g[e] * d[e] - m1 - ((x[e] - mean) * rstd) * m2);
-      if (G.res) {
-        const f4 rr = *reinterpret_cast<const f4*>(G.res + eo[v]);
+    for (int e = 0; e < 4; ++e) o[e] = rstd * (gv[v][e] * dv[v][e] - m1 - ((xv[v][e] - mean) * rstd) * m2);
+    if (G.res) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += rr[e];
-      }
+      for (int e = 0; e < 4; ++e) o[e] += rv[v][e];
+    }
+    if (ok[v]) {
       *reinterpret_cast<f4*>(G.y + eo[v]) = o;
       mx = absmax4(mx, o);
     }
