@@ -329,11 +329,11 @@ hipError_t layernorm_bwd(const LnArgs& a, hipStream_t s) {
 // ============================================================================
 constexpr int WN_ = 16;
 
-__device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* table, int win, int h, int i,
-                                                int j) {
+// tb: this block's heads' slices of the relative-position table, staged in LDS as [hl][(2ws-1)^2]
+__device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* tb, int win, int hl, int i, int j) {
   const int ws = a.ws;
   const int ri = i / ws, ci = i - ri * ws, rj = j / ws, cj = j - rj * ws;
-  float b = table[((ri - rj + ws - 1) * (2 * ws - 1) + (ci - cj + ws - 1)) * a.heads + h];
+  float b = tb[hl * (2 * ws - 1) * (2 * ws - 1) + (ri - rj + ws - 1) * (2 * ws - 1) + (ci - cj + ws - 1)];
   if (a.shift > 0) {
     // quirk Q1 (swinblock.py:240-258): labels depend on the (shifted-frame) row only
     const int wr = (win % (a.nWh * a.nWw)) / a.nWw;
@@ -437,8 +437,17 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_fwd(AttnArgs a) {
   float* q = sm;
   float* k = q + WN_ * S.st;
   float* v = k + WN_ * S.st;
-  float* p = v + WN_ * S.st;  // [hpb][16][17]
+  float* p = v + WN_ * S.st;          // [hpb][16][17]
+  float* tb = p + S.hpb * WN_ * 17;   // [hpb][49]: the block's relative-position bias (ws = 4)
   const float* base = G.qkv + (size_t)win * WN_ * ldq + h0 * S.hd;
+  // the bias slice is loaded with the q/k/v rows (one memory round trip), not inside the score loop
+  constexpr int NTB = 49;
+  float tv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = min(tid + i * kAttnThreads, S.hpb * NTB - 1);
+    tv[i] = G.table[(idx % NTB) * a.heads + h0 + idx / NTB];
+  }
   if (W <= 192) {
     const float* const srcs[3] = {base, base + C, base + 2 * C};
     const int lds_[3] = {ldq, ldq, ldq};
@@ -449,6 +458,9 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_fwd(AttnArgs a) {
     attn_rows(base + C, ldq, k, S.st, W);
     attn_rows(base + 2 * C, ldq, v, S.st, W);
   }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (tid + i * kAttnThreads < S.hpb * NTB) tb[tid + i * kAttnThreads] = tv[i];
   __syncthreads();
   // S = (q k^T) scale + bias + mask -> softmax (swinblock.py:151-168)
   const int dpi = tid % S.dp;
@@ -459,7 +471,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_fwd(AttnArgs a) {
     float mx = -INFINITY;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      sv[jj] = sv[jj] * a.scale + attn_bias_mask(a, G.table, win, h, i, j0 + jj);
+      sv[jj] = sv[jj] * a.scale + attn_bias_mask(a, tb, win, hl, i, j0 + jj);
       mx = fmaxf(mx, sv[jj]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, S.dp));
@@ -516,6 +528,12 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_bwd(AttnArgs a) {
   float* ds = p + S.hpb * WN_ * 17;  // [hpb][16][17]
   const float* base = G.qkv + (size_t)win * WN_ * ldq + h0 * S.hd;
   const float* dOb = G.dO + (size_t)win * WN_ * C + h0 * S.hd;
+  // the block's P (hpb x 16 x 16 <= 3 per thread for hpb <= 3) is loaded with the rows: one round trip
+  const float* Pg = G.P + ((size_t)win * a.heads + h0) * WN_ * WN_;
+  const int np = S.hpb * WN_ * WN_;
+  float pv[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pv[i] = Pg[min(tid + i * kAttnThreads, np - 1)];
   if (W <= 192) {
     const float* const srcs[4] = {base, base + C, base + 2 * C, dOb};
     const int lds_[4] = {ldq, ldq, ldq, C};
@@ -527,8 +545,12 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_bwd(AttnArgs a) {
     attn_rows(base + 2 * C, ldq, v, S.st, W);
     attn_rows(dOb, C, dO, S.st, W);
   }
-  const float* Pg = G.P + ((size_t)win * a.heads + h0) * WN_ * WN_;
-  for (int idx = tid; idx < S.hpb * WN_ * WN_; idx += kAttnThreads) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int idx = tid + i * kAttnThreads;
+    if (idx < np) p[(idx >> 4) * 17 + (idx & 15)] = pv[i];
+  }
+  for (int idx = tid + 3 * kAttnThreads; idx < np; idx += kAttnThreads) p[(idx >> 4) * 17 + (idx & 15)] = Pg[idx];
   __syncthreads();
   // dP = dO v^T ; dS = P (dP - rowsum(P dP))
   const int dpi = tid % S.dp;
@@ -597,7 +619,8 @@ static bool attn_ok(const AttnArgs& a) {
 hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
   if (!attn_ok(a)) return hipErrorInvalidValue;
   const int hpb = attn_hpb(a), st = hpb * (a.C / a.heads) + 4;
-  const size_t lds = (3 * WN_ * st + hpb * WN_ * 17) * sizeof(float);
+  if (2 * kAttnThreads < hpb * 49) return hipErrorInvalidValue;  // the staged bias slice (ws = 4)
+  const size_t lds = (3 * WN_ * st + hpb * WN_ * 17 + hpb * 49) * sizeof(float);
   const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
   prof_end(ph, s, PC_ATTN, 4.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
