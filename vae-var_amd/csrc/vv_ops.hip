@@ -1182,9 +1182,11 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* x, int64_t n, double
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = t;
 }
-__global__ __launch_bounds__(256) void k_dot(const float* a, const float* b, int64_t n, double* partial) {
+__global__ __launch_bounds__(256) void k_dot(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                             double* partial) {
   __shared__ double red[4];
   double acc = 0.0;
+#pragma unroll 4
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     acc += (double)a[i] * (double)b[i];
   const double t = block_sum(acc, red);
@@ -1286,7 +1288,7 @@ hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s) {
 // history pair instead of 3
 constexpr int kTwoLoopBlocks = 256;
 __global__ __launch_bounds__(256) void k_twoloop_axpy(float* y, const float* x, const double* partial, int nblk,
-                                                      float ro, float* al, int i, int mode, int64_t n) {
+                                                      float ro, float* al, int i, int mode, int64_t n, int vec4) {
   __shared__ double red[4];
   __shared__ float coef;
   double acc = 0.0;
@@ -1303,20 +1305,47 @@ __global__ __launch_bounds__(256) void k_twoloop_axpy(float* y, const float* x, 
   }
   __syncthreads();
   const float a = coef;
+  if (vec4) {
+    // float4 view (n % 4 == 0, 16-B aligned; checked on the host), four float4 of y and x per thread in flight
+    // together: the scalar loop's stores to y kept every next load behind them (x and y may alias for the
+    // compiler), one memory round trip per element
+    f4* y4 = reinterpret_cast<f4*>(y);
+    const f4* x4 = reinterpret_cast<const f4*>(x);
+    const int64_t n4 = n >> 2, G = (int64_t)gridDim.x * 256;
+    for (int64_t b = blockIdx.x * 256 + threadIdx.x; b < n4; b += 4 * G) {
+      f4 xv[4], yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t k = min(b + u * G, n4 - 1);
+        xv[u] = x4[k];
+        yv[u] = y4[k];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (b + u * G < n4) {
+          f4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = yv[u][e] + a * xv[u][e];
+          y4[b + u * G] = o;
+        }
+    }
+    return;
+  }
   for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) y[k] = y[k] + a * x[k];
 }
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,
                           int64_t n, double* partial, int nblk, float* al, hipStream_t s) {
+  auto v4 = [&](const float* x) { return (n % 4 == 0 && ((uintptr_t)q % 16) == 0 && ((uintptr_t)x % 16) == 0) ? 1 : 0; };
   for (int i = m - 1; i >= 0; --i) {
     hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, S[i], q, n, partial);
     hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, Y[i], partial, nblk, ro[i], al, i, 0,
-                       n);
+                       n, v4(Y[i]));
   }
   hipLaunchKernelGGL(k_scale, dim3(vgrid(n)), dim3(256), 0, s, q, H_diag, n);
   for (int i = 0; i < m; ++i) {
     hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, Y[i], q, n, partial);
     hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, S[i], partial, nblk, ro[i], al, i, 1,
-                       n);
+                       n, v4(S[i]));
   }
   return hipGetLastError();
 }
