@@ -13,6 +13,7 @@
 #include "vv_kernels.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <mutex>
 #include <utility>
@@ -142,9 +143,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nt) {
 // the n-blocks, so a contiguous range of logical tiles (what xcd_remap hands one XCD) covers a compact
 // GM x (range/GM) block of the output and its A/B panels are re-read from that XCD's L2, not the fabric.
 constexpr int kGroupM = 8;
-__device__ __forceinline__ void tile_mn(int t, int ntm, int ntn, int& mb, int& nb) {
-  const int g = t / (kGroupM * ntn), m0 = g * kGroupM;
-  const int gm = min(kGroupM, ntm - m0), r = t - g * kGroupM * ntn;
+// gm > 0: the launch's group size (GemmArgs.gm, chosen per shape by gemm_nt); the kernels without it use kGroupM
+__device__ __forceinline__ void tile_mn(int t, int ntm, int ntn, int& mb, int& nb, int GM = kGroupM) {
+  GM = GM > 0 ? GM : kGroupM;
+  const int g = t / (GM * ntn), m0 = g * GM;
+  const int gm = min(GM, ntm - m0), r = t - g * GM * ntn;
   mb = m0 + r % gm;
   nb = r / gm;
 }
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup(GemmArgs args) {
   const int S = args.tsplit;
   const int tile = args.tdp + blockIdx.x;
   int mb = tile / ntn, nb = tile % ntn;
-  if (GROUPED) tile_mn(tile, (M + BM - 1) / BM, ntn, mb, nb);
+  if (GROUPED) tile_mn(tile, (M + BM - 1) / BM, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const size_t items = (size_t)gridDim.x * S;
   const float* w = args.ws + ((size_t)blockIdx.z * items + (size_t)blockIdx.x * S) * (size_t)(NREG * NT);
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup_sub(GemmArgs args) 
   const int S = args.tsplit;
   const int tile = args.tdp + blockIdx.x;
   int mb, nb;
-  tile_mn(tile, ntm, ntn, mb, nb);
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int a = blockIdx.y / TN, b = blockIdx.y % TN;
   const int wm = wave / WN, wn = wave % WN;
   const size_t items = (size_t)gridDim.x * S;
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
     ke = ((c + 1) * nkt) / S;
   }
   int mb, nb;
-  tile_mn(tile, ntm, ntn, mb, nb);
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const int lr = tid / TPR, lc = (tid % TPR) * 4;
   // LDS element offset of (row, k) within a plane: 16-B chunk k/8 XOR-swizzled by (row >> 2) & 3
@@ -785,7 +788,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bs2(GemmArgs args) {
     ke = ((c + 1) * nkt) / S;
   }
   int mb, nb;
-  tile_mn(tile, ntm, ntn, mb, nb);
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const int lr = tid / TPR, lc = (tid % TPR) * 4;
   auto swz = [](int row, int k) { return row * LSB + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); };
@@ -1144,7 +1147,7 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3(GemmArgs args, const floa
     ke = ((c + 1) * nkt) / S;
   }
   int mb, nb;
-  tile_mn(tile, ntm, ntn, mb, nb);
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const int lr = tid / TPR, lc = (tid % TPR) * 4;
   auto swz = [](int row, int k) { return row * LSB + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); };
@@ -1327,7 +1330,7 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3m(GemmArgs args, const flo
     ke = ((c + 1) * nkt) / S;
   }
   int mb, nb;
-  tile_mn(tile, ntm, ntn, mb, nb);
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const int lr = tid / TPR, lc = (tid % TPR) * 4;
   // 16-B chunk c of row r at chunk c ^ h((r >> 2) & 3), h = {0, 2, 3, 1}: the four lane groups of a ds_read_b128
@@ -1730,6 +1733,16 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   a.tdp = 0;
   a.tsplit = 1;
   a.ws = ws;
+  {
+    // grouped tile order: one XCD runs ~T/8 consecutive logical tiles, a gm x (T/8/gm) block re-reading gm A
+    // m-blocks (BM rows) and T/8/gm B n-blocks (BN rows); gm = sqrt(T/8 x BN/BM) minimises those bytes
+    // (2048 x 3456 x 1152 on 256 x 128 tiles: 8 -> 4, FETCH 94 -> 73 MB per launch, profiles/r02/tile_group/)
+    int bm, bn, bk;
+    variant_tile(t, bm, bn, bk);
+    const int ntm = (a.M + bm - 1) / bm, ntn = (a.N + bn - 1) / bn;
+    const double tx = (double)ntm * ntn / 8.0;
+    a.gm = std::max(1, std::min(ntm, (int)std::lround(std::sqrt(tx * bn / bm))));
+  }
   a.ascale_phys = 0;
   static int ln_scales = -1;  // VAEVAR_LN_SCALES=0: ignore producer scales, run k_rowscale for every fp16x3 GEMM
   if (ln_scales < 0) {

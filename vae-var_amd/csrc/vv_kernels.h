@@ -48,6 +48,9 @@ struct GemmArgs {
   // tail split (filled in by gemm_nt): the first tdp tiles run whole; each remaining tile is split into
   // tsplit k-chunks whose fp32 partials go to ws and are summed (in chunk order) by the fixup kernel
   int tdp, tsplit;
+  // m-blocks per group of the grouped tile order (filled in by gemm_nt: ~sqrt(tiles per XCD x BN / BM), so the
+  // block of tiles one XCD runs re-reads the least A + B through the fabric)
+  int gm;
   float* ws;
   int math;  // GemmMath of this GEMM (the context's setting)
   // GEMM_SPLIT16: null, or the row scales of A as its producer wrote them (LayerNorm rs), indexed by the physical A
