@@ -114,7 +114,7 @@ def test_gemm_rejects_non_library_tiles(ctx):
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 48, 1000):
+    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 48, 49, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
@@ -216,3 +216,4 @@ def test_resample_nearest_matches_interpolate(ctx, src, dst):
     xr = x.clone().requires_grad_(True)
     torch.nn.functional.interpolate(xr, dst).backward(cot)
     assert float((xd.grad.cpu() - xr.grad).abs().max()) <= 1e-5 * float(xr.grad.abs().max())
+

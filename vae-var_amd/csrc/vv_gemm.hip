@@ -1481,7 +1481,6 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3m(GemmArgs args, const flo
     epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
-
 template <int EPI, int BM>
 static hipError_t launch_h3m_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc) {
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h3m<EPI, BM>, lds)) return e;
@@ -1546,9 +1545,8 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
 //   exact f32 MFMA   0: 128x128   2: 64x64   4: 32x64            (GEMM_F32)
 //   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
 //   fp16x3 split    36: 128x128, 44: 256x128 (8 waves of 64x64); 46 / 47: the same on 16x16x32 MFMAs
-bool valid_tile(int t) {
-  return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || t == 36 || t == 44 || t == 46 || t == 47;
-}
+static bool h3_tile(int t) { return t == 36 || t == 44 || t == 46 || t == 47; }
+bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || h3_tile(t); }
 
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
@@ -1777,7 +1775,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
         a.tdp = tdp;
         a.tsplit = S;
       }
-    } else if (tdp == 0 && (t == 36 || t == 44 || t == 46 || t == 47) && small_split_enabled()) {
+    } else if (tdp == 0 && h3_tile(t) && small_split_enabled()) {
       // fewer fp16x3 tiles than CUs (N = 1152 at 2048 tokens: 144 tiles): every tile split along K so that
       // two workgroups share most CUs (the co-resident pair overlaps one's staging with the other's MFMAs)
       // chunks of >= 24 k-tiles (K >= 2304 at S = 3): at K = 1152 the fixup costs more than the split gains
@@ -1798,7 +1796,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   const double G = a.ngroups;
   double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);
   if (a.epi == EPI_RESID || a.epi == EPI_GELU || a.epi == EPI_DGELU) bytes += 4.0 * G * (double)a.M * a.N;
-  prof_end(ph, s, (t == 36 || t == 44 || t == 46 || t == 47) && h3_ready(a) ? PC_GEMM16 : PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
+  prof_end(ph, s, h3_tile(t) && h3_ready(a) ? PC_GEMM16 : PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
   return e;
 }
 
