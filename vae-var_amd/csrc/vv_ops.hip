@@ -354,7 +354,10 @@ __device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* 
 //           reduced by xor shuffles; softmax over the 4 jq lanes of a row (same wave)
 //   outputs: item = (token t, head hl, 4 consecutive d), d fastest -> coalesced row writes
 // LDS: rows of HPB*hd + 4 floats (16-B aligned, consecutive rows start 4 banks apart).
-constexpr int kAttnThreads = 256;
+#ifndef VV_ATTN_THREADS
+#define VV_ATTN_THREADS 256
+#endif
+constexpr int kAttnThreads = VV_ATTN_THREADS;  // threads per attention workgroup
 
 struct AttnShape {
   int hd, hpb, dp, st;  // head dim, heads per block, lanes per score quad, LDS row stride
