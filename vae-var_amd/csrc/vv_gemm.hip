@@ -1768,7 +1768,12 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
     const int tdp = (T / P) * P, tail = T - tdp;
     if (tdp > 0 && tail > 0 && tail <= P / 2) {
       // chunks of >= 12 k-tiles: below that the fixup launch and partial traffic cost more than the tail
-      int S = std::min(P / tail, nkt / 12);
+      static int tail_minkt = -1;  // VAEVAR_TAIL_MINKT: k-tiles per tail chunk at least (default 12)
+      if (tail_minkt < 0) {
+        const char* e = getenv("VAEVAR_TAIL_MINKT");
+        tail_minkt = e ? std::max(1, atoi(e)) : 12;
+      }
+      int S = std::min(P / tail, nkt / tail_minkt);
       const size_t tile_f = (size_t)bm * bn;
       while (S > 1 && (size_t)tail * S * tile_f > kWsFloats) --S;
       if (S > 1) {
