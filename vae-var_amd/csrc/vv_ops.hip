@@ -358,6 +358,7 @@ __device__ __forceinline__ float attn_bias_mask(const AttnArgs& a, const float* 
 #define VV_ATTN_THREADS 256
 #endif
 constexpr int kAttnThreads = VV_ATTN_THREADS;  // threads per attention workgroup
+static_assert(kAttnThreads >= 256 && kAttnThreads % 64 == 0, "attn_rows_all stages 3 float4 per thread (768 per block)");
 
 struct AttnShape {
   int hd, hpb, dp, st;  // head dim, heads per block, lanes per score quad, LDS row stride
