@@ -21,6 +21,8 @@ are stored):
   g9_metrics.npz        G9: the genuine utils.metrics.Metrics WRMSE / Bias as one_step_DA calls them
                         (da_4dvar.py:1256-1262) at 128x256 and 721x1440
   g7_tiny_lgunet1.npz   G7: tiny networks.LGUnet_all_1 (RoPE, -inf mask, global LG window, 3 levels): out
+  g13_config3_trajectory.npz  G13 (--g13, ~30 min): config 3 (T=2, decoder + flow stand-in) with torch.optim.LBFGS,
+                        Nit 10 at 128x256: J per pass, line-search steps, sampled xa
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
                         and one config-2 closure (J_b, J_o, sampled dJ/dz)
 """
@@ -456,6 +458,33 @@ def g10(tr):
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
 
+def g13(tr):
+    """G13 (BASELINE config 3 at its full budget): the reference's networks_old.LGUnet_all decoder AND
+    the flow stand-in (the same module class with C.FLOW's channel lists) inside the restated 4D-Var closure with
+    T = 2 (da_4dvar.py:1183-1208: the flow applied once through integrate, :666-681), torch.optim.LBFGS(history 10,
+    max_iter 10, strong Wolfe), Nit = 10 outer passes at 128x256: J per pass, every line search's (t, evals),
+    sampled xa. Parameters frozen as in G10 (the unused weight gradients only cost time)."""
+    m, _ = build_ref(tr, C.DECODER)
+    fm, _ = build_ref(tr, {k: v for k, v in C.FLOW.items() if k != "arch"})
+    for v in list(m.parameters()) + list(fm.parameters()):
+        v.requires_grad_(False)
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=2, seed=20250620)
+    rp = RefProblem(prob, m, C.DECODER["img_size"], fm)
+    t0 = time.time()
+    with LineSearchRecorder() as ls:
+        xa, z, js, nev, nit = one_step_da_ref(rp, 10, (32, 128, 256),
+                                              log=lambda k, j: print(f"G13 pass {k}: J_b {j[0]:.6e} J_o {j[1]:.6e} "
+                                                                     f"({time.time() - t0:.0f}s)", flush=True))
+    xa = xa.numpy().astype(np.float32)
+    idx = sample_idx(xa.size, 8192, 1313)
+    flat = xa.reshape(-1).astype(np.float64)
+    print(f"G13 config-3 trajectory: {time.time() - t0:.0f}s, evals {nev}, iters {nit}, J {js}")
+    np.savez(os.path.join(GOLD, "g13_config3_trajectory.npz"), J=np.array(js, np.float64), n_eval=nev, n_iter=nit,
+             ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]),
+             idx_xa=idx, xa_sample=xa.reshape(-1)[idx], xa_sum=flat.sum(),
+             dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+
+
 def g11():
     """G11: the reference's networks.LGUnet_all.LGUnet_all_1 at the full 0.25-degree
     configuration (training_options.yaml:64-119: 69ch 721x1440, 16,200-token global LG window), synthetic weights,
@@ -519,6 +548,7 @@ def main():
     ap.add_argument("--g8", action="store_true", help="also generate G8 (genuine real-obs one_step_DA, ~3 min)")
     ap.add_argument("--g10", action="store_true", help="also generate G10 (config-2 trajectory, Nit 10, ~10 min)")
     ap.add_argument("--g11", action="store_true", help="also generate G11 (0.25-deg LGUnet_all_1 forward, ~3 min)")
+    ap.add_argument("--g13", action="store_true", help="also generate G13 (config-3 T=2 trajectory, Nit 10, ~30 min)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.set_num_threads(8)
@@ -537,6 +567,8 @@ def main():
         steps["g10"] = lambda: g10(tr)
     if a.g11:
         steps["g11"] = g11
+    if a.g13:
+        steps["g13"] = lambda: g13(tr)
     for k, f in steps.items():
         if a.only and k not in a.only.split(","):
             continue

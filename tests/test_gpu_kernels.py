@@ -80,6 +80,23 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
 _keep = []
 
 
+@pytest.mark.parametrize("tile", [-1, 44, 47, 36])
+def test_gemm_h3_tile_unregistered_b(ctx, tile):
+    """An fp16x3 tile (or the auto pick) with a B that has no fp16 planes runs the bf16x6 128x128 kernel; its split-K
+    tail must be sized for THAT kernel's tiles (256-row tail geometry with 128-row fallback tiles wrote
+    past the GEMM workspace at 16384x1152x4608)."""
+    M, N, K = 16384, 1152, 4608
+    g = torch.Generator().manual_seed(4242)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.03).cuda()
+    C = ctx.gemm(A, B, tile=tile).double()
+    ref = A.double() @ B.double().t()
+    scale = (A.double().abs() @ B.double().abs().t()).max()
+    err = float((C - ref).abs().max() / scale)
+    print(f"unregistered B, tile {tile}: {err:.2e}")
+    assert err < 2e-6, err
+
+
 @pytest.mark.parametrize("tile", [36, 44, 46, 47])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
 def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):

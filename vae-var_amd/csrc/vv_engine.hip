@@ -320,6 +320,7 @@ struct vv_ctx {
   struct ClosureGraph {
     hipGraphExec_t exec = nullptr;
     int eager_runs = 0;
+    bool eager_only = false;  // capture or instantiation failed once: this kind runs eagerly until rebind
   } graphs[2];
   hipStream_t cap_stream = nullptr;
   bool use_graphs = true;  // vv_set_closure_graph / VAEVAR_GRAPH
@@ -1323,7 +1324,7 @@ int closure_graphed(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hip
   auto& g = ctx->graphs[grad_z ? 1 : 0];
   float* gz = grad_z ? P.GZ : nullptr;
   VV_HIP(hipMemcpyAsync(P.Z, z, P.zn * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if (!g.exec && g.eager_runs == 0) {
+  if (g.eager_only || (!g.exec && g.eager_runs == 0)) {
     // the first evaluation of each kind runs eagerly (it also performs the one-time kernel attribute set-up)
     g.eager_runs = 1;
     int r = closure_enqueue(ctx, P.Z, gz, nullptr, st);
@@ -1331,23 +1332,29 @@ int closure_graphed(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hip
   } else {
     if (!g.exec) {
       if (!ctx->cap_stream) VV_HIP(hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking));
-      VV_HIP(hipStreamBeginCapture(ctx->cap_stream, hipStreamCaptureModeRelaxed));
-      const int r = closure_enqueue(ctx, P.Z, gz, nullptr, ctx->cap_stream);
+      hipError_t ec = hipStreamBeginCapture(ctx->cap_stream, hipStreamCaptureModeRelaxed);
+      int r = 0;
       hipGraph_t graph = nullptr;
-      const hipError_t ec = hipStreamEndCapture(ctx->cap_stream, &graph);
-      if (r) {
-        if (graph) (void)hipGraphDestroy(graph);
-        return r;
+      if (ec == hipSuccess) {
+        r = closure_enqueue(ctx, P.Z, gz, nullptr, ctx->cap_stream);
+        ec = hipStreamEndCapture(ctx->cap_stream, &graph);
       }
-      VV_HIP(ec);
-      const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      if (ei != hipSuccess) {
+      hipError_t ei = hipSuccess;
+      if (!r && ec == hipSuccess) ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+      if (graph) (void)hipGraphDestroy(graph);
+      if (r || ec != hipSuccess || ei != hipSuccess) {
+        // one failed capture must not disable the closure: record the error once, run this kind eagerly from now
+        // on (nothing of the failed capture executed, so this evaluation is complete after the eager run)
         g.exec = nullptr;
-        return fail((int)ei, "closure graph instantiate: %s", hipGetErrorString(ei));
+        g.eager_only = true;
+        (void)hipGetLastError();
+        (void)fail(r ? r : (int)(ec != hipSuccess ? ec : ei), "closure graph capture failed (%s); eager launches",
+                   hipGetErrorString(ec != hipSuccess ? ec : ei));
+        const int r2 = closure_enqueue(ctx, P.Z, gz, nullptr, st);
+        if (r2) return r2;
       }
     }
-    VV_HIP(hipGraphLaunch(g.exec, st));
+    if (g.exec) VV_HIP(hipGraphLaunch(g.exec, st));
   }
   if (grad_z) VV_HIP(hipMemcpyAsync(grad_z, P.GZ, P.zn * sizeof(float), hipMemcpyDeviceToDevice, st));
   if (d_J) VV_HIP(hipMemcpyAsync(d_J, P.dJ, 2 * P.B * sizeof(double), hipMemcpyDeviceToDevice, st));

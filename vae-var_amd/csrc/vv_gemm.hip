@@ -1515,7 +1515,7 @@ static bool h3_ready(const GemmArgs& a) {
 template <int BM, int MF = 32>
 static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
   if (a.K % 32 || a.ksplit % 32) return hipErrorInvalidValue;
-  if (!h3_ready(a)) return launch_bs2(a, s);
+  if (!h3_ready(a)) return hipErrorInvalidValue;  // gemm_nt routes such GEMMs to tile 34 before sizing the split
   const float* sc = a.ws + kWsFloats;
   if (a.ascale_phys && !a.arow)
     sc = a.ascale;  // row scales written by the producer of A (LayerNorm), already in GEMM row order
@@ -1724,23 +1724,12 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
-  const int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
+  int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
   if (!valid_tile(t)) return hipErrorInvalidValue;
-  // data-parallel rounds of whole tiles + the remaining tiles split along K over the idle CUs
   const int num_cu = device_cus();
   a.tdp = 0;
   a.tsplit = 1;
   a.ws = ws;
-  {
-    // grouped tile order: one XCD runs ~T/8 consecutive logical tiles, a gm x (T/8/gm) block re-reading gm A
-    // m-blocks (BM rows) and T/8/gm B n-blocks (BN rows); gm = sqrt(T/8 x BN/BM) minimises those bytes
-    // (2048 x 3456 x 1152 on 256 x 128 tiles: 8 -> 4, FETCH 94 -> 73 MB per launch, profiles/r02/tile_group/)
-    int bm, bn, bk;
-    variant_tile(t, bm, bn, bk);
-    const int ntm = (a.M + bm - 1) / bm, ntn = (a.N + bn - 1) / bn;
-    const double tx = (double)ntm * ntn / 8.0;
-    a.gm = std::max(1, std::min(ntm, (int)std::lround(std::sqrt(tx * bn / bm))));
-  }
   a.ascale_phys = 0;
   static int ln_scales = -1;  // VAEVAR_LN_SCALES=0: ignore producer scales, run k_rowscale for every fp16x3 GEMM
   if (ln_scales < 0) {
@@ -1753,12 +1742,28 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
     a.ascale_phys = ok ? 1 : 0;
   }
   for (int g = 0; g < a.ngroups; ++g) {
+    a.g[g].Bh = nullptr;
+    a.g[g].Bs = nullptr;
+    if (h3_tile(t) && (!a.ldb || a.ldb == a.K)) split16_of(a.g[g].B, a.K, a.g[g].Bh, a.g[g].Bs);
+  }
+  // the fp16x3 kernels need every group's fp16 B planes and the scale workspace; without them the GEMM runs the
+  // pipelined bf16x6 kernel. Decide that BEFORE the tile geometry below: the split-K tail sizes its partials from
+  // the tile edge of the kernel that actually runs (a 256-row tile count with 128-row fallback tiles overran ws).
+  if (h3_tile(t) && !h3_ready(a)) t = 34;
+  for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start
     a.g[g].Ap = (t >= 21 && t < 36 && !a.g[g].A2 && !a.g[g].Ap) ? split_planes_exact(a.g[g].A) : a.g[g].Ap;
-    a.g[g].Bh = nullptr;
-    a.g[g].Bs = nullptr;
-    if (t >= 36 && (!a.ldb || a.ldb == a.K)) split16_of(a.g[g].B, a.K, a.g[g].Bh, a.g[g].Bs);
+  }
+  {
+    // grouped tile order: one XCD runs ~T/8 consecutive logical tiles, a gm x (T/8/gm) block re-reading gm A
+    // m-blocks (BM rows) and T/8/gm B n-blocks (BN rows); gm = sqrt(T/8 x BN/BM) minimises those bytes
+    // (2048 x 3456 x 1152 on 256 x 128 tiles: 8 -> 4, FETCH 94 -> 73 MB per launch, profiles/r02/tile_group/)
+    int bm, bn, bk;
+    variant_tile(t, bm, bn, bk);
+    const int ntm = (a.M + bm - 1) / bm, ntn = (a.N + bn - 1) / bn;
+    const double tx = (double)ntm * ntn / 8.0;
+    a.gm = std::max(1, std::min(ntm, (int)std::lround(std::sqrt(tx * bn / bm))));
   }
   if (ws && a.ngroups == 1) {
     int bm, bn, bk;

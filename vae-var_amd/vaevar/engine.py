@@ -106,7 +106,7 @@ class Context:
 
     @property
     def gemm_math(self) -> str:
-        """'split16' (fp16x3 scaled split, default), 'split' (bf16x6 split) or 'f32' (exact f32 MFMA); process-wide.
+        """'split16' (fp16x3 scaled split, default), 'split' (bf16x6 split) or 'f32' (exact f32 MFMA); per context.
 
         Both split modes carry fp32-level error (measured against fp64 in tests/test_gpu_kernels.py)."""
         v = ctypes.c_int()
