@@ -88,6 +88,16 @@ def physical_cores():
     return len(cores), len(cpus), int(share) if share and share.isdigit() else None
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the process's cgroup may use (cgroup v2 cpu.max 'quota period'), or None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # CPU baseline: the oracle restatement (oracle/, a torch-CPU port of the reference path) on the host cores
 def cpu_baseline(prob_np, T, evals_per_iter, gpu_evals_per_analysis, evals, threads, cores_note, all_cores=None):
@@ -137,7 +147,11 @@ def cpu_baseline(prob_np, T, evals_per_iter, gpu_evals_per_analysis, evals, thre
         per_all = timed(True, 1, all_cores)
         out["value_all_cores"] = 1.0 / (per_all * evals_per_iter)
         out["cores_all"] = all_cores
-        sample += f"; all {all_cores} physical cores: 1 evaluation after 1 warm-up, {per_all:.3f} s/eval"
+        quota = cgroup_cpu_quota()
+        sample += (f"; all {all_cores} physical cores: 1 evaluation after 1 warm-up, {per_all:.3f} s/eval"
+                   + (f" (the cgroup CPU quota is {quota:.0f} CPUs, so {all_cores} threads oversubscribe it"
+                      + (": slower than the share" if per_all > per_eval else "") + ")" if quota else ""))
+        out["cgroup_cpu_quota"] = quota
         torch.set_num_threads(threads)
     out["sample"] = sample + (f"; iters/s = 1 / (s_per_eval x {evals_per_iter:.3f} evals per iteration of the GPU "
                               f"run)")

@@ -105,7 +105,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
 int vv_closure(vv_ctx* ctx, const float* z, float* grad_z, double* J_b, double* J_o, void* stream);
 /* same, leaving {J_b, J_o} per analysis in device memory d_J[2B]; no synchronisation */
 int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, void* stream);
-/* replay the closure from a hipGraph (default on; VAEVAR_GRAPH=0 at vv_ctx_create turns it off): the evaluation's
+/* replay the closure from a hipGraph (default on; the Python Context turns it off for VAEVAR_GRAPH=0): the evaluation's
    ~540 kernel launches are captured once per kind (J only / J + gradient) and replayed as one graph launch, with z
    and grad_z copied through problem-owned buffers; results are bit-identical to the eager launches */
 int vv_set_closure_graph(vv_ctx* ctx, int enable);
@@ -189,8 +189,8 @@ int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* 
    decoder_hr (nf_model/vae.py:90) and integrate (da_4dvar.py:671, 679); map has out_size entries (host) */
 int vv_nearest_map(int in_size, int out_size, int* map);
 
-/* GEMM arithmetic for every nn.Linear of the context's models (per context; default VV_GEMM_SPLIT16, or the
-   VAEVAR_GEMM_MATH=f32|split|split16 environment variable at vv_ctx_create):
+/* GEMM arithmetic for every nn.Linear of the context's models (per context; default VV_GEMM_SPLIT16; the Python
+   Context applies VAEVAR_GEMM_MATH=f32|split|split16 through this call, the library reads no environment):
    VV_GEMM_F32     = v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (torch fp32 matmul semantics);
    VV_GEMM_SPLIT   = each fp32 operand split exactly into three bf16 planes (x = h + m + l) and the six
                      products of order >= 2^-16 accumulated in fp32 by v_mfma_f32_32x32x16_bf16;
@@ -203,6 +203,17 @@ int vv_nearest_map(int in_size, int out_size, int* map);
 #define VV_GEMM_SPLIT16 2
 int vv_set_gemm_math(vv_ctx* ctx, int math);
 int vv_get_gemm_math(vv_ctx* ctx, int* math);
+
+/* Per-context dispatch knobs, for A/B runs without a rebuild (defaults = the measured choices).
+   Keys: "h3_mink" (smallest K on the fp16x3 kernels, 768), "h3_big" (256x128 fp16x3 tiles, 1), "h3_mf16" (their
+   16x16x32-MFMA form, 1), "small_split" (whole-grid split-K of sub-chip fp16x3 GEMMs, 1), "small_split_minkt"
+   (24), "tail_minkt" (k-tiles per split-K tail chunk, 12), "ln_scales" (row scales from the LayerNorm, 1),
+   "win_attn" (LGUnet_all_1 LDS window attention, 1). Results stay fp32-level for every value; a change drops the
+   context's captured closure graphs. Unknown key: VV_E_ARG. */
+int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
+int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);
+/* process-wide debug aid: synchronise after every library launch and report the first failing op (default 0) */
+int vv_set_debug_sync(int enable);
 
 /* give a device weight B[N][K] (used as the B operand of vv_gemm) precomputed split planes, as the
    engine does for every model weight at vv_load_weights; B must stay alive and unchanged until

@@ -119,3 +119,24 @@ def test_new_entry_points_reject_bad_arguments():
     buf = ctypes.create_string_buffer(256)
     lib.vv_last_error(buf, 256)
     assert buf.value  # a message describes the failure
+
+
+def test_tuning_api_keys_and_rejection():
+    """The per-context dispatch knobs (vv_set_tuning / vv_get_tuning) replace the environment reads the library
+    once did: every key the Python Context knows is documented in include/vaevar.h, a null context or an unknown
+    key returns VV_E_ARG, and the library binary names no VAEVAR_ environment variable any more."""
+    import ctypes
+
+    from vaevar import _lib
+    from vaevar.engine import Context
+
+    lib = _lib.lib
+    hdr = open(os.path.join(ROOT, "include", "vaevar.h")).read()
+    for k in Context.TUNING_KEYS:
+        assert f'"{k}"' in hdr, k
+    v = ctypes.c_int()
+    assert lib.vv_set_tuning(None, b"h3_mink", 384) == 1001
+    assert lib.vv_get_tuning(None, b"h3_mink", ctypes.byref(v)) == 1001
+    assert lib.vv_set_debug_sync(0) == 0
+    so = open(_lib.LIB_PATH, "rb").read()
+    assert b"VAEVAR_" not in so and b"getenv" not in so

@@ -97,6 +97,37 @@ def test_gemm_h3_tile_unregistered_b(ctx, tile):
     assert err < 2e-6, err
 
 
+def test_tuning_knobs_per_context():
+    """vv_set_tuning / vv_get_tuning: every key round-trips on a fresh context, an unknown key is refused, and a
+    routing knob (h3_big = 0: 128x128 fp16x3 tiles; tail_minkt 40: no split-K tail) changes only the kernel, not
+    the fp32-level result; a second context on the same device keeps the defaults (knobs are per context)."""
+    from vaevar.engine import Context
+    from vaevar._lib import VVError
+
+    c1, c2 = Context(0), Context(0)
+    for k in Context.TUNING_KEYS:
+        v = c1.get_tuning(k)
+        c1.set_tuning(k, v + 1)
+        assert c1.get_tuning(k) == v + 1
+        assert c2.get_tuning(k) == v
+        c1.set_tuning(k, v)
+    with pytest.raises(VVError):
+        c1.set_tuning("no_such_knob", 1)
+    M, N, K = 2048, 3456, 1152
+    g = torch.Generator().manual_seed(99)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.03).cuda()
+    c1.gemm_register_weight(B)
+    c2.gemm_register_weight(B)
+    c1.set_tuning("h3_big", 0)
+    c1.set_tuning("tail_minkt", 40)
+    ref = A.double() @ B.double().t()
+    scale = float((A.double().abs() @ B.double().abs().t()).max())
+    for c in (c1, c2):
+        err = float((c.gemm(A, B).double() - ref).abs().max()) / scale
+        assert err < 2e-6, err
+
+
 @pytest.mark.parametrize("tile", [36, 44, 46, 47])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
 def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):

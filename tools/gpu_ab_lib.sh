@@ -1,4 +1,4 @@
-# same-box A/B of two builds: REF=<path to reference .so> bash tools/gpu_ab2.sh TAG [bench args]
+# same-box A/B of two library builds: REF=<path to the other .so> bash tools/gpu_ab_lib.sh TAG [bench args]
 set -e
 T=${1:-ab}
 shift || true

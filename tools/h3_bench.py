@@ -1,6 +1,6 @@
 """fp16x3 GEMM microbenchmark over the LG-stage shapes at 2048 tokens per analysis (registered weights, the
-engine's tile choice incl. split-K). Development tool: run once per VAEVAR_H3_APRE setting to A/B the in-loop A
-split against k_split_rows. Times one GEMM call (the whole launch sequence: scaling/split pass, main kernel,
+engine's tile choice incl. split-K). Development tool: TILES=a,b,... picks the tiles, MROWS scales the rows, tuning
+knobs come from VAEVAR_<KEY>. Times one GEMM call (the whole launch sequence: row-scale pass, main kernel, split-K
 fixup) with HIP events on the current stream."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -56,4 +56,4 @@ for (M, N, K) in shapes:
     print(json.dumps({"M": M, "N": N, "K": K, "us": round(us, 2), "tflops": round(2 * M * N * K / us / 1e6, 1),
                       "frac_833": round(2 * M * N * K / us / 1e6 / 833.3, 3), "err": err}), flush=True)
     del A, B
-print(json.dumps({"total_us": round(tot, 1), "apre": os.environ.get("VAEVAR_H3_APRE", "1")}), flush=True)
+print(json.dumps({"total_us": round(tot, 1)}), flush=True)

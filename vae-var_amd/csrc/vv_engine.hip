@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -220,6 +221,7 @@ struct Scratch {
   float* rs;  // fp16x3 row scales of a LayerNorm output / input gradient, consumed by the GEMM that follows
   float* ws;  // GEMM tail-split partials (vv::gemm_ws_floats())
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic (the context's vv_set_gemm_math)
+  const vv::Tuning* tune = nullptr;  // the context's dispatch knobs (vv_set_tuning)
 };
 
 struct Save {
@@ -297,6 +299,7 @@ struct Sc4Problem {
 struct vv_ctx {
   int device = 0;
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic of every model of this context (vv_set_gemm_math)
+  vv::Tuning tune;              // dispatch knobs of every model of this context (vv_set_tuning)
   std::vector<std::unique_ptr<Model>> models;
   Problem prob;
   std::unique_ptr<Sc4Problem> sc4;  // vv_sc4dvar_bind
@@ -458,10 +461,11 @@ int bind_weights(Model& m) {
 // ----------------------------------------------------------------------------
 // forward / backward of one Swin stage (BasicLayer / BasicLayer_up / Layer: blocks only)
 // ----------------------------------------------------------------------------
-GemmArgs gemm_base(int M, int N, int K, int G, int epi, int math) {
+GemmArgs gemm_base(int M, int N, int K, int G, int epi, int math, const vv::Tuning* tune) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.math = math;
+  a.tune = tune;
   a.M = M;
   a.N = N;
   a.K = K;
@@ -488,22 +492,16 @@ LnArgs ln_base(int rows, int C, int G, float eps) {
   return a;
 }
 
-// VAEVAR_SYNC_CHECK=1: synchronise after every launch and report the first failing op (debug only)
-bool sync_check() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VAEVAR_SYNC_CHECK");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
+// vv_set_debug_sync(1): synchronise after every launch and report the first failing op (debug only)
+std::atomic<int> g_sync_check{0};
+bool sync_check() { return g_sync_check.load(std::memory_order_relaxed) != 0; }
 
 #define CK(expr)                                                                                   \
   do {                                                                                             \
     hipError_t e_ = (expr);                                                                        \
     if (e_ == hipSuccess && sync_check()) {                                                        \
       e_ = hipDeviceSynchronize();                                                                 \
-      if (e_ != hipSuccess) fprintf(stderr, "VAEVAR_SYNC_CHECK: %s:%d %s -> %s\n", __FILE__, __LINE__, \
+      if (e_ != hipSuccess) fprintf(stderr, "debug sync: %s:%d %s -> %s\n", __FILE__, __LINE__, \
                                     #expr, hipGetErrorString(e_));                                 \
     }                                                                                              \
     if (e_ != hipSuccess) return fail((int)e_, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,         \
@@ -525,7 +523,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                  nullptr, nullptr, sc.rs + (size_t)g * M};
     CK(layernorm_fwd(ln, st));
     // qkv (A's fp16x3 row scales from LN1)
-    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc.math);
+    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc.math, sc.tune);
     q.ascale = sc.rs;
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
@@ -548,7 +546,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                  sv.P[b] + (size_t)g * nwin * S.heads * 256, nullptr, nullptr};
     CK(attn_fwd(at, st));
     // proj + window reverse + residual
-    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID, sc.math);
+    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID, sc.math, sc.tune);
     p.crow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
@@ -561,14 +559,14 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                   nullptr, nullptr, sc.rs + (size_t)g * M};
     CK(layernorm_fwd(ln2, st));
     // fc1 + GELU (row scales from LN2)
-    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc.math);
+    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc.math, sc.tune);
     f1.ascale = sc.rs;
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, sc.h + g * MC * 4, nullptr,
                  sv.h1[b] + g * MC * 4};
     CK(gemm_nt(f1, st, -1, sc.ws));
     // fc2 + residual
-    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc.math);
+    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc.math, sc.tune);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, sv.x[b + 1] + g * MC, sv.x1[b] + g * MC,
                  nullptr};
@@ -585,12 +583,12 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
   for (int b = S.depth - 1; b >= 0; --b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
-    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc.math);
+    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc.math, sc.tune);
     if (b < S.depth - 1) f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
     for (int g = 0; g < G; ++g)
       f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
     CK(gemm_nt(f2, st, -1, sc.ws));
-    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc.math);
+    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc.math, sc.tune);
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     CK(gemm_nt(f1, st, -1, sc.ws));
@@ -599,7 +597,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
                   sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M};
     CK(layernorm_bwd(ln2, st));
-    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc.math);
+    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc.math, sc.tune);
     p.arow = idx;
     p.ascale = sc.rs;  // per physical row of gx (the gather is applied to the scales too)
     for (int g = 0; g < G; ++g)
@@ -621,7 +619,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, nullptr, sv.P[b] + (size_t)g * nwin * S.heads * 256,
                  sc.t2 + g * MC, sc.dqkv + g * MC * 3};
     CK(attn_bwd(at, st));
-    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE, sc.math);
+    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE, sc.math, sc.tune);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     CK(gemm_nt(q, st, -1, sc.ws));
@@ -801,7 +799,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
                w(eg(g) + ".layers.1.downsample.norm.bias"), m.xm + (size_t)g * M1 * 4 * C0,
                sv.st_m + (size_t)g * M1 * 2, nullptr, nullptr};
   CK(layernorm_fwd(lm, st));
-  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE, m.sc.math);
+  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE, m.sc.math, m.sc.tune);
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.xm + (size_t)g * M1 * 4 * C0, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight"), nullptr,
                 sv.enc1.x[0] + g * M1C1, nullptr, nullptr};
@@ -817,7 +815,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   CK(layernorm_fwd(le, st));
   // Enc_net.proj (+ LG_net.pos_embed, transformer.py:704)
   float* lg_in = m.lg.empty() ? sv.dec1.x[0] : sv.lg[0].x[0];
-  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID, m.sc.math);
+  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID, m.sc.math, m.sc.tune);
   ep.rmod = c.H1 * c.W1;
   ep.ldr = E;
   ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
@@ -827,11 +825,11 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
     if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st))) return r;
   const float* lg_out = m.lg.empty() ? lg_in : sv.lg.back().x.back();
   // ---- Dec_net.proj (transformer.py:600)
-  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math);
+  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math, m.sc.tune);
   dp.g[0] = {lg_out, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m.dp, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
   // concat_back_dim[0]: cat(x, skip1) (transformer.py:468-469)
-  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math);
+  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math, m.sc.tune);
   c0.lda = G * C1;
   c0.ksplit = C1;
   c0.lda2 = C1;
@@ -841,7 +839,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   CK(gemm_nt(c0, st, -1, m.sc.ws));
   if ((r = stage_fwd(m.dec1, sv.dec1, m.sc, c.ws, st))) return r;
   // PatchExpand: expand (no bias) + rearrange + LN(C0, eps 1e-6) (transformer.py:106-118)
-  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE, m.sc.math);
+  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE, m.sc.math, m.sc.tune);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {sv.dec1.x.back() + g * M1C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight"), nullptr,
                sv.ex + (size_t)g * M1 * 2 * C1, nullptr, nullptr};
@@ -857,7 +855,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
                nullptr};
   CK(layernorm_fwd(lx, st));
   // concat_back_dim[1]: cat(x, skip0)
-  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE, m.sc.math);
+  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE, m.sc.math, m.sc.tune);
   c1.lda = C0;
   c1.ksplit = C0;
   c1.lda2 = C0;
@@ -942,7 +940,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   if ((r = stage_bwd(m.dec0, sv.dec0, m.sc, c.ws, m.gd0, st))) return r;
   // concat_back_dim[1] backward: left -> PatchExpand output, right -> skip0
   for (int half = 0; half < 2; ++half) {
-    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE, m.sc.math);
+    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE, m.sc.math, m.sc.tune);
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd0 + g * M0C0, nullptr, w(dg(g) + ".concat_back_dim.1.weight^T") + (size_t)half * C0 * C0,
                  nullptr, (half ? m.gsk0 : m.gxe) + g * M0C0, nullptr, nullptr};
@@ -958,7 +956,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
     lx.g[g] = {sv.ex + (size_t)g * M1 * 2 * C1, w(dg(g) + ".layers_up.0.upsample.norm.weight"), nullptr,
                m.gex + (size_t)g * M1 * 2 * C1, sv.st_ex + (size_t)g * M0 * 2, m.gxe + g * M0C0, nullptr};
   CK(layernorm_bwd(lx, st));
-  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math);
+  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math, m.sc.tune);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {m.gex + (size_t)g * M1 * 2 * C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight^T"), nullptr,
                m.gd1 + g * M1C1, nullptr, nullptr};
@@ -966,7 +964,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   if ((r = stage_bwd(m.dec1, sv.dec1, m.sc, c.ws, m.gd1, st))) return r;
   // concat_back_dim[0] backward: left -> Dec_net.proj output slice g, right -> skip1
   for (int half = 0; half < 2; ++half) {
-    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE, m.sc.math);
+    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE, m.sc.math, m.sc.tune);
     if (!half) cb.ldc = G * C1;
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd1 + g * M1C1, nullptr, w(dg(g) + ".concat_back_dim.0.weight^T") + (size_t)half * C1 * C1,
@@ -975,13 +973,13 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   }
   // Dec_net.proj backward
   float* glg = m.glg;
-  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE, m.sc.math);
+  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE, m.sc.math, m.sc.tune);
   dp.g[0] = {m.gdp, nullptr, w("dec.proj.weight^T"), nullptr, glg, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
   for (int l = (int)m.lg.size() - 1; l >= 0; --l)
     if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st))) return r;
   // pos_embed: identity ; Enc_net.proj backward
-  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math);
+  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math, m.sc.tune);
   ep.g[0] = {glg, nullptr, w("enc.proj.weight^T"), nullptr, m.gcat, nullptr, nullptr};
   CK(gemm_nt(ep, st, -1, m.sc.ws));
   // encoder norm backward (+ skip1 gradient), in place on gsk1
@@ -994,7 +992,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   CK(layernorm_bwd(le, st));
   if ((r = stage_bwd(m.enc1, sv.enc1, m.sc, c.ws, m.gsk1, st))) return r;
   // PatchMerging backward: reduction^T, then LN (merge mode) scattered onto level-0 tokens (+ skip0 grad)
-  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE, m.sc.math);
+  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE, m.sc.math, m.sc.tune);
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.gsk1 + g * M1C1, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight^T"), nullptr,
                 m.gxm + (size_t)g * M1 * 4 * C0, nullptr, nullptr};
@@ -1432,9 +1430,6 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
-  if (const char* e = getenv("VAEVAR_GRAPH")) c->use_graphs = e[0] != '0';
-  if (const char* e = getenv("VAEVAR_GEMM_MATH"))
-    c->math = strcmp(e, "f32") == 0 ? vv::GEMM_F32 : strcmp(e, "split") == 0 ? vv::GEMM_SPLIT : vv::GEMM_SPLIT16;
   *out = c;
   return 0;
 }
@@ -1474,6 +1469,7 @@ int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_s
     std::string err;
     if ((r = vvf::create(cfg, batch, &m->fm, err))) return fail(r, "%s", err.c_str());
     vvf::set_math(m->fm, ctx->math);
+    vvf::set_tuning(m->fm, &ctx->tune);
     m->B = batch;
     m->nslots = 1;
     m->workspace = vvf::workspace_bytes(m->fm);
@@ -1489,6 +1485,7 @@ int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_s
   if (cfg->arch != VV_ARCH_LGUNET) return fail(VV_E_ARG, "unknown arch %d", cfg->arch);
   if ((r = create_model(ctx, cfg, batch, n_slots, model_id))) return r;
   ctx->models[*model_id]->sc.math = ctx->math;
+  ctx->models[*model_id]->sc.tune = &ctx->tune;
   return 0;
 }
 
@@ -1907,6 +1904,28 @@ int vv_set_gemm_math(vv_ctx* ctx, int math) {
   return 0;
 }
 
+int vv_set_tuning(vv_ctx* ctx, const char* key, int value) {
+  if (!ctx) return fail(VV_E_ARG, "null context");
+  int* f = vv::tuning_field(ctx->tune, key);
+  if (!f) return fail(VV_E_ARG, "unknown tuning key '%s'", key ? key : "(null)");
+  if (*f != value) drop_graphs(ctx);
+  *f = value;
+  return 0;
+}
+
+int vv_get_tuning(vv_ctx* ctx, const char* key, int* value) {
+  if (!ctx || !value) return fail(VV_E_ARG, "null argument");
+  int* f = vv::tuning_field(ctx->tune, key);
+  if (!f) return fail(VV_E_ARG, "unknown tuning key '%s'", key ? key : "(null)");
+  *value = *f;
+  return 0;
+}
+
+int vv_set_debug_sync(int enable) {
+  g_sync_check.store(enable ? 1 : 0, std::memory_order_relaxed);
+  return 0;
+}
+
 int vv_set_closure_graph(vv_ctx* ctx, int enable) {
   if (!ctx) return fail(VV_E_ARG, "null context");
   int r = set_dev(ctx);
@@ -2013,7 +2032,7 @@ int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, co
   if (M <= 0 || N <= 0 || K <= 0 || K % 32) return fail(VV_E_ARG, "bad GEMM shape %dx%dx%d (K a multiple of 32)", M, N, K);
   int r = set_dev(ctx);
   if (r) return r;
-  GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE, ctx->math);
+  GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE, ctx->math, &ctx->tune);
   a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
   VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
   return 0;

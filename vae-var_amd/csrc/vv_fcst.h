@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/vaevar.h"
+#include "vv_kernels.h"
 
 namespace vvf {
 
@@ -28,6 +29,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
 int64_t workspace_bytes(const FModel* m);
 // GEMM arithmetic (vv::GemmMath) of the model's forward
 void set_math(FModel* m, int math);
+void set_tuning(FModel* m, const vv::Tuning* t);  // the owning context's knobs (kept by pointer)
 int in_channels(const FModel* m);
 int out_channels(const FModel* m);
 int img_h(const FModel* m);

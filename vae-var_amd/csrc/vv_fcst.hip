@@ -730,6 +730,7 @@ struct FModel {
   std::vector<float*> Wp, W2;
   int Kp = 0, NT = 0;
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic (the owning context's setting)
+  const vv::Tuning* tune = nullptr;  // the owning context's dispatch knobs
   // global-window attention through the split GEMM when the window is large: S/P [heads][N][Np], V^T [heads][hd][Np]
   float *att_s = nullptr, *att_vt = nullptr;
 };
@@ -821,10 +822,11 @@ FBlock blk(FModel& m, const std::string& pre) {
           w(pre + ".mlp.fc1.bias"),    w(pre + ".mlp.fc2.weight"), w(pre + ".mlp.fc2.bias")};
 }
 
-GemmArgs gbase(int M, int N, int K, int G, int epi, int math) {
+GemmArgs gbase(int M, int N, int K, int G, int epi, int math, const vv::Tuning* tune) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.math = math;
+  a.tune = tune;
   a.M = M;
   a.N = N;
   a.K = K;
@@ -848,17 +850,9 @@ LnArgs lbase(int rows, int C, int G) {
   return a;
 }
 
-static bool win_attn_enabled() {
-  static int v = -1;  // VAEVAR_WIN_ATTN=0: the streaming kernel for small windows too
-  if (v < 0) {
-    const char* e = getenv("VAEVAR_WIN_ATTN");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
-hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st) {
-  if (a.N <= kWinMaxN && hd <= kWinMaxHd && hd % 4 == 0 && win_attn_enabled()) {
+// win_attn: the tuning knob (0: the streaming kernel for small windows too)
+hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st, bool win_attn) {
+  if (a.N <= kWinMaxN && hd <= kWinMaxHd && hd % 4 == 0 && win_attn) {
     const size_t lds = (3 * (size_t)a.N * (hd + 4) + (size_t)a.N * (a.N + 1)) * sizeof(float);
     static bool init = false;
     if (!init) {
@@ -898,7 +892,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     for (int g = 0; g < G; ++g)
       ln.g[g] = {S.x + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, m.t1 + g * MC, nullptr, nullptr, nullptr};
     FH(layernorm_fwd(ln, st));
-    GemmArgs q = gbase(M, 3 * C, C, G, EPI_STORE, m.math);
+    GemmArgs q = gbase(M, 3 * C, C, G, EPI_STORE, m.math, m.tune);
     for (int g = 0; g < G; ++g)
       q.g[g] = {m.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, m.qkv + g * MC * 3, nullptr, nullptr};
     FH(gemm_nt(q, st, -1, m.ws));
@@ -942,7 +936,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
       const int Np = (N + 31) / 32 * 32, hd = S.hd;
       for (int b0 = 0; b0 < nwin; ++b0) {
         const float* qkv = m.qkv + (size_t)b0 * N * 3 * C;
-        GemmArgs sq = gbase(N, N, hd, S.heads, EPI_STORE, m.math);
+        GemmArgs sq = gbase(N, N, hd, S.heads, EPI_STORE, m.math, m.tune);
         sq.lda = 3 * C;
         sq.ldb = 3 * C;
         sq.ldc = Np;
@@ -960,7 +954,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
                            hd);
         FH(hipGetLastError());
         prof_end(ph, st, PC_ATTN, 4.0 * S.heads * N * (double)Np, 12.0 * S.heads * N * (double)Np);
-        GemmArgs pv = gbase(N, hd, Np, S.heads, EPI_STORE, m.math);
+        GemmArgs pv = gbase(N, hd, Np, S.heads, EPI_STORE, m.math, m.tune);
         pv.ldc = C;
         for (int hh = 0; hh < S.heads; ++hh)
           pv.g[hh] = {m.att_s + (size_t)hh * N * Np, nullptr, m.att_vt + (size_t)hh * hd * Np, nullptr,
@@ -969,11 +963,11 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
       }
     } else {
       ph = prof_begin(st);
-      FH(flash(fa, S.hd, nwin, G, st));
+      FH(flash(fa, S.hd, nwin, G, st, (m.tune ? *m.tune : vv::kDefaultTuning).win_attn != 0));
       prof_end(ph, st, PC_ATTN, 4.0 * G * (double)M * N * C, 16.0 * G * (double)M * C);
     }
     // proj + window reverse / roll back + residual, in place
-    GemmArgs p = gbase(M, C, C, G, EPI_RESID, m.math);
+    GemmArgs p = gbase(M, C, C, G, EPI_RESID, m.math, m.tune);
     p.crow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {m.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, S.x + g * MC, S.x + g * MC, nullptr};
@@ -982,12 +976,12 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     for (int g = 0; g < G; ++g)
       ln2.g[g] = {S.x + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, m.t1 + g * MC, nullptr, nullptr, nullptr};
     FH(layernorm_fwd(ln2, st));
-    GemmArgs f1 = gbase(M, 4 * C, C, G, EPI_GELU, m.math);
+    GemmArgs f1 = gbase(M, 4 * C, C, G, EPI_GELU, m.math, m.tune);
     for (int g = 0; g < G; ++g)
       f1.g[g] = {m.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, m.h + g * MC * 4, nullptr,
                  m.aux + g * MC * 4};
     FH(gemm_nt(f1, st, -1, m.ws));
-    GemmArgs f2 = gbase(M, C, 4 * C, G, EPI_RESID, m.math);
+    GemmArgs f2 = gbase(M, C, 4 * C, G, EPI_RESID, m.math, m.tune);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {m.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, S.x + g * MC, S.x + g * MC, nullptr};
     FH(gemm_nt(f2, st, -1, m.ws));
@@ -1215,7 +1209,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
   hipLaunchKernelGGL(k_im2col, dim3(grid_for(colg), G), dim3(256), 0, st, pa, m->h, m->Kp, colg);
   FH(hipGetLastError());
   prof_end(ph, st, PC_PATCH, 0.0, 8.0 * G * colg);
-  GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID, m->math);
+  GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID, m->math, m->tune);
   pe.rmod = c.Hl[0] * c.Wl[0];
   pe.ldr = c.Cl[0];
   for (int g = 0; g < G; ++g)
@@ -1235,7 +1229,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
         lm.g[g] = {m->enc[l - 1].x + g * S[l - 1], w(eg(g) + pl + ".norm.weight"), w(eg(g) + pl + ".norm.bias"),
                    m->xm + (size_t)g * M[l] * 4 * Cp, nullptr, nullptr, nullptr};
       FH(layernorm_fwd(lm, st));
-      GemmArgs red = gbase(M[l], c.Cl[l], 4 * Cp, G, EPI_STORE, m->math);
+      GemmArgs red = gbase(M[l], c.Cl[l], 4 * Cp, G, EPI_STORE, m->math, m->tune);
       for (int g = 0; g < G; ++g)
         red.g[g] = {m->xm + (size_t)g * M[l] * 4 * Cp, nullptr, w(eg(g) + pl + ".reduction.weight"), nullptr,
                     m->enc[l].x + g * S[l], nullptr, nullptr};
@@ -1250,7 +1244,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     le.g[g] = {m->enc[L - 1].x + g * S[L - 1], w(eg(g) + ".norm.weight"), w(eg(g) + ".norm.bias"), m->cat + g * CL,
                nullptr, nullptr, nullptr};
   FH(layernorm_fwd(le, st));
-  GemmArgs ep = gbase(Mg, c.E, G * CL, 1, EPI_RESID, m->math);
+  GemmArgs ep = gbase(Mg, c.E, G * CL, 1, EPI_RESID, m->math, m->tune);
   ep.rmod = c.Hg * c.Wg;  // + LG_net.pos_embed (LGUnet_all.py:727)
   ep.ldr = c.E;
   ep.g[0] = {m->cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), m->lgx, w("net.pos_embed"), nullptr};
@@ -1259,13 +1253,13 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
   for (auto& s : m->lg)
     if ((r = stage_fwd(*m, s, st, err))) return r;
   // ---- Dec_net (LGUnet_all.py:624-650)
-  GemmArgs dp = gbase(Mg, G * CL, c.E, 1, EPI_STORE, m->math);
+  GemmArgs dp = gbase(Mg, G * CL, c.E, 1, EPI_STORE, m->math, m->tune);
   dp.g[0] = {m->lgx, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m->dp, nullptr, nullptr};
   FH(gemm_nt(dp, st, -1, m->ws));
   for (int i = 0; i < L; ++i) {
     const int lev = L - 1 - i, Cv = c.Cl[lev];
     // cat(x, skip) -> concat_back_dim[i] (LGUnet_all.py:473-476)
-    GemmArgs cb = gbase(M[lev], Cv, 2 * Cv, G, EPI_STORE, m->math);
+    GemmArgs cb = gbase(M[lev], Cv, 2 * Cv, G, EPI_STORE, m->math, m->tune);
     cb.ksplit = Cv;
     cb.lda = i == 0 ? G * CL : Cv;
     cb.lda2 = Cv;
@@ -1278,7 +1272,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     if (i < L - 1) {
       // PatchExpand (LGUnet_all.py:107-118): expand (no bias) + rearrange + LN(C/2)
       const std::string pu = ".layers_up." + std::to_string(i) + ".upsample";
-      GemmArgs ex = gbase(M[lev], 2 * Cv, Cv, G, EPI_STORE, m->math);
+      GemmArgs ex = gbase(M[lev], 2 * Cv, Cv, G, EPI_STORE, m->math, m->tune);
       for (int g = 0; g < G; ++g)
         ex.g[g] = {m->dec[lev].x + g * S[lev], nullptr, w(dg(g) + pu + ".expand.weight"), nullptr,
                    m->ex + (size_t)g * M[lev] * 2 * Cv, nullptr, nullptr};
@@ -1331,7 +1325,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
   }
   // ConvTranspose2d = GEMM (tokens x transposed weight) + col2im of the overlapping taps
   const size_t yg = (size_t)M[0] * m->NT;
-  GemmArgs ct = gbase(M[0], m->NT, c.Cl[0], G, EPI_STORE, m->math);
+  GemmArgs ct = gbase(M[0], m->NT, c.Cl[0], G, EPI_STORE, m->math, m->tune);
   for (int g = 0; g < G; ++g) ct.g[g] = {pu.tok[g], nullptr, m->W2[g], nullptr, m->h + g * yg, nullptr, nullptr};
   FH(gemm_nt(ct, st, -1, m->ws));
   ph = prof_begin(st);
@@ -1344,6 +1338,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
 
 int64_t workspace_bytes(const FModel* m) { return m->bytes; }
 void set_math(FModel* m, int math) { m->math = math; }
+void set_tuning(FModel* m, const vv::Tuning* t) { m->tune = t; }
 int in_channels(const FModel* m) { return m->c.Cin; }
 int out_channels(const FModel* m) { return m->c.Cout; }
 int img_h(const FModel* m) { return m->c.Himg; }

@@ -1546,6 +1546,21 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
 //   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
 //   fp16x3 split    36: 128x128, 44: 256x128 (8 waves of 64x64); 46 / 47: the same on 16x16x32 MFMAs
 static bool h3_tile(int t) { return t == 36 || t == 44 || t == 46 || t == 47; }
+const Tuning kDefaultTuning{};
+int* tuning_field(Tuning& t, const char* key) {
+  if (!key) return nullptr;
+  const std::string k(key);
+  if (k == "h3_mink") return &t.h3_mink;
+  if (k == "h3_big") return &t.h3_big;
+  if (k == "h3_mf16") return &t.h3_mf16;
+  if (k == "small_split") return &t.small_split;
+  if (k == "small_split_minkt") return &t.small_split_minkt;
+  if (k == "tail_minkt") return &t.tail_minkt;
+  if (k == "ln_scales") return &t.ln_scales;
+  if (k == "win_attn") return &t.win_attn;
+  return nullptr;
+}
+
 bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || h3_tile(t); }
 
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
@@ -1664,29 +1679,17 @@ size_t gemm_ws_floats() { return kWsFloats + kScaleFloats; }
 
 // tile choice (measured on MI355X, tools/gemm_bench.py, tools/gemm_split_check.py)
 static int pick_tile(const GemmArgs& a) {
+  const Tuning& T = a.tune ? *a.tune : kDefaultTuning;
   if (a.math == GEMM_SPLIT16 || a.math == GEMM_SPLIT) {
     // GEMM_SPLIT16: fp16x3 128x128 for the deep-K GEMMs that give >= 128 tiles; the bf16x6 64x64 kernel for the
-    // short-K / few-tile GEMMs of the Swin towers (its pipeline prologue and epilogue dominate there)
-    static int h3_mink = -1;  // VAEVAR_H3_MINK: smallest K sent to the fp16x3 kernel (default 768)
-    if (h3_mink < 0) {
-      const char* e = getenv("VAEVAR_H3_MINK");
-      h3_mink = e ? std::max(64, atoi(e)) : 768;
-    }
-    // 256x128 tiles where they measured faster than 128x128 (profiles/r02/h3big: 2048 rows x (N 3456, K 1152):
-    // 69.0 vs 73.4 us, (1152, 4608): 93.1 vs 98.5, (1152, 3456): 76.1 vs 79.3; slower at N 4608 x K 1152 and far
-    // slower at 1152 x 1152, where 72 tiles leave most CUs idle); VAEVAR_H3_BIG=0 keeps 128x128 everywhere
-    static int h3_big = -1;
-    if (h3_big < 0) {
-      const char* e = getenv("VAEVAR_H3_BIG");
-      h3_big = e ? atoi(e) : 1;
-    }
-    // VAEVAR_H3_MF16 (default 1): the 16x16x32-MFMA form of the 256x128 kernel for N 2048..4095 x short K
-    // (profiles/r02/mf16: 2048 x 3456 x 1152 at 64.3 vs 69.6 us; slower on the deep-K shapes)
-    static int h3_mf16 = -1;
-    if (h3_mf16 < 0) {
-      const char* e = getenv("VAEVAR_H3_MF16");
-      h3_mf16 = e ? atoi(e) : 1;
-    }
+    // short-K / few-tile GEMMs of the Swin towers (its pipeline prologue and epilogue dominate there).
+    // h3_mink: smallest K sent to the fp16x3 kernel.
+    // h3_big: 256x128 tiles where they measured faster than 128x128 (profiles/r02/h3big: 2048 rows x (N 3456,
+    // K 1152): 69.0 vs 73.4 us, (1152, 4608): 93.1 vs 98.5, (1152, 3456): 76.1 vs 79.3; slower at N 4608 x K 1152
+    // and far slower at 1152 x 1152, where 72 tiles leave most CUs idle).
+    // h3_mf16: the 16x16x32-MFMA form of the 256x128 kernel for N 2048..4095 x short K (profiles/r02/mf16:
+    // 2048 x 3456 x 1152 at 64.3 vs 69.6 us; slower on the deep-K shapes)
+    const int h3_mink = std::max(64, T.h3_mink), h3_big = T.h3_big, h3_mf16 = T.h3_mf16;
     if (a.math == GEMM_SPLIT16 && a.K >= h3_mink && h3_big && tiles_of(a, 256, 128) >= 64 &&
         (a.K >= 3456 || (a.N >= 2048 && a.N < 4096)))
       return h3_mf16 && a.K < 3456 ? 47 : 44;
@@ -1710,15 +1713,6 @@ static void variant_tile(int t, int& bm, int& bn, int& bk) {
   bn = t == 0 || t >= 34 ? 128 : 64;
 }
 
-static bool small_split_enabled() {
-  static int v = -1;  // VAEVAR_SMALL_SPLIT=0 disables the whole-grid split-K of sub-chip fp16x3 GEMMs
-  if (v < 0) {
-    const char* e = getenv("VAEVAR_SMALL_SPLIT");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
 hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
   GemmArgs a = a_in;
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
@@ -1731,12 +1725,9 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   a.tsplit = 1;
   a.ws = ws;
   a.ascale_phys = 0;
-  static int ln_scales = -1;  // VAEVAR_LN_SCALES=0: ignore producer scales, run k_rowscale for every fp16x3 GEMM
-  if (ln_scales < 0) {
-    const char* e = getenv("VAEVAR_LN_SCALES");
-    ln_scales = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (a.ascale && ln_scales) {
+  const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+  // ln_scales = 0: ignore producer scales, run k_rowscale for every fp16x3 GEMM
+  if (a.ascale && TU.ln_scales) {
     bool ok = true;
     for (int g = 0; g < a.ngroups; ++g) ok = ok && !a.g[g].A2;
     a.ascale_phys = ok ? 1 : 0;
@@ -1773,11 +1764,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
     const int tdp = (T / P) * P, tail = T - tdp;
     if (tdp > 0 && tail > 0 && tail <= P / 2) {
       // chunks of >= 12 k-tiles: below that the fixup launch and partial traffic cost more than the tail
-      static int tail_minkt = -1;  // VAEVAR_TAIL_MINKT: k-tiles per tail chunk at least (default 12)
-      if (tail_minkt < 0) {
-        const char* e = getenv("VAEVAR_TAIL_MINKT");
-        tail_minkt = e ? std::max(1, atoi(e)) : 12;
-      }
+      const int tail_minkt = std::max(1, TU.tail_minkt);  // k-tiles per tail chunk at least
       int S = std::min(P / tail, nkt / tail_minkt);
       const size_t tile_f = (size_t)bm * bn;
       while (S > 1 && (size_t)tail * S * tile_f > kWsFloats) --S;
@@ -1785,15 +1772,11 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
         a.tdp = tdp;
         a.tsplit = S;
       }
-    } else if (tdp == 0 && h3_tile(t) && small_split_enabled()) {
+    } else if (tdp == 0 && h3_tile(t) && TU.small_split) {
       // fewer fp16x3 tiles than CUs (N = 1152 at 2048 tokens: 144 tiles): every tile split along K so that
       // two workgroups share most CUs (the co-resident pair overlaps one's staging with the other's MFMAs)
       // chunks of >= 24 k-tiles (K >= 2304 at S = 3): at K = 1152 the fixup costs more than the split gains
-      static int min_kt = -1;  // VAEVAR_SMALL_SPLIT_MINKT: k-tiles per chunk at least (default 24)
-      if (min_kt < 0) {
-        const char* e = getenv("VAEVAR_SMALL_SPLIT_MINKT");
-        min_kt = e ? std::max(1, atoi(e)) : 24;
-      }
+      const int min_kt = std::max(1, TU.small_split_minkt);  // k-tiles per chunk at least
       int S = std::min(((t == 36 || t == 46 ? 2 : 1) * P) / T, nkt / min_kt);  // resident workgroups per CU: 2 / 1
       const size_t tile_f = (size_t)bm * bn;
       while (S > 1 && (size_t)T * S * tile_f > kWsFloats) --S;

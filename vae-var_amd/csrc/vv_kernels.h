@@ -9,6 +9,23 @@ namespace vv {
 
 constexpr int kMaxGroups = 8;
 
+// Per-context tuning knobs (vv_set_tuning / vv_get_tuning): the measured routing choices of the GEMM and
+// attention dispatch, kept settable so that A/B runs need no rebuild. The defaults are the shipped choices
+// (DESIGN.md §3 / §9 give the measurements behind each one); kernels never read them, only host dispatch does.
+struct Tuning {
+  int h3_mink = 768;            // smallest K sent to the fp16x3 kernels (profiles/r02/mink)
+  int h3_big = 1;               // 256x128 fp16x3 tiles where they measured faster (profiles/r02/h3big)
+  int h3_mf16 = 1;              // the 16x16x32-MFMA form of the 256x128 tile for N 2048..4095 x short K
+  int small_split = 1;          // whole-grid split-K of sub-chip fp16x3 GEMMs
+  int small_split_minkt = 24;   // k-tiles per chunk at least, for that split (profiles/r02/smallk)
+  int tail_minkt = 12;          // k-tiles per chunk at least, for the split-K tail (profiles/r02/tailk)
+  int ln_scales = 1;            // fp16x3 row scales from the LayerNorm producer (0: k_rowscale everywhere)
+  int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
+};
+extern const Tuning kDefaultTuning;
+// the tuning key names (vv_set_tuning); returns the field or null
+int* tuning_field(Tuning& t, const char* key);
+
 // ---------------------------------------------------------------------------
 // GEMM: C[o(r)][n] = epi( sum_k A(r,k) * B[n][k] )      (B is [N][K] = nn.Linear weight)
 //   A(r,k) = k <  ksplit : A [arow ? arow[r] : r][k]          (row stride lda)
@@ -57,6 +74,7 @@ struct GemmArgs {
   // row (arow[r] when gathered), z * M + row; the fp16x3 kernels then skip k_rowscale (no concat A2 allowed)
   const float* ascale;
   int ascale_phys;  // set by gemm_nt: the kernel indexes its row scales by physical row
+  const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   GemmGroup g[kMaxGroups];
 };
 

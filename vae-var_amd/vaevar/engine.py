@@ -10,6 +10,7 @@ torch is plumbing here (device memory, streams); every FLOP runs in libvaevar.so
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -36,10 +37,35 @@ class Context:
 
     _by_dev: dict = {}
 
+    # per-context dispatch knobs (vv_set_tuning; defaults = the measured choices). A/B runs set them from the
+    # environment as VAEVAR_<KEY> (e.g. VAEVAR_H3_MINK=384); the library itself reads no environment.
+    TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
+                   "win_attn")
+
     def __init__(self, device: int = 0):
         self.device = device
         self.h = ctypes.c_void_p()
         check(lib.vv_ctx_create(device, ctypes.byref(self.h)), "ctx_create")
+        env = os.environ
+        if env.get("VAEVAR_GEMM_MATH"):
+            self.gemm_math = env["VAEVAR_GEMM_MATH"]
+        if env.get("VAEVAR_GRAPH", "1")[:1] == "0":
+            self.set_closure_graph(False)
+        if env.get("VAEVAR_SYNC_CHECK", "0")[:1] == "1":
+            check(lib.vv_set_debug_sync(1), "set_debug_sync")
+        for k in self.TUNING_KEYS:
+            v = env.get("VAEVAR_" + k.upper())
+            if v is not None and v != "":
+                self.set_tuning(k, int(v))
+
+    def set_tuning(self, key: str, value: int):
+        """Set one dispatch knob of this context (keys: TUNING_KEYS; include/vaevar.h vv_set_tuning)."""
+        check(lib.vv_set_tuning(self.h, key.encode(), int(value)), f"set_tuning({key})")
+
+    def get_tuning(self, key: str) -> int:
+        v = ctypes.c_int()
+        check(lib.vv_get_tuning(self.h, key.encode(), ctypes.byref(v)), f"get_tuning({key})")
+        return v.value
 
     @classmethod
     def get(cls, device: int = 0) -> "Context":
@@ -106,7 +132,8 @@ class Context:
 
     @property
     def gemm_math(self) -> str:
-        """'split16' (fp16x3 scaled split, default), 'split' (bf16x6 split) or 'f32' (exact f32 MFMA); per context.
+        """'split16' (fp16x3 scaled split, default), 'split' (bf16x6 split) or 'f32' (exact f32 MFMA); per context
+        (VAEVAR_GEMM_MATH sets it at construction).
 
         Both split modes carry fp32-level error (measured against fp64 in tests/test_gpu_kernels.py)."""
         v = ctypes.c_int()
