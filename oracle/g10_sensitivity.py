@@ -4,9 +4,10 @@ with a different torch thread count (so the CPU GEMMs block and sum differently)
 torch.optim.LBFGS and (b) as a fixed-step replay of G10's recorded line-search steps through the product's L-BFGS
 mirror (vaevar.lbfgs.LBFGS with torch-CPU vector primitives). The relative J difference per outer pass against G10
 is the intrinsic sensitivity of the problem; tests/test_gpu_parity.py::test_config2_trajectory_g10 takes its
-tolerance from it (written to tests/golden/g10_sensitivity.npz).
+tolerance from it (written to tests/golden/g10_sensitivity.npz). `--case g13` does the same for G13 (config 3:
+T = 2 with the flow stand-in) into tests/golden/g13_sensitivity.npz (test_config3_trajectory_g13).
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python -B oracle/g10_sensitivity.py [--threads 4]
+Run:  PYTHONDONTWRITEBYTECODE=1 python -B oracle/g10_sensitivity.py [--threads 4] [--case g13]
 """
 from __future__ import annotations
 
@@ -61,18 +62,21 @@ class CpuPrims:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--case", default="g10", choices=["g10", "g13"])
     a = ap.parse_args()
-    g = np.load(os.path.join(GOLD, "g10_config2_trajectory.npz"))
+    T = 2 if a.case == "g13" else 1
+    g = np.load(os.path.join(GOLD, "g10_config2_trajectory.npz" if T == 1 else "g13_config3_trajectory.npz"))
     Jr = g["J"].sum(1)
     torch.set_num_threads(a.threads)
     cwd = os.getcwd()
     tr, _ = ref_harness.import_reference()
     os.chdir(cwd)
     m, _ = build_ref(tr, C.DECODER)
-    for v in m.parameters():
+    fm = build_ref(tr, {k: v for k, v in C.FLOW.items() if k != "arch"})[0] if T > 1 else None
+    for v in list(m.parameters()) + (list(fm.parameters()) if fm is not None else []):
         v.requires_grad_(False)
-    prob = make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620)
-    rp = RefProblem(prob, m, C.DECODER["img_size"])
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=T, seed=20250620)
+    rp = RefProblem(prob, m, C.DECODER["img_size"], fm) if fm is not None else RefProblem(prob, m, C.DECODER["img_size"])
     t0 = time.time()
     _, _, js, _, _ = one_step_da_ref(rp, 10, (32, 128, 256))
     free = np.abs(np.array(js).sum(1) - Jr) / np.abs(Jr)
@@ -99,7 +103,7 @@ def main():
             opt.step(closure)
     rep = np.abs(np.array(jr) - Jr) / np.abs(Jr)
     print(f"replay, {a.threads} threads ({time.time() - t0:.0f}s): J rel per pass {rep.tolist()}", flush=True)
-    np.savez(os.path.join(GOLD, "g10_sensitivity.npz"), threads=a.threads, free_rel=free, replay_rel=rep)
+    np.savez(os.path.join(GOLD, f"{a.case}_sensitivity.npz"), threads=a.threads, free_rel=free, replay_rel=rep)
 
 
 if __name__ == "__main__":

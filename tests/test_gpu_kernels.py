@@ -128,7 +128,7 @@ def test_tuning_knobs_per_context():
         assert err < 2e-6, err
 
 
-@pytest.mark.parametrize("tile", [36, 44, 46, 47])
+@pytest.mark.parametrize("tile", [36, 44, 46, 47, 48])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 1152), (1000, 520, 4608)])
 def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):
     """fp16x3 split (tiles 36 = 128x128, 44 = 256x128 of 8 waves, 46 / 47 the same on 16x16x32 MFMAs) keeps fp32-level error when row magnitudes of A span 2^+-17 and vary along K
@@ -155,23 +155,39 @@ def test_gemm_split16_dynamic_range(ctx, M, N, K, tile):
     _keep.append(Bd)
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 3456, 1152), (2048, 1152, 4608), (2048, 4608, 1152), (1000, 520, 4608),
+                                   (300, 200, 96)])
+def test_gemm_h4_bitwise_h3m(ctx, M, N, K):
+    """Tile 48 (A split once by k_rowsplit into fp16 planes, both operands staged by LDS-DMA through a 3-stage ring)
+    computes the same products in the same order as tile 47 (in-loop split, register staging): C bit-identical,
+    including the split-K tail shapes (K 4608 at N 1152, N 4608) and ragged edges."""
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = (torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-4, 4, generator=g))).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.03).cuda()
+    ctx.gemm_register_weight(B)
+    c47 = ctx.gemm(A, B, tile=47)
+    c48 = ctx.gemm(A, B, tile=48)
+    assert torch.equal(c47, c48), float((c47 - c48).abs().max())
+    _keep.append(B)
+
+
 def test_gemm_rejects_non_library_tiles(ctx):
-    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47): any other hint, e.g. the r01
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47, 48): any other hint, e.g. the r01
     timing experiments 37-39, returns VV_E_ARG instead of running something."""
     from vaevar._lib import VVError
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 48, 49, 1000):
+    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 49, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
-    for t in (0, 2, 4, 24, 34, 36, 44, 46, 47):
+    for t in (0, 2, 4, 24, 34, 36, 44, 46, 47, 48):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [36, 44, 46, 47])
+@pytest.mark.parametrize("tile", [36, 44, 46, 47, 48])
 @pytest.mark.parametrize("M,N,K", [(2048, 1152, 4608), (2048, 4608, 1152), (2048, 1152, 3456)])
 def test_gemm_splitk_deterministic(ctx, M, N, K, tile):
     """fp16x3 GEMMs whose tiles are split along K (every tile at N = 1152, the tail at N = 4608): the fixup sums

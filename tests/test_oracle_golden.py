@@ -128,6 +128,28 @@ def test_g10_g11_fixtures_consistent():
     assert float(f["out_sumsq"]) > 0 and len(f["idx"]) == len(f["out_sample"])
 
 
+def test_g13_fixture_consistent_and_oracle_pass0():
+    """G13 (config 3, T = 2, the reference modules + torch.optim.LBFGS) is self-consistent, and the oracle
+    restatement of the T = 2 closure (decoder + flow through integrate) reproduces its pass-0 J at z = 0."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.problem import make_problem
+
+    g = gold("g13_config3_trajectory.npz")
+    J = g["J"].sum(1)
+    assert len(J) == 11 and np.all(np.diff(J) < 0)
+    assert int(g["n_iter"]) <= 100 and len(g["ls_t"]) == int(g["n_iter"])
+    assert int(g["ls_evals"].sum()) + 10 == int(g["n_eval"])
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=2, seed=20250620)
+    ro = oracle_problem(prob, synth_params(C.DECODER), C.DECODER, synth_params(C.FLOW), C.FLOW)
+    with torch.no_grad():
+        jb, jo = ro.loss_terms(torch.zeros(1, 32, 128, 256))
+    assert float(jb) == 0.0
+    assert abs(float(jo) - float(g["J"][0][1])) < 1e-5 * float(g["J"][0][1]), (float(jo), float(g["J"][0][1]))
+
+
 def test_g5_tiny_lbfgs_trajectory():
     from oracle.da_ref import one_step_da_ref, oracle_problem
     from oracle.lgunet_ref import synth_params

@@ -21,9 +21,14 @@ for (M, N, K) in shapes:
     scale = A.double().abs() @ B.double().abs().T
     tiles = [int(t) for t in os.environ.get("TILES", "-1").split(",")]
     row = {"M": M, "N": N, "K": K}
+    C0 = None
     for t in tiles:
         C = ctx.gemm(A, B, tile=t)
         err = float(((C.double() - ref).abs() / scale).max())
+        if C0 is None:
+            C0 = C.clone()
+        else:
+            row[f"t{t}_bitwise_vs_t{tiles[0]}"] = bool(torch.equal(C, C0))
         for _ in range(3):
             ctx.gemm(A, B, tile=t)
         torch.cuda.synchronize()

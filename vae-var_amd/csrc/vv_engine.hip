@@ -222,6 +222,8 @@ struct Scratch {
   float* ws;  // GEMM tail-split partials (vv::gemm_ws_floats())
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic (the context's vv_set_gemm_math)
   const vv::Tuning* tune = nullptr;  // the context's dispatch knobs (vv_set_tuning)
+  unsigned short* apl = nullptr;     // fp16x3 A planes of the tile-48 GEMMs (k_rowsplit or the LayerNorm writes them)
+  size_t apl_halfs = 0;
 };
 
 struct Save {
@@ -300,6 +302,8 @@ struct vv_ctx {
   int device = 0;
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic of every model of this context (vv_set_gemm_math)
   vv::Tuning tune;              // dispatch knobs of every model of this context (vv_set_tuning)
+  unsigned short* apl = nullptr;  // vv_gemm's A-plane workspace (tile 48), grown on demand
+  size_t apl_halfs = 0;
   std::vector<std::unique_ptr<Model>> models;
   Problem prob;
   std::unique_ptr<Sc4Problem> sc4;  // vv_sc4dvar_bind
@@ -480,6 +484,20 @@ GemmArgs gemm_base(int M, int N, int K, int G, int epi, int math, const vv::Tuni
   return a;
 }
 
+GemmArgs gemm_base(int M, int N, int K, int G, int epi, const Scratch& sc) {
+  GemmArgs a = gemm_base(M, N, K, G, epi, sc.math, sc.tune);
+  a.apl = sc.apl;
+  a.apl_halfs = sc.apl_halfs;
+  return a;
+}
+
+// the LayerNorm feeding GEMM `a` writes the fp16x3 planes of its output (and no fp32 copy when `fp32_too` is false)
+// if the GEMM runs the split-operand kernel (tile 48); returns whether it does
+bool ln_feeds_planes(const GemmArgs& a, const Scratch& sc) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  return sc.apl && T.ln_planes && T.ln_scales && vv::gemm_tile_of(a) == 48;
+}
+
 LnArgs ln_base(int rows, int C, int G, float eps) {
   LnArgs a;
   memset(&a, 0, sizeof(a));
@@ -515,18 +533,21 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
   for (int b = 0; b < S.depth; ++b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
+    // qkv (A's fp16x3 row scales from LN1; with tile 48 also A's planes, and LN1 writes no fp32 copy)
+    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc);
+    q.ascale = sc.rs;
+    for (int g = 0; g < G; ++g)
+      q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
+    const bool q_pl = ln_feeds_planes(q, sc);
     // LN1 -> window order
     LnArgs ln = ln_base(M, C, G, 1e-5f);
     ln.map = idx;
     for (int g = 0; g < G; ++g)
-      ln.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, sc.t1 + g * MC, sv.st1[b] + (size_t)g * M * 2,
-                 nullptr, nullptr, sc.rs + (size_t)g * M};
+      ln.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, q_pl ? nullptr : sc.t1 + g * MC,
+                 sv.st1[b] + (size_t)g * M * 2, nullptr, nullptr, sc.rs + (size_t)g * M,
+                 q_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
     CK(layernorm_fwd(ln, st));
-    // qkv (A's fp16x3 row scales from LN1)
-    GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc.math, sc.tune);
-    q.ascale = sc.rs;
-    for (int g = 0; g < G; ++g)
-      q.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, sv.qkv[b] + g * MC * 3, nullptr, nullptr};
+    if (q_pl) q.apre = sc.apl;
     CK(gemm_nt(q, st, -1, sc.ws));
     // window attention
     AttnArgs at;
@@ -546,27 +567,30 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                  sv.P[b] + (size_t)g * nwin * S.heads * 256, nullptr, nullptr};
     CK(attn_fwd(at, st));
     // proj + window reverse + residual
-    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID, sc.math, sc.tune);
+    GemmArgs p = gemm_base(M, C, C, G, EPI_RESID, sc);
     p.crow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
                 nullptr};
     CK(gemm_nt(p, st, -1, sc.ws));
-    // LN2
-    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
-    for (int g = 0; g < G; ++g)
-      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, sc.t1 + g * MC, sv.st2[b] + (size_t)g * M * 2,
-                  nullptr, nullptr, sc.rs + (size_t)g * M};
-    CK(layernorm_fwd(ln2, st));
-    // fc1 + GELU (row scales from LN2)
-    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc.math, sc.tune);
+    // fc1 + GELU (row scales, and with tile 48 the planes, from LN2)
+    GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc);
     f1.ascale = sc.rs;
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, sc.h + g * MC * 4, nullptr,
                  sv.h1[b] + g * MC * 4};
+    const bool f1_pl = ln_feeds_planes(f1, sc);
+    // LN2
+    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
+    for (int g = 0; g < G; ++g)
+      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, f1_pl ? nullptr : sc.t1 + g * MC,
+                  sv.st2[b] + (size_t)g * M * 2, nullptr, nullptr, sc.rs + (size_t)g * M,
+                  f1_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
+    CK(layernorm_fwd(ln2, st));
+    if (f1_pl) f1.apre = sc.apl;
     CK(gemm_nt(f1, st, -1, sc.ws));
     // fc2 + residual
-    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc.math, sc.tune);
+    GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, sv.x[b + 1] + g * MC, sv.x1[b] + g * MC,
                  nullptr};
@@ -580,28 +604,39 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
   const int nwin = M / 16;
+  // the fc2 input-gradient GEMM of every block but the last takes gx from the LN1 backward of the block above it
+  // (same shapes in every block): with tile 48 that LayerNorm writes gx's planes too
+  GemmArgs f2x = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc);
+  f2x.ascale = sc.rs;
+  for (int g = 0; g < G; ++g) f2x.g[g] = {gx, nullptr, S.w[0][g].fc2WT, nullptr, sc.h, nullptr, sv.h1[0]};
+  const bool f2_pl = ln_feeds_planes(f2x, sc);
   for (int b = S.depth - 1; b >= 0; --b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
-    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc.math, sc.tune);
-    if (b < S.depth - 1) f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
+    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc);
+    if (b < S.depth - 1) {
+      f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
+      if (f2_pl) f2.apre = sc.apl;
+    }
     for (int g = 0; g < G; ++g)
       f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
     CK(gemm_nt(f2, st, -1, sc.ws));
-    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc.math, sc.tune);
+    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc);
     for (int g = 0; g < G; ++g)
       f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     CK(gemm_nt(f1, st, -1, sc.ws));
-    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
-    for (int g = 0; g < G; ++g)
-      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
-                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M};
-    CK(layernorm_bwd(ln2, st));
-    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc.math, sc.tune);
+    GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc);
     p.arow = idx;
     p.ascale = sc.rs;  // per physical row of gx (the gather is applied to the scales too)
     for (int g = 0; g < G; ++g)
       p.g[g] = {gx + g * MC, nullptr, S.w[b][g].projWT, nullptr, sc.t2 + g * MC, nullptr, nullptr};
+    const bool p_pl = ln_feeds_planes(p, sc);
+    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
+    for (int g = 0; g < G; ++g)
+      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
+                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, p_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
+    CK(layernorm_bwd(ln2, st));
+    if (p_pl) p.apre = sc.apl;  // planes in physical row order: the kernel gathers them through arow
     CK(gemm_nt(p, st, -1, sc.ws));
     AttnArgs at;
     memset(&at, 0, sizeof(at));
@@ -619,15 +654,16 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, nullptr, sv.P[b] + (size_t)g * nwin * S.heads * 256,
                  sc.t2 + g * MC, sc.dqkv + g * MC * 3};
     CK(attn_bwd(at, st));
-    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE, sc.math, sc.tune);
+    GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE, sc);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     CK(gemm_nt(q, st, -1, sc.ws));
     LnArgs ln1 = ln_base(M, C, G, 1e-5f);
     ln1.map = idx;
+    const bool l1_pl = f2_pl && b > 0;  // planes for the next block's fc2 input-gradient GEMM
     for (int g = 0; g < G; ++g)
       ln1.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, nullptr, gx + g * MC, sv.st1[b] + (size_t)g * M * 2,
-                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M};
+                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, l1_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
     CK(layernorm_bwd(ln1, st));
   }
   return 0;
@@ -703,6 +739,9 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
     for (auto& st : m->lg) mrows = std::max(mrows, (size_t)st.G * st.M);
     m->sc.rs = P.f(mrows);
     m->sc.ws = P.f(vv::gemm_ws_floats());
+    // tile-48 A planes: the largest A of a stage GEMM (fc2 forward / fc1 input gradient, K = 4C) as two fp16 planes
+    m->sc.apl = reinterpret_cast<unsigned short*>(P.f(mx * 4));
+    m->sc.apl_halfs = mx * 8;
     m->xm = P.f(G * M1 * 4 * c.C0);
     m->cat = P.f(M1 * G * c.C1);
     m->dp = P.f(M1 * G * c.C1);
@@ -799,7 +838,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
                w(eg(g) + ".layers.1.downsample.norm.bias"), m.xm + (size_t)g * M1 * 4 * C0,
                sv.st_m + (size_t)g * M1 * 2, nullptr, nullptr};
   CK(layernorm_fwd(lm, st));
-  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs red = gemm_base(M1, C1, 4 * C0, G, EPI_STORE, m.sc);
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.xm + (size_t)g * M1 * 4 * C0, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight"), nullptr,
                 sv.enc1.x[0] + g * M1C1, nullptr, nullptr};
@@ -815,7 +854,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   CK(layernorm_fwd(le, st));
   // Enc_net.proj (+ LG_net.pos_embed, transformer.py:704)
   float* lg_in = m.lg.empty() ? sv.dec1.x[0] : sv.lg[0].x[0];
-  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID, m.sc.math, m.sc.tune);
+  GemmArgs ep = gemm_base(M1, E, G * C1, 1, EPI_RESID, m.sc);
   ep.rmod = c.H1 * c.W1;
   ep.ldr = E;
   ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
@@ -825,11 +864,11 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
     if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st))) return r;
   const float* lg_out = m.lg.empty() ? lg_in : sv.lg.back().x.back();
   // ---- Dec_net.proj (transformer.py:600)
-  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc);
   dp.g[0] = {lg_out, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m.dp, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
   // concat_back_dim[0]: cat(x, skip1) (transformer.py:468-469)
-  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs c0 = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc);
   c0.lda = G * C1;
   c0.ksplit = C1;
   c0.lda2 = C1;
@@ -839,7 +878,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   CK(gemm_nt(c0, st, -1, m.sc.ws));
   if ((r = stage_fwd(m.dec1, sv.dec1, m.sc, c.ws, st))) return r;
   // PatchExpand: expand (no bias) + rearrange + LN(C0, eps 1e-6) (transformer.py:106-118)
-  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs ex = gemm_base(M1, 2 * C1, C1, G, EPI_STORE, m.sc);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {sv.dec1.x.back() + g * M1C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight"), nullptr,
                sv.ex + (size_t)g * M1 * 2 * C1, nullptr, nullptr};
@@ -855,7 +894,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
                nullptr};
   CK(layernorm_fwd(lx, st));
   // concat_back_dim[1]: cat(x, skip0)
-  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs c1 = gemm_base(M0, C0, 2 * C0, G, EPI_STORE, m.sc);
   c1.lda = C0;
   c1.ksplit = C0;
   c1.lda2 = C0;
@@ -940,7 +979,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   if ((r = stage_bwd(m.dec0, sv.dec0, m.sc, c.ws, m.gd0, st))) return r;
   // concat_back_dim[1] backward: left -> PatchExpand output, right -> skip0
   for (int half = 0; half < 2; ++half) {
-    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE, m.sc.math, m.sc.tune);
+    GemmArgs cb = gemm_base(M0, C0, C0, G, EPI_STORE, m.sc);
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd0 + g * M0C0, nullptr, w(dg(g) + ".concat_back_dim.1.weight^T") + (size_t)half * C0 * C0,
                  nullptr, (half ? m.gsk0 : m.gxe) + g * M0C0, nullptr, nullptr};
@@ -956,7 +995,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
     lx.g[g] = {sv.ex + (size_t)g * M1 * 2 * C1, w(dg(g) + ".layers_up.0.upsample.norm.weight"), nullptr,
                m.gex + (size_t)g * M1 * 2 * C1, sv.st_ex + (size_t)g * M0 * 2, m.gxe + g * M0C0, nullptr};
   CK(layernorm_bwd(lx, st));
-  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs ex = gemm_base(M1, C1, 2 * C1, G, EPI_STORE, m.sc);
   for (int g = 0; g < G; ++g)
     ex.g[g] = {m.gex + (size_t)g * M1 * 2 * C1, nullptr, w(dg(g) + ".layers_up.0.upsample.expand.weight^T"), nullptr,
                m.gd1 + g * M1C1, nullptr, nullptr};
@@ -964,7 +1003,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   if ((r = stage_bwd(m.dec1, sv.dec1, m.sc, c.ws, m.gd1, st))) return r;
   // concat_back_dim[0] backward: left -> Dec_net.proj output slice g, right -> skip1
   for (int half = 0; half < 2; ++half) {
-    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE, m.sc.math, m.sc.tune);
+    GemmArgs cb = gemm_base(M1, C1, C1, G, EPI_STORE, m.sc);
     if (!half) cb.ldc = G * C1;
     for (int g = 0; g < G; ++g)
       cb.g[g] = {m.gd1 + g * M1C1, nullptr, w(dg(g) + ".concat_back_dim.0.weight^T") + (size_t)half * C1 * C1,
@@ -973,13 +1012,13 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   }
   // Dec_net.proj backward
   float* glg = m.glg;
-  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE, m.sc);
   dp.g[0] = {m.gdp, nullptr, w("dec.proj.weight^T"), nullptr, glg, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
   for (int l = (int)m.lg.size() - 1; l >= 0; --l)
     if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st))) return r;
   // pos_embed: identity ; Enc_net.proj backward
-  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc);
   ep.g[0] = {glg, nullptr, w("enc.proj.weight^T"), nullptr, m.gcat, nullptr, nullptr};
   CK(gemm_nt(ep, st, -1, m.sc.ws));
   // encoder norm backward (+ skip1 gradient), in place on gsk1
@@ -992,7 +1031,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   CK(layernorm_bwd(le, st));
   if ((r = stage_bwd(m.enc1, sv.enc1, m.sc, c.ws, m.gsk1, st))) return r;
   // PatchMerging backward: reduction^T, then LN (merge mode) scattered onto level-0 tokens (+ skip0 grad)
-  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE, m.sc.math, m.sc.tune);
+  GemmArgs red = gemm_base(M1, 4 * C0, C1, G, EPI_STORE, m.sc);
   for (int g = 0; g < G; ++g)
     red.g[g] = {m.gsk1 + g * M1C1, nullptr, w(eg(g) + ".layers.1.downsample.reduction.weight^T"), nullptr,
                 m.gxm + (size_t)g * M1 * 4 * C0, nullptr, nullptr};
@@ -1456,6 +1495,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   (void)hipFree(ctx->dout);
   (void)hipFree(ctx->doutf);
   (void)hipFree(ctx->gemm_ws);
+  if (ctx->apl) (void)hipFree(ctx->apl);
   delete ctx;
   return 0;
 }
@@ -2034,6 +2074,20 @@ int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, co
   if (r) return r;
   GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE, ctx->math, &ctx->tune);
   a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
+  if (ctx->math == vv::GEMM_SPLIT16) {
+    // A-plane workspace of the split-operand kernel (tile 48), grown on demand (vv_gemm is never graph-captured)
+    const size_t need = (size_t)M * 2 * K;
+    if (need > ctx->apl_halfs) {
+      VV_HIP(hipStreamSynchronize((hipStream_t)stream));
+      if (ctx->apl) VV_HIP(hipFree(ctx->apl));
+      ctx->apl = nullptr;
+      ctx->apl_halfs = 0;
+      VV_HIP(hipMalloc(&ctx->apl, need * sizeof(unsigned short)));
+      ctx->apl_halfs = need;
+    }
+    a.apl = ctx->apl;
+    a.apl_halfs = ctx->apl_halfs;
+  }
   VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
   return 0;
 }

@@ -386,6 +386,49 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup_sub(GemmArgs args) 
     epilogue<32, 32, 1, 1, EPI, 32, false>(args, G, acc, m0, n0, 0, 0, rin, hh);
 }
 
+// The same for the 16x16-MFMA layout (k_gemm_h3m / k_gemm_h4, 4 x 4 fragments of 16x16 per wave): one workgroup
+// per (tail tile, fragment row a of every wave); each thread sums the S chunk partials of its 16 registers of the
+// 16 x 64 strip (a, b = 0..3) in chunk order and runs the epilogue on the strip.
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup_sub16(GemmArgs args) {
+  constexpr int NT = 64 * WM * WN, TM = BM / WM / 16, TN = BN / WN / 16, NREG = TM * TN * 4;
+  typedef float accv __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int S = args.tsplit;
+  const int tile = args.tdp + blockIdx.x;
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
+  const int a = blockIdx.y;
+  const int wm = wave / WN, wn = wave % WN;
+  const size_t items = (size_t)gridDim.x * S;
+  const float* w = args.ws + ((size_t)blockIdx.z * items + (size_t)blockIdx.x * S) * (size_t)(NREG * NT);
+  accv acc[1][TN];
+  const size_t j0 = (size_t)(a * TN * 4) * NT + tid;
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[0][b][r] = w[j0 + (size_t)(b * 4 + r) * NT];
+  for (int c = 1; c < S; ++c) {  // one chunk's loads in flight together, chunks summed in order
+    const float* wc = w + (size_t)c * NREG * NT + j0;
+    accv t[TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[b][r] = wc[(size_t)(b * 4 + r) * NT];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[0][b] += t[b];
+  }
+  const int m0 = mb * BM + wm * TM * 16 + a * 16, n0 = nb * BN + wn * TN * 16;
+  const int rin = lane & 15, hh = lane >> 4;
+  if (m0 + 16 <= M && n0 + TN * 16 <= N)
+    epilogue<16, TN * 16, 1, 1, EPI, 16, true>(args, G, acc, m0, n0, 0, 0, rin, hh);
+  else
+    epilogue<16, TN * 16, 1, 1, EPI, 16, false>(args, G, acc, m0, n0, 0, 0, rin, hh);
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // fp32 GEMM as six bf16 MFMA products (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate on gfx950).
 //
@@ -1481,13 +1524,244 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3m(GemmArgs args, const flo
     epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// fp16x3 on pre-split operands, both staged by LDS-DMA (tile 48).
+//
+// k_rowsplit writes A once per GEMM as fp16 planes in GEMM row order (the arow gather and the A2 concat applied),
+// row r = [h(K) | l(K)] scaled by 2^e (the same scale and split arithmetic as k_rowscale + the in-loop split of
+// k_gemm_h3m, so the products are bit-identical), exactly B's plane layout. k_gemm_h4 then streams both operands
+// HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write, no VALU split in the loop) through a
+// three-stage ring (3 x 48 KB of 160 KB), keeping two k-tiles in flight across the one raw s_barrier per k-tile
+// (counted vmcnt(6), never 0 in the loop: cdna_hip_programming.md "Pipelining across barriers"). The LDS image is
+// lane-linear per DMA instruction; the bank swizzle of the 16x16x32 fragment reads (chunk c of row r at
+// c ^ h((r >> 2) & 3)) is applied to each lane's global source address instead (rule 21). The fragments of k-tile
+// t+1 are read under the second half of k-tile t's 48 MFMAs (two register sets). Geometry, MFMA order, split-K
+// tail and epilogue are those of k_gemm_h3m<EPI, 256>, so C is bit-identical to tile 47.
+
+// one wave per logical row: max |A| of the row -> scale 2^(141 - e) (k_rowscale's formula), then the scaled row
+// split into fp16 h = fp16(v), l = fp16(v - h) and stored as planes[r] = [h(K) | l(K)]; NV float4 per lane
+template <int NV>
+__global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restrict__ rs, unsigned short* __restrict__ pl) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= args.M) return;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int K = args.K;
+  const int ar = args.arow ? args.arow[r] : r;
+  const float* a1 = G.A + (size_t)ar * args.lda;
+  const float* a2 = G.A2 ? G.A2 + (size_t)r * args.lda2 - args.ksplit : a1;
+  f4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int k = min(lane * 4 + 256 * i, K - 4);
+    v[i] = *reinterpret_cast<const f4*>((k < args.ksplit ? a1 : a2) + k);
+  }
+  unsigned mx = 0;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    mx = max(mx, max(max(__float_as_uint(fabsf(v[i][0])), __float_as_uint(fabsf(v[i][1]))),
+                     max(__float_as_uint(fabsf(v[i][2])), __float_as_uint(fabsf(v[i][3])))));
+  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  const float s = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
+  const size_t zr = (size_t)blockIdx.z * args.M + r;
+  if (lane == 0) rs[zr] = s;
+  unsigned short* ph = pl + zr * 2 * (size_t)K;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int k = lane * 4 + 256 * i;
+    if (k >= K) break;
+    h4v hv, lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = v[i][e] * s;
+      hv[e] = (_Float16)x;
+      lv[e] = (_Float16)(x - (float)hv[e]);
+    }
+    *reinterpret_cast<h4v*>(ph + k) = hv;
+    *reinterpret_cast<h4v*>(ph + K + k) = lv;
+  }
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* __restrict__ ascale,
+                                                    const unsigned short* __restrict__ apl) {
+  constexpr int BM = 256, BN = 128, BK = 32, NT = 512, WN = 2, WM = 4, TM = 4, TN = 4;
+  constexpr int LSB = BK;                                  // halfs per LDS row (64 B)
+  constexpr int APL = BM * LSB, BPL = BN * LSB;            // halfs per A / B plane of one stage
+  constexpr int STG = 2 * APL + 2 * BPL;                   // 24576 halfs = 48 KB per stage
+  typedef float accv __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N, K = args.K;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nkt = K / BK;
+  int tile, kb = 0, ke = nkt, part = -1;
+  if (args.tsplit <= 1) {
+    tile = xcd_remap(blockIdx.x, ntm * ntn);
+  } else if ((int)blockIdx.x < args.tdp) {
+    tile = xcd_remap(blockIdx.x, args.tdp);
+  } else {
+    const int items = gridDim.x - args.tdp, S = args.tsplit, tt = items / S;
+    const int L = xcd_remap(blockIdx.x - args.tdp, items), c = L / tt, tl = L - c * tt;
+    part = tl * S + c;
+    tile = args.tdp + tl;
+    kb = (c * nkt) / S;
+    ke = ((c + 1) * nkt) / S;
+  }
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
+  const int m0 = mb * BM, n0 = nb * BN;
+  auto hsw = [](int q) { return (0x78 >> (2 * (q & 3))) & 3; };  // 0, 2, 3, 1
+  const float* rs = ascale + (size_t)blockIdx.z * M;
+
+  // DMA sources: wave w stages A pieces w, w + 8, w + 16, w + 24 (piece p: plane p >> 4, rows 16 (p & 15) ..) and
+  // B pieces w, w + 8 (plane p >> 3, rows 16 (p & 7) ..); lane i fills LDS bytes 16 i of the piece: row i >> 2,
+  // slot i & 3, which holds the row's k-chunk (i & 3) ^ h((row >> 2) & 3)
+  const int prow = lane >> 2, pslot = lane & 3;
+  const unsigned short* asrc[4];
+  const unsigned short* bsrc[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = wave + 8 * j, row = 16 * (p & 15) + prow;
+    int gr = min(m0 + row, M - 1);
+    if (args.apre && args.arow) gr = args.arow[gr];  // producer planes are in physical row order
+    asrc[j] = apl + ((size_t)blockIdx.z * M + gr) * 2 * K + (p >> 4) * K + 8 * (pslot ^ hsw(row >> 2));
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = wave + 8 * j, row = 16 * (p & 7) + prow;
+    const int gn = min(n0 + row, N - 1);
+    bsrc[j] = G.Bh + (size_t)gn * 2 * K + (p >> 3) * K + 8 * (pslot ^ hsw(row >> 2));
+  }
+  // LDS destinations (wave-uniform): A piece p at (p >> 4) * APL + 16 (p & 15) rows; B after the two A planes
+  auto stage = [&](int kt, int buf) {
+    unsigned short* S = lds16 + buf * STG;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = wave + 8 * j;
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[j] + k0),
+                                       (lds_ptr_t)(S + (p >> 4) * APL + 16 * (p & 15) * LSB), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = wave + 8 * j;
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[j] + k0),
+                                       (lds_ptr_t)(S + 2 * APL + (p >> 3) * BPL + 16 * (p & 7) * LSB), 16, 0, 0);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int rin = lane & 15, hh = lane >> 4;
+  const int ck = ((hh ^ hsw(rin >> 2)) & 3) * 8;
+  const int aoff = (wm * TM * 16 + rin) * LSB + ck, boff = 2 * APL + (wn * TN * 16 + rin) * LSB + ck;
+  auto frags = [&](int buf, h8v (&fa)[TM][2], h8v (&fb)[TN][2]) {
+    const unsigned short* S = lds16 + buf * STG;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fa[a][p] = *reinterpret_cast<const h8v*>(S + aoff + p * APL + a * 16 * LSB);
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fb[b][p] = *reinterpret_cast<const h8v*>(S + boff + p * BPL + b * 16 * LSB);
+  };
+
+  accv acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.0f;
+
+  // 48 MFMA slots of one k-tile: product (l h, h l, h h: smallest first), then (a, b) -- k_gemm_h3m's order
+  auto mfmas = [&](const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int pr = i / 16, a = (i % 16) / 4, b = i % 4;
+      acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][pr == 0 ? 1 : 0], fb[b][pr == 1 ? 1 : 0], acc[a][b],
+                                                         0, 0, 0);
+    }
+  };
+  // one k-tile t (fragments in cur): issue the DMA of k-tile t + 2 (clamped: the last two iterations re-stage the
+  // last k-tile into a buffer nobody reads again), 24 MFMAs, wait for my k-tile t + 1 DMA (the 6 of t + 2 may stay
+  // in flight), barrier (everyone's t + 1 landed; everyone's reads of the buffer t + 2 overwrites, k-tile t - 1,
+  // retired before the previous barrier), read k-tile t + 1's fragments under the other 24 MFMAs
+  const int nk = ke - kb;
+  auto step = [&](int t, const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], h8v (&na)[TM][2], h8v (&nbv)[TN][2]) {
+    stage(min(kb + t + 2, ke - 1), (t + 2) % 3);
+    mfmas(fa, fb, 0, 24);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    frags((t + 1) % 3, na, nbv);
+    mfmas(fa, fb, 24, 48);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  h8v fa0[TM][2], fb0[TN][2], fa1[TM][2], fb1[TN][2];
+  stage(kb, 0);
+  stage(min(kb + 1, ke - 1), 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  frags(0, fa0, fb0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    step(t, fa0, fb0, fa1, fb1);
+    step(t + 1, fa1, fb1, fa0, fb0);
+  }
+  if (t < nk) step(t, fa0, fb0, fa1, fb1);
+  // drain the DMAs still in flight before the workgroup can exit (their LDS must not be reassigned under them)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // undo the scales: rows of A (2^-e_a), rows of B = columns of C (2^-e_b); 16x16 tile: row 4 hh + r, col rin
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = min(n0 + wn * TN * 16 + b * 16 + rin, N - 1);
+    const float sb = G.Bs[(size_t)col * (K / 32)];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(m0 + wm * TM * 16 + a * 16 + 4 * hh + r, M - 1);
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));   // 2^-e_a
+        acc[a][b][r] *= ia * sb;
+      }
+  }
+
+  if (part >= 0) {
+    float* w = args.ws + ((size_t)blockIdx.z * (gridDim.x - args.tdp) + part) * (size_t)(TM * TN * 4 * NT);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[(size_t)((a * TN + b) * 4 + r) * NT + tid] = acc[a][b][r];
+    return;
+  }
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, WM, WN, EPI, 16, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  else
+    epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+}
+
 template <int EPI, int BM>
 static hipError_t launch_h3m_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc) {
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h3m<EPI, BM>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_h3m<EPI, BM>), grid, dim3(2 * BM), lds, s, a, sc);
-  if (tail)
-    hipLaunchKernelGGL((k_gemm_fixup<BM, 128, BM / 64, 2, EPI, 16, true>), dim3(tail, 1, a.ngroups), dim3(2 * BM), 0,
-                       s, a);
+  if (tail)  // y: the 4 fragment rows of each wave
+    hipLaunchKernelGGL((k_gemm_fixup_sub16<BM, 128, BM / 64, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(2 * BM), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1510,6 +1784,58 @@ static bool h3_ready(const GemmArgs& a) {
   bool pre = a.ws && (size_t)a.ngroups * a.M <= kScaleFloats;
   for (int g = 0; g < a.ngroups; ++g) pre = pre && a.g[g].Bh && a.g[g].Bs;
   return pre;
+}
+
+// tile 48: the A split pass (k_rowsplit into the caller's plane workspace, GEMM row order) + k_gemm_h4
+static bool h4_ready(const GemmArgs& a) {
+  if (a.K % 32 || a.K > 4608) return false;
+  if (a.apre) return a.ascale != nullptr;
+  return a.apl && (size_t)a.ngroups * a.M * 2 * (size_t)a.K <= a.apl_halfs;
+}
+
+template <int EPI>
+static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc,
+                              const unsigned short* planes) {
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_h4<EPI>), grid, dim3(512), lds, s, a, sc, planes);
+  if (tail)  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
+    hipLaunchKernelGGL((k_gemm_fixup_sub16<256, 128, 4, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
+static hipError_t launch_h4(const GemmArgs& a, hipStream_t s) {
+  if (a.K % 32 || a.ksplit % 32 || !h3_ready(a) || !h4_ready(a)) return hipErrorInvalidValue;
+  float* sc = a.ws + kWsFloats;
+  const unsigned short* planes = a.apl;
+  if (a.apre) {
+    // planes and scales from the producer (physical rows); the kernel gathers plane rows through arow itself
+    planes = a.apre;
+    if (!a.arow)
+      sc = const_cast<float*>(a.ascale);
+    else
+      hipLaunchKernelGGL(k_gather_scales, dim3((a.M + 255) / 256, 1, a.ngroups), dim3(256), 0, s, a.ascale, a.arow,
+                         sc, a.M);
+  } else {
+    const dim3 grid((a.M + 3) / 4, 1, a.ngroups);
+    const int nv = (a.K + 255) / 256;
+    switch (nv <= 5 ? 5 : nv <= 9 ? 9 : nv <= 14 ? 14 : 18) {
+      case 5: hipLaunchKernelGGL(k_rowsplit<5>, grid, dim3(256), 0, s, a, sc, a.apl); break;
+      case 9: hipLaunchKernelGGL(k_rowsplit<9>, grid, dim3(256), 0, s, a, sc, a.apl); break;
+      case 14: hipLaunchKernelGGL(k_rowsplit<14>, grid, dim3(256), 0, s, a, sc, a.apl); break;
+      default: hipLaunchKernelGGL(k_rowsplit<18>, grid, dim3(256), 0, s, a, sc, a.apl); break;
+    }
+  }
+  const size_t lds = 3 * (2 * (256 + 128) * 32) * sizeof(unsigned short);
+  const int T = ((a.N + 127) / 128) * ((a.M + 255) / 256);
+  const int tail = a.tsplit > 1 ? T - a.tdp : 0;
+  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  switch (a.epi) {
+    case EPI_STORE: return launch_h4_k<EPI_STORE>(a, s, grid, lds, tail, sc, planes);
+    case EPI_GELU: return launch_h4_k<EPI_GELU>(a, s, grid, lds, tail, sc, planes);
+    case EPI_RESID: return launch_h4_k<EPI_RESID>(a, s, grid, lds, tail, sc, planes);
+    case EPI_DGELU: return launch_h4_k<EPI_DGELU>(a, s, grid, lds, tail, sc, planes);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int BM, int MF = 32>
@@ -1545,7 +1871,7 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
 //   exact f32 MFMA   0: 128x128   2: 64x64   4: 32x64            (GEMM_F32)
 //   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
 //   fp16x3 split    36: 128x128, 44: 256x128 (8 waves of 64x64); 46 / 47: the same on 16x16x32 MFMAs
-static bool h3_tile(int t) { return t == 36 || t == 44 || t == 46 || t == 47; }
+static bool h3_tile(int t) { return t == 36 || t == 44 || t == 46 || t == 47 || t == 48; }
 const Tuning kDefaultTuning{};
 int* tuning_field(Tuning& t, const char* key) {
   if (!key) return nullptr;
@@ -1558,6 +1884,8 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "tail_minkt") return &t.tail_minkt;
   if (k == "ln_scales") return &t.ln_scales;
   if (k == "win_attn") return &t.win_attn;
+  if (k == "h4") return &t.h4;
+  if (k == "ln_planes") return &t.ln_planes;
   return nullptr;
 }
 
@@ -1574,6 +1902,7 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 44: return launch_h3<256>(a, s);
     case 46: return launch_h3<128, 16>(a, s);
     case 47: return launch_h3<256, 16>(a, s);
+    case 48: return launch_h4(a, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1709,8 +2038,34 @@ static int pick_tile(const GemmArgs& a) {
 // tile edge of each variant (for the tail split)
 static void variant_tile(int t, int& bm, int& bn, int& bk) {
   bk = 32;
-  bm = t == 44 || t == 47 ? 256 : t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
+  bm = t == 44 || t == 47 || t == 48 ? 256 : t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
   bn = t == 0 || t >= 34 ? 128 : 64;
+}
+
+// the routed tile plus the fallbacks gemm_nt applies (no fp16 B planes: bf16x6 34; no A-plane workspace: 47);
+// fills the fp16 B plane pointers of `a` (Bh, Bs) as a side effect; -1 for an invalid hint
+static int resolve_tile(GemmArgs& a, int tile_hint) {
+  int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
+  if (!valid_tile(t)) return -1;
+  const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+  if (tile_hint < 0 && (t == 44 || t == 47) && TU.h4) t = 48;
+  for (int g = 0; g < a.ngroups; ++g) {
+    a.g[g].Bh = nullptr;
+    a.g[g].Bs = nullptr;
+    if (h3_tile(t) && (!a.ldb || a.ldb == a.K)) split16_of(a.g[g].B, a.K, a.g[g].Bh, a.g[g].Bs);
+  }
+  // the fp16x3 kernels need every group's fp16 B planes and the scale workspace; without them the GEMM runs the
+  // pipelined bf16x6 kernel. Decided BEFORE the tile geometry: the split-K tail sizes its partials from the tile
+  // edge of the kernel that actually runs (a 256-row tile count with 128-row fallback tiles overran ws).
+  if (h3_tile(t) && !h3_ready(a)) t = 34;
+  if (t == 48 && !h4_ready(a)) t = 47;  // no plane workspace (or too small): the in-loop-split kernel, same geometry
+  return t;
+}
+
+int gemm_tile_of(const GemmArgs& a_in, int tile_hint) {
+  GemmArgs a = a_in;
+  if (!a.ws) a.ws = reinterpret_cast<float*>(1);  // h3_ready only checks that a workspace is passed
+  return resolve_tile(a, tile_hint);
 }
 
 hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
@@ -1718,8 +2073,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
-  int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
-  if (!valid_tile(t)) return hipErrorInvalidValue;
+  if (a.apre && (!a.ascale || a.g[0].A2)) return hipErrorInvalidValue;
   const int num_cu = device_cus();
   a.tdp = 0;
   a.tsplit = 1;
@@ -1732,15 +2086,10 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
     for (int g = 0; g < a.ngroups; ++g) ok = ok && !a.g[g].A2;
     a.ascale_phys = ok ? 1 : 0;
   }
-  for (int g = 0; g < a.ngroups; ++g) {
-    a.g[g].Bh = nullptr;
-    a.g[g].Bs = nullptr;
-    if (h3_tile(t) && (!a.ldb || a.ldb == a.K)) split16_of(a.g[g].B, a.K, a.g[g].Bh, a.g[g].Bs);
-  }
-  // the fp16x3 kernels need every group's fp16 B planes and the scale workspace; without them the GEMM runs the
-  // pipelined bf16x6 kernel. Decide that BEFORE the tile geometry below: the split-K tail sizes its partials from
-  // the tile edge of the kernel that actually runs (a 256-row tile count with 128-row fallback tiles overran ws).
-  if (h3_tile(t) && !h3_ready(a)) t = 34;
+  const int t = resolve_tile(a, tile_hint);
+  if (t < 0) return hipErrorInvalidValue;
+  // producer planes are only read by tile 48; every other kernel reads A itself (which the producer then wrote)
+  if (a.apre && t != 48) return hipErrorInvalidValue;
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start

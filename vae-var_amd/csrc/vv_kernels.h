@@ -20,6 +20,8 @@ struct Tuning {
   int small_split_minkt = 24;   // k-tiles per chunk at least, for that split (profiles/r02/smallk)
   int tail_minkt = 12;          // k-tiles per chunk at least, for the split-K tail (profiles/r02/tailk)
   int ln_scales = 1;            // fp16x3 row scales from the LayerNorm producer (0: k_rowscale everywhere)
+  int h4 = 1;                   // the split-operand LDS-DMA fp16x3 kernel (tile 48) where the 256x128 tiles run
+  int ln_planes = 1;            // LayerNorm writes the fp16x3 planes of the tile-48 GEMM it feeds (no split pass)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
 };
 extern const Tuning kDefaultTuning;
@@ -74,12 +76,21 @@ struct GemmArgs {
   // row (arow[r] when gathered), z * M + row; the fp16x3 kernels then skip k_rowscale (no concat A2 allowed)
   const float* ascale;
   int ascale_phys;  // set by gemm_nt: the kernel indexes its row scales by physical row
+  // GEMM_SPLIT16 tile 48: workspace for A's fp16 planes in GEMM row order (groups x M x 2K halfs), or null
+  unsigned short* apl;
+  size_t apl_halfs;
+  // null, or A's planes as its producer wrote them (LayerNorm pl, same layout, indexed by the physical A row like
+  // ascale, which must be set); tile 48 then reads them directly (no k_rowsplit pass)
+  const unsigned short* apre;
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   GemmGroup g[kMaxGroups];
 };
 
 // ws: scratch of at least gemm_ws_floats() floats (may be null: no tail split)
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);
+// the kernel gemm_nt would run for `a` (tile hint -1: the routed choice, incl. the fallbacks), so a producer can
+// decide what form to write A in (tile 48: fp16x3 planes)
+int gemm_tile_of(const GemmArgs& a, int tile_hint = -1);
 size_t gemm_ws_floats();
 
 // GEMM arithmetic:
@@ -124,6 +135,8 @@ struct LnGroup {
   const float* res;   // bwd: added to dx (may alias y), may be null
   float* rs;          // null, or the fp16x3 GEMM row scale of every row written (k_rowscale's value, indexed by
                       // the physical output row: fwd r, bwd map[r]); LN_ROWMAP only
+  unsigned short* pl; // null, or (with rs) the written rows as fp16x3 planes [row][h(C) | l(C)] scaled by rs (the
+                      // split of k_rowsplit, bit for bit), same row index as rs; fwd: y may then be null
 };
 
 struct LnArgs {

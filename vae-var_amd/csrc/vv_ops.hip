@@ -102,6 +102,28 @@ __device__ __forceinline__ unsigned absmax4(unsigned m, const f4& o) {
              max(__float_as_uint(fabsf(o[2])), __float_as_uint(fabsf(o[3]))));
 }
 
+// the row (this lane's float4s ov[v] = elements 4 (sl + v L) ..) scaled by sc and split into fp16 planes
+// [h(C) | l(C)] at p: h = fp16(x sc), l = fp16(x sc - h) -- k_rowsplit's arithmetic, bit for bit
+template <int L, int NV>
+__device__ __forceinline__ void store_planes(unsigned short* p, int C, int sl, const bool (&ok)[NV], const f4 (&ov)[NV],
+                                             float sc) {
+  typedef _Float16 h4t __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (!ok[v]) continue;
+    const int k = 4 * (sl + v * L);
+    h4t hv, lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = ov[v][e] * sc;
+      hv[e] = (_Float16)x;
+      lv[e] = (_Float16)(x - (float)hv[e]);
+    }
+    *reinterpret_cast<h4t*>(p + k) = hv;
+    *reinterpret_cast<h4t*>(p + C + k) = lv;
+  }
+}
+
 // element offsets (relative to the input base, row stride ld) of this lane's float4s of output row r; float4
 // indices past the row end are clamped to its last float4 (always a valid address)
 template <int L, int NV>
@@ -181,22 +203,24 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnArgs a) {
     }
   }
   const float rstd = 1.0f / sqrtf(sub_sum<L>(q) / (float)C + a.eps);
-  float* y = G.y + (size_t)r * a.ldy;
+  float* y = G.y ? G.y + (size_t)r * a.ldy : nullptr;
   unsigned mx = 0;
+  f4 ov[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int j = sl + v * L;
-    f4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (xv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
+    for (int e = 0; e < 4; ++e) ov[v][e] = (xv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
     if (ok[v]) {
-      *reinterpret_cast<f4*>(y + 4 * j) = o;
-      mx = absmax4(mx, o);
+      if (y) *reinterpret_cast<f4*>(y + 4 * j) = ov[v];
+      mx = absmax4(mx, ov[v]);
     }
   }
   if (G.rs) {
     mx = sub_max<L>(mx);
-    if (sl == 0) G.rs[r] = row_scale_of(mx);
+    const float sc = row_scale_of(mx);
+    if (sl == 0) G.rs[r] = sc;
+    if (G.pl) store_planes<L, NV>(G.pl + (size_t)r * 2 * C, C, sl, ok, ov, sc);
   }
   if (sl == 0 && G.stats) {
     G.stats[2 * r] = mean;
@@ -246,23 +270,26 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
   const float m1 = sub_sum<L>(s1) / (float)C;
   const float m2 = sub_sum<L>(s2) / (float)C;
   unsigned mx = 0;
+  f4 ov[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    f4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = rstd * (gv[v][e] * dv[v][e] - m1 - ((xv[v][e] - mean) * rstd) * m2);
+    for (int e = 0; e < 4; ++e) ov[v][e] = rstd * (gv[v][e] * dv[v][e] - m1 - ((xv[v][e] - mean) * rstd) * m2);
     if (G.res) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] += rv[v][e];
+      for (int e = 0; e < 4; ++e) ov[v][e] += rv[v][e];
     }
     if (ok[v]) {
-      *reinterpret_cast<f4*>(G.y + eo[v]) = o;
-      mx = absmax4(mx, o);
+      *reinterpret_cast<f4*>(G.y + eo[v]) = ov[v];
+      mx = absmax4(mx, ov[v]);
     }
   }
   if (G.rs) {  // LN_ROWMAP: the row written is map[r]
     mx = sub_max<L>(mx);
-    if (sl == 0) G.rs[a.map ? a.map[r] : r] = row_scale_of(mx);
+    const float sc = row_scale_of(mx);
+    const int pr = a.map ? a.map[r] : r;
+    if (sl == 0) G.rs[pr] = sc;
+    if (G.pl) store_planes<L, NV>(G.pl + (size_t)pr * 2 * C, C, sl, ok, ov, sc);
   }
 }
 
@@ -282,8 +309,11 @@ static hipError_t ln_launch(const LnArgs& a, hipStream_t s) {
   if ((a.ldx & 3) || (a.ldy & 3) || (a.lddy & 3) || (a.ldres & 3)) return hipErrorInvalidValue;
   if (a.mode == LN_MERGE && ((a.C / 4) & 3)) return hipErrorInvalidValue;
   if (!FWD && (a.ldy != a.ldx || (a.g[0].res && a.ldres != a.ldx))) return hipErrorInvalidValue;
-  for (int g = 0; g < a.ngroups; ++g)
+  for (int g = 0; g < a.ngroups; ++g) {
     if (a.g[g].rs && a.mode != LN_ROWMAP) return hipErrorInvalidValue;
+    if (a.g[g].pl && !a.g[g].rs) return hipErrorInvalidValue;
+    if (FWD && !a.g[g].y && !a.g[g].pl) return hipErrorInvalidValue;
+  }
   const int L = ln_lanes(a.C);
   const int need = (a.C / 4 + L - 1) / L;
   const int NV = need <= 1 ? 1 : need <= 2 ? 2 : need <= 3 ? 3 : need <= 5 ? 5 : 8;
