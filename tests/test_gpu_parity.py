@@ -461,6 +461,31 @@ def test_closure_edge_cases(tiny):
     assert e < 1e-6
 
 
+def test_ln_planes_bitwise(full_dec):
+    """The tile-48 GEMMs fed by a LayerNorm read the fp16x3 planes the LayerNorm kernel wrote (forward: instead of
+    its fp32 output; backward: beside it) instead of a k_rowsplit pass: the config-2 closure (J and dJ/dz) is
+    bit-identical with the per-context knob ln_planes on and off, and so is the J-only evaluation."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    z = torch.from_numpy(0.3 * smooth_field(11, (1, 32, 128, 256), sigma=2.0)).cuda()
+    out = []
+    try:
+        for v in (1, 0):
+            prob.ctx.set_tuning("ln_planes", v)
+            g = torch.empty_like(z)
+            jb, jo = prob.closure(z, g)
+            jb2, jo2 = prob.closure(z, None)
+            out.append((jb, jo, jb2, jo2, g.clone()))
+    finally:
+        prob.ctx.set_tuning("ln_planes", 1)
+    print(f"LN planes on/off: J {out[0][:2]} vs {out[1][:2]}")
+    assert out[0][:4] == out[1][:4]
+    assert torch.equal(out[0][4], out[1][4])
+
+
 def test_ln_row_scales_bitwise(tmp_path):
     """The fp16x3 GEMMs fed by a LayerNorm (qkv, fc1 forward; the proj and fc2 input gradients backward) take the row
     scales the LayerNorm kernel wrote instead of a k_rowscale pass: the config-2 closure (J and dJ/dz) must be

@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3(GemmArgs args, const floa
   f4 ra[AI];
   u4v rq[BQ][2];
   auto aload = [&](int i, int k0) { ra[i] = *reinterpret_cast<const f4*>((k0 < ksplit ? a1p[i] : a2p[i]) + k0); };
-  auto bload = [&](int q, int p, int k0) { rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + p * K + k0); };
+  auto bload = [&](int q, int p, int k0) { rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + 2 * k0 + p * 32); };
   auto asplit = [&](unsigned short* P, int i) {
     const int o = swz(lr + RPP * i, lc);
     h4v hv, lv;
@@ -1404,7 +1404,7 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3m(GemmArgs args, const flo
   f4 ra[AI];
   u4v rq[BQ][2];
   auto aload = [&](int i, int k0) { ra[i] = *reinterpret_cast<const f4*>((k0 < ksplit ? a1p[i] : a2p[i]) + k0); };
-  auto bload = [&](int q, int p, int k0) { rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + p * K + k0); };
+  auto bload = [&](int q, int p, int k0) { rq[q][p] = *reinterpret_cast<const u4v*>(bq[q] + 2 * k0 + p * 32); };
   auto asplit = [&](unsigned short* P, int i) {
     const int o = swz(lr + RPP * i, lc);
     h4v hv, lv;
@@ -1528,7 +1528,7 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3m(GemmArgs args, const flo
 // fp16x3 on pre-split operands, both staged by LDS-DMA (tile 48).
 //
 // k_rowsplit writes A once per GEMM as fp16 planes in GEMM row order (the arow gather and the A2 concat applied),
-// row r = [h(K) | l(K)] scaled by 2^e (the same scale and split arithmetic as k_rowscale + the in-loop split of
+// row r scaled by 2^e and stored chunk-interleaved: [h(k 0..31) | l(k 0..31) | h(k 32..63) | l(k 32..63) | ...] (the same scale and split arithmetic as k_rowscale + the in-loop split of
 // k_gemm_h3m, so the products are bit-identical), exactly B's plane layout. k_gemm_h4 then streams both operands
 // HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write, no VALU split in the loop) through a
 // three-stage ring (3 x 48 KB of 160 KB), keeping two k-tiles in flight across the one raw s_barrier per k-tile
@@ -1539,7 +1539,7 @@ __global__ __launch_bounds__(2 * BM, 1) void k_gemm_h3m(GemmArgs args, const flo
 // tail and epilogue are those of k_gemm_h3m<EPI, 256>, so C is bit-identical to tile 47.
 
 // one wave per logical row: max |A| of the row -> scale 2^(141 - e) (k_rowscale's formula), then the scaled row
-// split into fp16 h = fp16(v), l = fp16(v - h) and stored as planes[r] = [h(K) | l(K)]; NV float4 per lane
+// split into fp16 h = fp16(v), l = fp16(v - h) and stored as chunk-interleaved planes of row r; NV float4 per lane
 template <int NV>
 __global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restrict__ rs, unsigned short* __restrict__ pl) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1576,20 +1576,21 @@ __global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restri
       hv[e] = (_Float16)x;
       lv[e] = (_Float16)(x - (float)hv[e]);
     }
-    *reinterpret_cast<h4v*>(ph + k) = hv;
-    *reinterpret_cast<h4v*>(ph + K + k) = lv;
+    *reinterpret_cast<h4v*>(ph + 2 * (k & ~31) + (k & 31)) = hv;  // chunk-interleaved planes
+    *reinterpret_cast<h4v*>(ph + 2 * (k & ~31) + 32 + (k & 31)) = lv;
   }
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+#ifndef VV_H4_ABL
+#define VV_H4_ABL 0
+#endif
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* __restrict__ ascale,
                                                     const unsigned short* __restrict__ apl) {
   constexpr int BM = 256, BN = 128, BK = 32, NT = 512, WN = 2, WM = 4, TM = 4, TN = 4;
-  constexpr int LSB = BK;                                  // halfs per LDS row (64 B)
-  constexpr int APL = BM * LSB, BPL = BN * LSB;            // halfs per A / B plane of one stage
-  constexpr int STG = 2 * APL + 2 * BPL;                   // 24576 halfs = 48 KB per stage
+  constexpr int STG = (BM + BN) * 2 * BK;                  // [row][h 32 | l 32] halfs: 24576 halfs = 48 KB per stage
   typedef float accv __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
 
@@ -1614,60 +1615,64 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   int mb, nb;
   tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
-  auto hsw = [](int q) { return (0x78 >> (2 * (q & 3))) & 3; };  // 0, 2, 3, 1
   const float* rs = ascale + (size_t)blockIdx.z * M;
 
-  // DMA sources: wave w stages A pieces w, w + 8, w + 16, w + 24 (piece p: plane p >> 4, rows 16 (p & 15) ..) and
-  // B pieces w, w + 8 (plane p >> 3, rows 16 (p & 7) ..); lane i fills LDS bytes 16 i of the piece: row i >> 2,
-  // slot i & 3, which holds the row's k-chunk (i & 3) ^ h((row >> 2) & 3)
-  const int prow = lane >> 2, pslot = lane & 3;
+  // Planes are chunk-interleaved in memory (per row and 32-deep k-tile: h 64 B | l 64 B, one 128-B line) and in
+  // LDS ([row][128 B], A rows then B rows). One DMA instruction fills 8 rows: lane i writes LDS bytes 16 i, row
+  // i >> 3, slot i & 7, which holds the row's 16-B chunk (i & 7) ^ ((row >> 1) & 7) -- the swizzle under which the
+  // 16 rows x one chunk of a fragment read land on 16 distinct 16-B slots of the 256-B bank row (rule 21: applied
+  // to the source address, the LDS image stays lane-linear). Wave w stages A pieces w + 8 j (rows 8 (w + 8 j) ..,
+  // j < 4) and B pieces w + 8 j (j < 2).
+  const int prow = lane >> 3, pslot = lane & 7;
   const unsigned short* asrc[4];
   const unsigned short* bsrc[2];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int p = wave + 8 * j, row = 16 * (p & 15) + prow;
+    const int row = 8 * (wave + 8 * j) + prow;
     int gr = min(m0 + row, M - 1);
     if (args.apre && args.arow) gr = args.arow[gr];  // producer planes are in physical row order
-    asrc[j] = apl + ((size_t)blockIdx.z * M + gr) * 2 * K + (p >> 4) * K + 8 * (pslot ^ hsw(row >> 2));
+    asrc[j] = apl + ((size_t)blockIdx.z * M + gr) * 2 * K + 8 * (pslot ^ ((row >> 1) & 7));
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int p = wave + 8 * j, row = 16 * (p & 7) + prow;
+    const int row = 8 * (wave + 8 * j) + prow;
     const int gn = min(n0 + row, N - 1);
-    bsrc[j] = G.Bh + (size_t)gn * 2 * K + (p >> 3) * K + 8 * (pslot ^ hsw(row >> 2));
+    bsrc[j] = G.Bh + (size_t)gn * 2 * K + 8 * (pslot ^ ((row >> 1) & 7));
   }
-  // LDS destinations (wave-uniform): A piece p at (p >> 4) * APL + 16 (p & 15) rows; B after the two A planes
-  auto stage = [&](int kt, int buf) {
+  // DMA piece q (0..3: A pieces, 4..5: B pieces) of k-tile kt into stage buffer buf
+  auto piece = [&](int kt, int buf, int q) {
     unsigned short* S = lds16 + buf * STG;
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = wave + 8 * j;
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[j] + k0),
-                                       (lds_ptr_t)(S + (p >> 4) * APL + 16 * (p & 15) * LSB), 16, 0, 0);
+    const int k2 = 2 * kt * BK;  // halfs of the row before k-tile kt
+    if (q < 4) {
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[q] + k2), (lds_ptr_t)(S + 8 * (wave + 8 * q) * 64), 16, 0,
+                                       0);
+    } else {
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[q - 4] + k2),
+                                       (lds_ptr_t)(S + (BM + 8 * (wave + 8 * (q - 4))) * 64), 16, 0, 0);
     }
+  };
+  auto stage = [&](int kt, int buf) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int p = wave + 8 * j;
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc[j] + k0),
-                                       (lds_ptr_t)(S + 2 * APL + (p >> 3) * BPL + 16 * (p & 7) * LSB), 16, 0, 0);
-    }
+    for (int q = 0; q < 6; ++q) piece(kt, buf, q);
   };
 
   const int wm = wave / WN, wn = wave % WN;
   const int rin = lane & 15, hh = lane >> 4;
-  const int ck = ((hh ^ hsw(rin >> 2)) & 3) * 8;
-  const int aoff = (wm * TM * 16 + rin) * LSB + ck, boff = 2 * APL + (wn * TN * 16 + rin) * LSB + ck;
+  // fragment (row rin of a 16-row block, k-chunk hh) of plane p: LDS 16-B slot (4 p + hh) ^ ((rin >> 1) & 7)
+  const int ck0 = (hh ^ ((rin >> 1) & 7)) * 8, ck1 = ((4 + hh) ^ ((rin >> 1) & 7)) * 8;
+  const int aoff = (wm * TM * 16 + rin) * 64, boff = (BM + wn * TN * 16 + rin) * 64;
   auto frags = [&](int buf, h8v (&fa)[TM][2], h8v (&fb)[TN][2]) {
     const unsigned short* S = lds16 + buf * STG;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) fa[a][p] = *reinterpret_cast<const h8v*>(S + aoff + p * APL + a * 16 * LSB);
+      for (int p = 0; p < 2; ++p)
+        fa[a][p] = *reinterpret_cast<const h8v*>(S + aoff + a * 16 * 64 + (p ? ck1 : ck0));
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) fb[b][p] = *reinterpret_cast<const h8v*>(S + boff + p * BPL + b * 16 * LSB);
+      for (int p = 0; p < 2; ++p)
+        fb[b][p] = *reinterpret_cast<const h8v*>(S + boff + b * 16 * 64 + (p ? ck1 : ck0));
   };
 
   accv acc[TM][TN];
@@ -1679,10 +1684,27 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
       for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.0f;
 
   // 48 MFMA slots of one k-tile: product (l h, h l, h h: smallest first), then (a, b) -- k_gemm_h3m's order
-  auto mfmas = [&](const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], int i0, int i1) {
+  // Slot order: the 16 (l h), then (h l) for b = 0, 1, [barrier], (h l) for b = 2, 3, then the 16 (h h). Every
+  // accumulator still gets l h, h l, h h in that order (k_gemm_h3m's per-accumulator order, so C is unchanged),
+  // but A's l-plane fragments and B's l-plane fragments b = 0, 1 die in the first half: the next k-tile's
+  // fragments are read right after the barrier into those registers plus 40 fresh ones, under all 24 MFMAs of
+  // the second half.
+  // sk >= 0: also issue DMA pieces 3 h .. 3 h + 2 of k-tile sk into buffer sb, one every 8 MFMA slots (h = i0 / 24)
+  auto mfmas = [&](const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], int i0, int i1, int sk = -1, int sb = 0) {
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
-      const int pr = i / 16, a = (i % 16) / 4, b = i % 4;
+      if (sk >= 0 && ((i - i0) & 7) == 0) {
+        piece(sk, sb, 3 * (i0 / 24) + (i - i0) / 8);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      int pr, a, b;
+      if (i < 16) {
+        pr = 0, a = i / 4, b = i % 4;
+      } else if (i < 32) {
+        pr = 1, b = (i - 16) / 4, a = (i - 16) % 4;
+      } else {
+        pr = 2, a = (i - 32) / 4, b = (i - 32) % 4;
+      }
       acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][pr == 0 ? 1 : 0], fb[b][pr == 1 ? 1 : 0], acc[a][b],
                                                          0, 0, 0);
     }
@@ -1692,16 +1714,31 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   // in flight), barrier (everyone's t + 1 landed; everyone's reads of the buffer t + 2 overwrites, k-tile t - 1,
   // retired before the previous barrier), read k-tile t + 1's fragments under the other 24 MFMAs
   const int nk = ke - kb;
+  // VV_H4_ABL (timing ablations of a tools build only, results wrong): 1 no DMA in the loop, 2 no MFMAs, 3 no
+  // fragment reads in the loop, 4 no wait / barrier in the loop
   auto step = [&](int t, const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], h8v (&na)[TM][2], h8v (&nbv)[TN][2]) {
-    stage(min(kb + t + 2, ke - 1), (t + 2) % 3);
-    mfmas(fa, fb, 0, 24);
+    const int sk = VV_H4_ABL == 1 ? -1 : min(kb + t + 2, ke - 1), sb = (t + 2) % 3;
+    // the DMA of k-tile t + 2 spread over both halves (3 pieces each); at the wait my k-tile t + 1 pieces must have
+    // landed, the 3 first-half pieces of t + 2 may stay in flight
+    if (VV_H4_ABL != 2) mfmas(fa, fb, 0, 24, sk, sb);
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (VV_H4_ABL != 4 && VV_H4_ABL != 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if (VV_H4_ABL != 4) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    frags((t + 1) % 3, na, nbv);
-    mfmas(fa, fb, 24, 48);
+    if (VV_H4_ABL != 3) frags((t + 1) % 3, na, nbv);
+    if (VV_H4_ABL == 2 || VV_H4_ABL == 3) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          asm volatile("" ::"v"(na[a][p]), "v"(fa[a][p]));
+          asm volatile("" ::"v"(nbv[a][p]), "v"(fb[a][p]));
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (VV_H4_ABL != 2) mfmas(fa, fb, 24, 48, sk, sb);
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1983,8 +2020,8 @@ __global__ __launch_bounds__(256) void k_split16_rows(const float* __restrict__ 
     const float v = x[k] * s;
     const _Float16 h = (_Float16)v;
     const _Float16 l = (_Float16)(v - (float)h);
-    d[k] = __builtin_bit_cast(unsigned short, h);
-    d[K + k] = __builtin_bit_cast(unsigned short, l);
+    d[2 * (k & ~31) + (k & 31)] = __builtin_bit_cast(unsigned short, h);  // chunk-interleaved planes
+    d[2 * (k & ~31) + 32 + (k & 31)] = __builtin_bit_cast(unsigned short, l);
   }
   if (tid == 0) sc[(size_t)r * K / 32] = __uint_as_float((E - 14u) << 23);
 }

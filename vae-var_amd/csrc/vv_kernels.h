@@ -51,7 +51,8 @@ struct GemmGroup {
   float* aux;
   const unsigned short* Bp;  // filled in by gemm_nt: bf16 split planes of B (registered weight arena) or null
   const unsigned short* Ap;  // bf16 split planes of A, rows [3][lda] (caller-provided or registered), or null
-  const unsigned short* Bh;  // filled in by gemm_nt (GEMM_SPLIT16): fp16 planes of B, per row [h | l] x K, or null
+  const unsigned short* Bh;  // filled in by gemm_nt (GEMM_SPLIT16): fp16 planes of B, per row 2K halfs chunk-interleaved
+                             // ([h(k 0..31) | l(k 0..31) | h(k 32..63) | ...]), or null
   const float* Bs;           // ... and the row scales: row n of B has 2^-e = Bs[n * K / 32]
 };
 
@@ -104,7 +105,8 @@ bool valid_tile(int t);
 // Weight arenas with precomputed split planes. The planes buffer of an arena of n floats holds, at these
 // offsets (split_arena_bytes(n) bytes in all):
 //   bf16: [0, 3n) unsigned shorts; row r of the [N][K] operand at float offset o = B - base: 3*(o + r*K) = h[K], m[K], l[K]
-//   fp16: [3n, 5n) unsigned shorts; at 3n + 2*(o + r*K): h[K], l[K] of the row scaled by 2^e
+//   fp16: [3n, 5n) unsigned shorts; at 3n + 2*(o + r*K): the row scaled by 2^e as h / l fp16 planes, interleaved
+//         per 32-element k-chunk (h(32) | l(32) per chunk: one 128-B line per row and k-tile)
 //   row scales: floats after that; 2^-e of the row starting at float offset f at index f / 32
 size_t split_arena_bytes(size_t n);
 void register_split_arena(const float* base, size_t n, const unsigned short* planes);
@@ -135,7 +137,7 @@ struct LnGroup {
   const float* res;   // bwd: added to dx (may alias y), may be null
   float* rs;          // null, or the fp16x3 GEMM row scale of every row written (k_rowscale's value, indexed by
                       // the physical output row: fwd r, bwd map[r]); LN_ROWMAP only
-  unsigned short* pl; // null, or (with rs) the written rows as fp16x3 planes [row][h(C) | l(C)] scaled by rs (the
+  unsigned short* pl; // null, or (with rs) the written rows as fp16x3 planes [row][2C], chunk-interleaved, scaled by rs (the
                       // split of k_rowsplit, bit for bit), same row index as rs; fwd: y may then be null
 };
 

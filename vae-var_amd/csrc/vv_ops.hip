@@ -102,8 +102,8 @@ __device__ __forceinline__ unsigned absmax4(unsigned m, const f4& o) {
              max(__float_as_uint(fabsf(o[2])), __float_as_uint(fabsf(o[3]))));
 }
 
-// the row (this lane's float4s ov[v] = elements 4 (sl + v L) ..) scaled by sc and split into fp16 planes
-// [h(C) | l(C)] at p: h = fp16(x sc), l = fp16(x sc - h) -- k_rowsplit's arithmetic, bit for bit
+// the row (this lane's float4s ov[v] = elements 4 (sl + v L) ..) scaled by sc and split into fp16 planes at p,
+// chunk-interleaved per 32 elements ([h(32) | l(32)] ...): h = fp16(x sc), l = fp16(x sc - h) -- k_rowsplit's arithmetic, bit for bit
 template <int L, int NV>
 __device__ __forceinline__ void store_planes(unsigned short* p, int C, int sl, const bool (&ok)[NV], const f4 (&ov)[NV],
                                              float sc) {
@@ -119,8 +119,8 @@ __device__ __forceinline__ void store_planes(unsigned short* p, int C, int sl, c
       hv[e] = (_Float16)x;
       lv[e] = (_Float16)(x - (float)hv[e]);
     }
-    *reinterpret_cast<h4t*>(p + k) = hv;
-    *reinterpret_cast<h4t*>(p + C + k) = lv;
+    *reinterpret_cast<h4t*>(p + 2 * (k & ~31) + (k & 31)) = hv;  // chunk-interleaved (k_rowsplit's layout)
+    *reinterpret_cast<h4t*>(p + 2 * (k & ~31) + 32 + (k & 31)) = lv;
   }
 }
 
