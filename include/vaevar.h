@@ -209,7 +209,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    16x16x32-MFMA form, 1), "small_split" (whole-grid split-K of sub-chip fp16x3 GEMMs, 1), "small_split_minkt"
    (24), "tail_minkt" (k-tiles per split-K tail chunk, 12), "ln_scales" (row scales from the LayerNorm, 1),
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
-   the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1). Results stay fp32-level for every value; a change drops the
+   the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1), "gattn" (the
+   LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key: VV_E_ARG. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);
@@ -220,6 +221,13 @@ int vv_set_debug_sync(int enable);
    engine does for every model weight at vv_load_weights; B must stay alive and unchanged until
    vv_ctx_destroy (which frees the planes) */
 int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K);
+
+/* global-window attention as LGUnet_all_1's LG layer 0 runs it (networks/LGUnet_all.py:689, 696; SD_attn without
+   mask, networks/utils/Attention.py:599-664): out[t][h d_h + d] = sum_j softmax_j(q_t . k_j) v_j[d] per head h, for
+   qkv [N][3C] (q already scaled by head_dim^-0.5 and rotated, k rotated, as the kernel after the qkv projection
+   sees them) and out [N][C]; the flash MFMA kernel of vv_gattn.hip (fp16x3 products, fp32 softmax). head_dim 64,
+   96, 128 or 192, otherwise VV_E_ARG. Kernel tests and tools; the forecast model calls the kernel itself. */
+int vv_attention_global(vv_ctx* ctx, const float* qkv, float* out, int N, int C, int heads, void* stream);
 
 /* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), K a multiple of 32. tile = -1 picks the
    kernel as the engine does; otherwise one of the library kernels: 0 / 2 / 4 exact-f32 MFMA 128x128 / 64x64 /

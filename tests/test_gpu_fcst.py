@@ -120,3 +120,60 @@ def test_integrate_forecast(grid):
     e = rel(out.cpu(), ref)
     print(f"integrate {grid}: rel {e:.2e}")
     assert e < 1e-5
+
+
+def _attn_ref_fp64(qkv, heads):
+    """softmax(q k^T) v per head in fp64 on the GPU (the global-window SD_attn without mask, Attention.py:599-664)."""
+    N, C3 = qkv.shape
+    C = C3 // 3
+    hd = C // heads
+    q, k, v = qkv.double().split(C, dim=1)
+    out = torch.empty(N, C, dtype=torch.float64, device=qkv.device)
+    for h in range(heads):
+        sl = slice(h * hd, (h + 1) * hd)
+        s = q[:, sl] @ k[:, sl].t()
+        out[:, sl] = torch.softmax(s, dim=1) @ v[:, sl]
+    return out
+
+
+@pytest.mark.parametrize("N,C,heads,logit", [(300, 384, 2, 1.0), (1000, 1152, 6, 3.0), (777, 256, 4, 8.0),
+                                             (2049, 384, 3, 2.0), (16200, 1152, 6, 1.0)])
+def test_attention_global_vs_fp64(N, C, heads, logit):
+    """vv_attention_global (the flash MFMA kernel of the 0.25-degree global LG window: fp16x3 products, fp32 online
+    softmax) against fp64 softmax attention: N not a multiple of the 32-key stage or the 128-query block, head_dim
+    64 / 96 / 192, logits up to ~|logit| x 20 (online-softmax rescales in most stages, one query spiked 6x), token
+    norms of q and k spanning e^+-1 and of v e^+-4, and the full 16,200-token / 6-head / hd-192 shape. Error <=
+    max(1e-5, 2x torch fp32's) of max |out|."""
+    from vaevar.engine import Context
+
+    ctx = Context.get(0)
+    g = torch.Generator(device="cuda").manual_seed(N + C + heads)
+    qkv = torch.randn(N, 3 * C, device="cuda", generator=g)
+    qkv[:, :C] *= logit / (C // heads) ** 0.25
+    qkv[:, C:2 * C] /= (C // heads) ** 0.25
+    qkv[:, :2 * C] *= torch.exp(torch.empty(N, 1, device="cuda").uniform_(-1, 1, generator=g))
+    qkv[:, 2 * C:] *= torch.exp(torch.empty(N, 1, device="cuda").uniform_(-4, 4, generator=g))
+    qkv[N // 3, :C] *= 6.0  # one query with a logit spike
+    out = ctx.attention_global(qkv, heads)
+    ref = _attn_ref_fp64(qkv, heads)
+    e = float((out.double() - ref).abs().max() / ref.abs().max())
+    # the same attention in torch fp32 (what the reference computes) against fp64, for scale
+    q, k, v = qkv.split(C, dim=1)
+    hd = C // heads
+    e32 = 0.0
+    for h in range(heads):
+        sl = slice(h * hd, (h + 1) * hd)
+        o32 = torch.softmax(q[:, sl] @ k[:, sl].t(), dim=1) @ v[:, sl]
+        e32 = max(e32, float((o32.double() - ref[:, sl]).abs().max() / ref.abs().max()))
+    print(f"global attention N {N} C {C} heads {heads}: rel {e:.2e} (torch fp32: {e32:.2e})")
+    assert torch.isfinite(out).all() and e < max(1e-5, 2 * e32), (e, e32)
+
+
+def test_attention_global_rejects():
+    from vaevar._lib import VVError
+    from vaevar.engine import Context
+
+    ctx = Context.get(0)
+    qkv = torch.zeros(64, 3 * 80, device="cuda")
+    with pytest.raises(VVError, match="1001"):
+        ctx.attention_global(qkv, 5)  # head_dim 16

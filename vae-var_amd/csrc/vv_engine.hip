@@ -304,6 +304,8 @@ struct vv_ctx {
   vv::Tuning tune;              // dispatch knobs of every model of this context (vv_set_tuning)
   unsigned short* apl = nullptr;  // vv_gemm's A-plane workspace (tile 48), grown on demand
   size_t apl_halfs = 0;
+  void* gattn_ws = nullptr;       // vv_attention_global's workspace, grown on demand
+  size_t gattn_bytes = 0;
   std::vector<std::unique_ptr<Model>> models;
   Problem prob;
   std::unique_ptr<Sc4Problem> sc4;  // vv_sc4dvar_bind
@@ -1496,6 +1498,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   (void)hipFree(ctx->doutf);
   (void)hipFree(ctx->gemm_ws);
   if (ctx->apl) (void)hipFree(ctx->apl);
+  if (ctx->gattn_ws) (void)hipFree(ctx->gattn_ws);
   delete ctx;
   return 0;
 }
@@ -2089,6 +2092,26 @@ int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, co
     a.apl_halfs = ctx->apl_halfs;
   }
   VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
+  return 0;
+}
+
+int vv_attention_global(vv_ctx* ctx, const float* qkv, float* out, int N, int C, int heads, void* stream) {
+  if (!ctx || !qkv || !out) return fail(VV_E_ARG, "null argument");
+  if (N <= 0 || !vv::gattn_supported(C, heads))
+    return fail(VV_E_ARG, "global attention needs N > 0 and head_dim 64, 96, 128 or 192 (N %d, C %d, heads %d)", N, C,
+                heads);
+  int r = set_dev(ctx);
+  if (r) return r;
+  const size_t need = vv::gattn_ws_bytes(N, C, heads);
+  if (need > ctx->gattn_bytes) {
+    VV_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (ctx->gattn_ws) VV_HIP(hipFree(ctx->gattn_ws));
+    ctx->gattn_ws = nullptr;
+    ctx->gattn_bytes = 0;
+    VV_HIP(hipMalloc(&ctx->gattn_ws, need));
+    ctx->gattn_bytes = need;
+  }
+  VV_HIP(vv::gattn(qkv, out, C, N, C, heads, ctx->gattn_ws, (hipStream_t)stream));
   return 0;
 }
 

@@ -733,6 +733,7 @@ struct FModel {
   const vv::Tuning* tune = nullptr;  // the owning context's dispatch knobs
   // global-window attention through the split GEMM when the window is large: S/P [heads][N][Np], V^T [heads][hd][Np]
   float *att_s = nullptr, *att_vt = nullptr;
+  void* gattn_ws = nullptr;  // the flash MFMA kernel's planes and scales (vv::gattn_ws_bytes), when it applies
 };
 
 namespace {
@@ -931,7 +932,15 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     fa.sh = sh;
     fa.nWh = S.H / S.wh;
     fa.nWw = S.W / S.ww;
-    if (S.global && N >= kGemmAttnMin && m.att_s && G == 1) {
+    const bool use_gattn = S.global && m.gattn_ws && G == 1 && gattn_supported(C, S.heads) &&
+                           (m.tune ? *m.tune : vv::kDefaultTuning).gattn;
+    if (use_gattn) {
+      // one window over the whole grid per image: the flash MFMA kernel (vv_gattn.hip), scores never in HBM
+      ph = prof_begin(st);
+      for (int b0 = 0; b0 < nwin; ++b0)
+        FH(gattn(m.qkv + (size_t)b0 * N * 3 * C, m.t2 + (size_t)b0 * N * C, C, N, C, S.heads, m.gattn_ws, st));
+      prof_end(ph, st, PC_ATTN, 4.0 * nwin * (double)N * N * C, 16.0 * nwin * (double)N * C);
+    } else if (S.global && N >= kGemmAttnMin && m.att_s && G == 1) {
       // S_h = Q_h K_h^T (heads as GEMM groups; q rotated + scaled, k rotated), P = softmax_rows(S), O_h = P V_h
       const int Np = (N + 31) / 32 * 32, hd = S.hd;
       for (int b0 = 0; b0 < nwin; ++b0) {
@@ -1097,7 +1106,16 @@ int create(const vv_lgunet_config* cfg, int batch, FModel** out, std::string& er
       return bail(r);
   {
     const size_t N = (size_t)c.Hg * c.Wg, Np = (N + 31) / 32 * 32;
-    if (N >= (size_t)kGemmAttnMin) {
+    const int h0 = c.lg_heads[0];  // LG layer 0 is the global window
+    if (gattn_supported(c.E, h0)) {
+      void* p = nullptr;
+      if (hipMalloc(&p, gattn_ws_bytes((int)N, c.E, h0)) != hipSuccess)
+        return bail(ferr(err, VV_E_ALLOC, "global-attention workspace"));
+      m->owned.push_back(p);
+      m->bytes += (int64_t)gattn_ws_bytes((int)N, c.E, h0);
+      m->gattn_ws = p;
+    }
+    if (N >= (size_t)kGemmAttnMin && !m->gattn_ws) {
       const int hmax = *std::max_element(c.lg_heads.begin(), c.lg_heads.end());
       if ((r = dalloc(*m, (size_t)hmax * N * Np, &m->att_s, err)) || (r = dalloc(*m, (size_t)c.E * Np, &m->att_vt, err)))
         return bail(r);

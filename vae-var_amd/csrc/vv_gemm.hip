@@ -1582,9 +1582,7 @@ __global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restri
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-#ifndef VV_H4_ABL
-#define VV_H4_ABL 0
-#endif
+
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* __restrict__ ascale,
@@ -1683,62 +1681,64 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.0f;
 
-  // 48 MFMA slots of one k-tile: product (l h, h l, h h: smallest first), then (a, b) -- k_gemm_h3m's order
-  // Slot order: the 16 (l h), then (h l) for b = 0, 1, [barrier], (h l) for b = 2, 3, then the 16 (h h). Every
-  // accumulator still gets l h, h l, h h in that order (k_gemm_h3m's per-accumulator order, so C is unchanged),
-  // but A's l-plane fragments and B's l-plane fragments b = 0, 1 die in the first half: the next k-tile's
-  // fragments are read right after the barrier into those registers plus 40 fresh ones, under all 24 MFMAs of
-  // the second half.
-  // sk >= 0: also issue DMA pieces 3 h .. 3 h + 2 of k-tile sk into buffer sb, one every 8 MFMA slots (h = i0 / 24)
-  auto mfmas = [&](const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], int i0, int i1, int sk = -1, int sb = 0) {
+  // 48 MFMA slots of one k-tile. Slot order: the 16 (l h), then (h l) for b = 0, 1, [barrier], (h l) for b = 2, 3,
+  // then the 16 (h h). Every accumulator still gets l h, h l, h h in that order (k_gemm_h3m's per-accumulator order,
+  // so C is unchanged), but A's l-plane fragments and B's l-plane fragments b = 0, 1 die in the first half.
+  auto mfma1 = [&](const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], int i) {
+    int pr, a, b;
+    if (i < 16) {
+      pr = 0, a = i / 4, b = i % 4;
+    } else if (i < 32) {
+      pr = 1, b = (i - 16) / 4, a = (i - 16) % 4;
+    } else {
+      pr = 2, a = (i - 32) / 4, b = (i - 32) % 4;
+    }
+    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][pr == 0 ? 1 : 0], fb[b][pr == 1 ? 1 : 0], acc[a][b], 0, 0,
+                                                       0);
+  };
+  // fragment read j (0..15) of k-tile buffer buf, in the order the next k-tile's slots need them: A l-plane
+  // (a = 0..3), B h-plane, A h-plane, B l-plane
+  auto read1 = [&](int buf, int j, h8v (&na)[TM][2], h8v (&nbv)[TN][2]) {
+    const unsigned short* S = lds16 + buf * STG;
+    if (j < 4)
+      na[j][1] = *reinterpret_cast<const h8v*>(S + aoff + j * 16 * 64 + ck1);
+    else if (j < 8)
+      nbv[j - 4][0] = *reinterpret_cast<const h8v*>(S + boff + (j - 4) * 16 * 64 + ck0);
+    else if (j < 12)
+      na[j - 8][0] = *reinterpret_cast<const h8v*>(S + aoff + (j - 8) * 16 * 64 + ck0);
+    else
+      nbv[j - 12][1] = *reinterpret_cast<const h8v*>(S + boff + (j - 12) * 16 * 64 + ck1);
+  };
+  // One k-tile t (fragments in cur): the DMA of k-tile t + 2 (clamped: the last two iterations re-stage the last
+  // k-tile into a buffer nobody reads again) is issued as 6 pieces, one every 8 MFMA slots; after the first 24 slots
+  // wait for my k-tile t + 1 pieces (the 3 first-half pieces of t + 2 may stay in flight) and barrier (everyone's
+  // t + 1 landed; everyone's reads of the buffer t + 2 overwrites, k-tile t - 1, retired before the previous
+  // barrier); then k-tile t + 1's 16 fragment reads, one beside each of the next 16 MFMA slots (a burst of 16
+  // ds_read_b128 per wave stalls the wave's MFMA issue behind the LDS queue).
+  const int nk = ke - kb;
+  auto step = [&](int t, const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], h8v (&na)[TM][2], h8v (&nbv)[TN][2]) {
+    const int sk = min(kb + t + 2, ke - 1), sb = (t + 2) % 3, rb = (t + 1) % 3;
 #pragma unroll
-    for (int i = i0; i < i1; ++i) {
-      if (sk >= 0 && ((i - i0) & 7) == 0) {
-        piece(sk, sb, 3 * (i0 / 24) + (i - i0) / 8);
+    for (int i = 0; i < 24; ++i) {
+      if ((i & 7) == 0) {
+        piece(sk, sb, i / 8);
         __builtin_amdgcn_sched_barrier(0);
       }
-      int pr, a, b;
-      if (i < 16) {
-        pr = 0, a = i / 4, b = i % 4;
-      } else if (i < 32) {
-        pr = 1, b = (i - 16) / 4, a = (i - 16) % 4;
-      } else {
-        pr = 2, a = (i - 32) / 4, b = (i - 32) % 4;
-      }
-      acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][pr == 0 ? 1 : 0], fb[b][pr == 1 ? 1 : 0], acc[a][b],
-                                                         0, 0, 0);
-    }
-  };
-  // one k-tile t (fragments in cur): issue the DMA of k-tile t + 2 (clamped: the last two iterations re-stage the
-  // last k-tile into a buffer nobody reads again), 24 MFMAs, wait for my k-tile t + 1 DMA (the 6 of t + 2 may stay
-  // in flight), barrier (everyone's t + 1 landed; everyone's reads of the buffer t + 2 overwrites, k-tile t - 1,
-  // retired before the previous barrier), read k-tile t + 1's fragments under the other 24 MFMAs
-  const int nk = ke - kb;
-  // VV_H4_ABL (timing ablations of a tools build only, results wrong): 1 no DMA in the loop, 2 no MFMAs, 3 no
-  // fragment reads in the loop, 4 no wait / barrier in the loop
-  auto step = [&](int t, const h8v (&fa)[TM][2], const h8v (&fb)[TN][2], h8v (&na)[TM][2], h8v (&nbv)[TN][2]) {
-    const int sk = VV_H4_ABL == 1 ? -1 : min(kb + t + 2, ke - 1), sb = (t + 2) % 3;
-    // the DMA of k-tile t + 2 spread over both halves (3 pieces each); at the wait my k-tile t + 1 pieces must have
-    // landed, the 3 first-half pieces of t + 2 may stay in flight
-    if (VV_H4_ABL != 2) mfmas(fa, fb, 0, 24, sk, sb);
-    __builtin_amdgcn_sched_barrier(0);
-    if (VV_H4_ABL != 4 && VV_H4_ABL != 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (VV_H4_ABL != 4) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (VV_H4_ABL != 3) frags((t + 1) % 3, na, nbv);
-    if (VV_H4_ABL == 2 || VV_H4_ABL == 3) {
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          asm volatile("" ::"v"(na[a][p]), "v"(fa[a][p]));
-          asm volatile("" ::"v"(nbv[a][p]), "v"(fb[a][p]));
-        }
+      mfma1(fa, fb, i);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (VV_H4_ABL != 2) mfmas(fa, fb, 24, 48, sk, sb);
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 24; i < 48; ++i) {
+      if ((i & 7) == 0) piece(sk, sb, 3 + (i - 24) / 8);
+      if (i - 24 < 16) read1(rb, i - 24, na, nbv);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma1(fa, fb, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1923,6 +1923,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "win_attn") return &t.win_attn;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
+  if (k == "gattn") return &t.gattn;
   return nullptr;
 }
 

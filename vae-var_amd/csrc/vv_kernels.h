@@ -22,6 +22,7 @@ struct Tuning {
   int ln_scales = 1;            // fp16x3 row scales from the LayerNorm producer (0: k_rowscale everywhere)
   int h4 = 1;                   // the split-operand LDS-DMA fp16x3 kernel (tile 48) where the 256x128 tiles run
   int ln_planes = 1;            // LayerNorm writes the fp16x3 planes of the tile-48 GEMM it feeds (no split pass)
+  int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
 };
 extern const Tuning kDefaultTuning;
@@ -86,6 +87,20 @@ struct GemmArgs {
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   GemmGroup g[kMaxGroups];
 };
+
+// Global-window attention (vv_gattn.hip): out[t][h hd + d] = softmax_j(q_t . k_j) v_j per head, for N tokens of a
+// qkv buffer [N][3C] (q already scaled / rotated); fp16x3 MFMA products, fp32 softmax. ws: gattn_ws_bytes().
+struct GattnArgs {
+  const float* qkv;
+  float* out;
+  int ldo, N, Np, C, heads;
+  unsigned short *qp, *kp, *vp;  // fragment-ordered fp16 planes (k_gattn_prep)
+  float* qs;                     // [heads][Np] score scale per query: 2^-eq 2^-ek
+  float* vsc;                    // [heads] output scale 2^-ev 2^-14
+};
+bool gattn_supported(int C, int heads);
+size_t gattn_ws_bytes(int N, int C, int heads);
+hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads, void* ws, hipStream_t st);
 
 // ws: scratch of at least gemm_ws_floats() floats (may be null: no tail split)
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);

@@ -110,6 +110,7 @@ _SIGS = {
     "vv_set_tuning": (c_int, [c_void_p, ctypes.c_char_p, c_int]),
     "vv_get_tuning": (c_int, [c_void_p, ctypes.c_char_p, P(c_int)]),
     "vv_set_debug_sync": (c_int, [c_int]),
+    "vv_attention_global": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "vv_gemm_register_weight": (c_int, [c_void_p, c_void_p, c_int, c_int]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "vv_sc4dvar_bind": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

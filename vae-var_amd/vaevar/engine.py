@@ -40,7 +40,7 @@ class Context:
     # per-context dispatch knobs (vv_set_tuning; defaults = the measured choices). A/B runs set them from the
     # environment as VAEVAR_<KEY> (e.g. VAEVAR_H3_MINK=384); the library itself reads no environment.
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
-                   "win_attn", "h4", "ln_planes")
+                   "win_attn", "h4", "ln_planes", "gattn")
 
     def __init__(self, device: int = 0):
         self.device = device
@@ -147,6 +147,13 @@ class Context:
     def set_closure_graph(self, enable: bool):
         """Replay the closure from a captured hipGraph (default) or launch its kernels eagerly."""
         check(lib.vv_set_closure_graph(self.h, 1 if enable else 0), "set_closure_graph")
+
+    def attention_global(self, qkv, heads: int):
+        """softmax(q k^T) v per head over all N tokens of qkv [N, 3C] (vv_attention_global); returns out [N, C]."""
+        N, C3 = qkv.shape
+        out = torch.empty(N, C3 // 3, device=qkv.device, dtype=torch.float32)
+        check(lib.vv_attention_global(self.h, _ptr(qkv), _ptr(out), N, C3 // 3, heads, _stream()), "attention_global")
+        return out
 
     def gemm_register_weight(self, B):
         """Precompute B's split planes (bf16 and fp16; B must outlive the context and stay unchanged)."""
