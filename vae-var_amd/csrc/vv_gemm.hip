@@ -2086,7 +2086,12 @@ static int resolve_tile(GemmArgs& a, int tile_hint) {
   int t = tile_hint >= 0 ? tile_hint : pick_tile(a);
   if (!valid_tile(t)) return -1;
   const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
-  if (tile_hint < 0 && (t == 44 || t == 47) && TU.h4) t = 48;
+  // tile 48 wherever the 256x128 fp16x3 tiles run, and for the 128x128-routed ones that still give >= 144 256-row
+  // tiles (N 4608 at 2048 rows: fc1 forward, the fc2 input gradient; same-box 2048 x 4608 x 1152: 75.9 us incl. the
+  // split pass vs 91.3 / ~90 for tiles 47 / 36); the 72-tile 1152 x 1152 GEMMs stay on 128x128 tiles
+  if (tile_hint < 0 && TU.h4 && a.math == GEMM_SPLIT16 &&
+      (t == 44 || t == 47 || (t == 36 && tiles_of(a, 256, 128) >= 144)))
+    t = 48;
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bh = nullptr;
     a.g[g].Bs = nullptr;
