@@ -2111,7 +2111,7 @@ int vv_attention_global(vv_ctx* ctx, const float* qkv, float* out, int N, int C,
     VV_HIP(hipMalloc(&ctx->gattn_ws, need));
     ctx->gattn_bytes = need;
   }
-  VV_HIP(vv::gattn(qkv, out, C, N, C, heads, ctx->gattn_ws, (hipStream_t)stream));
+  VV_HIP(vv::gattn(qkv, out, C, N, C, heads, ctx->gattn_ws, (hipStream_t)stream, ctx->tune.gattn_qf));
   return 0;
 }
 

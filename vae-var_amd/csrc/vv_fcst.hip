@@ -938,7 +938,8 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
       // one window over the whole grid per image: the flash MFMA kernel (vv_gattn.hip), scores never in HBM
       ph = prof_begin(st);
       for (int b0 = 0; b0 < nwin; ++b0)
-        FH(gattn(m.qkv + (size_t)b0 * N * 3 * C, m.t2 + (size_t)b0 * N * C, C, N, C, S.heads, m.gattn_ws, st));
+        FH(gattn(m.qkv + (size_t)b0 * N * 3 * C, m.t2 + (size_t)b0 * N * C, C, N, C, S.heads, m.gattn_ws, st,
+                 (m.tune ? *m.tune : vv::kDefaultTuning).gattn_qf));
       prof_end(ph, st, PC_ATTN, 4.0 * nwin * (double)N * N * C, 16.0 * nwin * (double)N * C);
     } else if (S.global && N >= kGemmAttnMin && m.att_s && G == 1) {
       // S_h = Q_h K_h^T (heads as GEMM groups; q rotated + scaled, k rotated), P = softmax_rows(S), O_h = P V_h

@@ -34,9 +34,7 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_t;
 
-constexpr int kQW = 32;          // queries per wave (two 16-query column blocks)
-constexpr int kWaves = 4;        // one wave per SIMD (the kernel holds ~300 registers per lane)
-constexpr int kQB = kQW * kWaves;  // queries per workgroup
+constexpr int kQB = 128;         // queries per workgroup: QF 16-query column blocks per wave x 8 / QF waves
 constexpr int kKB = 32;          // keys per LDS stage
 constexpr int kVmaxBlocks = 64;  // partial-maximum blocks of k_gattn_max
 
@@ -154,13 +152,13 @@ __global__ __launch_bounds__(256) void k_gattn_prep(GattnArgs a, const unsigned*
   if (b == 0 && tid == 0) a.vsc[h] = __uint_as_float((254u << 23) - __float_as_uint(vs)) * (1.0f / 16384.0f);
 }
 
-// softmax(q k^T) v for one head and 128 queries (4 waves x 32). Per 32-key stage (three-stage LDS ring filled by
-// LDS-DMA, two stages in flight across the one barrier per stage, as k_gemm_h4): S^T = K Q^T (72 MFMAs per wave),
-// online softmax on S^T in registers (the keys of a query live on 4 registers x 4 lane groups x 2 blocks), then
-// O^T += V^T P^T (72 MFMAs). KS = head_dim / 32.
-template <int KS>
-__global__ __launch_bounds__(256, 1) void k_gattn(GattnArgs a) {
+// softmax(q k^T) v for one head and 128 queries (8 waves of 16 or 4 of 32). Per 32-key block (three-stage LDS
+// ring filled by LDS-DMA): S^T = K Q^T (36 QF MFMAs per wave), online softmax on S^T in registers (the keys of a
+// query live on 4 registers x 4 lane groups x 2 blocks), O^T += V^T P^T (36 QF MFMAs). KS = head_dim / 32.
+template <int KS, int QF>
+__global__ __launch_bounds__(64 * 8 / QF, 1) void k_gattn(GattnArgs a) {
   constexpr int HD = 32 * KS, DB = HD / 16;
+  constexpr int kWaves = 8 / QF, kQW = 16 * QF;  // QF = 2: one wave per SIMD (~300 registers); 1: two per SIMD
   constexpr int KBLK = 2 * KS * 2, VBLK = DB * 2, SKB = KBLK + VBLK;  // 1 KB blocks per stage (48 at hd 192)
   constexpr int PW = SKB / kWaves;                                    // DMA instructions per wave per stage
   static_assert(SKB % kWaves == 0, "stage blocks per wave");
@@ -172,17 +170,17 @@ __global__ __launch_bounds__(256, 1) void k_gattn(GattnArgs a) {
   const unsigned short* Vg = a.vp + (size_t)h * a.Np * 2 * HD;
 
   // this wave's Q fragments (B operands of S^T = K Q^T) and score scales, for the whole kernel
-  h8 qf[2][KS][2];
+  h8 qf[QF][KS][2];
   const unsigned short* Qg = a.qp + ((size_t)h * a.Np + q0) * 2 * HD + lane * 8;
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < QF; ++j)
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int p = 0; p < 2; ++p) qf[j][s][p] = *reinterpret_cast<const h8*>(Qg + ((j * KS + s) * 2 + p) * 512);
-  float qsc[2];
+  float qsc[QF];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) qsc[j] = a.qs[(size_t)h * a.Np + q0 + 16 * j + (lane & 15)];
+  for (int j = 0; j < QF; ++j) qsc[j] = a.qs[(size_t)h * a.Np + q0 + 16 * j + (lane & 15)];
 
   auto stage = [&](int b, int buf) {
     unsigned short* S = lds + buf * SKB * 512;
@@ -194,29 +192,22 @@ __global__ __launch_bounds__(256, 1) void k_gattn(GattnArgs a) {
     }
   };
 
-  f4v O[DB][2];
+  f4v O[DB][QF];
 #pragma unroll
   for (int d = 0; d < DB; ++d)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) O[d][j] = f4v{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
+    for (int j = 0; j < QF; ++j) O[d][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  float m[QF], lsum[QF];
+#pragma unroll
+  for (int j = 0; j < QF; ++j) m[j] = -INFINITY, lsum[j] = 0.f;
 
-  stage(0, 0);
-  stage(min(1, nb - 1), 1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int b = 0; b < nb; ++b) {
-    stage(min(b + 2, nb - 1), (b + 2) % 3);
+  // S^T(b) = K(b) Q^T: rows = keys 16 kb + 4 g + r, columns = queries 16 j + (lane & 15)
+  auto smfma = [&](int b, f4v (&sc)[2][QF]) {
     const unsigned short* S = lds + (b % 3) * SKB * 512 + lane * 8;
-    // S^T tile: rows = keys 16 kb + 4 g + r, columns = queries 16 j + (lane & 15)
-    f4v sc[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) sc[kb][j] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < QF; ++j) sc[kb][j] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -224,17 +215,18 @@ __global__ __launch_bounds__(256, 1) void k_gattn(GattnArgs a) {
         const h8 kh = *reinterpret_cast<const h8*>(S + ((kb * KS + s) * 2) * 512);
         const h8 kl = *reinterpret_cast<const h8*>(S + ((kb * KS + s) * 2 + 1) * 512);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < QF; ++j) {
           sc[kb][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qf[j][s][0], sc[kb][j], 0, 0, 0);
           sc[kb][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qf[j][s][1], sc[kb][j], 0, 0, 0);
           sc[kb][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qf[j][s][0], sc[kb][j], 0, 0, 0);
         }
       }
-    // online softmax per query column
-    h8 ph[2], pl[2];
-    float alpha[2];
+  };
+  // online softmax of block b per query column: P (scaled by 2^14, split into fp16 planes in the B-operand order of
+  // the PV product), the rescale alpha of what O holds, the running max and the lane-partial row sums
+  auto softmax = [&](int b, f4v (&sc)[2][QF], h8 (&ph)[QF], h8 (&pl)[QF], float (&alpha)[QF]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < QF; ++j) {
       float mb = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -264,19 +256,45 @@ __global__ __launch_bounds__(256, 1) void k_gattn(GattnArgs a) {
         }
       lsum[j] = lsum[j] * alpha[j] + ps;
     }
-    // O^T = O^T alpha + V^T P^T: rows = d 16 db + 4 g + r, columns = queries
+  };
+  // O^T += V^T(b) P^T(b): rows = d 16 db + 4 g + r, columns = queries
+  auto pv = [&](int b, const h8 (&ph)[QF], const h8 (&pl)[QF]) {
+    const unsigned short* S = lds + (b % 3) * SKB * 512 + lane * 8;
 #pragma unroll
     for (int db = 0; db < DB; ++db) {
       const h8 vh = *reinterpret_cast<const h8*>(S + (KBLK + db * 2) * 512);
       const h8 vl = *reinterpret_cast<const h8*>(S + (KBLK + db * 2 + 1) * 512);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        O[db][j] *= alpha[j];
+      for (int j = 0; j < QF; ++j) {
         O[db][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl[j], O[db][j], 0, 0, 0);
         O[db][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph[j], O[db][j], 0, 0, 0);
         O[db][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph[j], O[db][j], 0, 0, 0);
       }
     }
+  };
+
+  // Per key block b: the DMA of block b + 2 (clamped: the last two iterations re-stage the last block into a buffer
+  // nobody reads again), S(b), the softmax, O = O alpha + V^T P^T; then wait for my block b + 1 pieces (those of
+  // b + 2 may stay in flight) and barrier (everyone's b + 1 landed; everyone's reads of the buffer b + 2
+  // overwrites, block b - 1, retired before the previous barrier) -- k_gemm_h4's ring protocol.
+  stage(0, 0);
+  stage(min(1, nb - 1), 1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  for (int b = 0; b < nb; ++b) {
+    stage(min(b + 2, nb - 1), (b + 2) % 3);
+    f4v sc[2][QF];
+    smfma(b, sc);
+    h8 ph[QF], pl[QF];
+    float alpha[QF];
+    softmax(b, sc, ph, pl, alpha);
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int j = 0; j < QF; ++j) O[db][j] *= alpha[j];
+    pv(b, ph, pl);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
@@ -289,7 +307,7 @@ __global__ __launch_bounds__(256, 1) void k_gattn(GattnArgs a) {
   // 1 / row sum (the lane partial sums of a query over its 4 lane groups) and the head's V / P scales
   const float vs = a.vsc[h];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < QF; ++j) {
     float l = lsum[j];
     l += __shfl_xor(l, 16);
     l += __shfl_xor(l, 32);
@@ -317,7 +335,8 @@ bool gattn_supported(int C, int heads) {
   return heads > 0 && C % heads == 0 && (hd == 64 || hd == 96 || hd == 128 || hd == 192);
 }
 
-hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads, void* ws, hipStream_t st) {
+hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads, void* ws, hipStream_t st,
+                 int qf_per_wave) {
   if (!qkv || !out || !ws || N <= 0 || !gattn_supported(C, heads) || ldo < C || (ldo & 3)) return hipErrorInvalidValue;
   GattnArgs a;
   a.qkv = qkv;
@@ -340,21 +359,22 @@ hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads,
   const size_t lp = 3 * 32 * (size_t)(hd + 1) * sizeof(float);
   hipLaunchKernelGGL(k_gattn_prep, dim3(a.Np / 32, heads), dim3(256), lp, st, a, (const unsigned*)part);
   const dim3 grid(a.Np / kQB, heads);
-  switch (hd / 32) {
-#define GA(KS)                                                                                              \
-  case KS: {                                                                                                \
+  const int qf = qf_per_wave == 1 ? 1 : 2;
+  switch (hd / 32 * 4 + qf) {
+#define GA(KS, QF)                                                                                          \
+  case KS * 4 + QF: {                                                                                       \
     constexpr size_t lds = 3 * (2 * KS * 2 + KS * 2 * 2) * 1024;                                            \
     static bool init = false;                                                                               \
     if (!init) {                                                                                            \
-      if (hipError_t e = hipFuncSetAttribute((const void*)k_gattn<KS>,                                      \
+      if (hipError_t e = hipFuncSetAttribute((const void*)k_gattn<KS, QF>,                                  \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))        \
         return e;                                                                                           \
       init = true;                                                                                          \
     }                                                                                                       \
-    hipLaunchKernelGGL(k_gattn<KS>, grid, dim3(256), lds, st, a);                                           \
+    hipLaunchKernelGGL((k_gattn<KS, QF>), grid, dim3(64 * 8 / QF), lds, st, a);                             \
     break;                                                                                                  \
   }
-    GA(2) GA(3) GA(4) GA(6)
+    GA(2, 1) GA(3, 1) GA(4, 1) GA(6, 1) GA(2, 2) GA(3, 2) GA(4, 2) GA(6, 2)
 #undef GA
     default:
       return hipErrorInvalidValue;

@@ -1924,6 +1924,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;
+  if (k == "gattn_qf") return &t.gattn_qf;
   return nullptr;
 }
 

@@ -23,6 +23,7 @@ struct Tuning {
   int h4 = 1;                   // the split-operand LDS-DMA fp16x3 kernel (tile 48) where the 256x128 tiles run
   int ln_planes = 1;            // LayerNorm writes the fp16x3 planes of the tile-48 GEMM it feeds (no split pass)
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
+  int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
 };
 extern const Tuning kDefaultTuning;
@@ -100,7 +101,9 @@ struct GattnArgs {
 };
 bool gattn_supported(int C, int heads);
 size_t gattn_ws_bytes(int N, int C, int heads);
-hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads, void* ws, hipStream_t st);
+// qf_per_wave: 16-query blocks per wave (2: 4 waves of 32 queries, one per SIMD; 1: 8 waves of 16, two per SIMD)
+hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads, void* ws, hipStream_t st,
+                 int qf_per_wave = 1);
 
 // ws: scratch of at least gemm_ws_floats() floats (may be null: no tail split)
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);
