@@ -209,11 +209,13 @@ def gemm_rocprof(key="gemm16_avg_us_per_call"):
 def gemm_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes of `bench.py` (FETCH_SIZE x2 +
     WRITE_SIZE with the gfx950 corrections, tools/pmc_traffic.py); PMC counters cannot be read live."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, "gemm_traffic.json")
         try:
             with open(path) as f:
-                return json.load(f)[kernel]["hbm_bytes_per_launch"], f"profiles/{rnd}/gemm_traffic.json"
+                d = json.load(f)
+            rec = d.get(kernel) or (d.get("k_gemm_h3") if kernel == "fp16x3" else None)
+            return rec["hbm_bytes_per_launch"], f"profiles/{rnd}/gemm_traffic.json"
         except (OSError, KeyError, ValueError, TypeError):
             continue
     return None, None
@@ -480,11 +482,12 @@ def main():
         g16, g6 = pr["gemm16"], pr["gemm"]
         allg = {k: g16[k] + g6[k] for k in ("ms", "flops", "bytes", "launches")}
         if math == "split16":
-            dom, peak, tkey = g16, PEAK_SPLIT16_TFLOPS, "k_gemm_h3"
-            kname = ("k_gemm_h3 (+ its split-K fixup and the A row scaling): every GEMM launch that ran the fp16x3 "
+            dom, peak, tkey = g16, PEAK_SPLIT16_TFLOPS, "fp16x3"
+            kname = ("the fp16x3 GEMM class: k_gemm_h4 (tile 48, LDS-DMA on pre-split planes) / k_gemm_h3(m) with "
+                     "their split-K fixups and the A split / row-scale passes: every GEMM launch that ran an fp16x3 "
                      "kernel in a HIP-event-profiled repeat of one timed analysis")
             desc = ("fp16x3 split: fp32 operands scaled per row by 2^e and split into 2 fp16 planes, 3 "
-                    "v_mfma_f32_32x32x16_f16 products per fp32 product; peak = 2.5 PF fp16 dense / 3")
+                    "fp16 MFMA products (v_mfma_f32_16x16x32_f16) per fp32 product; peak = 2.5 PF fp16 dense / 3")
         elif math == "split":
             dom, peak, tkey = allg, PEAK_SPLIT_TFLOPS, "all"
             kname = "every GEMM launch of a HIP-event-profiled repeat of one timed analysis"

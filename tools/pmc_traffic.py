@@ -34,14 +34,14 @@ def summary(keys, what):
 
 
 out = {
-    # one fp16x3 GEMM = k_rowscale (reads A) + k_gemm_h3 (+ fixup): counted per k_gemm_h3 launch
-    "k_gemm_h3": summary(("k_gemm_h3",), "k_gemm_h3 main-kernel launches"),
-    "k_rowscale": summary(("k_rowscale",), "k_rowscale launches (one per fp16x3 GEMM)"),
-    "all": summary(("k_gemm_nt", "k_gemm_bs", "k_gemm_h3"), "every GEMM main-kernel launch"),
+    # one fp16x3 GEMM = its A pass (k_rowsplit / k_rowscale, or none when the LayerNorm wrote the planes / scales) +
+    # the main kernel (k_gemm_h4 tile 48, k_gemm_h3(m)) + fixup: counted per main-kernel launch
+    "fp16x3": summary(("k_gemm_h4", "k_gemm_h3"), "fp16x3 main-kernel launches (k_gemm_h4 + k_gemm_h3(m))"),
+    "k_gemm_h4": summary(("k_gemm_h4",), "k_gemm_h4 (tile 48) launches"),
+    "k_gemm_h3": summary(("k_gemm_h3",), "k_gemm_h3(m) launches"),
+    "a_pass": summary(("k_rowsplit", "k_rowscale"), "A split / row-scale passes (k_rowsplit, k_rowscale)"),
+    "all": summary(("k_gemm_nt", "k_gemm_bs", "k_gemm_h3", "k_gemm_h4"), "every GEMM main-kernel launch"),
     "note": "FETCH_SIZE doubled (gfx950 wide-load undercount), both in KB -> bytes; means over launches",
 }
-if out["k_gemm_h3"] and out["k_rowscale"]:
-    out["k_gemm_h3"]["hbm_bytes_per_launch_incl_rowscale"] = (out["k_gemm_h3"]["hbm_bytes_per_launch"] +
-                                                              out["k_rowscale"]["hbm_bytes_per_launch"])
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(out))

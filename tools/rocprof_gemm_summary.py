@@ -1,7 +1,8 @@
 """Summarise a rocprofv3 --stats kernel_stats.csv for the GEMM classes as bench.py reports them (dev tool).
 
 One bench 'GEMM launch' = one gemm_nt call:
-  gemm16 (fp16x3): k_rowscale + k_gemm_h3 + its split-K k_gemm_fixup_sub<128, 128, ...>; per call = sum / k_gemm_h3 calls
+  gemm16 (fp16x3): the A pass (k_rowsplit / k_rowscale / k_gather_scales) + k_gemm_h4 / k_gemm_h3(m) + their split-K
+                   fixups (k_gemm_fixup_sub / _sub16); per call = sum / main-kernel calls
   all:             every GEMM kernel (main + fixups + k_rowscale); per call = sum / main-kernel calls
 Usage: rocprof_gemm_summary.py <run_kernel_stats.csv> [out.json]"""
 import csv, json, sys
@@ -12,15 +13,15 @@ main_n = main_ns = fix_ns = 0
 other = {}
 for r in rows:
     n, calls, tot = r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])
-    if "k_gemm_h3" in n:
+    if "k_gemm_h3" in n or "k_gemm_h4" in n:
         h3_n += calls
         h3_ns += tot
         main_n += calls
         main_ns += tot
-    elif "k_rowscale" in n:
+    elif "k_rowscale" in n or "k_rowsplit" in n or "k_gather_scales" in n:
         rs_ns += tot
         fix_ns += tot
-    elif "k_gemm_fixup_sub<128, 128" in n:
+    elif "k_gemm_fixup_sub" in n:
         fs_ns += tot
         fix_ns += tot
     elif "k_gemm_fixup" in n:
