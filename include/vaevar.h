@@ -211,7 +211,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
    the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1), "gattn" (the
    LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1), "gattn_qf" (its 16-query blocks per
-   wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1). Results stay fp32-level for every value; a change drops the
+   wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1), "h4_small" (tile 48 with whole-chip split-K
+   also for 64..143 256-row tiles, 0), "h4_split_minkt" (k-tiles per chunk of that split, 12). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key: VV_E_ARG. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);

@@ -1925,6 +1925,8 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;
   if (k == "gattn_qf") return &t.gattn_qf;
+  if (k == "h4_small") return &t.h4_small;
+  if (k == "h4_split_minkt") return &t.h4_split_minkt;
   return nullptr;
 }
 
@@ -2090,8 +2092,10 @@ static int resolve_tile(GemmArgs& a, int tile_hint) {
   // tile 48 wherever the 256x128 fp16x3 tiles run, and for the 128x128-routed ones that still give >= 144 256-row
   // tiles (N 4608 at 2048 rows: fc1 forward, the fc2 input gradient; same-box 2048 x 4608 x 1152: 75.9 us incl. the
   // split pass vs 91.3 / ~90 for tiles 47 / 36); the 72-tile 1152 x 1152 GEMMs stay on 128x128 tiles
+  // h4_small: also the 128x128-routed GEMMs with 64..143 256-row tiles (1152 x 1152 at 2048 rows: 72 tiles), which
+  // then split along K over the whole chip (tile-48 chunks of >= h4_split_minkt k-tiles, below)
   if (tile_hint < 0 && TU.h4 && a.math == GEMM_SPLIT16 &&
-      (t == 44 || t == 47 || (t == 36 && tiles_of(a, 256, 128) >= 144)))
+      (t == 44 || t == 47 || (t == 36 && tiles_of(a, 256, 128) >= (TU.h4_small ? 64 : 144))))
     t = 48;
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bh = nullptr;
@@ -2169,7 +2173,8 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
       // fewer fp16x3 tiles than CUs (N = 1152 at 2048 tokens: 144 tiles): every tile split along K so that
       // two workgroups share most CUs (the co-resident pair overlaps one's staging with the other's MFMAs)
       // chunks of >= 24 k-tiles (K >= 2304 at S = 3): at K = 1152 the fixup costs more than the split gains
-      const int min_kt = std::max(1, TU.small_split_minkt);  // k-tiles per chunk at least
+      // k-tiles per chunk at least (tile 48, one workgroup per CU and no co-resident partner: its own floor)
+      const int min_kt = std::max(1, t == 48 ? TU.h4_split_minkt : TU.small_split_minkt);
       int S = std::min(((t == 36 || t == 46 ? 2 : 1) * P) / T, nkt / min_kt);  // resident workgroups per CU: 2 / 1
       const size_t tile_f = (size_t)bm * bn;
       while (S > 1 && (size_t)T * S * tile_f > kWsFloats) --S;

@@ -22,6 +22,9 @@ struct Tuning {
   int ln_scales = 1;            // fp16x3 row scales from the LayerNorm producer (0: k_rowscale everywhere)
   int h4 = 1;                   // the split-operand LDS-DMA fp16x3 kernel (tile 48) where the 256x128 tiles run
   int ln_planes = 1;            // LayerNorm writes the fp16x3 planes of the tile-48 GEMM it feeds (no split pass)
+  int h4_small = 0;             // tile 48 + whole-chip split-K also for 64..143 256-row tiles (1152 x 1152 at 2048 rows;
+                                // same-box config 2: 77.5 / 77.4 off vs 77.4 / 76.3 on, profiles/r03/ab_h4small)
+  int h4_split_minkt = 12;      // k-tiles per chunk at least, for that split of tile 48
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)

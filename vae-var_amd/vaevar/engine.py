@@ -40,7 +40,7 @@ class Context:
     # per-context dispatch knobs (vv_set_tuning; defaults = the measured choices). A/B runs set them from the
     # environment as VAEVAR_<KEY> (e.g. VAEVAR_H3_MINK=384); the library itself reads no environment.
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
-                   "win_attn", "h4", "ln_planes", "gattn", "gattn_qf")
+                   "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt")
 
     def __init__(self, device: int = 0):
         self.device = device
