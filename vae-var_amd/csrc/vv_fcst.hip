@@ -734,6 +734,8 @@ struct FModel {
   // global-window attention through the split GEMM when the window is large: S/P [heads][N][Np], V^T [heads][hd][Np]
   float *att_s = nullptr, *att_vt = nullptr;
   void* gattn_ws = nullptr;  // the flash MFMA kernel's planes and scales (vv::gattn_ws_bytes), when it applies
+  unsigned short* apl = nullptr;  // tile-48 A planes (k_rowsplit): the largest fp16x3 A, G x M x 4C of a stage
+  size_t apl_halfs = 0;
 };
 
 namespace {
@@ -823,11 +825,13 @@ FBlock blk(FModel& m, const std::string& pre) {
           w(pre + ".mlp.fc1.bias"),    w(pre + ".mlp.fc2.weight"), w(pre + ".mlp.fc2.bias")};
 }
 
-GemmArgs gbase(int M, int N, int K, int G, int epi, int math, const vv::Tuning* tune) {
+GemmArgs gbase(int M, int N, int K, int G, int epi, const FModel& m) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
-  a.math = math;
-  a.tune = tune;
+  a.math = m.math;
+  a.tune = m.tune;
+  a.apl = m.apl;  // the tile-48 A-plane workspace (k_rowsplit)
+  a.apl_halfs = m.apl_halfs;
   a.M = M;
   a.N = N;
   a.K = K;
@@ -893,7 +897,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     for (int g = 0; g < G; ++g)
       ln.g[g] = {S.x + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, m.t1 + g * MC, nullptr, nullptr, nullptr};
     FH(layernorm_fwd(ln, st));
-    GemmArgs q = gbase(M, 3 * C, C, G, EPI_STORE, m.math, m.tune);
+    GemmArgs q = gbase(M, 3 * C, C, G, EPI_STORE, m);
     for (int g = 0; g < G; ++g)
       q.g[g] = {m.t1 + g * MC, nullptr, S.w[b][g].qkvW, S.w[b][g].qkvb, m.qkv + g * MC * 3, nullptr, nullptr};
     FH(gemm_nt(q, st, -1, m.ws));
@@ -946,7 +950,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
       const int Np = (N + 31) / 32 * 32, hd = S.hd;
       for (int b0 = 0; b0 < nwin; ++b0) {
         const float* qkv = m.qkv + (size_t)b0 * N * 3 * C;
-        GemmArgs sq = gbase(N, N, hd, S.heads, EPI_STORE, m.math, m.tune);
+        GemmArgs sq = gbase(N, N, hd, S.heads, EPI_STORE, m);
         sq.lda = 3 * C;
         sq.ldb = 3 * C;
         sq.ldc = Np;
@@ -964,7 +968,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
                            hd);
         FH(hipGetLastError());
         prof_end(ph, st, PC_ATTN, 4.0 * S.heads * N * (double)Np, 12.0 * S.heads * N * (double)Np);
-        GemmArgs pv = gbase(N, hd, Np, S.heads, EPI_STORE, m.math, m.tune);
+        GemmArgs pv = gbase(N, hd, Np, S.heads, EPI_STORE, m);
         pv.ldc = C;
         for (int hh = 0; hh < S.heads; ++hh)
           pv.g[hh] = {m.att_s + (size_t)hh * N * Np, nullptr, m.att_vt + (size_t)hh * hd * Np, nullptr,
@@ -977,7 +981,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
       prof_end(ph, st, PC_ATTN, 4.0 * G * (double)M * N * C, 16.0 * G * (double)M * C);
     }
     // proj + window reverse / roll back + residual, in place
-    GemmArgs p = gbase(M, C, C, G, EPI_RESID, m.math, m.tune);
+    GemmArgs p = gbase(M, C, C, G, EPI_RESID, m);
     p.crow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {m.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, S.x + g * MC, S.x + g * MC, nullptr};
@@ -986,12 +990,11 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     for (int g = 0; g < G; ++g)
       ln2.g[g] = {S.x + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, m.t1 + g * MC, nullptr, nullptr, nullptr};
     FH(layernorm_fwd(ln2, st));
-    GemmArgs f1 = gbase(M, 4 * C, C, G, EPI_GELU, m.math, m.tune);
+    GemmArgs f1 = gbase(M, 4 * C, C, G, EPI_GELU, m);
     for (int g = 0; g < G; ++g)
-      f1.g[g] = {m.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, m.h + g * MC * 4, nullptr,
-                 m.aux + g * MC * 4};
+      f1.g[g] = {m.t1 + g * MC, nullptr, S.w[b][g].fc1W, S.w[b][g].fc1b, m.h + g * MC * 4, nullptr, nullptr};
     FH(gemm_nt(f1, st, -1, m.ws));
-    GemmArgs f2 = gbase(M, C, 4 * C, G, EPI_RESID, m.math, m.tune);
+    GemmArgs f2 = gbase(M, C, 4 * C, G, EPI_RESID, m);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {m.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, S.x + g * MC, S.x + g * MC, nullptr};
     FH(gemm_nt(f2, st, -1, m.ws));
@@ -1061,12 +1064,20 @@ int create(const vv_lgunet_config* cfg, int batch, FModel** out, std::string& er
   }
   if ((r = dalloc(*m, smax, &m->t1, err)) || (r = dalloc(*m, smax, &m->t2, err)) ||
       (r = dalloc(*m, 3 * smax, &m->qkv, err)) || (r = dalloc(*m, 4 * smax, &m->h, err)) ||
-      (r = dalloc(*m, 4 * smax, &m->aux, err)) || (r = dalloc(*m, s2max, &m->xm, err)) ||
+      (r = dalloc(*m, s2max, &m->xm, err)) ||
       (r = dalloc(*m, s2max, &m->ex, err)) || (r = dalloc(*m, smax, &m->xe, err)) ||
       (r = dalloc(*m, Mg * G * c.Cl.back(), &m->cat, err)) || (r = dalloc(*m, Mg * G * c.Cl.back(), &m->dp, err)) ||
       (r = dalloc(*m, S[0], &m->yn, err)) || (r = dalloc(*m, Mg * c.E, &m->lgx, err)) ||
       (r = dalloc(*m, gemm_ws_floats(), &m->ws, err)))
     return bail(r);
+  {
+    // tile-48 A planes: the widest A of the stages that reach the fp16x3 kernels (K >= 768: the LG stage's fc2
+    // forward, Mg x 4E), two fp16 planes = 4 B per element
+    float* p = nullptr;
+    if ((r = dalloc(*m, (size_t)Mg * 4 * c.E, &p, err))) return bail(r);
+    m->apl = reinterpret_cast<unsigned short*>(p);
+    m->apl_halfs = (size_t)Mg * 4 * c.E * 2;
+  }
   {
     int kmax = 0, nmax = 0;
     for (int g = 0; g < G; ++g) {
@@ -1228,7 +1239,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
   hipLaunchKernelGGL(k_im2col, dim3(grid_for(colg), G), dim3(256), 0, st, pa, m->h, m->Kp, colg);
   FH(hipGetLastError());
   prof_end(ph, st, PC_PATCH, 0.0, 8.0 * G * colg);
-  GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID, m->math, m->tune);
+  GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID, *m);
   pe.rmod = c.Hl[0] * c.Wl[0];
   pe.ldr = c.Cl[0];
   for (int g = 0; g < G; ++g)
@@ -1248,7 +1259,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
         lm.g[g] = {m->enc[l - 1].x + g * S[l - 1], w(eg(g) + pl + ".norm.weight"), w(eg(g) + pl + ".norm.bias"),
                    m->xm + (size_t)g * M[l] * 4 * Cp, nullptr, nullptr, nullptr};
       FH(layernorm_fwd(lm, st));
-      GemmArgs red = gbase(M[l], c.Cl[l], 4 * Cp, G, EPI_STORE, m->math, m->tune);
+      GemmArgs red = gbase(M[l], c.Cl[l], 4 * Cp, G, EPI_STORE, *m);
       for (int g = 0; g < G; ++g)
         red.g[g] = {m->xm + (size_t)g * M[l] * 4 * Cp, nullptr, w(eg(g) + pl + ".reduction.weight"), nullptr,
                     m->enc[l].x + g * S[l], nullptr, nullptr};
@@ -1263,7 +1274,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     le.g[g] = {m->enc[L - 1].x + g * S[L - 1], w(eg(g) + ".norm.weight"), w(eg(g) + ".norm.bias"), m->cat + g * CL,
                nullptr, nullptr, nullptr};
   FH(layernorm_fwd(le, st));
-  GemmArgs ep = gbase(Mg, c.E, G * CL, 1, EPI_RESID, m->math, m->tune);
+  GemmArgs ep = gbase(Mg, c.E, G * CL, 1, EPI_RESID, *m);
   ep.rmod = c.Hg * c.Wg;  // + LG_net.pos_embed (LGUnet_all.py:727)
   ep.ldr = c.E;
   ep.g[0] = {m->cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), m->lgx, w("net.pos_embed"), nullptr};
@@ -1272,13 +1283,13 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
   for (auto& s : m->lg)
     if ((r = stage_fwd(*m, s, st, err))) return r;
   // ---- Dec_net (LGUnet_all.py:624-650)
-  GemmArgs dp = gbase(Mg, G * CL, c.E, 1, EPI_STORE, m->math, m->tune);
+  GemmArgs dp = gbase(Mg, G * CL, c.E, 1, EPI_STORE, *m);
   dp.g[0] = {m->lgx, nullptr, w("dec.proj.weight"), w("dec.proj.bias"), m->dp, nullptr, nullptr};
   FH(gemm_nt(dp, st, -1, m->ws));
   for (int i = 0; i < L; ++i) {
     const int lev = L - 1 - i, Cv = c.Cl[lev];
     // cat(x, skip) -> concat_back_dim[i] (LGUnet_all.py:473-476)
-    GemmArgs cb = gbase(M[lev], Cv, 2 * Cv, G, EPI_STORE, m->math, m->tune);
+    GemmArgs cb = gbase(M[lev], Cv, 2 * Cv, G, EPI_STORE, *m);
     cb.ksplit = Cv;
     cb.lda = i == 0 ? G * CL : Cv;
     cb.lda2 = Cv;
@@ -1291,7 +1302,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     if (i < L - 1) {
       // PatchExpand (LGUnet_all.py:107-118): expand (no bias) + rearrange + LN(C/2)
       const std::string pu = ".layers_up." + std::to_string(i) + ".upsample";
-      GemmArgs ex = gbase(M[lev], 2 * Cv, Cv, G, EPI_STORE, m->math, m->tune);
+      GemmArgs ex = gbase(M[lev], 2 * Cv, Cv, G, EPI_STORE, *m);
       for (int g = 0; g < G; ++g)
         ex.g[g] = {m->dec[lev].x + g * S[lev], nullptr, w(dg(g) + pu + ".expand.weight"), nullptr,
                    m->ex + (size_t)g * M[lev] * 2 * Cv, nullptr, nullptr};
@@ -1344,7 +1355,7 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
   }
   // ConvTranspose2d = GEMM (tokens x transposed weight) + col2im of the overlapping taps
   const size_t yg = (size_t)M[0] * m->NT;
-  GemmArgs ct = gbase(M[0], m->NT, c.Cl[0], G, EPI_STORE, m->math, m->tune);
+  GemmArgs ct = gbase(M[0], m->NT, c.Cl[0], G, EPI_STORE, *m);
   for (int g = 0; g < G; ++g) ct.g[g] = {pu.tok[g], nullptr, m->W2[g], nullptr, m->h + g * yg, nullptr, nullptr};
   FH(gemm_nt(ct, st, -1, m->ws));
   ph = prof_begin(st);

@@ -118,7 +118,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& 
         const int o = ov[r];
         float v = acc[a][b][r] + bv[b];
         if constexpr (EPI == EPI_GELU) {
-          G.aux[(size_t)o * args.ldaux + col] = v;
+          if (G.aux) G.aux[(size_t)o * args.ldaux + col] = v;  // the pre-activation, for a backward only
           v = gelu_f(v);
         } else if constexpr (EPI == EPI_RESID) {
           v = ex[r] + v;

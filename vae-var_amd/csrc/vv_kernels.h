@@ -41,7 +41,7 @@ int* tuning_field(Tuning& t, const char* key);
 // ---------------------------------------------------------------------------
 enum Epi : int {
   EPI_STORE = 0,   // C = acc (+bias)
-  EPI_GELU = 1,    // aux = acc + bias ; C = gelu(aux)        (Mlp fc1 fwd, swinblock.py:23-29)
+  EPI_GELU = 1,    // aux = acc + bias (unless aux is null) ; C = gelu(acc + bias)   (Mlp fc1 fwd, swinblock.py:23-29)
   EPI_RESID = 2,   // C = R[o % rmod] + acc (+bias)            (residual adds)
   EPI_DGELU = 3,   // C = acc * gelu'(aux[o])                  (fc1 backward)
 };
