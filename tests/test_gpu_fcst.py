@@ -80,6 +80,28 @@ def test_fcst_mid_vs_oracle(name):
     assert e < 1e-4
 
 
+def test_fcst_window_attention_mfma_vs_valu():
+    """The exact-f32 MFMA window-attention kernel (win_mfma=1, default) against the VALU kernel (win_mfma=0) on
+    the MID_FCST shapes (head_dim 32/64, [6,12] windows with and without the -inf row mask): both compute fp32
+    products with fp32 sums, so the forecasts agree to rounding (rel <= 1e-5)."""
+    from vaevar import config as C
+    from vaevar.synth import smooth_field
+
+    cfg = C.MID_FCST
+    x = torch.from_numpy(smooth_field(704, (1, C.in_channels(cfg)) + tuple(cfg["img_size"]))).cuda()
+    m = _model(cfg)
+    try:
+        m.ctx.set_tuning("win_mfma", 0)
+        a = m.forward_raw(x).clone()
+        m.ctx.set_tuning("win_mfma", 1)
+        b = m.forward_raw(x).clone()
+    finally:
+        m.ctx.set_tuning("win_mfma", 1)
+    e = rel(b.cpu(), a.cpu())
+    print(f"window attention MFMA vs VALU: forecast rel {e:.2e}")
+    assert torch.isfinite(b).all() and e < 1e-5
+
+
 def test_fcst_backward_refused():
     from vaevar import config as C
     from vaevar._lib import VVError

@@ -264,6 +264,140 @@ __global__ __launch_bounds__(256) void k_attn_win(FlashArgs a) {
   }
 }
 
+// The same window attention on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32: fp32 products, fp32 accumulation, as
+// torch's fp32 matmul), with rope2 + the q scale fused into the LDS staging (the same rounded products and sums as
+// k_rope, so q and k are bit-identical to the unfused path). One workgroup per (window, head), one wave per
+// 16-query tile. Per tile: S^T = K Q^T (keys on the accumulator rows, queries on the lanes; the NT key tiles are
+// independent accumulators, so the MFMA chain never waits on itself), the -inf row-label mask from per-lane label
+// bitmasks built once per wave, softmax over the keys (registers x the 4 lane groups), then O^T = V^T P^T with
+// P^T straight from the score registers: the k index of each 16x16x4 step is the lane group, so the step over
+// register r pairs keys 4 g + r with V rows 4 g + r read from LDS. N <= 96 (kWinMaxN), hd a multiple of 16 <= 64.
+template <int HD, int NT>
+__global__ __launch_bounds__(64 * NT) void k_attn_win_mf(FlashArgs a, RopeArgs ra) {
+  typedef float f4m __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int g = blockIdx.z, w = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, nth = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int hd = HD, ld = HD + 1, q4 = HD / 4, half = HD / 2;
+  constexpr int NP = NT * 16;
+  const int N = a.N, C = a.C;
+  float* q = smf;
+  float* k = q + NP * ld;
+  float* v = k + NP * ld;
+  int* lab = reinterpret_cast<int*>(v + NP * ld);  // row label per token, -1 past N
+  const int wr = (w / a.nWw) % a.nWh, li = lane & 15, gq = lane >> 4;
+  for (int t = tid; t < NP; t += nth)
+    lab[t] = t >= N ? -1 : (a.masked ? row_label(wr * a.wh + t / a.ww, a.H, a.wh, a.sh) : 0);
+  const float* base = a.qkv[g] + (size_t)w * N * 3 * C + h * hd;
+  for (int e = tid; e < NP * q4; e += nth) {
+    const int t = e / q4, c = (e - t * q4) * 4;
+    f4 x = {0.f, 0.f, 0.f, 0.f}, y = x, z = x;
+    if (t < N) {
+      const float* src = base + (size_t)t * 3 * C + c;
+      x = *reinterpret_cast<const f4*>(src);
+      y = *reinterpret_cast<const f4*>(src + C);
+      z = *reinterpret_cast<const f4*>(src + 2 * C);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      q[t * ld + c + i] = x[i];
+      k[t * ld + c + i] = y[i];
+      v[t * ld + c + i] = z[i];
+    }
+  }
+  __syncthreads();
+  if (ra.c1) {  // rope2 (positional_encodings.py:261-270) on q and k, then q * scale, as k_rope
+    for (int e = tid; e < N * half; e += nth) {
+      const int t = e / half, j = e - t * half;
+      float c, sn;
+      if (j < ra.d1) {
+        c = ra.c1[t * ra.d1 + j];
+        sn = ra.s1[t * ra.d1 + j];
+      } else {
+        c = ra.c2[t * ra.d2 + (j - ra.d1)];
+        sn = ra.s2[t * ra.d2 + (j - ra.d1)];
+      }
+      float* pq = q + t * ld;
+      float* pk = k + t * ld;
+      float x0 = pq[j], x1 = pq[j + half];
+      pq[j] = __fmul_rn(__fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, sn)), ra.scale);
+      pq[j + half] = __fmul_rn(__fadd_rn(__fmul_rn(x1, c), __fmul_rn(x0, sn)), ra.scale);
+      x0 = pk[j];
+      x1 = pk[j + half];
+      pk[j] = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, sn));
+      pk[j + half] = __fadd_rn(__fmul_rn(x1, c), __fmul_rn(x0, sn));
+    }
+    __syncthreads();
+  }
+  float* ob = a.out[g] + (size_t)w * N * C + h * hd;
+  const int qt = wave;  // one wave per query tile (blockDim = 64 NT)
+  const int qi = 16 * qt + li;
+  const int lq = lab[min(qi, N - 1)];
+  float qf[q4];
+#pragma unroll
+  for (int s4 = 0; s4 < q4; ++s4)
+    qf[s4] = q[qi * ld + 4 * s4 + gq];
+  f4m sc[NT];
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) sc[kt] = f4m{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s4 = 0; s4 < q4; ++s4) {
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+      sc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(k[(16 * kt + li) * ld + 4 * s4 + gq], qf[s4], sc[kt], 0, 0, 0);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = lab[16 * kt + 4 * gq + r] == lq ? sc[kt][r] : -INFINITY;
+        sc[kt][r] = x;
+        mx = fmaxf(mx, x);
+      }
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = expf(sc[kt][r] - mx);
+        sc[kt][r] = e;
+        sum += e;
+      }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc[kt][r] *= inv;
+  // O^T tiles: rows d = 16 dt + 4 gq + r, columns = queries; the hd/16 tiles are independent accumulators
+  constexpr int DT = HD / 16;
+  f4m o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f4m{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float* vr = v + (16 * kt + 4 * gq + r) * ld + li;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], sc[kt][r], o[dt], 0, 0, 0);
+    }
+  }
+  if (qi < N)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      *reinterpret_cast<f4*>(ob + (size_t)qi * C + 16 * dt + 4 * gq) = f4{o[dt][0], o[dt][1], o[dt][2], o[dt][3]};
+}
+
+bool win_mf_ok(int N, int hd, const vv::Tuning& TU) {
+  return N <= kWinMaxN && hd <= kWinMaxHd && hd % 16 == 0 && TU.win_attn && TU.win_mfma;
+}
+
 struct ConvArgs {
   int B, Cimg, Himg, Wimg;  // image (B, Cimg, Himg, Wimg)
   int Ho, Wo, Ctok, kh, kw, sh, sw;
@@ -830,6 +964,7 @@ GemmArgs gbase(int M, int N, int K, int G, int epi, const FModel& m) {
   memset(&a, 0, sizeof(a));
   a.math = m.math;
   a.tune = m.tune;
+  a.h3_mink = (m.tune ? *m.tune : vv::kDefaultTuning).fc_h3_mink;
   a.apl = m.apl;  // the tile-48 A-plane workspace (k_rowsplit)
   a.apl_halfs = m.apl_halfs;
   a.M = M;
@@ -856,7 +991,36 @@ LnArgs lbase(int rows, int C, int G) {
 }
 
 // win_attn: the tuning knob (0: the streaming kernel for small windows too)
-hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st, bool win_attn) {
+hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st, const vv::Tuning& TU,
+                 const RopeArgs* rope) {
+  const bool win_attn = TU.win_attn != 0;
+  if (rope) {  // rope fused (win_mf_ok)
+    const int NT = (a.N + 15) / 16;
+    const size_t lds = (3 * (size_t)NT * 16 * (hd + 1) + NT * 16) * sizeof(float);
+    const dim3 grid(nwin, a.heads, G), block(64 * NT);
+    hipError_t e = hipSuccess;
+    switch (hd * 8 + NT) {
+#define WM(D, T)                                                                                           \
+  case D * 8 + T: {                                                                                        \
+    static bool init = false;                                                                              \
+    if (lds > 65536 && !init) { /* only past 64 KB: the attribute is not needed below */                  \
+      e = hipFuncSetAttribute((const void*)k_attn_win_mf<D, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              (int)((3 * kWinMaxN * (kWinMaxHd + 1) + kWinMaxN) * 4));                     \
+      if (e != hipSuccess) return e;                                                                       \
+      init = true;                                                                                         \
+    }                                                                                                      \
+    hipLaunchKernelGGL((k_attn_win_mf<D, T>), grid, block, lds, st, a, *rope);                             \
+    break;                                                                                                 \
+  }
+#define WM6(D) WM(D, 1) WM(D, 2) WM(D, 3) WM(D, 4) WM(D, 5) WM(D, 6)
+      WM6(16) WM6(32) WM6(48) WM6(64)
+#undef WM6
+#undef WM
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (a.N <= kWinMaxN && hd <= kWinMaxHd && hd % 4 == 0 && win_attn) {
     const size_t lds = (3 * (size_t)a.N * (hd + 4) + (size_t)a.N * (a.N + 1)) * sizeof(float);
     static bool init = false;
@@ -916,10 +1080,17 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     ra.c2 = S.c2;
     ra.s2 = S.s2;
     ra.scale = (float)std::pow((double)S.hd, -0.5);
-    int ph = prof_begin(st);
-    hipLaunchKernelGGL(k_rope, dim3(grid_for((size_t)M * S.heads * (S.hd / 2)), G), dim3(256), 0, st, ra);
-    FH(hipGetLastError());
-    prof_end(ph, st, PC_ATTN, 6.0 * G * M * C, 16.0 * G * M * C);
+    const vv::Tuning& TU = m.tune ? *m.tune : vv::kDefaultTuning;
+    const bool use_gattn = S.global && m.gattn_ws && G == 1 && gattn_supported(C, S.heads) && TU.gattn;
+    const bool use_gemm_attn = !use_gattn && S.global && N >= kGemmAttnMin && m.att_s && G == 1;
+    const bool rope_fused = !use_gattn && !use_gemm_attn && S.c1 && win_mf_ok(N, S.hd, TU);
+    int ph = -1;
+    if (!rope_fused) {
+      ph = prof_begin(st);
+      hipLaunchKernelGGL(k_rope, dim3(grid_for((size_t)M * S.heads * (S.hd / 2)), G), dim3(256), 0, st, ra);
+      FH(hipGetLastError());
+      prof_end(ph, st, PC_ATTN, 6.0 * G * M * C, 16.0 * G * M * C);
+    }
     FlashArgs fa;
     memset(&fa, 0, sizeof(fa));
     for (int g = 0; g < G; ++g) {
@@ -936,16 +1107,14 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
     fa.sh = sh;
     fa.nWh = S.H / S.wh;
     fa.nWw = S.W / S.ww;
-    const bool use_gattn = S.global && m.gattn_ws && G == 1 && gattn_supported(C, S.heads) &&
-                           (m.tune ? *m.tune : vv::kDefaultTuning).gattn;
     if (use_gattn) {
       // one window over the whole grid per image: the flash MFMA kernel (vv_gattn.hip), scores never in HBM
       ph = prof_begin(st);
       for (int b0 = 0; b0 < nwin; ++b0)
         FH(gattn(m.qkv + (size_t)b0 * N * 3 * C, m.t2 + (size_t)b0 * N * C, C, N, C, S.heads, m.gattn_ws, st,
-                 (m.tune ? *m.tune : vv::kDefaultTuning).gattn_qf));
+                 TU.gattn_qf));
       prof_end(ph, st, PC_ATTN, 4.0 * nwin * (double)N * N * C, 16.0 * nwin * (double)N * C);
-    } else if (S.global && N >= kGemmAttnMin && m.att_s && G == 1) {
+    } else if (use_gemm_attn) {
       // S_h = Q_h K_h^T (heads as GEMM groups; q rotated + scaled, k rotated), P = softmax_rows(S), O_h = P V_h
       const int Np = (N + 31) / 32 * 32, hd = S.hd;
       for (int b0 = 0; b0 < nwin; ++b0) {
@@ -977,7 +1146,7 @@ int stage_fwd(FModel& m, FStage& S, hipStream_t st, std::string& err) {
       }
     } else {
       ph = prof_begin(st);
-      FH(flash(fa, S.hd, nwin, G, st, (m.tune ? *m.tune : vv::kDefaultTuning).win_attn != 0));
+      FH(flash(fa, S.hd, nwin, G, st, TU, rope_fused ? &ra : nullptr));
       prof_end(ph, st, PC_ATTN, 4.0 * G * (double)M * N * C, 16.0 * G * (double)M * C);
     }
     // proj + window reverse / roll back + residual, in place

@@ -1914,6 +1914,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (!key) return nullptr;
   const std::string k(key);
   if (k == "h3_mink") return &t.h3_mink;
+  if (k == "fc_h3_mink") return &t.fc_h3_mink;
   if (k == "h3_big") return &t.h3_big;
   if (k == "h3_mf16") return &t.h3_mf16;
   if (k == "small_split") return &t.small_split;
@@ -1921,6 +1922,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "tail_minkt") return &t.tail_minkt;
   if (k == "ln_scales") return &t.ln_scales;
   if (k == "win_attn") return &t.win_attn;
+  if (k == "win_mfma") return &t.win_mfma;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;
@@ -2059,7 +2061,7 @@ static int pick_tile(const GemmArgs& a) {
     // and far slower at 1152 x 1152, where 72 tiles leave most CUs idle).
     // h3_mf16: the 16x16x32-MFMA form of the 256x128 kernel for N 2048..4095 x short K (profiles/r02/mf16:
     // 2048 x 3456 x 1152 at 64.3 vs 69.6 us; slower on the deep-K shapes)
-    const int h3_mink = std::max(64, T.h3_mink), h3_big = T.h3_big, h3_mf16 = T.h3_mf16;
+    const int h3_mink = std::max(64, a.h3_mink > 0 ? a.h3_mink : T.h3_mink), h3_big = T.h3_big, h3_mf16 = T.h3_mf16;
     if (a.math == GEMM_SPLIT16 && a.K >= h3_mink && h3_big && tiles_of(a, 256, 128) >= 64 &&
         (a.K >= 3456 || (a.N >= 2048 && a.N < 4096)))
       return h3_mf16 && a.K < 3456 ? 47 : 44;

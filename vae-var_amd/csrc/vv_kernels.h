@@ -14,6 +14,7 @@ constexpr int kMaxGroups = 8;
 // (DESIGN.md §3 / §9 give the measurements behind each one); kernels never read them, only host dispatch does.
 struct Tuning {
   int h3_mink = 768;            // smallest K sent to the fp16x3 kernels (profiles/r02/mink)
+  int fc_h3_mink = 192;         // ... in the forecast network LGUnet_all_1 (profiles/r03/fcst_mink)
   int h3_big = 1;               // 256x128 fp16x3 tiles where they measured faster (profiles/r02/h3big)
   int h3_mf16 = 1;              // the 16x16x32-MFMA form of the 256x128 tile for N 2048..4095 x short K
   int small_split = 1;          // whole-grid split-K of sub-chip fp16x3 GEMMs
@@ -28,6 +29,7 @@ struct Tuning {
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
+  int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
@@ -89,6 +91,7 @@ struct GemmArgs {
   // ascale, which must be set); tile 48 then reads them directly (no k_rowsplit pass)
   const unsigned short* apre;
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
+  int h3_mink;         // > 0: this GEMM's own smallest K for the fp16x3 kernels (the forecast: Tuning.fc_h3_mink)
   GemmGroup g[kMaxGroups];
 };
 

@@ -40,7 +40,8 @@ class Context:
     # per-context dispatch knobs (vv_set_tuning; defaults = the measured choices). A/B runs set them from the
     # environment as VAEVAR_<KEY> (e.g. VAEVAR_H3_MINK=384); the library itself reads no environment.
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
-                   "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt")
+                   "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt",
+                   "win_mfma", "fc_h3_mink")
 
     def __init__(self, device: int = 0):
         self.device = device
