@@ -180,7 +180,8 @@ int vv_adam(vv_ctx* ctx, float* p, const float* g, float* m, float* v, int64_t n
             float beta2, float eps, int step, void* stream);
 
 /* live profiler: HIP events around every kernel launch, summed per kernel class
-   (0 GEMM, 1 window attention, 2 LayerNorm, 3 patch conv/convT, 4 misfit, 5 vector); ncls >= 6.
+   (0 GEMM (bf16x6 / f32), 1 window attention, 2 LayerNorm, 3 patch conv/convT, 4 misfit, 5 vector, 6 fp16x3 GEMM,
+   7 fused Swin-tower sub-blocks); ncls >= 8.
    ms = summed launch durations, flops/bytes = algorithmic work, launches = count. stop synchronises. */
 int vv_profile_start(vv_ctx* ctx);
 int vv_profile_stop(vv_ctx* ctx, double* ms, double* flops, double* bytes, int* launches, int ncls);
@@ -209,7 +210,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    16x16x32-MFMA form, 1), "small_split" (whole-grid split-K of sub-chip fp16x3 GEMMs, 1), "small_split_minkt"
    (24), "tail_minkt" (k-tiles per split-K tail chunk, 12), "ln_scales" (row scales from the LayerNorm, 1),
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "win_mfma" (that kernel on the exact-f32 MFMA, 1),
-   "fc_h3_mink" (smallest K of the forecast network's fp16x3 GEMMs, 192), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
+   "fc_h3_mink" (smallest K of the forecast network's fp16x3 GEMMs, 192), "fuse_mlp" (the fused Swin-tower
+   LN2 + fc1 + GELU + fc2 + residual sub-block and its backward at dim 96, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
    the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1), "gattn" (the
    LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1), "gattn_qf" (its 16-query blocks per
    wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1), "h4_small" (tile 48 with whole-chip split-K

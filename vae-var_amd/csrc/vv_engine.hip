@@ -528,6 +528,44 @@ bool sync_check() { return g_sync_check.load(std::memory_order_relaxed) != 0; }
                                       hipGetErrorString(e_));                                      \
   } while (0)
 
+// the fused MLP sub-block (vv_tower.hip) for block b of a stage, fwd or bwd (gx: the stage gradient, in place);
+// false where it does not apply (fp16x3 math only, dim 96, weights with fp16 planes): the unfused launches run
+bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, bool fwd, float* gx, vv::MlpArgs& ma) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.fuse_mlp || sc.math != vv::GEMM_SPLIT16 || !vv::mlp_supported(S.C, S.M)) return false;
+  memset(&ma, 0, sizeof(ma));
+  const int M = S.M, C = S.C;
+  const size_t MC = (size_t)M * C;
+  ma.M = M;
+  ma.C = C;
+  ma.ngroups = S.G;
+  ma.eps = 1e-5f;
+  for (int g = 0; g < S.G; ++g) {
+    const auto& w = S.w[b][g];
+    vv::MlpGroup& G = ma.g[g];
+    G.x = sv.x1[b] + g * MC;
+    G.gamma = w.n2g;
+    G.stats = sv.st2[b] + (size_t)g * M * 2;
+    G.h1 = sv.h1[b] + g * MC * 4;
+    if (fwd) {
+      G.beta = w.n2b;
+      vv::fp16_planes_of(w.fc1W, C, &G.w1h, &G.w1s);
+      vv::fp16_planes_of(w.fc2W, 4 * C, &G.w2h, &G.w2s);
+      G.b1 = w.fc1b;
+      G.b2 = w.fc2b;
+      G.out = sv.x[b + 1] + g * MC;
+    } else {
+      vv::fp16_planes_of(w.fc2WT, C, &G.w1h, &G.w1s);
+      vv::fp16_planes_of(w.fc1WT, 4 * C, &G.w2h, &G.w2s);
+      G.dy = gx + g * MC;
+      G.out = gx + g * MC;
+      G.rs = sc.rs + (size_t)g * M;
+    }
+    if (!G.w1h || !G.w2h) return false;
+  }
+  return true;
+}
+
 int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st) {
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
@@ -575,6 +613,11 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
                 nullptr};
     CK(gemm_nt(p, st, -1, sc.ws));
+    vv::MlpArgs ma;
+    if (mlp_args(S, b, sv, sc, true, nullptr, ma)) {  // LN2 + fc1 + GELU + fc2 + residual in one launch
+      CK(vv::mlp_fwd(ma, st));
+      continue;
+    }
     // fc1 + GELU (row scales, and with tile 48 the planes, from LN2)
     GemmArgs f1 = gemm_base(M, 4 * C, C, G, EPI_GELU, sc);
     f1.ascale = sc.rs;
@@ -615,29 +658,34 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
   for (int b = S.depth - 1; b >= 0; --b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
-    GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc);
-    if (b < S.depth - 1) {
-      f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
-      if (f2_pl) f2.apre = sc.apl;
-    }
-    for (int g = 0; g < G; ++g)
-      f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
-    CK(gemm_nt(f2, st, -1, sc.ws));
-    GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc);
-    for (int g = 0; g < G; ++g)
-      f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
-    CK(gemm_nt(f1, st, -1, sc.ws));
     GemmArgs p = gemm_base(M, C, C, G, EPI_STORE, sc);
     p.arow = idx;
     p.ascale = sc.rs;  // per physical row of gx (the gather is applied to the scales too)
     for (int g = 0; g < G; ++g)
       p.g[g] = {gx + g * MC, nullptr, S.w[b][g].projWT, nullptr, sc.t2 + g * MC, nullptr, nullptr};
     const bool p_pl = ln_feeds_planes(p, sc);
-    LnArgs ln2 = ln_base(M, C, G, 1e-5f);
-    for (int g = 0; g < G; ++g)
-      ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
-                  sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, p_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
-    CK(layernorm_bwd(ln2, st));
+    vv::MlpArgs ma;
+    if (!p_pl && mlp_args(S, b, sv, sc, false, gx, ma)) {
+      CK(vv::mlp_bwd(ma, st));  // fc2^T + GELU' + fc1^T + LN2 backward + residual, gx in place (+ its row scales)
+    } else {
+      GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc);
+      if (b < S.depth - 1) {
+        f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
+        if (f2_pl) f2.apre = sc.apl;
+      }
+      for (int g = 0; g < G; ++g)
+        f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
+      CK(gemm_nt(f2, st, -1, sc.ws));
+      GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc);
+      for (int g = 0; g < G; ++g)
+        f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
+      CK(gemm_nt(f1, st, -1, sc.ws));
+      LnArgs ln2 = ln_base(M, C, G, 1e-5f);
+      for (int g = 0; g < G; ++g)
+        ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
+                    sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, p_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
+      CK(layernorm_bwd(ln2, st));
+    }
     if (p_pl) p.apre = sc.apl;  // planes in physical row order: the kernel gathers them through arow
     CK(gemm_nt(p, st, -1, sc.ws));
     AttnArgs at;

@@ -1923,6 +1923,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "ln_scales") return &t.ln_scales;
   if (k == "win_attn") return &t.win_attn;
   if (k == "win_mfma") return &t.win_mfma;
+  if (k == "fuse_mlp") return &t.fuse_mlp;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;
@@ -2030,6 +2031,10 @@ __global__ __launch_bounds__(256) void k_split16_rows(const float* __restrict__ 
     d[2 * (k & ~31) + 32 + (k & 31)] = __builtin_bit_cast(unsigned short, l);
   }
   if (tid == 0) sc[(size_t)r * K / 32] = __uint_as_float((E - 14u) << 23);
+}
+
+void fp16_planes_of(const float* W, int K, const unsigned short** h, const float** sc) {
+  split16_of(W, K, *h, *sc);
 }
 
 hipError_t split_registered(const float* W, size_t n, int K, hipStream_t s) {

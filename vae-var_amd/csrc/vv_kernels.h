@@ -30,6 +30,7 @@ struct Tuning {
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
+  int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
@@ -346,8 +347,9 @@ hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, fl
 // live profiler: HIP events around every launch, bucketed by kernel class
 // ---------------------------------------------------------------------------
 // PC_GEMM16: the GEMMs that ran the fp16x3 kernel (k_rowscale + k_gemm_h3 [+ fixup]); PC_GEMM: every other GEMM
+// PC_TOWER: the fused Swin-tower sub-blocks (vv_tower.hip)
 enum ProfClass : int { PC_GEMM = 0, PC_ATTN = 1, PC_LN = 2, PC_PATCH = 3, PC_MISFIT = 4, PC_VEC = 5, PC_GEMM16 = 6,
-                       PC_N = 7 };
+                       PC_TOWER = 7, PC_N = 8 };
 int prof_begin(hipStream_t s);                                        // -1 when disabled
 void prof_end(int h, hipStream_t s, int cls, double flops, double bytes);
 void prof_enable(bool on);
@@ -356,6 +358,37 @@ bool prof_enabled();
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 
 hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Fused Swin-tower MLP sub-block (vv_tower.hip): fwd x2 = x1 + fc2(GELU(fc1(LN2(x1)))), writing the LN2 statistics
+// and the fc1 pre-activation; bwd dx1 = dx2 + LN2-backward(fc1^T-path(GELU'(h1) * fc2^T-path(dx2))), in place
+// allowed (out == dy). Weights as fp16x3 planes + row scales (fp16_planes_of).
+// ---------------------------------------------------------------------------
+struct MlpGroup {
+  const float* x;                    // x1 [M][C]: LN2 input (and the forward residual)
+  const float *gamma, *beta;         // LN2 weight / bias (beta: forward only)
+  float* stats;                      // [M][2] mean, rstd: written (fwd) / read (bwd)
+  const unsigned short* w1h;         // fwd fc1.weight [4C][C], bwd fc2.weight^T [4C][C]: fp16 planes
+  const float* w1s;                  //   their row scales (stride K / 32)
+  const float* b1;                   // fc1.bias (fwd)
+  const unsigned short* w2h;         // fwd fc2.weight [C][4C], bwd fc1.weight^T [C][4C]
+  const float* w2s;
+  const float* b2;                   // fc2.bias (fwd)
+  float* h1;                         // [M][4C] fc1 pre-activation: written (fwd) / read (bwd)
+  const float* dy;                   // bwd: dx2 [M][C]
+  float* out;                        // fwd x2, bwd dx1 [M][C]
+  float* rs;                         // bwd, optional: fp16x3 row scales of dx1 (k_rowscale's formula)
+};
+struct MlpArgs {
+  int M, C, ngroups;
+  float eps;
+  MlpGroup g[kMaxGroups];
+};
+bool mlp_supported(int C, int M);
+hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s);
+hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s);
+// fp16 planes and row scales of a registered weight W [N][K] (null when it has none: K or offset not 32-aligned)
+void fp16_planes_of(const float* W, int K, const unsigned short** h, const float** sc);
 
 // ---------------------------------------------------------------------------
 // sc4dvar B-matrix transform (da_4dvar.py:878-931; vv_sc4dvar.hip) on the fixed 128 x 256 grid

@@ -1,0 +1,382 @@
+// Fused Swin-tower MLP sub-block (networks_old/utils/swinblock.py:13-29 Mlp, :296-309 the second residual of
+// SwinTransformerBlock.forward): x2 = x1 + fc2(GELU(fc1(LN2(x1)))) and its input gradient, one launch each instead
+// of LayerNorm + two GEMM launches, with the 4C-wide hidden layer never in HBM except the pre-activation the
+// backward needs (quirk Q5: input gradients only, so no weight-gradient GEMM wants the hidden layer either).
+//
+// One workgroup per 16 NW tokens, one wave per 16 tokens; the hidden layer runs in chunks of HC units:
+//   GEMM1^T  S[h][t] = sum_k W1[h][k] Y[t][k]     (Y = LN2(x1) fwd / dx2 bwd, per-token fp16 planes in LDS)
+//   epilogue v = S + b1 -> h1 (fwd) ; u = GELU(v)  |  bwd: u = S * GELU'(h1)
+//   GEMM2^T  O[n][t] += sum_h W2[n][h] u[t][h]     (u's fp16 planes built in registers straight from the
+//                                                   GEMM1 accumulators: they ARE the B operand, in the permuted
+//                                                   hidden order the W2 chunk is staged in)
+//   epilogue x2 = x1 + (O + b2)  |  bwd: dx1 = dx2 + LayerNorm-backward(O) over the full row in registers.
+// Arithmetic: fp16x3 (vv_gemm.hip k_gemm_h3 §): every operand row scaled by a power of two and split into fp16
+// h / l planes, products l.h + h.l + h.h on v_mfma_f32_16x16x32_f16, scales applied after the k loop. The hidden
+// operand u gets one scale per (token, HC chunk) -- no cross-workgroup row maximum -- and each chunk's partial
+// product is rescaled into the fp32 accumulator (exact: powers of two).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <mutex>
+
+#include "vv_kernels.h"
+
+namespace vv {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef unsigned short u16;
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float gelu_t(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float dgelu_t(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+// fp16x3 row scale 2^(141 - E) of a row whose largest |value| has bit pattern mx, and its inverse 2^(E - 141)
+__device__ __forceinline__ float sc_of(unsigned mx) { return __uint_as_float((268u - max(mx >> 23, 15u)) << 23); }
+__device__ __forceinline__ float inv_of(unsigned mx) { return __uint_as_float((max(mx >> 23, 15u) - 14u) << 23); }
+__device__ __forceinline__ unsigned amax(unsigned m, float v) { return max(m, __float_as_uint(fabsf(v))); }
+// [rows][32 halves] plane blocks: 16-B chunk q of row r at q ^ h((r >> 2) & 3), h = {0, 2, 3, 1}, so the four lane
+// groups of a 16x16x32 fragment read (rows lane & 15, chunk lane >> 4) hit 16 distinct 16-B slots
+__device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
+__device__ __forceinline__ int frag(int r, int q) { return r * 32 + ((q ^ hsw(r >> 2)) << 3); }
+
+template <int C, int NW, int HC, bool FWD>
+__global__ __launch_bounds__(64 * NW, 3) void k_mlp(MlpArgs a) {
+  constexpr int NT = 64 * NW, KS1 = C / 32, KS2 = HC / 32, NJ = HC / 16, NQ = C / 16, NC = 4 * C / HC;
+  constexpr int CQ = C / 4;                  // channels per lane in the row phases (4 lanes per token)
+  constexpr int A1W = KS1 * 2 * 16 * 32;     // halves of one wave's Y planes
+  constexpr int W1S = KS1 * 2 * HC * 32;     // halves of a W1 chunk (HC rows x C)
+  static_assert(C % 32 == 0 && HC % 32 == 0 && (4 * C) % HC == 0 && CQ % 4 == 0, "shape");
+  extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
+  const MlpGroup G = a.g[blockIdx.z];
+  u16* A1 = lds + wave * A1W;
+  u16* W1 = lds + NW * A1W;
+  u16* W2 = W1 + W1S;
+  // per-row tables: W1 row scales / fc1 bias [4C], W2 row scales / fc2 bias [C] (fwd; bwd: no biases)
+  float* T1s = reinterpret_cast<float*>(W2 + (HC / 32) * 2 * C * 32);
+  float* T1b = T1s + 4 * C;
+  float* T2s = T1b + 4 * C;
+  float* T2b = T2s + C;
+  for (int i = tid; i < 4 * C; i += 64 * NW) {
+    T1s[i] = G.w1s[(size_t)i * (C / 32)];
+    T1b[i] = FWD ? G.b1[i] : 0.f;
+  }
+  for (int i = tid; i < C; i += 64 * NW) {
+    T2s[i] = G.w2s[(size_t)i * (4 * C / 32)];
+    T2b[i] = FWD ? G.b2[i] : 0.f;
+  }
+  const int t0 = blockIdx.x * 16 * NW + 16 * wave;  // this wave's first token
+
+  // ---- row phase: Y = LN2(x1) (fwd) or dx2 (bwd), scaled per token and split into planes ----
+  const int tt = lane >> 2, qd = lane & 3;  // token, quarter of the row
+  float iy_own;                             // 2^-e of token tt's Y row
+  {
+    const f4* src = reinterpret_cast<const f4*>((FWD ? G.x : G.dy) + (size_t)(t0 + tt) * C + qd * CQ);
+    f4 yv[CQ / 4];
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
+    if (FWD) {
+      f4 gv[CQ / 4], bv[CQ / 4];
+#pragma unroll
+      for (int v = 0; v < CQ / 4; ++v) {
+        gv[v] = reinterpret_cast<const f4*>(G.gamma + qd * CQ)[v];
+        bv[v] = reinterpret_cast<const f4*>(G.beta + qd * CQ)[v];
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < CQ / 4; ++v) s += (yv[v][0] + yv[v][1]) + (yv[v][2] + yv[v][3]);
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      const float mean = s / (float)C;
+      float q = 0.f;
+#pragma unroll
+      for (int v = 0; v < CQ / 4; ++v)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = yv[v][e] - mean;
+          q += d * d;
+        }
+      q += __shfl_xor(q, 1);
+      q += __shfl_xor(q, 2);
+      const float rstd = 1.0f / sqrtf(q / (float)C + a.eps);
+#pragma unroll
+      for (int v = 0; v < CQ / 4; ++v)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) yv[v][e] = (yv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
+      if (qd == 0) *reinterpret_cast<float2*>(G.stats + 2 * (size_t)(t0 + tt)) = make_float2(mean, rstd);
+    }
+    unsigned mx = 0;
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = amax(mx, yv[v][e]);
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    const float sy = sc_of(mx);
+    iy_own = inv_of(mx);
+    typedef _Float16 h4t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) {
+      const int k = qd * CQ + 4 * v, ks = k >> 5, kk = k & 31;
+      h4t hv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = yv[v][e] * sy;
+        hv[e] = (_Float16)x;
+        lv[e] = (_Float16)(x - (float)hv[e]);
+      }
+      *reinterpret_cast<h4t*>(A1 + frag((ks * 2 + 0) * 16 + tt, kk >> 3) + (kk & 7)) = hv;
+      *reinterpret_cast<h4t*>(A1 + frag((ks * 2 + 1) * 16 + tt, kk >> 3) + (kk & 7)) = lv;
+    }
+  }
+  const float iy = __shfl(iy_own, li << 2);  // this lane's token (li) in the fragment layouts
+  const size_t trow = (size_t)(t0 + li);
+
+  f4 acc2[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc2[q] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // weight chunks: global -> registers one chunk ahead (every load of a chunk in flight at once, under the
+  // previous chunk's MFMAs), registers -> LDS between two barriers
+  constexpr int P1 = HC * KS1 * 8 / NT, P2 = C * KS2 * 16 / NT;
+  static_assert(P1 * NT == HC * KS1 * 8 && P2 * NT == C * KS2 * 16, "staging split");
+  u4v r1[P1];
+  u2v r2[P2];
+  // W1 chunk: rows c HC + r, the whole K = C; global row = KS1 x [h(32) | l(32)]. W2 chunk: rows n < C, hidden units
+  // [c HC, c HC + HC) in the order of the u fragments: position 8 g + e of k-step kk holds hidden
+  // 32 kk + (e < 4 ? 4 g + e : 16 + 4 g + e - 4). (Plain unrolled loops, no lambdas: the staging registers must
+  // not become a stack array.)
+#define VV_MLP_LOAD(c)                                                                                            \
+  {                                                                                                               \
+    _Pragma("unroll") for (int i = 0; i < P1; ++i) {                                                             \
+      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8);                                     \
+      r1[i] = *reinterpret_cast<const u4v*>(G.w1h + (size_t)((c) * HC + r) * 2 * C + (rem >> 3) * 64 +          \
+                                              ((rem >> 2) & 1) * 32 + (rem & 3) * 8);                             \
+    }                                                                                                             \
+    _Pragma("unroll") for (int i = 0; i < P2; ++i) {                                                             \
+      const int e = tid + i * NT, n = e / (KS2 * 16), rem = e - n * (KS2 * 16);                                   \
+      r2[i] = *reinterpret_cast<const u2v*>(G.w2h + (size_t)n * 2 * (4 * C) + ((c) * KS2 + (rem >> 4)) * 64 +   \
+                                              ((rem >> 3) & 1) * 32 + 4 * ((rem >> 1) & 3) + 16 * (rem & 1));     \
+    }                                                                                                             \
+  }
+  VV_MLP_LOAD(0)
+
+  for (int c = 0; c < NC; ++c) {
+    // bwd: this chunk's pre-activations, in flight before the next chunk's weight loads (vmcnt is in order)
+    f4 ex[NJ];
+    if (!FWD) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        ex[j] = *reinterpret_cast<const f4*>(G.h1 + trow * (4 * C) + c * HC + 16 * j + 4 * g4);
+    }
+    __syncthreads();  // the previous chunk's W1 / W2 fragment reads are done (and, at c = 0, the Y planes written)
+#pragma unroll
+    for (int i = 0; i < P1; ++i) {
+      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8);
+      *reinterpret_cast<u4v*>(W1 + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * HC * 32 + frag(r, rem & 3)) = r1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < P2; ++i) {
+      const int e = tid + i * NT, n = e / (KS2 * 16), rem = e - n * (KS2 * 16);
+      *reinterpret_cast<u2v*>(W2 + ((rem >> 4) * 2 + ((rem >> 3) & 1)) * C * 32 + frag(n, (rem >> 1) & 3) +
+                                4 * (rem & 1)) = r2[i];
+    }
+    __syncthreads();
+    if (c + 1 < NC) VV_MLP_LOAD(c + 1)
+    float s1[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = c * HC + 16 * j + 4 * g4;
+      const f4 sv = *reinterpret_cast<const f4*>(T1s + n);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s1[j][i] = sv[i];
+      if (FWD) ex[j] = *reinterpret_cast<const f4*>(T1b + n);
+    }
+
+    // GEMM1^T: rows = hidden units 16 j + 4 g4 + i of the chunk, columns = tokens
+    f4 acc1[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc1[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const h8v yh = *reinterpret_cast<const h8v*>(A1 + frag((ks * 2 + 0) * 16 + li, g4));
+      const h8v yl = *reinterpret_cast<const h8v*>(A1 + frag((ks * 2 + 1) * 16 + li, g4));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const h8v wh = *reinterpret_cast<const h8v*>(W1 + (ks * 2 + 0) * HC * 32 + frag(16 * j + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(W1 + (ks * 2 + 1) * HC * 32 + frag(16 * j + li, g4));
+        acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, yh, acc1[j], 0, 0, 0);
+        acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yl, acc1[j], 0, 0, 0);
+        acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yh, acc1[j], 0, 0, 0);
+      }
+    }
+    // epilogue 1
+    float u[NJ][4];
+    unsigned mx = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = c * HC + 16 * j + 4 * g4;
+      if (FWD) {
+        f4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc1[j][i] * (iy * s1[j][i]) + ex[j][i];
+        *reinterpret_cast<f4*>(G.h1 + trow * (4 * C) + n) = v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[j][i] = gelu_t(v[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[j][i] = acc1[j][i] * (iy * s1[j][i]) * dgelu_t(ex[j][i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = amax(mx, u[j][i]);
+    }
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 16));
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 32));
+    const float su = sc_of(mx), iu = inv_of(mx);
+    // GEMM2^T: rows = output channels 16 q + 4 g4 + i, columns = tokens; u's planes are the B fragments
+    f4 tmp[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) tmp[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KS2; ++kk) {
+      h8v bh, bl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = u[2 * kk + (e >> 2)][e & 3] * su;
+        bh[e] = (_Float16)x;
+        bl[e] = (_Float16)(x - (float)bh[e]);
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const h8v wh = *reinterpret_cast<const h8v*>(W2 + (kk * 2 + 0) * C * 32 + frag(16 * q + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(W2 + (kk * 2 + 1) * C * 32 + frag(16 * q + li, g4));
+        tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, tmp[q], 0, 0, 0);
+        tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, tmp[q], 0, 0, 0);
+        tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, tmp[q], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc2[q][i] += tmp[q][i] * iu;
+  }
+
+  // ---- epilogue 2 (lane: token li, channels 16 q + 4 g4 + i) ----
+  float o[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int n = 16 * q + 4 * g4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[q][i] = acc2[q][i] * T2s[n + i];
+  }
+  if (FWD) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int n = 16 * q + 4 * g4;
+      const f4 bv = *reinterpret_cast<const f4*>(T2b + n);
+      const f4 xv = *reinterpret_cast<const f4*>(G.x + trow * C + n);
+      f4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = xv[i] + (o[q][i] + bv[i]);
+      *reinterpret_cast<f4*>(G.out + trow * C + n) = v;
+    }
+  } else {
+    // LayerNorm backward over the row (this lane's 4 NQ channels + the other three lane groups):
+    // dx = rstd (g dy - mean(g dy) - xhat mean(g dy xhat)), then + dx2 (the residual), k_ln_bwd's formula
+    const float2 st = *reinterpret_cast<const float2*>(G.stats + 2 * trow);
+    const float mean = st.x, rstd = st.y;
+    f4 xv[NQ], gv[NQ];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int n = 16 * q + 4 * g4;
+      xv[q] = *reinterpret_cast<const f4*>(G.x + trow * C + n);
+      gv[q] = *reinterpret_cast<const f4*>(G.gamma + n);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gd = gv[q][i] * o[q][i];
+        s1 += gd;
+        s2 += gd * ((xv[q][i] - mean) * rstd);
+      }
+    }
+    s1 += __shfl_xor(s1, 16);
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 16);
+    s2 += __shfl_xor(s2, 32);
+    const float m1 = s1 / (float)C, m2 = s2 / (float)C;
+    unsigned omx = 0;
+    f4 dv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) dv[q] = *reinterpret_cast<const f4*>(G.dy + trow * C + 16 * q + 4 * g4);
+    // every lane has read its dy before any lane of the workgroup writes (out may alias dy: same rows only)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      f4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = rstd * (gv[q][i] * o[q][i] - m1 - ((xv[q][i] - mean) * rstd) * m2) + dv[q][i];
+        omx = amax(omx, v[i]);
+      }
+      *reinterpret_cast<f4*>(G.out + trow * C + 16 * q + 4 * g4) = v;
+    }
+    if (G.rs) {
+      omx = max(omx, (unsigned)__shfl_xor((int)omx, 16));
+      omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
+      if (g4 == 0) G.rs[trow] = sc_of(omx);
+    }
+  }
+}
+
+#undef VV_MLP_LOAD
+
+template <int C, int NW, int HC, bool FWD>
+hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
+  constexpr size_t lds = 2 * ((size_t)NW * (C / 32) * 2 * 16 * 32 + (size_t)(C / 32) * 2 * HC * 32 +
+                              (size_t)(HC / 32) * 2 * C * 32) + 4 * (8 * C + 2 * C);
+  static std::mutex mu;
+  static bool init[64] = {false};
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!init[dev]) {
+      if (hipError_t e = hipFuncSetAttribute((const void*)k_mlp<C, NW, HC, FWD>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
+        return e;
+      init[dev] = true;
+    }
+  }
+  hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD>), dim3(a.M / (16 * NW), 1, a.ngroups), dim3(64 * NW), lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool mlp_supported(int C, int M) { return C == 96 && M > 0 && M % 64 == 0; }
+
+static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
+  if (!mlp_supported(a.C, a.M) || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  for (int g = 0; g < a.ngroups; ++g) {
+    const MlpGroup& G = a.g[g];
+    if (!G.x || !G.gamma || !G.stats || !G.w1h || !G.w1s || !G.w2h || !G.w2s || !G.h1 || !G.out)
+      return hipErrorInvalidValue;
+    if (fwd ? (!G.beta || !G.b1 || !G.b2) : !G.dy) return hipErrorInvalidValue;
+  }
+  const int ph = prof_begin(s);
+  const hipError_t e = fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s);
+  // 2 GEMMs of M x 4C x C per group; bytes: x1 / dx2 (+ out, + x1 bwd) and the 4C-wide pre-activation
+  prof_end(ph, s, PC_TOWER, 4.0 * a.ngroups * a.M * 4.0 * a.C * a.C,
+           (double)a.ngroups * a.M * 4.0 * (fwd ? 2.0 * a.C + 4.0 * a.C : 3.0 * a.C + 4.0 * a.C));
+  return e;
+}
+hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, true); }
+hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, false); }
+
+}  // namespace vv

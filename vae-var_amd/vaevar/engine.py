@@ -41,7 +41,7 @@ class Context:
     # environment as VAEVAR_<KEY> (e.g. VAEVAR_H3_MINK=384); the library itself reads no environment.
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
                    "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt",
-                   "win_mfma", "fc_h3_mink")
+                   "win_mfma", "fc_h3_mink", "fuse_mlp")
 
     def __init__(self, device: int = 0):
         self.device = device
@@ -115,7 +115,7 @@ class Context:
         check(lib.vv_adam(self.h, _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), lr, beta1, beta2, eps, step,
                           _stream()), "adam")
 
-    PROF_CLASSES = ("gemm", "attention", "layernorm", "patch", "misfit", "vector", "gemm16")
+    PROF_CLASSES = ("gemm", "attention", "layernorm", "patch", "misfit", "vector", "gemm16", "tower")
 
     def profile_start(self):
         check(lib.vv_profile_start(self.h), "profile_start")
