@@ -515,12 +515,13 @@ def test_ln_row_scales_bitwise(tmp_path):
     assert np.array_equal(outs[0], outs[1])
 
 
-def test_fused_mlp_vs_unfused(full_dec):
-    """The fused Swin-tower MLP sub-block (vv_tower.hip: LN2 + fc1 + GELU + fc2 + residual in one launch, and its
-    input gradient) against the unfused LayerNorm + GEMM launches (tuning fuse_mlp 0) on the config-2 decoder: the
-    dim-96 tower blocks change arithmetic (fp16x3 with a scale per 64-unit hidden chunk instead of bf16x6), so
-    forward output and input gradient agree to rounding (rel <= 2e-6 of max), the closure J to 1e-7 and dJ/dz to 1e-5
-    (the G3 closure-gradient bound is 1e-4)."""
+@pytest.mark.parametrize("knob", ["fuse_mlp", "fuse_attn"])
+def test_fused_tower_vs_unfused(full_dec, knob):
+    """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
+    at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient) and fuse_attn (LN1 + qkv +
+    window attention + proj + residual, forward). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
+    per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
+    max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
     from vaevar.engine import DAProblem
     from vaevar.problem import make_problem
     from vaevar.synth import smooth_field, uniform_sym
@@ -530,9 +531,10 @@ def test_fused_mlp_vs_unfused(full_dec):
     prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
     zc = torch.from_numpy(0.3 * smooth_field(403, (1, 32, 128, 256))).cuda()
     res = []
+    default = full_dec.ctx.get_tuning(knob)
     try:
         for v in (0, 1):
-            full_dec.ctx.set_tuning("fuse_mlp", v)
+            full_dec.ctx.set_tuning(knob, v)
             out = full_dec.forward_raw(z).clone()
             dz = torch.empty_like(z)
             full_dec.backward_raw(cot, dz)
@@ -540,10 +542,10 @@ def test_fused_mlp_vs_unfused(full_dec):
             jb, jo = prob.closure(zc, g)
             res.append((out, dz, jb, jo, g))
     finally:
-        full_dec.ctx.set_tuning("fuse_mlp", 1)
+        full_dec.ctx.set_tuning(knob, default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     e_o, e_d, e_g = rel(o1.cpu(), o0.cpu()), rel(d1.cpu(), d0.cpu()), rel(g1.cpu(), g0.cpu())
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
-    print(f"fused MLP vs unfused: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
+    print(f"{knob} on vs off: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert not torch.equal(o0, o1), "the fused kernel did not run"
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7

@@ -566,6 +566,46 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
   return true;
 }
 
+// the fused attention sub-block (vv_tower.hip) for block b, forward; false where it does not apply
+bool ablk_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, int shift, const int* idx,
+               vv::AblkArgs& aa) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.fuse_attn || sc.math != vv::GEMM_SPLIT16 || !vv::ablk_supported(S.C, S.heads, ws, S.M)) return false;
+  memset(&aa, 0, sizeof(aa));
+  const int M = S.M, C = S.C;
+  const size_t MC = (size_t)M * C;
+  aa.M = M;
+  aa.C = C;
+  aa.heads = S.heads;
+  aa.ngroups = S.G;
+  aa.nWh = S.nWh;
+  aa.nWw = S.nWw;
+  aa.ws = ws;
+  aa.shift = shift;
+  aa.H = S.H;
+  aa.scale = (float)std::pow((double)(C / S.heads), -0.5);
+  aa.eps = 1e-5f;
+  aa.map = idx;
+  for (int g = 0; g < S.G; ++g) {
+    const auto& w = S.w[b][g];
+    vv::AblkGroup& G = aa.g[g];
+    G.x = sv.x[b] + g * MC;
+    G.n1g = w.n1g;
+    G.n1b = w.n1b;
+    G.stats = sv.st1[b] + (size_t)g * M * 2;
+    vv::fp16_planes_of(w.qkvW, C, &G.wqh, &G.wqs);
+    G.wqb = w.qkvb;
+    G.table = w.table;
+    G.qkv = sv.qkv[b] + g * MC * 3;
+    G.P = sv.P[b] + (size_t)g * (M / 16) * S.heads * 256;
+    vv::fp16_planes_of(w.projW, C, &G.wph, &G.wps);
+    G.wpb = w.projb;
+    G.out = sv.x1[b] + g * MC;
+    if (!G.wqh || !G.wph || !G.wqb || !G.wpb) return false;
+  }
+  return true;
+}
+
 int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st) {
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
@@ -573,6 +613,10 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
   for (int b = 0; b < S.depth; ++b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
+    vv::AblkArgs aa;
+    if (ablk_args(S, b, sv, sc, ws, shift, idx, aa)) {
+      CK(vv::ablk_fwd(aa, st));  // LN1 + qkv + window attention + proj + residual in one launch
+    } else {
     // qkv (A's fp16x3 row scales from LN1; with tile 48 also A's planes, and LN1 writes no fp32 copy)
     GemmArgs q = gemm_base(M, 3 * C, C, G, EPI_STORE, sc);
     q.ascale = sc.rs;
@@ -613,6 +657,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
                 nullptr};
     CK(gemm_nt(p, st, -1, sc.ws));
+    }
     vv::MlpArgs ma;
     if (mlp_args(S, b, sv, sc, true, nullptr, ma)) {  // LN2 + fc1 + GELU + fc2 + residual in one launch
       CK(vv::mlp_fwd(ma, st));

@@ -31,6 +31,7 @@ struct Tuning {
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
   int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
+  int fuse_attn = 0;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported (off: §3c)
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
@@ -385,6 +386,31 @@ struct MlpArgs {
   MlpGroup g[kMaxGroups];
 };
 bool mlp_supported(int C, int M);
+// Fused Swin-tower attention sub-block (vv_tower.hip), forward: LN1 (window gather) + qkv + window attention
+// (rel-pos bias, quirk-Q1 mask) + proj + residual (window reverse), writing what the backward reads: LN1 stats and
+// qkv in window order, the softmax P. ws = 4 (16-token windows), head dim 32.
+struct AblkGroup {
+  const float* x;                    // stage input rows [M][C] (physical order); the residual
+  const float *n1g, *n1b;            // LN1
+  float* stats;                      // [M][2] LN1 mean, rstd (window order)
+  const unsigned short* wqh;         // qkv.weight [3C][C] fp16 planes
+  const float *wqs, *wqb;            //   row scales (stride C / 32), qkv.bias
+  const float* table;                // relative_position_bias_table [49][heads]
+  float* qkv;                        // [M][3C] window order (saved for the backward)
+  float* P;                          // [nwin][heads][16][16] softmax (saved)
+  const unsigned short* wph;         // proj.weight [C][C] fp16 planes
+  const float *wps, *wpb;            //   row scales, proj.bias
+  float* out;                        // x1 [M][C] physical order
+};
+struct AblkArgs {
+  int M, C, heads, ngroups;
+  int nWh, nWw, ws, shift, H;        // window grid per image, window size, shift (mask labels, quirk Q1)
+  float scale, eps;
+  const int* map;                    // window-order row -> physical row (the cyclic shift + partition)
+  AblkGroup g[kMaxGroups];
+};
+bool ablk_supported(int C, int heads, int ws, int M);
+hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s);
 hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s);
 hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s);
 // fp16 planes and row scales of a registered weight W [N][K] (null when it has none: K or offset not 32-aligned)

@@ -357,6 +357,345 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Fused Swin-tower attention sub-block, forward (swinblock.py:265-296 SwinTransformerBlock.forward up to the first
+// residual; WindowAttention :133-172): x1 = x + proj(WindowAttention(LN1(x) in window order)) in window-reverse
+// order. One wave per 16-token window, four windows per workgroup. Per head h four 8C-half weight chunks go
+// through LDS (two chunks ahead in registers): the q, k and v rows of the qkv weight (GEMM^T: 2 tiles x C/32
+// k-steps, fp16x3) -- the head's 16 x 32 q / k / v go to HBM (saved for the backward) and to a per-wave LDS buffer,
+// scores + bias + mask, softmax and P.V run on the VALU in fp32 as in k_attn_fwd -- then the head's 32 columns of
+// the proj weight: the head output, scaled per (token, head) and split in registers, is already the B fragment of
+// that k-step (lane = token, 8 consecutive channels), and its partial product is rescaled into the proj
+// accumulator (exact). No O buffer, and the scores come from q / k fragments in registers (fp16x3 MFMA): 54 KB of
+// LDS, three workgroups per CU.
+template <int C>
+__global__ __launch_bounds__(256, 3) void k_ablk_fwd(AblkArgs a) {
+  constexpr int NW = 4, NT = 256, KS = C / 32, H = C / 32, CQ = C / 4, NQ = C / 16;
+  constexpr int YW = KS * 2 * 16 * 32;        // halves of one wave's Y planes
+  constexpr int WCH = 8 * C * 8;              // halves of a weight chunk (8 C 16-B pieces)
+  constexpr int HBS = 36;                     // fp32 row stride of the per-wave q / k / v head buffers
+  constexpr int PBS = 16;                     // fp32 row stride of the per-wave P buffer
+  constexpr int NSC = 4 * H;                  // chunks: q, k, v rows and proj columns per head
+  constexpr int PC = 8 * C / NT;              // 16-B staging pieces per thread and chunk
+  static_assert(PC * NT == 8 * C, "staging split");
+  extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
+  const AblkGroup G = a.g[blockIdx.z];
+  u16* Ypl = lds + wave * YW;
+  u16* Wc = lds + NW * YW;
+  float* fl = reinterpret_cast<float*>(Wc + WCH);
+  float* hb = fl + wave * 16 * HBS;                       // [16][HBS]: v of the head
+  float* pb = fl + NW * 16 * HBS + wave * 16 * PBS;       // [16][PBS]: P of the head
+  float* tb = fl + NW * (16 * HBS + 16 * PBS);            // [H][49]
+  float* Tqs = tb + H * 49;      // qkv row scales [3C]
+  float* Tqb = Tqs + 3 * C;      // qkv bias [3C]
+  float* Tps = Tqb + 3 * C;      // proj row scales [C]
+  float* Tpb = Tps + C;          // proj bias [C]
+  const int win = blockIdx.x * NW + wave;  // this wave's window (over the batch)
+  const int r0 = win * 16;                 // its first window-order row
+
+  for (int i = tid; i < H * 49; i += NT) tb[i] = G.table[(i % 49) * a.heads + i / 49];
+  for (int i = tid; i < 3 * C; i += NT) {
+    Tqs[i] = G.wqs[(size_t)i * (C / 32)];
+    Tqb[i] = G.wqb[i];
+  }
+  for (int i = tid; i < C; i += NT) {
+    Tps[i] = G.wps[(size_t)i * (C / 32)];
+    Tpb[i] = G.wpb[i];
+  }
+
+  // weight chunk sc = 4 h + part: part < 3 -> rows part C + 32 h + r (r < 32) of the qkv weight, the whole K = C
+  // ([ks][plane][32 rows][32]); part 3 -> k-chunk h of every proj row n < C ([plane][C rows][32])
+  u4v rw[2][PC];
+#define VV_ABLK_LOAD(buf, sc)                                                                                    \
+  {                                                                                                              \
+    const int h_ = (sc) >> 2, part_ = (sc)&3;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < PC; ++i) {                                                            \
+      const int e = tid + i * NT;                                                                                \
+      if (part_ < 3) {                                                                                           \
+        const int r = e / (KS * 8), rem = e - r * (KS * 8);                                                      \
+        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wqh + (size_t)(part_ * C + 32 * h_ + r) * 2 * C +            \
+                                                   (rem >> 3) * 64 + ((rem >> 2) & 1) * 32 + (rem & 3) * 8);     \
+      } else {                                                                                                   \
+        const int n = e >> 3, rem = e & 7;                                                                       \
+        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wph + (size_t)n * 2 * C + h_ * 64 + (rem >> 2) * 32 +         \
+                                                   (rem & 3) * 8);                                               \
+      }                                                                                                          \
+    }                                                                                                            \
+  }
+  VV_ABLK_LOAD(0, 0)
+  VV_ABLK_LOAD(1, 1)
+
+  // ---- LN1 of the window's 16 rows (gathered through the window map), planes in LDS ----
+  const int tt = lane >> 2, qd = lane & 3;
+  float iy_own;
+  {
+    const size_t prow = (size_t)a.map[r0 + tt];
+    const f4* src = reinterpret_cast<const f4*>(G.x + prow * C + qd * CQ);
+    f4 yv[CQ / 4], gv[CQ / 4], bv[CQ / 4];
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) {
+      yv[v] = src[v];
+      gv[v] = reinterpret_cast<const f4*>(G.n1g + qd * CQ)[v];
+      bv[v] = reinterpret_cast<const f4*>(G.n1b + qd * CQ)[v];
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) sm += (yv[v][0] + yv[v][1]) + (yv[v][2] + yv[v][3]);
+    sm += __shfl_xor(sm, 1);
+    sm += __shfl_xor(sm, 2);
+    const float mean = sm / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = yv[v][e] - mean;
+        q += d * d;
+      }
+    q += __shfl_xor(q, 1);
+    q += __shfl_xor(q, 2);
+    const float rstd = 1.0f / sqrtf(q / (float)C + a.eps);
+    unsigned mx = 0;
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        yv[v][e] = (yv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
+        mx = amax(mx, yv[v][e]);
+      }
+    if (qd == 0) *reinterpret_cast<float2*>(G.stats + 2 * (size_t)(r0 + tt)) = make_float2(mean, rstd);
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    const float sy = sc_of(mx);
+    iy_own = inv_of(mx);
+    typedef _Float16 h4t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) {
+      const int k = qd * CQ + 4 * v, ks = k >> 5, kk = k & 31;
+      h4t hv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = yv[v][e] * sy;
+        hv[e] = (_Float16)x;
+        lv[e] = (_Float16)(x - (float)hv[e]);
+      }
+      *reinterpret_cast<h4t*>(Ypl + frag((ks * 2 + 0) * 16 + tt, kk >> 3) + (kk & 7)) = hv;
+      *reinterpret_cast<h4t*>(Ypl + frag((ks * 2 + 1) * 16 + tt, kk >> 3) + (kk & 7)) = lv;
+    }
+  }
+  const float iy = __shfl(iy_own, li << 2);
+  const size_t trow = (size_t)(r0 + li);         // this lane's token, window order
+  const size_t tphys = (size_t)a.map[r0 + li];   // ... physical row
+  const int wr = (win % (a.nWh * a.nWw)) / a.nWw;
+  auto lab = [&](int rr) {
+    const int y = wr * 4 + rr;
+    return y < a.H - 4 ? 0 : (y < a.H - a.shift ? 1 : 2);
+  };
+  const bool masked_row = a.shift > 0 && lab(g4) != lab(li >> 2);
+
+  f4 pacc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) pacc[q] = f4{0.f, 0.f, 0.f, 0.f};
+  h8v oh, ol;  // the current head's output planes (B fragment: token li, channels 8 g4 .. 8 g4 + 7)
+  float io = 0.f;
+  h8v qh, ql, kh, kl;  // the head's q (A operand) and k (B operand) planes, token li
+  float iq = 0.f, ik = 0.f;
+  for (int sc = 0; sc < NSC; ++sc) {
+    const int h = sc >> 2, part = sc & 3;
+    __syncthreads();
+    // chunk sc from register set sc & 1 into LDS, then chunk sc + 2 into that set
+#define VV_ABLK_STORE(buf)                                                                                       \
+  _Pragma("unroll") for (int i = 0; i < PC; ++i) {                                                              \
+    const int e = tid + i * NT;                                                                                  \
+    if (part < 3) {                                                                                              \
+      const int r = e / (KS * 8), rem = e - r * (KS * 8);                                                        \
+      *reinterpret_cast<u4v*>(Wc + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * 32 * 32 + frag(r, rem & 3)) = rw[buf][i]; \
+    } else {                                                                                                     \
+      const int n = e >> 3, rem = e & 7;                                                                         \
+      *reinterpret_cast<u4v*>(Wc + (rem >> 2) * C * 32 + frag(n, rem & 3)) = rw[buf][i];                         \
+    }                                                                                                            \
+  }
+    if (sc & 1) {
+      VV_ABLK_STORE(1)
+    } else {
+      VV_ABLK_STORE(0)
+    }
+    __syncthreads();
+    if (sc + 2 < NSC) {
+      if (sc & 1) {
+        VV_ABLK_LOAD(1, sc + 2)
+      } else {
+        VV_ABLK_LOAD(0, sc + 2)
+      }
+    }
+    if (part < 3) {
+      f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const h8v yh = *reinterpret_cast<const h8v*>(Ypl + frag((ks * 2 + 0) * 16 + li, g4));
+        const h8v yl = *reinterpret_cast<const h8v*>(Ypl + frag((ks * 2 + 1) * 16 + li, g4));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const h8v wh = *reinterpret_cast<const h8v*>(Wc + (ks * 2 + 0) * 32 * 32 + frag(16 * j + li, g4));
+          const h8v wl = *reinterpret_cast<const h8v*>(Wc + (ks * 2 + 1) * 32 * 32 + frag(16 * j + li, g4));
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, yh, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yh, acc[j], 0, 0, 0);
+        }
+      }
+      // q / k / v of head h for token li, channels 16 j + 4 g4 + i of the head
+      f4 val[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = 16 * j + 4 * g4, R = part * C + h * 32 + c;
+        const f4 sv = *reinterpret_cast<const f4*>(Tqs + R);
+        const f4 bv = *reinterpret_cast<const f4*>(Tqb + R);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) val[j][i] = acc[j][i] * (iy * sv[i]) + bv[i];
+        *reinterpret_cast<f4*>(G.qkv + trow * (3 * C) + R) = val[j];
+        if (part == 2) *reinterpret_cast<f4*>(hb + li * HBS + c) = val[j];
+      }
+      if (part < 2) {
+        // q (part 0) / k (part 1) of the head as fp16x3 fragments straight from the accumulators: lane = token,
+        // k index e <-> channel 16 (e >> 2) + 4 g4 + (e & 3) (the same permutation for both operands)
+        unsigned mx = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mx = amax(mx, val[j][i]);
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, 16));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, 32));
+        const float ss = sc_of(mx);
+        h8v fh, fl8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = val[e >> 2][e & 3] * ss;
+          fh[e] = (_Float16)x;
+          fl8[e] = (_Float16)(x - (float)fh[e]);
+        }
+        if (part == 0) {
+          qh = fh;
+          ql = fl8;
+          iq = inv_of(mx);
+        } else {
+          kh = fh;
+          kl = fl8;
+          ik = inv_of(mx);
+        }
+      } else {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's v stores to LDS are done
+        __builtin_amdgcn_wave_barrier();
+        // S[t1][t2] (t1 = 4 g4 + i, t2 = li) = q[t1].k[t2] (fp16x3 MFMA) scale + bias + mask; softmax over t2
+        f4 sacc = {0.f, 0.f, 0.f, 0.f};
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql, kh, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh, kl, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh, kh, sacc, 0, 0, 0);
+        float sv4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv4[i] = sacc[i] * (__shfl(iq, 4 * g4 + i) * ik);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int cj = li & 3, rj = li >> 2;
+          float b = tb[h * 49 + (g4 - rj + 3) * 7 + (i - cj + 3)];
+          if (masked_row) b += -100.0f;
+          float x = sv4[i] * a.scale + b;
+          float mx = x;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+          x = expf(x - mx);
+          float sum = x;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o);
+          const float pv = x * (1.0f / sum);
+          G.P[(((size_t)win * a.heads + h) * 16 + 4 * g4 + i) * 16 + li] = pv;
+          pb[(4 * g4 + i) * PBS + li] = pv;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // O[t][c] (t = li, c = 8 g4 + e of the head) = sum_t2 P[t][t2] v[t2][c]
+        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t2 = 0; t2 < 16; t2 += 4) {
+          const f4 p4 = *reinterpret_cast<const f4*>(pb + li * PBS + t2);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float* vr = hb + (t2 + u) * HBS + 8 * g4;
+            const f4 v0 = *reinterpret_cast<const f4*>(vr), v1 = *reinterpret_cast<const f4*>(vr + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              o[e] += p4[u] * v0[e];
+              o[4 + e] += p4[u] * v1[e];
+            }
+          }
+        }
+        unsigned omx = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) omx = amax(omx, o[e]);
+        omx = max(omx, (unsigned)__shfl_xor((int)omx, 16));
+        omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
+        const float so = sc_of(omx);
+        io = inv_of(omx);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = o[e] * so;
+          oh[e] = (_Float16)x;
+          ol[e] = (_Float16)(x - (float)oh[e]);
+        }
+      }
+    } else {
+      // proj^T k-step h: rows n = 16 q + 4 g4 + i, columns = tokens; rescaled by the head output's scale
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const h8v wh = *reinterpret_cast<const h8v*>(Wc + frag(16 * q + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(Wc + C * 32 + frag(16 * q + li, g4));
+        f4 t = {0.f, 0.f, 0.f, 0.f};
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, oh, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ol, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, oh, t, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pacc[q][i] += t[i] * io;
+      }
+    }
+  }
+#undef VV_ABLK_STORE
+#undef VV_ABLK_LOAD
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int n = 16 * q + 4 * g4;
+    const f4 sv = *reinterpret_cast<const f4*>(Tps + n);
+    const f4 bv = *reinterpret_cast<const f4*>(Tpb + n);
+    const f4 xv = *reinterpret_cast<const f4*>(G.x + tphys * C + n);
+    f4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = xv[i] + (pacc[q][i] * sv[i] + bv[i]);
+    *reinterpret_cast<f4*>(G.out + tphys * C + n) = v;
+  }
+}
+
+template <int C>
+hipError_t launch_ablk_fwd(const AblkArgs& a, hipStream_t s) {
+  constexpr int NW = 4, KS = C / 32, H = C / 32;
+  constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
+                         4 * ((size_t)NW * (16 * 36 + 16 * 16) + H * 49 + 8 * C);
+  static std::mutex mu;
+  static bool init[64] = {false};
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!init[dev]) {
+      if (hipError_t e = hipFuncSetAttribute((const void*)k_ablk_fwd<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds))
+        return e;
+      init[dev] = true;
+    }
+  }
+  hipLaunchKernelGGL(k_ablk_fwd<C>, dim3(a.M / (16 * NW), 1, a.ngroups), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 bool mlp_supported(int C, int M) { return C == 96 && M > 0 && M % 64 == 0; }
@@ -377,6 +716,25 @@ static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
   return e;
 }
 hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, true); }
+
+bool ablk_supported(int C, int heads, int ws, int M) { return C == 96 && heads == 3 && ws == 4 && M > 0 && M % 64 == 0; }
+
+hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s) {
+  if (!ablk_supported(a.C, a.heads, a.ws, a.M) || a.ngroups <= 0 || a.ngroups > kMaxGroups || !a.map)
+    return hipErrorInvalidValue;
+  for (int g = 0; g < a.ngroups; ++g) {
+    const AblkGroup& G = a.g[g];
+    if (!G.x || !G.n1g || !G.n1b || !G.stats || !G.wqh || !G.wqs || !G.wqb || !G.table || !G.qkv || !G.P ||
+        !G.wph || !G.wps || !G.wpb || !G.out)
+      return hipErrorInvalidValue;
+  }
+  const int ph = prof_begin(s);
+  const hipError_t e = launch_ablk_fwd<96>(a, s);
+  // qkv + proj GEMMs (2 M 4C C) and the window attention (4 M 16 C); bytes: x in, qkv + P + stats + x1 out
+  prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 64.0 * a.M * a.C),
+           (double)a.ngroups * a.M * 4.0 * (a.C + 3 * a.C + 16 * a.heads + 2 + a.C));
+  return e;
+}
 hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, false); }
 
 }  // namespace vv
