@@ -31,7 +31,7 @@ struct Tuning {
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
   int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
-  int fuse_attn = 0;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported (off: §3c)
+  int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
