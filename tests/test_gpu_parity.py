@@ -515,11 +515,11 @@ def test_ln_row_scales_bitwise(tmp_path):
     assert np.array_equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("knob", ["fuse_mlp", "fuse_attn"])
-def test_fused_tower_vs_unfused(full_dec, knob):
+@pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_attn", 1), ("fuse_attn", 3)])
+def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient) and fuse_attn (LN1 + qkv +
-    window attention + proj + residual, forward). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
+    window attention + proj + residual: 1 the forward, 3 also its input gradient). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
     per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
     max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
     from vaevar.engine import DAProblem
@@ -533,7 +533,7 @@ def test_fused_tower_vs_unfused(full_dec, knob):
     res = []
     default = full_dec.ctx.get_tuning(knob)
     try:
-        for v in (0, 1):
+        for v in (0, on):
             full_dec.ctx.set_tuning(knob, v)
             out = full_dec.forward_raw(z).clone()
             dz = torch.empty_like(z)
@@ -546,6 +546,6 @@ def test_fused_tower_vs_unfused(full_dec, knob):
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     e_o, e_d, e_g = rel(o1.cpu(), o0.cpu()), rel(d1.cpu(), d0.cpu()), rel(g1.cpu(), g0.cpu())
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
-    print(f"{knob} on vs off: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
+    print(f"{knob} {on} vs 0: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert not torch.equal(o0, o1), "the fused kernel did not run"
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7

@@ -568,9 +568,11 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
 
 // the fused attention sub-block (vv_tower.hip) for block b, forward; false where it does not apply
 bool ablk_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, int shift, const int* idx,
-               vv::AblkArgs& aa) {
+               vv::AblkArgs& aa, float* gx = nullptr) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  if (!T.fuse_attn || sc.math != vv::GEMM_SPLIT16 || !vv::ablk_supported(S.C, S.heads, ws, S.M)) return false;
+  // fuse_attn: bit 0 the forward, bit 1 the backward
+  if (!(T.fuse_attn & (gx ? 2 : 1)) || sc.math != vv::GEMM_SPLIT16 || !vv::ablk_supported(S.C, S.heads, ws, S.M))
+    return false;
   memset(&aa, 0, sizeof(aa));
   const int M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
@@ -602,6 +604,13 @@ bool ablk_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, in
     G.wpb = w.projb;
     G.out = sv.x1[b] + g * MC;
     if (!G.wqh || !G.wph || !G.wqb || !G.wpb) return false;
+    if (gx) {  // backward: the stage gradient in place, the transposed weights
+      G.out = gx + g * MC;
+      G.rs = sc.rs + (size_t)g * M;
+      vv::fp16_planes_of(w.projWT, C, &G.wpth, &G.wpts);
+      vv::fp16_planes_of(w.qkvWT, 3 * C, &G.wqth, &G.wqts);
+      if (!G.wpth || !G.wqth) return false;
+    }
   }
   return true;
 }
@@ -732,6 +741,11 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       CK(layernorm_bwd(ln2, st));
     }
     if (p_pl) p.apre = sc.apl;  // planes in physical row order: the kernel gathers them through arow
+    vv::AblkArgs ab;
+    if (!(f2_pl && b > 0) && ablk_args(S, b, sv, sc, ws, shift, idx, ab, gx)) {
+      CK(vv::ablk_bwd(ab, st));  // proj^T + window-attention backward + qkv^T + LN1 backward + residual, in place
+      continue;
+    }
     CK(gemm_nt(p, st, -1, sc.ws));
     AttnArgs at;
     memset(&at, 0, sizeof(at));

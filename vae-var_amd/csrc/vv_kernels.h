@@ -31,7 +31,8 @@ struct Tuning {
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
   int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
-  int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported
+  int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
+                                // the forward, bit 1 the backward (measured neutral, profiles/r03/ab_fuse_attn)
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
@@ -401,6 +402,12 @@ struct AblkGroup {
   const unsigned short* wph;         // proj.weight [C][C] fp16 planes
   const float *wps, *wpb;            //   row scales, proj.bias
   float* out;                        // x1 [M][C] physical order
+  // backward (ablk_bwd): dy = out = the stage gradient (physical rows, in place); qkv, P, stats, x read
+  const unsigned short* wpth;        // proj.weight^T [C][C] planes (dO = dx1 W_proj)
+  const float* wpts;
+  const unsigned short* wqth;        // qkv.weight^T [C][3C] planes (dY = dqkv W_qkv)
+  const float* wqts;
+  float* rs;                         // optional: fp16x3 row scales of the result (physical rows)
 };
 struct AblkArgs {
   int M, C, heads, ngroups;
@@ -411,6 +418,9 @@ struct AblkArgs {
 };
 bool ablk_supported(int C, int heads, int ws, int M);
 hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s);
+// backward of the same sub-block: gx (G.out, physical rows) <- gx + LN1-backward(dqkv W_qkv) with
+// dqkv = WindowAttention-backward(gx gathered W_proj), in place
+hipError_t ablk_bwd(const AblkArgs& a, hipStream_t s);
 hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s);
 hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s);
 // fp16 planes and row scales of a registered weight W [N][K] (null when it has none: K or offset not 32-aligned)

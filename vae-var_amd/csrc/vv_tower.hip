@@ -673,6 +673,345 @@ __global__ __launch_bounds__(256, 3) void k_ablk_fwd(AblkArgs a) {
   }
 }
 
+// Backward of the attention sub-block (the input gradient only, quirk Q5), one wave per window:
+//   dO = gx[window rows] W_proj                      (GEMM^T per head: projW^T rows of the head, B = gx planes)
+//   dP = dO v^T (fp16x3 MFMA from registers), dS = P (dP - rowsum(P dP)); dq = scale dS k, dk = scale dS^T q,
+//   dv = P^T dO on the VALU (fp32, as k_attn_bwd), each already a B fragment of the dY GEMM (8 consecutive
+//   channels of the token) scaled per (token, k-step)
+//   dY = dqkv W_qkv                                 (qkvW^T k-chunks of q_h, k_h, v_h, rescaled per k-step)
+//   gx[window rows] += LN1-backward(dY)             (full rows in registers, k_ln_bwd's formula), in place.
+template <int C>
+__global__ __launch_bounds__(256, 2) void k_ablk_bwd(AblkArgs a) {
+  constexpr int NW = 4, NT = 256, KS = C / 32, H = C / 32, CQ = C / 4, NQ = C / 16;
+  constexpr int YW = KS * 2 * 16 * 32;        // halves of one wave's gx planes
+  constexpr int WCH = 8 * C * 8;              // halves of a weight chunk
+  constexpr int BS = 36;                      // fp32 row stride of the per-wave q / k / dO buffers
+  constexpr int SS = 17;                      // ... of dS / P
+  constexpr int PWAVE = 3 * 16 * BS + 2 * 16 * SS;
+  constexpr int NSC = 4 * H;
+  constexpr int PC = 8 * C / NT;
+  static_assert(PC * NT == 8 * C, "staging split");
+  extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
+  const AblkGroup G = a.g[blockIdx.z];
+  u16* Dpl = lds + wave * YW;
+  u16* Wc = lds + NW * YW;
+  float* fl = reinterpret_cast<float*>(Wc + WCH);
+  float* qb = fl + wave * PWAVE;   // [16][BS] q of the head
+  float* kb = qb + 16 * BS;        // [16][BS] k
+  float* ob = kb + 16 * BS;        // [16][BS] dO
+  float* sb = ob + 16 * BS;        // [16][SS] dS
+  float* pb = sb + 16 * SS;        // [16][SS] P
+  float* Tos = fl + NW * PWAVE;    // proj^T row scales [C]
+  float* Tqs = Tos + C;            // qkv^T row scales [C]
+  const int win = blockIdx.x * NW + wave;
+  const int r0 = win * 16;
+  for (int i = tid; i < C; i += NT) {
+    Tos[i] = G.wpts[(size_t)i * (C / 32)];
+    Tqs[i] = G.wqts[(size_t)i * (3 * C / 32)];
+  }
+  // chunk sc = 4 h + part: part 0 -> proj^T rows 32 h + r, the whole K = C ([ks][plane][32][32]); part 1..3 ->
+  // k-chunk (part - 1) KS + h of every qkv^T row c < C ([plane][C][32])
+  u4v rw[2][PC];
+#define VV_ABWD_LOAD(buf, sc)                                                                                    \
+  {                                                                                                              \
+    const int h_ = (sc) >> 2, part_ = (sc)&3;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < PC; ++i) {                                                            \
+      const int e = tid + i * NT;                                                                                \
+      if (part_ == 0) {                                                                                          \
+        const int r = e / (KS * 8), rem = e - r * (KS * 8);                                                      \
+        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wpth + (size_t)(32 * h_ + r) * 2 * C + (rem >> 3) * 64 +     \
+                                                   ((rem >> 2) & 1) * 32 + (rem & 3) * 8);                       \
+      } else {                                                                                                   \
+        const int n = e >> 3, rem = e & 7;                                                                       \
+        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wqth + (size_t)n * 2 * (3 * C) +                            \
+                                                   ((part_ - 1) * KS + h_) * 64 + (rem >> 2) * 32 + (rem & 3) * 8); \
+      }                                                                                                          \
+    }                                                                                                            \
+  }
+  VV_ABWD_LOAD(0, 0)
+  VV_ABWD_LOAD(1, 1)
+
+  // ---- gx rows of the window (gathered), scaled per token and split into planes ----
+  const int tt = lane >> 2, qd = lane & 3;
+  float id_own;
+  {
+    const size_t prow = (size_t)a.map[r0 + tt];
+    const f4* src = reinterpret_cast<const f4*>(G.out + prow * C + qd * CQ);
+    f4 yv[CQ / 4];
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
+    unsigned mx = 0;
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = amax(mx, yv[v][e]);
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    const float sy = sc_of(mx);
+    id_own = inv_of(mx);
+    typedef _Float16 h4t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) {
+      const int k = qd * CQ + 4 * v, ks = k >> 5, kk = k & 31;
+      h4t hv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = yv[v][e] * sy;
+        hv[e] = (_Float16)x;
+        lv[e] = (_Float16)(x - (float)hv[e]);
+      }
+      *reinterpret_cast<h4t*>(Dpl + frag((ks * 2 + 0) * 16 + tt, kk >> 3) + (kk & 7)) = hv;
+      *reinterpret_cast<h4t*>(Dpl + frag((ks * 2 + 1) * 16 + tt, kk >> 3) + (kk & 7)) = lv;
+    }
+  }
+  const float idx1 = __shfl(id_own, li << 2);
+  const size_t trow = (size_t)(r0 + li);
+  const size_t tphys = (size_t)a.map[r0 + li];
+
+  f4 yacc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) yacc[q] = f4{0.f, 0.f, 0.f, 0.f};
+  h8v fh[3], fl8[3];  // dq, dk, dv planes of the head (token li, 8 consecutive channels of the k-step)
+  float fi[3] = {0.f, 0.f, 0.f};
+  for (int sc = 0; sc < NSC; ++sc) {
+    const int h = sc >> 2, part = sc & 3;
+    __syncthreads();
+#define VV_ABWD_STORE(buf)                                                                                       \
+  _Pragma("unroll") for (int i = 0; i < PC; ++i) {                                                              \
+    const int e = tid + i * NT;                                                                                  \
+    if (part == 0) {                                                                                             \
+      const int r = e / (KS * 8), rem = e - r * (KS * 8);                                                        \
+      *reinterpret_cast<u4v*>(Wc + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * 32 * 32 + frag(r, rem & 3)) = rw[buf][i]; \
+    } else {                                                                                                     \
+      const int n = e >> 3, rem = e & 7;                                                                         \
+      *reinterpret_cast<u4v*>(Wc + (rem >> 2) * C * 32 + frag(n, rem & 3)) = rw[buf][i];                         \
+    }                                                                                                            \
+  }
+    if (sc & 1) {
+      VV_ABWD_STORE(1)
+    } else {
+      VV_ABWD_STORE(0)
+    }
+    __syncthreads();
+    if (sc + 2 < NSC) {
+      if (sc & 1) {
+        VV_ABWD_LOAD(1, sc + 2)
+      } else {
+        VV_ABWD_LOAD(0, sc + 2)
+      }
+    }
+    if (part == 0) {
+      // this head's saved q, k, v rows and P (HBM), issued ahead of the dO GEMM
+      const float* qr = G.qkv + trow * (3 * C) + h * 32;
+      f4 qv[2], kv[2], vv[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        qv[j] = *reinterpret_cast<const f4*>(qr + 16 * j + 4 * g4);
+        kv[j] = *reinterpret_cast<const f4*>(qr + C + 16 * j + 4 * g4);
+        vv[j] = *reinterpret_cast<const f4*>(qr + 2 * C + 16 * j + 4 * g4);
+      }
+      float pv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = G.P[(((size_t)win * a.heads + h) * 16 + 4 * g4 + i) * 16 + li];
+      // dO^T rows c = 32 h + 16 j + 4 g4 + i, columns = tokens
+      f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const h8v yh = *reinterpret_cast<const h8v*>(Dpl + frag((ks * 2 + 0) * 16 + li, g4));
+        const h8v yl = *reinterpret_cast<const h8v*>(Dpl + frag((ks * 2 + 1) * 16 + li, g4));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const h8v wh = *reinterpret_cast<const h8v*>(Wc + (ks * 2 + 0) * 32 * 32 + frag(16 * j + li, g4));
+          const h8v wl = *reinterpret_cast<const h8v*>(Wc + (ks * 2 + 1) * 32 * 32 + frag(16 * j + li, g4));
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, yh, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yh, acc[j], 0, 0, 0);
+        }
+      }
+      f4 dov[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = 16 * j + 4 * g4;
+        const f4 sv = *reinterpret_cast<const f4*>(Tos + h * 32 + c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dov[j][i] = acc[j][i] * (idx1 * sv[i]);
+        *reinterpret_cast<f4*>(ob + li * BS + c) = dov[j];
+        *reinterpret_cast<f4*>(qb + li * BS + c) = qv[j];
+        *reinterpret_cast<f4*>(kb + li * BS + c) = kv[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pb[(4 * g4 + i) * SS + li] = pv[i];
+      // dP[t1][t2] = dO[t1] . v[t2]: dO (A, row = token) and v (B, column = token) fragments from registers
+      unsigned mo = 0, mv = 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          mo = amax(mo, dov[j][i]);
+          mv = amax(mv, vv[j][i]);
+        }
+      mo = max(mo, (unsigned)__shfl_xor((int)mo, 16));
+      mo = max(mo, (unsigned)__shfl_xor((int)mo, 32));
+      mv = max(mv, (unsigned)__shfl_xor((int)mv, 16));
+      mv = max(mv, (unsigned)__shfl_xor((int)mv, 32));
+      const float so = sc_of(mo), svs = sc_of(mv);
+      h8v oh, ol, vh, vl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = dov[e >> 2][e & 3] * so, y = vv[e >> 2][e & 3] * svs;
+        oh[e] = (_Float16)x;
+        ol[e] = (_Float16)(x - (float)oh[e]);
+        vh[e] = (_Float16)y;
+        vl[e] = (_Float16)(y - (float)vh[e]);
+      }
+      f4 dp = {0.f, 0.f, 0.f, 0.f};
+      dp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ol, vh, dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_16x16x32_f16(oh, vl, dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_16x16x32_f16(oh, vh, dp, 0, 0, 0);
+      const float io_ = inv_of(mo), iv_ = inv_of(mv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = dp[i] * (__shfl(io_, 4 * g4 + i) * iv_);
+        float rsum = pv[i] * d;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) rsum += __shfl_xor(rsum, o);
+        sb[(4 * g4 + i) * SS + li] = pv[i] * (d - rsum);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores are done
+      __builtin_amdgcn_wave_barrier();
+      // dq / dk / dv for token li, channels 8 g4 + e of the head
+      float dq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dk[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f},
+            dv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float s_tu = sb[li * SS + u], s_ut = sb[u * SS + li], p_ut = pb[u * SS + li];
+        const f4 k0 = *reinterpret_cast<const f4*>(kb + u * BS + 8 * g4), k1 = *reinterpret_cast<const f4*>(kb + u * BS + 8 * g4 + 4);
+        const f4 q0 = *reinterpret_cast<const f4*>(qb + u * BS + 8 * g4), q1 = *reinterpret_cast<const f4*>(qb + u * BS + 8 * g4 + 4);
+        const f4 o0 = *reinterpret_cast<const f4*>(ob + u * BS + 8 * g4), o1 = *reinterpret_cast<const f4*>(ob + u * BS + 8 * g4 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dq[e] += s_tu * k0[e];
+          dq[4 + e] += s_tu * k1[e];
+          dk[e] += s_ut * q0[e];
+          dk[4 + e] += s_ut * q1[e];
+          dv[e] += p_ut * o0[e];
+          dv[4 + e] += p_ut * o1[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dq[e] *= a.scale;
+        dk[e] *= a.scale;
+      }
+      // per (token, k-step) scales and planes of dq, dk, dv
+#pragma unroll
+      for (int p3 = 0; p3 < 3; ++p3) {
+        const float* src = p3 == 0 ? dq : (p3 == 1 ? dk : dv);
+        unsigned m = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m = amax(m, src[e]);
+        m = max(m, (unsigned)__shfl_xor((int)m, 16));
+        m = max(m, (unsigned)__shfl_xor((int)m, 32));
+        const float sf = sc_of(m);
+        fi[p3] = inv_of(m);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = src[e] * sf;
+          fh[p3][e] = (_Float16)x;
+          fl8[p3][e] = (_Float16)(x - (float)fh[p3][e]);
+        }
+      }
+    } else {
+      // dY^T k-step (part - 1, h): rows c = 16 q + 4 g4 + i, columns = tokens
+      const int p3 = part - 1;
+      const h8v bh = p3 == 0 ? fh[0] : (p3 == 1 ? fh[1] : fh[2]);
+      const h8v bl = p3 == 0 ? fl8[0] : (p3 == 1 ? fl8[1] : fl8[2]);
+      const float bi = p3 == 0 ? fi[0] : (p3 == 1 ? fi[1] : fi[2]);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const h8v wh = *reinterpret_cast<const h8v*>(Wc + frag(16 * q + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(Wc + C * 32 + frag(16 * q + li, g4));
+        f4 t = {0.f, 0.f, 0.f, 0.f};
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, t, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) yacc[q][i] += t[i] * bi;
+      }
+    }
+  }
+#undef VV_ABWD_STORE
+#undef VV_ABWD_LOAD
+  // ---- LN1 backward over the row (lane: token li, channels 16 q + 4 g4 + i) + the residual gradient ----
+  const float2 st = *reinterpret_cast<const float2*>(G.stats + 2 * trow);
+  const float mean = st.x, rstd = st.y;
+  float o[NQ][4];
+  f4 xv[NQ], gv[NQ];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int n = 16 * q + 4 * g4;
+    const f4 sv = *reinterpret_cast<const f4*>(Tqs + n);
+    xv[q] = *reinterpret_cast<const f4*>(G.x + tphys * C + n);
+    gv[q] = *reinterpret_cast<const f4*>(G.n1g + n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[q][i] = yacc[q][i] * sv[i];
+      const float gd = gv[q][i] * o[q][i];
+      s1 += gd;
+      s2 += gd * ((xv[q][i] - mean) * rstd);
+    }
+  }
+  s1 += __shfl_xor(s1, 16);
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 16);
+  s2 += __shfl_xor(s2, 32);
+  const float m1 = s1 / (float)C, m2 = s2 / (float)C;
+  f4 dv4[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) dv4[q] = *reinterpret_cast<const f4*>(G.out + tphys * C + 16 * q + 4 * g4);
+  unsigned omx = 0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    f4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = rstd * (gv[q][i] * o[q][i] - m1 - ((xv[q][i] - mean) * rstd) * m2) + dv4[q][i];
+      omx = amax(omx, v[i]);
+    }
+    *reinterpret_cast<f4*>(G.out + tphys * C + 16 * q + 4 * g4) = v;
+  }
+  if (G.rs) {
+    omx = max(omx, (unsigned)__shfl_xor((int)omx, 16));
+    omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
+    if (g4 == 0) G.rs[tphys] = sc_of(omx);
+  }
+}
+
+template <int C>
+hipError_t launch_ablk_bwd(const AblkArgs& a, hipStream_t s) {
+  constexpr int NW = 4, KS = C / 32;
+  constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
+                         4 * ((size_t)NW * (3 * 16 * 36 + 2 * 16 * 17) + 2 * C);
+  static std::mutex mu;
+  static bool init[64] = {false};
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!init[dev]) {
+      if (hipError_t e = hipFuncSetAttribute((const void*)k_ablk_bwd<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds))
+        return e;
+      init[dev] = true;
+    }
+  }
+  hipLaunchKernelGGL(k_ablk_bwd<C>, dim3(a.M / (16 * NW), 1, a.ngroups), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
 template <int C>
 hipError_t launch_ablk_fwd(const AblkArgs& a, hipStream_t s) {
   constexpr int NW = 4, KS = C / 32, H = C / 32;
@@ -733,6 +1072,22 @@ hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s) {
   // qkv + proj GEMMs (2 M 4C C) and the window attention (4 M 16 C); bytes: x in, qkv + P + stats + x1 out
   prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 64.0 * a.M * a.C),
            (double)a.ngroups * a.M * 4.0 * (a.C + 3 * a.C + 16 * a.heads + 2 + a.C));
+  return e;
+}
+
+hipError_t ablk_bwd(const AblkArgs& a, hipStream_t s) {
+  if (!ablk_supported(a.C, a.heads, a.ws, a.M) || a.ngroups <= 0 || a.ngroups > kMaxGroups || !a.map)
+    return hipErrorInvalidValue;
+  for (int g = 0; g < a.ngroups; ++g) {
+    const AblkGroup& G = a.g[g];
+    if (!G.x || !G.n1g || !G.stats || !G.qkv || !G.P || !G.wpth || !G.wpts || !G.wqth || !G.wqts || !G.out)
+      return hipErrorInvalidValue;
+  }
+  const int ph = prof_begin(s);
+  const hipError_t e = launch_ablk_bwd<96>(a, s);
+  // proj^T and qkv^T GEMMs (2 M 4C C), the attention backward (8 M 16 C); bytes: gx in / out, qkv, P, x
+  prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 128.0 * a.M * a.C),
+           (double)a.ngroups * a.M * 4.0 * (2 * a.C + 3 * a.C + 16 * a.heads + 2 + a.C));
   return e;
 }
 hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, false); }
