@@ -63,13 +63,33 @@ __global__ __launch_bounds__(64 * NW, 3) void k_mlp(MlpArgs a) {
   float* T1b = T1s + 4 * C;
   float* T2s = T1b + 4 * C;
   float* T2b = T2s + C;
-  for (int i = tid; i < 4 * C; i += 64 * NW) {
-    T1s[i] = G.w1s[(size_t)i * (C / 32)];
-    T1b[i] = FWD ? G.b1[i] : 0.f;
-  }
-  for (int i = tid; i < C; i += 64 * NW) {
-    T2s[i] = G.w2s[(size_t)i * (4 * C / 32)];
-    T2b[i] = FWD ? G.b2[i] : 0.f;
+  {  // every table load issued before the first LDS store (one memory round trip)
+    constexpr int N1 = (4 * C + NT - 1) / NT, N2 = (C + NT - 1) / NT;
+    float a1[N1], c1[N1], a2[N2], c2[N2];
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      const int r = min(tid + i * NT, 4 * C - 1);
+      a1[i] = G.w1s[(size_t)r * (C / 32)];
+      c1[i] = FWD ? G.b1[r] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < N2; ++i) {
+      const int r = min(tid + i * NT, C - 1);
+      a2[i] = G.w2s[(size_t)r * (4 * C / 32)];
+      c2[i] = FWD ? G.b2[r] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < N1; ++i)
+      if (tid + i * NT < 4 * C) {
+        T1s[tid + i * NT] = a1[i];
+        T1b[tid + i * NT] = c1[i];
+      }
+#pragma unroll
+    for (int i = 0; i < N2; ++i)
+      if (tid + i * NT < C) {
+        T2s[tid + i * NT] = a2[i];
+        T2b[tid + i * NT] = c2[i];
+      }
   }
   const int t0 = blockIdx.x * 16 * NW + 16 * wave;  // this wave's first token
 
@@ -276,14 +296,16 @@ __global__ __launch_bounds__(64 * NW, 3) void k_mlp(MlpArgs a) {
     for (int i = 0; i < 4; ++i) o[q][i] = acc2[q][i] * T2s[n + i];
   }
   if (FWD) {
+    f4 xv[NQ];  // all residual loads before the first store (see k_ablk_fwd)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) xv[q] = *reinterpret_cast<const f4*>(G.x + trow * C + 16 * q + 4 * g4);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int n = 16 * q + 4 * g4;
       const f4 bv = *reinterpret_cast<const f4*>(T2b + n);
-      const f4 xv = *reinterpret_cast<const f4*>(G.x + trow * C + n);
       f4 v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = xv[i] + (o[q][i] + bv[i]);
+      for (int i = 0; i < 4; ++i) v[i] = xv[q][i] + (o[q][i] + bv[i]);
       *reinterpret_cast<f4*>(G.out + trow * C + n) = v;
     }
   } else {
@@ -394,14 +416,41 @@ __global__ __launch_bounds__(256, 3) void k_ablk_fwd(AblkArgs a) {
   const int win = blockIdx.x * NW + wave;  // this wave's window (over the batch)
   const int r0 = win * 16;                 // its first window-order row
 
-  for (int i = tid; i < H * 49; i += NT) tb[i] = G.table[(i % 49) * a.heads + i / 49];
-  for (int i = tid; i < 3 * C; i += NT) {
-    Tqs[i] = G.wqs[(size_t)i * (C / 32)];
-    Tqb[i] = G.wqb[i];
-  }
-  for (int i = tid; i < C; i += NT) {
-    Tps[i] = G.wps[(size_t)i * (C / 32)];
-    Tpb[i] = G.wpb[i];
+  {  // every table load issued before the first LDS store (one memory round trip)
+    constexpr int NB = (H * 49 + NT - 1) / NT, N1 = (3 * C + NT - 1) / NT, N2 = (C + NT - 1) / NT;
+    float tv[NB], a1[N1], c1[N1], a2[N2], c2[N2];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int r = min(tid + i * NT, H * 49 - 1);
+      tv[i] = G.table[(r % 49) * a.heads + r / 49];
+    }
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      const int r = min(tid + i * NT, 3 * C - 1);
+      a1[i] = G.wqs[(size_t)r * (C / 32)];
+      c1[i] = G.wqb[r];
+    }
+#pragma unroll
+    for (int i = 0; i < N2; ++i) {
+      const int r = min(tid + i * NT, C - 1);
+      a2[i] = G.wps[(size_t)r * (C / 32)];
+      c2[i] = G.wpb[r];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (tid + i * NT < H * 49) tb[tid + i * NT] = tv[i];
+#pragma unroll
+    for (int i = 0; i < N1; ++i)
+      if (tid + i * NT < 3 * C) {
+        Tqs[tid + i * NT] = a1[i];
+        Tqb[tid + i * NT] = c1[i];
+      }
+#pragma unroll
+    for (int i = 0; i < N2; ++i)
+      if (tid + i * NT < C) {
+        Tps[tid + i * NT] = a2[i];
+        Tpb[tid + i * NT] = c2[i];
+      }
   }
 
   // weight chunk sc = 4 h + part: part < 3 -> rows part C + 32 h + r (r < 32) of the qkv weight, the whole K = C
@@ -660,15 +709,19 @@ __global__ __launch_bounds__(256, 3) void k_ablk_fwd(AblkArgs a) {
   }
 #undef VV_ABLK_STORE
 #undef VV_ABLK_LOAD
+  // every residual load issued before the first store (out may alias x as far as the compiler knows: a load
+  // after a store would wait for it, one memory round trip per float4)
+  f4 xv[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) xv[q] = *reinterpret_cast<const f4*>(G.x + tphys * C + 16 * q + 4 * g4);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int n = 16 * q + 4 * g4;
     const f4 sv = *reinterpret_cast<const f4*>(Tps + n);
     const f4 bv = *reinterpret_cast<const f4*>(Tpb + n);
-    const f4 xv = *reinterpret_cast<const f4*>(G.x + tphys * C + n);
     f4 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = xv[i] + (pacc[q][i] * sv[i] + bv[i]);
+    for (int i = 0; i < 4; ++i) v[i] = xv[q][i] + (pacc[q][i] * sv[i] + bv[i]);
     *reinterpret_cast<f4*>(G.out + tphys * C + n) = v;
   }
 }
@@ -706,9 +759,21 @@ __global__ __launch_bounds__(256, 2) void k_ablk_bwd(AblkArgs a) {
   float* Tqs = Tos + C;            // qkv^T row scales [C]
   const int win = blockIdx.x * NW + wave;
   const int r0 = win * 16;
-  for (int i = tid; i < C; i += NT) {
-    Tos[i] = G.wpts[(size_t)i * (C / 32)];
-    Tqs[i] = G.wqts[(size_t)i * (3 * C / 32)];
+  {
+    constexpr int N1 = (C + NT - 1) / NT;
+    float a1[N1], c1[N1];
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      const int r = min(tid + i * NT, C - 1);
+      a1[i] = G.wpts[(size_t)r * (C / 32)];
+      c1[i] = G.wqts[(size_t)r * (3 * C / 32)];
+    }
+#pragma unroll
+    for (int i = 0; i < N1; ++i)
+      if (tid + i * NT < C) {
+        Tos[tid + i * NT] = a1[i];
+        Tqs[tid + i * NT] = c1[i];
+      }
   }
   // chunk sc = 4 h + part: part 0 -> proj^T rows 32 h + r, the whole K = C ([ks][plane][32][32]); part 1..3 ->
   // k-chunk (part - 1) KS + h of every qkv^T row c < C ([plane][C][32])
