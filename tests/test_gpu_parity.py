@@ -515,11 +515,13 @@ def test_ln_row_scales_bitwise(tmp_path):
     assert np.array_equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_attn", 1), ("fuse_attn", 3)])
+@pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_attn", 1), ("fuse_attn", 3), ("attn_mfma", 1)])
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient) and fuse_attn (LN1 + qkv +
-    window attention + proj + residual: 1 the forward, 3 also its input gradient). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
+    window attention + proj + residual: 1 the forward, 3 also its input gradient); attn_mfma (the LG-stage window
+    attention forward and backward on the exact-f32 MFMA instead of the VALU kernels: fp32 products either way,
+    only the summation order differs). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
     per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
     max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
     from vaevar.engine import DAProblem

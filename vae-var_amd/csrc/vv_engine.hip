@@ -655,6 +655,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     at.heads = S.heads;
     at.scale = (float)std::pow((double)(C / S.heads), -0.5);
     at.ngroups = G;
+    at.mfma = (sc.tune ? *sc.tune : vv::kDefaultTuning).attn_mfma;
     for (int g = 0; g < G; ++g)
       at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, sc.t2 + g * MC,
                  sv.P[b] + (size_t)g * nwin * S.heads * 256, nullptr, nullptr};
@@ -759,6 +760,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     at.heads = S.heads;
     at.scale = (float)std::pow((double)(C / S.heads), -0.5);
     at.ngroups = G;
+    at.mfma = (sc.tune ? *sc.tune : vv::kDefaultTuning).attn_mfma;
     for (int g = 0; g < G; ++g)
       at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, nullptr, sv.P[b] + (size_t)g * nwin * S.heads * 256,
                  sc.t2 + g * MC, sc.dqkv + g * MC * 3};

@@ -1925,6 +1925,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "win_mfma") return &t.win_mfma;
   if (k == "fuse_mlp") return &t.fuse_mlp;
   if (k == "fuse_attn") return &t.fuse_attn;
+  if (k == "attn_mfma") return &t.attn_mfma;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;

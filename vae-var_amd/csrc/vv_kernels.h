@@ -31,6 +31,7 @@ struct Tuning {
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
   int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
+  int attn_mfma = 1;            // LG-stage window attention (hd 192) on the exact-f32 MFMA (0: the VALU kernels)
   int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
                                 // the forward, bit 1 the backward (measured neutral, profiles/r03/ab_fuse_attn)
 };
@@ -201,6 +202,7 @@ struct AttnArgs {
   int C, heads;
   float scale;
   int ngroups;
+  int mfma;           // 1: the exact-f32 MFMA kernels where attn_mf_ok (one head of 192 per workgroup)
   AttnGroup g[kMaxGroups];
 };
 

@@ -636,6 +636,184 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_bwd(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// LG-stage window attention on the exact-f32 MFMA (v_mfma_f32_16x16x4f32: fp32 products, fp32 accumulation, as
+// torch's fp32 matmul; swinblock.py:151-172 for one head of hd = HD, one workgroup per (window, head)). Same
+// inputs, outputs and saved P as k_attn_fwd / k_attn_bwd. The VALU kernels read every FMA operand from LDS
+// (~490 KB of LDS reads per (window, head) against 36 KB of rows): their score and P.V phases are LDS-bound and
+// serialised behind the loads. Here each operand element is read from LDS once per product.
+//   scores (and dP = dO v^T): 16 x 16, K = HD split over the 4 waves (HD / 4 dims each); lane group g of a wave
+//     takes a contiguous run of R = HD / 16 dims (the same dim permutation on both operands, so the product is
+//     the plain dot product), loaded as float4s straight from global memory into the fragment registers; the four
+//     wave partials are summed in wave order through LDS
+//   softmax / dS: one thread per (i, j), the row reductions over the 16 lanes of the row
+//   products with K = 16 keys (P v, dS k, dS^T q, P^T dO): lane group g takes keys 4g .. 4g + 3 (one per k-step);
+//     wave w the output columns [w HD / 4, (w + 1) HD / 4) as HD / 64 tiles of 16 x 16
+// Only the operands of the key-indexed products (v; q, k, dO) are staged in LDS, rows of HD + 4 floats (196: rows
+// 4 banks apart, so the b32 reads of rows 4g + s x 16 consecutive columns are conflict-free); P and dS rows of 20.
+// LDS 18 KB forward / 45 KB backward: all 768 workgroups of the LG stage resident at once.
+typedef float f4m __attribute__((ext_vector_type(4)));
+constexpr int kAmfP = 20;  // row stride of P / dS in LDS
+
+// this lane's fragment run of a [16][HD] row block at src (row stride ld): row li, the R = HD / 16 dims of lane
+// group g inside wave w's HD / 4 (straight from global memory: operands used only in the row-indexed pattern)
+template <int HD>
+__device__ __forceinline__ void amf_frag(const float* src, int ld, int w, int li, int g, f4 (&fr)[HD / 64]) {
+  const float* r = src + (size_t)li * ld + w * (HD / 4) + g * (HD / 16);
+#pragma unroll
+  for (int s4 = 0; s4 < HD / 64; ++s4) fr[s4] = *reinterpret_cast<const f4*>(r + 4 * s4);
+}
+
+// S = X . Y^T partial of wave w over its HD / 4 dims (fragments from amf_frag), stored as part[w][16][17]
+template <int HD>
+__device__ __forceinline__ void amf_partial(const f4 (&xa)[HD / 64], const f4 (&yb)[HD / 64], float* part, int w,
+                                            int li, int g) {
+  static_assert(HD % 64 == 0, "HD must be a multiple of 64");
+  f4m acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s4 = 0; s4 < HD / 64; ++s4)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s4][e], yb[s4][e], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[(w * 16 + 4 * g + r) * 17 + li] = acc[r];
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_fwd_mf(AttnArgs a) {
+  constexpr int ST = HD + 4, NT = HD / 64;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* v = sm;                     // [16][ST]: the only operand read in the key-indexed pattern
+  float* part = v + WN_ * ST;        // [4][16][17]
+  float* p = part + 4 * WN_ * 17;    // [16][20]
+  float* tb = p + WN_ * kAmfP;       // [49]
+  const int win = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, li = l & 15, g = l >> 4;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int C = a.C, ldq = 3 * C;
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * HD;
+  // every load issued before the first wait: q / k fragments to registers, the bias slice, v rows to LDS
+  f4 qf[NT], kf[NT];
+  amf_frag<HD>(base, ldq, w, li, g, qf);
+  amf_frag<HD>(base + C, ldq, w, li, g, kf);
+  const float tv = G.table[min(tid, 48) * a.heads + h];
+  {
+    const float* const srcs[1] = {base + 2 * C};
+    const int lds_[1] = {ldq};
+    float* const dsts[1] = {v};
+    attn_rows_all<1>(srcs, lds_, dsts, ST, HD);
+  }
+  if (tid < 49) tb[tid] = tv;
+  amf_partial<HD>(qf, kf, part, w, li, g);
+  __syncthreads();
+  {
+    // S = (q k^T) scale + bias + mask -> softmax (swinblock.py:151-168); thread = (row i, column j)
+    const int i = tid >> 4, j = tid & 15;
+    const float* pp = part + i * 17 + j;
+    float s = ((pp[0] + pp[WN_ * 17]) + (pp[2 * WN_ * 17] + pp[3 * WN_ * 17])) * a.scale +
+              attn_bias_mask(a, tb, win, 0, i, j);
+    float mx = s;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float e = expf(s - mx);
+    float sum = e;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o);
+    const float pv = e * (1.0f / sum);
+    p[i * kAmfP + j] = pv;
+    G.P[((size_t)win * a.heads + h) * WN_ * WN_ + tid] = pv;
+  }
+  __syncthreads();
+  // O = P v: A = P[i][4g + s], B = v[4g + s][n]
+  const f4 pa = *reinterpret_cast<const f4*>(p + li * kAmfP + 4 * g);
+  float* ob = G.o + (size_t)win * WN_ * C + h * HD;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n0 = w * (HD / 4) + 16 * nt;
+    f4m acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s], v[(4 * g + s) * ST + n0 + li], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ob[(size_t)(4 * g + r) * C + n0 + li] = acc[r];
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_bwd_mf(AttnArgs a) {
+  constexpr int ST = HD + 4, NT = HD / 64;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* q = sm;                     // q, k, dO: read in the key-indexed pattern (dK, dQ, dV)
+  float* k = q + WN_ * ST;
+  float* dO = k + WN_ * ST;
+  float* part = dO + WN_ * ST;       // [4][16][17]
+  float* p = part + 4 * WN_ * 17;    // [16][20]
+  float* ds = p + WN_ * kAmfP;       // [16][20]
+  const int win = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, li = l & 15, g = l >> 4;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int C = a.C, ldq = 3 * C;
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * HD;
+  const float* dOg = G.dO + (size_t)win * WN_ * C + h * HD;
+  // every load issued before the first wait: dO / v fragments (dP) to registers, P, the q / k / dO rows to LDS
+  f4 of[NT], vf[NT];
+  amf_frag<HD>(dOg, C, w, li, g, of);
+  amf_frag<HD>(base + 2 * C, ldq, w, li, g, vf);
+  const float pij = G.P[((size_t)win * a.heads + h) * WN_ * WN_ + tid];  // thread = (i, j) = (tid >> 4, tid & 15)
+  {
+    const float* const srcs[3] = {base, base + C, dOg};
+    const int lds_[3] = {ldq, ldq, C};
+    float* const dsts[3] = {q, k, dO};
+    attn_rows_all<3>(srcs, lds_, dsts, ST, HD);
+  }
+  const int i = tid >> 4, j = tid & 15;
+  p[i * kAmfP + j] = pij;
+  amf_partial<HD>(of, vf, part, w, li, g);  // dP = dO v^T
+  __syncthreads();
+  {
+    // dS = P (dP - rowsum(P dP))
+    const float* pp = part + i * 17 + j;
+    const float dp = (pp[0] + pp[WN_ * 17]) + (pp[2 * WN_ * 17] + pp[3 * WN_ * 17]);
+    float rd = pij * dp;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) rd += __shfl_xor(rd, o);
+    ds[i * kAmfP + j] = pij * (dp - rd);
+  }
+  __syncthreads();
+  // dQ = scale dS k ; dK = scale dS^T q ; dV = P^T dO  (k-step s: key 4g + s)
+  const f4 dsa = *reinterpret_cast<const f4*>(ds + li * kAmfP + 4 * g);
+  float dst[4], pt[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    dst[s] = ds[(4 * g + s) * kAmfP + li];
+    pt[s] = p[(4 * g + s) * kAmfP + li];
+  }
+  float* gb = G.dqkv + (size_t)win * WN_ * ldq + h * HD;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n0 = w * (HD / 4) + 16 * nt;
+    f4m aq = {0.f, 0.f, 0.f, 0.f}, ak = aq, av = aq;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int rr = (4 * g + s) * ST + n0 + li;
+      aq = __builtin_amdgcn_mfma_f32_16x16x4f32(dsa[s], k[rr], aq, 0, 0, 0);
+      ak = __builtin_amdgcn_mfma_f32_16x16x4f32(dst[s], q[rr], ak, 0, 0, 0);
+      av = __builtin_amdgcn_mfma_f32_16x16x4f32(pt[s], dO[rr], av, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float* row = gb + (size_t)(4 * g + r) * ldq + n0 + li;
+      row[0] = aq[r] * a.scale;
+      row[C] = ak[r] * a.scale;
+      row[2 * C] = av[r];
+    }
+  }
+}
+
+// the MFMA kernels serve one head of 192 per workgroup (the LG stage, 6 heads of 192) with 4x4 windows
+static bool attn_mf_ok(const AttnArgs& a) {
+  return a.mfma && a.ws == 4 && a.heads > 0 && a.C == 192 * a.heads;
+}
+
 // heads per block: the largest divisor of heads with hpb * hd <= 192
 static int attn_hpb(const AttnArgs& a) {
   const int hd = a.C / a.heads;
@@ -656,7 +834,11 @@ hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
   if (2 * kAttnThreads < hpb * 49) return hipErrorInvalidValue;  // the staged bias slice (ws = 4)
   const size_t lds = (3 * WN_ * st + hpb * WN_ * 17 + hpb * 49) * sizeof(float);
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
+  if (attn_mf_ok(a)) {
+    const size_t lds_mf = (WN_ * 196 + 4 * WN_ * 17 + WN_ * kAmfP + 49) * sizeof(float);
+    hipLaunchKernelGGL(k_attn_fwd_mf<192>, dim3(a.nwin, a.heads, a.ngroups), dim3(256), lds_mf, s, a);
+  } else
+    hipLaunchKernelGGL(k_attn_fwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
   prof_end(ph, s, PC_ATTN, 4.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
            4.0 * a.ngroups * ((double)a.nwin * WN_ * 4 * a.C + (double)a.nwin * a.heads * WN_ * WN_));
   return hipGetLastError();
@@ -666,7 +848,11 @@ hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
   const int hpb = attn_hpb(a), st = hpb * (a.C / a.heads) + 4;
   const size_t lds = (4 * WN_ * st + 2 * hpb * WN_ * 17) * sizeof(float);
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
+  if (attn_mf_ok(a)) {
+    const size_t lds_mf = (3 * WN_ * 196 + 4 * WN_ * 17 + 2 * WN_ * kAmfP) * sizeof(float);
+    hipLaunchKernelGGL(k_attn_bwd_mf<192>, dim3(a.nwin, a.heads, a.ngroups), dim3(256), lds_mf, s, a);
+  } else
+    hipLaunchKernelGGL(k_attn_bwd, dim3(a.nwin, a.heads / hpb, a.ngroups), dim3(kAttnThreads), lds, s, a);
   prof_end(ph, s, PC_ATTN, 8.0 * a.nwin * WN_ * WN_ * a.C * a.ngroups,
            4.0 * a.ngroups * ((double)a.nwin * WN_ * 7 * a.C + (double)a.nwin * a.heads * WN_ * WN_));
   return hipGetLastError();
