@@ -212,8 +212,9 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "win_mfma" (that kernel on the exact-f32 MFMA, 1),
    "fc_h3_mink" (smallest K of the forecast network's fp16x3 GEMMs, 192), "fuse_mlp" (the fused Swin-tower
    LN2 + fc1 + GELU + fc2 + residual sub-block and its backward at dim 96, 1), "fuse_attn" (the fused Swin-tower
-   LN1 + qkv + window attention + proj + residual sub-block at dim 96: bit 0 forward, bit 1 backward, 1), "attn_mfma" (the LG-stage window
-   attention, one head of 192 per workgroup, on the exact-f32 MFMA, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
+   LN1 + qkv + window attention + proj + residual sub-block at dim 96: bit 0 forward, bit 1 backward, 1), "attn_mfma" (the window attention of
+   the LG stage, head dim 192, and of the unfused tower stages, head dim 32, on the exact-f32 MFMA, 1), "gelu_planes" (the LG-stage GELU / gelu' GEMM
+   epilogues write the fp16x3 planes of the K = 4C GEMM after them, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
    the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1), "gattn" (the
    LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1), "gattn_qf" (its 16-query blocks per
    wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1), "h4_small" (tile 48 with whole-chip split-K

@@ -519,9 +519,9 @@ def test_ln_row_scales_bitwise(tmp_path):
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient) and fuse_attn (LN1 + qkv +
-    window attention + proj + residual: 1 the forward, 3 also its input gradient); attn_mfma (the LG-stage window
-    attention forward and backward on the exact-f32 MFMA instead of the VALU kernels: fp32 products either way,
-    only the summation order differs). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
+    window attention + proj + residual: 1 the forward, 3 also its input gradient); attn_mfma (the window attention of
+    the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and backward on the exact-f32 MFMA instead of
+    the VALU kernels: fp32 products either way, only the summation order differs). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
     per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
     max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
     from vaevar.engine import DAProblem
@@ -550,4 +550,41 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
     print(f"{knob} {on} vs 0: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert not torch.equal(o0, o1), "the fused kernel did not run"
+    assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
+
+
+def test_gelu_planes_vs_rowsplit(full_dec):
+    """gelu_planes: the LG-stage fc1 (GELU) and fc2-input-gradient (gelu') GEMM epilogues write the fp16x3 planes of
+    the K = 4608 GEMM that follows, with row scales from an a-priori bound (vv_kernels.h GemmArgs.opl), instead of
+    fp32 C + a k_rowsplit pass. The scale only moves the planes' exponent, so the products match the split pass up to
+    fp16 l parts that fall below the normal range (absolute error <= 2^-25 of the scaled row, far below fp32's
+    rounding of the row maximum); the network then spreads those last-bit differences like any other change of
+    rounding: the bounds of the other arithmetic variants (test_fused_tower_vs_unfused) hold -- decoder output and
+    input gradient 2e-6 of max, dJ/dz 1e-5, closure J 1e-7 (measured 1.0e-6 / 9.9e-7 / 5.9e-6 / 4.9e-8)."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field, uniform_sym
+
+    z = torch.from_numpy(0.5 * smooth_field(411, (1, 32, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(412, (1, 69, 128, 256), 1.0)).cuda()
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    zc = torch.from_numpy(0.3 * smooth_field(413, (1, 32, 128, 256))).cuda()
+    res = []
+    default = full_dec.ctx.get_tuning("gelu_planes")
+    try:
+        for v in (0, 1):
+            full_dec.ctx.set_tuning("gelu_planes", v)
+            out = full_dec.forward_raw(z).clone()
+            dz = torch.empty_like(z)
+            full_dec.backward_raw(cot, dz)
+            g = torch.empty_like(zc)
+            jb, jo = prob.closure(zc, g)
+            res.append((out, dz, jb, jo, g))
+    finally:
+        full_dec.ctx.set_tuning("gelu_planes", default)
+    (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
+    e_o, e_d, e_g = rel(o1.cpu(), o0.cpu()), rel(d1.cpu(), d0.cpu()), rel(g1.cpu(), g0.cpu())
+    e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
+    print(f"gelu_planes 1 vs 0: out rel {e_o:.2e} (bitwise {torch.equal(o0, o1)}) grad rel {e_d:.2e} "
+          f"closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7

@@ -204,6 +204,7 @@ struct Planner {  // two-pass: first count bytes, then hand out pointers
 struct BlockW {
   const float *n1g, *n1b, *table, *qkvW, *qkvWT, *qkvb, *projW, *projWT, *projb, *n2g, *n2b, *fc1W, *fc1WT, *fc1b,
       *fc2W, *fc2WT, *fc2b;
+  const float *fc1Wmax, *fc1bmax, *fc2Wmax;  // device scalars max |w| (the plane-writing GEMM epilogues' bounds)
 };
 
 struct Stage {
@@ -219,6 +220,7 @@ struct StageSave {
 struct Scratch {
   float *t1, *t2, *h, *dqkv;
   float* rs;  // fp16x3 row scales of a LayerNorm output / input gradient, consumed by the GEMM that follows
+  float* rs2;  // row scales of the planes a GELU / gelu' epilogue writes (into h) for the K = 4C GEMM after it
   float* ws;  // GEMM tail-split partials (vv::gemm_ws_floats())
   int math = vv::GEMM_SPLIT16;  // GEMM arithmetic (the context's vv_set_gemm_math)
   const vv::Tuning* tune = nullptr;  // the context's dispatch knobs (vv_set_tuning)
@@ -238,8 +240,10 @@ struct Model {
   std::vector<PInfo> params;
   std::vector<float*> pptr;  // device pointer per param
   std::unordered_map<std::string, const float*> W;   // name -> weights ; name + "^T" -> transposed
+  std::unordered_map<std::string, const float*> Wmax;  // name -> device scalar max |param| (filled at load)
   std::unique_ptr<Arena> warena, aarena;
   std::unique_ptr<Arena> parena;  // bf16 split planes of warena (3 x 2 B per float), GEMM_SPLIT B operands
+  std::unique_ptr<Arena> marena;  // one float per param: max |param| (Wmax)
   Stage enc0, enc1, dec1, dec0;
   std::vector<Stage> lg;
   std::vector<Save> saves;
@@ -445,6 +449,13 @@ int bind_weights(Model& m) {
     b.fc2W = w(pre + ".mlp.fc2.weight");
     b.fc2WT = w(pre + ".mlp.fc2.weight^T");
     b.fc2b = w(pre + ".mlp.fc2.bias");
+    auto wm = [&](const std::string& n) -> const float* {
+      auto it = m.Wmax.find(n);
+      return it == m.Wmax.end() ? nullptr : it->second;
+    };
+    b.fc1Wmax = wm(pre + ".mlp.fc1.weight");
+    b.fc1bmax = wm(pre + ".mlp.fc1.bias");
+    b.fc2Wmax = wm(pre + ".mlp.fc2.weight");
     return b;
   };
   for (int g = 0; g < c.G; ++g) {
@@ -495,6 +506,25 @@ GemmArgs gemm_base(int M, int N, int K, int G, int epi, const Scratch& sc) {
 
 // the LayerNorm feeding GEMM `a` writes the fp16x3 planes of its output (and no fp32 copy when `fp32_too` is false)
 // if the GEMM runs the split-operand kernel (tile 48); returns whether it does
+// the GELU / gelu' GEMM p writes the fp16x3 A planes (into its output buffer h, same bytes as the fp32 C) and the
+// row scales (rs2) of the K = 4C GEMM c that consumes that output, when both run on tile 48 (GemmArgs.opl: the
+// row scale from an a-priori bound, so no k_rowsplit pass over the 2048 x 4608 activation)
+bool gelu_feeds_planes(GemmArgs& p, GemmArgs& c, const float* wmax, const float* bmax, const Scratch& sc) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.gelu_planes || !wmax || p.ngroups != 1 || c.ngroups != 1 || !sc.apl || c.g[0].A != p.g[0].C) return false;
+  GemmArgs cc = c;
+  cc.apre = reinterpret_cast<const unsigned short*>(p.g[0].C);
+  cc.ascale = sc.rs2;
+  if (vv::gemm_tile_of(p) != 48 || vv::gemm_tile_of(cc) != 48) return false;
+  p.opl = reinterpret_cast<unsigned short*>(p.g[0].C);
+  p.ors = sc.rs2;
+  p.obw = wmax;
+  p.obb = bmax;
+  c.apre = cc.apre;
+  c.ascale = sc.rs2;
+  return true;
+}
+
 bool ln_feeds_planes(const GemmArgs& a, const Scratch& sc) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
   return sc.apl && T.ln_planes && T.ln_scales && vv::gemm_tile_of(a) == 48;
@@ -688,12 +718,13 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                   f1_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
     CK(layernorm_fwd(ln2, st));
     if (f1_pl) f1.apre = sc.apl;
-    CK(gemm_nt(f1, st, -1, sc.ws));
-    // fc2 + residual
+    // fc2 + residual (with tile 48, fc1's epilogue writes its A planes)
     GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc);
     for (int g = 0; g < G; ++g)
       f2.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc2W, S.w[b][g].fc2b, sv.x[b + 1] + g * MC, sv.x1[b] + g * MC,
                  nullptr};
+    gelu_feeds_planes(f1, f2, S.w[b][0].fc1Wmax, S.w[b][0].fc1bmax, sc);
+    CK(gemm_nt(f1, st, -1, sc.ws));
     CK(gemm_nt(f2, st, -1, sc.ws));
   }
   return 0;
@@ -730,10 +761,11 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       }
       for (int g = 0; g < G; ++g)
         f2.g[g] = {gx + g * MC, nullptr, S.w[b][g].fc2WT, nullptr, sc.h + g * MC * 4, nullptr, sv.h1[b] + g * MC * 4};
-      CK(gemm_nt(f2, st, -1, sc.ws));
       GemmArgs f1 = gemm_base(M, C, 4 * C, G, EPI_STORE, sc);
       for (int g = 0; g < G; ++g)
         f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
+      gelu_feeds_planes(f2, f1, S.w[b][0].fc2Wmax, nullptr, sc);  // max |fc2^T| = max |fc2|
+      CK(gemm_nt(f2, st, -1, sc.ws));
       CK(gemm_nt(f1, st, -1, sc.ws));
       LnArgs ln2 = ln_base(M, C, G, 1e-5f);
       for (int g = 0; g < G; ++g)
@@ -808,6 +840,12 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
   m->parena->cap = pbytes;
   vv::register_split_arena(reinterpret_cast<const float*>(m->warena->base), wbytes / 4,
                            reinterpret_cast<const unsigned short*>(m->parena->base));
+  m->marena = std::make_unique<Arena>();
+  if (hipMalloc(&m->marena->base, m->params.size() * sizeof(float)) != hipSuccess)
+    return fail(VV_E_ALLOC, "param maxima");
+  m->marena->cap = m->params.size() * sizeof(float);
+  for (size_t i = 0; i < m->params.size(); ++i)
+    m->Wmax[m->params[i].name] = reinterpret_cast<const float*>(m->marena->base) + i;
   size_t off = 0;
   for (auto& p : m->params) {
     float* d = reinterpret_cast<float*>(m->warena->base + off);
@@ -849,6 +887,7 @@ int create_model(vv_ctx* ctx, const vv_lgunet_config* rc, int B, int nslots, int
     for (auto* st : {&m->enc0, &m->enc1, &m->dec1, &m->dec0}) mrows = std::max(mrows, (size_t)st->G * st->M);
     for (auto& st : m->lg) mrows = std::max(mrows, (size_t)st.G * st.M);
     m->sc.rs = P.f(mrows);
+    m->sc.rs2 = P.f(mrows);
     m->sc.ws = P.f(vv::gemm_ws_floats());
     // tile-48 A planes: the largest A of a stage GEMM (fc2 forward / fc1 input gradient, K = 4C) as two fp16 planes
     m->sc.apl = reinterpret_cast<unsigned short*>(P.f(mx * 4));
@@ -1665,6 +1704,8 @@ int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
     if (it == m->W.end()) continue;
     VV_HIP(vv::transpose2d(m->W[p.name], const_cast<float*>(it->second), (int)p.shape[0], (int)p.shape[1], 0));
   }
+  for (size_t i = 0; i < m->params.size(); ++i)
+    VV_HIP(vv::absmax(m->pptr[i], numel(m->params[i].shape), const_cast<float*>(m->Wmax[m->params[i].name]), 0));
   // split planes (bf16 and fp16) of every GEMM weight and its transpose (GEMM_SPLIT / GEMM_SPLIT16 B operands)
   for (auto& p : m->params) {
     auto it = m->W.find(p.name + "^T");

@@ -69,13 +69,29 @@ static int device_cus() {
 // dummy address, G.A, when the pointer is null) and selected afterwards: a load under a branch leaves the
 // compiler unable to count outstanding memory operations, and it then waits for ALL of them (vmcnt(0)) --
 // the next tile's prefetched A in a persistent kernel, and in partial tiles every previous store.
-template <int BM, int BN, int WM, int WN, int EPI, int MF, bool FULL, typename ACC>
+// Plane-writing forms of GELU / DGELU (tile 48 only, GemmArgs.opl): the value v of each element is stored as the
+// fp16x3 planes of the next GEMM's A, h = fp16(v s), l = fp16(v s - h) (k_rowsplit's arithmetic), with the row
+// scale s = 2^e chosen from the bound U_r (GemmArgs.opl) so that 2 U_r s < 2^15: every tile of a row derives the
+// same s from the same inputs, so no row maximum crosses tiles. s only moves the planes' exponent, so the planes
+// equal k_rowsplit's (up to the power of two the consumer undoes) unless an l part falls below fp16's normal range.
+constexpr int EPI_GELU_PL = 4, EPI_DGELU_PL = 5;
+
+template <int BM, int BN, int WM, int WN, int EPI_, int MF, bool FULL, typename ACC>
 __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& G, ACC& acc, int m0, int n0, int wm,
                                          int wn, int rin, int hh) {
+  constexpr bool PL = EPI_ == EPI_GELU_PL || EPI_ == EPI_DGELU_PL;
+  constexpr int EPI = EPI_ == EPI_GELU_PL ? EPI_GELU : EPI_ == EPI_DGELU_PL ? EPI_DGELU : EPI_;
   constexpr int TM = BM / WM / MF;
   constexpr int TN = BN / WN / MF;
   constexpr int NR = MF == 32 ? 16 : 4;
   const int M = args.M, N = args.N;
+  float ubw = 0.f, ubb = 0.f;  // f K max|B|, f max|bias|
+  if constexpr (PL) {
+    const float tw = *args.obw, tb = *(args.obb ? args.obb : args.obw);
+    constexpr float f = EPI == EPI_GELU ? 1.0f : 1.25f;
+    ubw = f * (float)args.K * tw;
+    ubb = args.obb ? f * tb : 0.0f;
+  }
   float bv[TN];
   int colv[TN];
 #pragma unroll
@@ -94,6 +110,15 @@ __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& 
       const int rc = FULL ? row : min(row, M - 1);
       const int t = *(args.crow ? args.crow + rc : reinterpret_cast<const int*>(G.A));
       ov[r] = args.crow ? t : rc;
+    }
+    float so[NR];  // plane forms: the row scales (GEMM row = output row: no crow)
+    if constexpr (PL) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(args.escale[ov[r]]));  // max|A_r| < 2^15 ia
+        const unsigned mx = __float_as_uint(2.0f * (ubw * (32768.0f * ia) + ubb));
+        so[r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
+      }
     }
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
@@ -125,7 +150,17 @@ __device__ __forceinline__ void epilogue(const GemmArgs& args, const GemmGroup& 
         } else if constexpr (EPI == EPI_DGELU) {
           v = acc[a][b][r] * dgelu_f(ex[r]);
         }
-        G.C[(size_t)o * args.ldc + col] = v;
+        if constexpr (PL) {
+          const float x = v * so[r];
+          const _Float16 hv = (_Float16)x;
+          const _Float16 lv = (_Float16)(x - (float)hv);
+          unsigned short* pp = args.opl + (size_t)o * 2 * N + 2 * (col & ~31) + (col & 31);  // chunk-interleaved
+          pp[0] = __builtin_bit_cast(unsigned short, hv);
+          pp[32] = __builtin_bit_cast(unsigned short, lv);
+          if (colv[b] == 0) args.ors[o] = so[r];
+        } else {
+          G.C[(size_t)o * args.ldc + col] = v;
+        }
       }
     }
   }
@@ -1866,11 +1901,17 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s) {
   const int T = ((a.N + 127) / 128) * ((a.M + 255) / 256);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
   dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  GemmArgs b = a;
+  b.escale = sc;  // the plane-writing epilogues bound |C| from the row scales the products used
   switch (a.epi) {
-    case EPI_STORE: return launch_h4_k<EPI_STORE>(a, s, grid, lds, tail, sc, planes);
-    case EPI_GELU: return launch_h4_k<EPI_GELU>(a, s, grid, lds, tail, sc, planes);
-    case EPI_RESID: return launch_h4_k<EPI_RESID>(a, s, grid, lds, tail, sc, planes);
-    case EPI_DGELU: return launch_h4_k<EPI_DGELU>(a, s, grid, lds, tail, sc, planes);
+    case EPI_STORE: return launch_h4_k<EPI_STORE>(b, s, grid, lds, tail, sc, planes);
+    case EPI_GELU:
+      return a.opl ? launch_h4_k<EPI_GELU_PL>(b, s, grid, lds, tail, sc, planes)
+                   : launch_h4_k<EPI_GELU>(b, s, grid, lds, tail, sc, planes);
+    case EPI_RESID: return launch_h4_k<EPI_RESID>(b, s, grid, lds, tail, sc, planes);
+    case EPI_DGELU:
+      return a.opl ? launch_h4_k<EPI_DGELU_PL>(b, s, grid, lds, tail, sc, planes)
+                   : launch_h4_k<EPI_DGELU>(b, s, grid, lds, tail, sc, planes);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1926,6 +1967,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "fuse_mlp") return &t.fuse_mlp;
   if (k == "fuse_attn") return &t.fuse_attn;
   if (k == "attn_mfma") return &t.attn_mfma;
+  if (k == "gelu_planes") return &t.gelu_planes;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;
@@ -2056,6 +2098,24 @@ hipError_t split_registered(const float* W, size_t n, int K, hipStream_t s) {
 }
 size_t gemm_ws_floats() { return kWsFloats + kScaleFloats; }
 
+__global__ __launch_bounds__(1024) void k_absmax(const float* __restrict__ x, size_t n, float* __restrict__ out) {
+  __shared__ unsigned red[16];
+  unsigned mx = 0;
+  for (size_t i = threadIdx.x; i < n; i += 1024) mx = max(mx, __float_as_uint(fabsf(x[i])));
+  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; ++i) mx = max(mx, red[i]);
+    out[0] = __uint_as_float(mx);
+  }
+}
+hipError_t absmax(const float* x, size_t n, float* out, hipStream_t s) {
+  if (!x || !out || !n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_absmax, dim3(1), dim3(1024), 0, s, x, n, out);
+  return hipGetLastError();
+}
+
 // tile choice (measured on MI355X, tools/gemm_bench.py, tools/gemm_split_check.py)
 static int pick_tile(const GemmArgs& a) {
   const Tuning& T = a.tune ? *a.tune : kDefaultTuning;
@@ -2147,6 +2207,10 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   if (t < 0) return hipErrorInvalidValue;
   // producer planes are only read by tile 48; every other kernel reads A itself (which the producer then wrote)
   if (a.apre && t != 48) return hipErrorInvalidValue;
+  // plane-writing epilogues: tile 48, GELU / DGELU, one group, output rows in GEMM order, N in whole k-tiles
+  if (a.opl && (t != 48 || (a.epi != EPI_GELU && a.epi != EPI_DGELU) || a.ngroups != 1 || a.crow || a.N % 32 ||
+                !a.ors || !a.obw))
+    return hipErrorInvalidValue;
   for (int g = 0; g < a.ngroups; ++g) {
     a.g[g].Bp = (t >= 21 && (!a.ldb || a.ldb == a.K)) ? split_planes_of(a.g[g].B) : nullptr;
     // activations are never registered by the engine; a registered A (tests, vv_gemm) must be a matrix's start

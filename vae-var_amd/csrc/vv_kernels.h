@@ -32,6 +32,8 @@ struct Tuning {
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
   int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
   int attn_mfma = 1;            // LG-stage window attention (hd 192) on the exact-f32 MFMA (0: the VALU kernels)
+  int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
+                                // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
   int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
                                 // the forward, bit 1 the backward (measured neutral, profiles/r03/ab_fuse_attn)
 };
@@ -94,6 +96,16 @@ struct GemmArgs {
   // null, or A's planes as its producer wrote them (LayerNorm pl, same layout, indexed by the physical A row like
   // ascale, which must be set); tile 48 then reads them directly (no k_rowsplit pass)
   const unsigned short* apre;
+  // tile 48, EPI_GELU / EPI_DGELU only (ngroups 1, no crow): write the result as fp16x3 A planes of the next tile-48
+  // GEMM (opl, k_rowsplit's layout, N halfs x 2 per row) and their row scales (ors) instead of fp32 C. The row scale
+  // comes from an a-priori bound on |C| (no pass over the output, no cross-tile row maximum):
+  //   |C[r][n]| <= f (K max|A_r| max|B| + max|bias|),  f = 1 (GELU: |gelu(x)| <= |x|), 1.25 (DGELU: |gelu'| < 1.13)
+  // with max|A_r| < 2^15 2^-e_r from A's own row scale and max|B|, max|bias| device scalars (obw, obb or null).
+  unsigned short* opl;
+  float* ors;
+  const float* obw;
+  const float* obb;
+  const float* escale;  // set by the tile-48 launch: A's row scales in GEMM row order (what the kernel used)
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   int h3_mink;         // > 0: this GEMM's own smallest K for the fp16x3 kernels (the forecast: Tuning.fc_h3_mink)
   GemmGroup g[kMaxGroups];
@@ -141,6 +153,8 @@ void register_split_arena(const float* base, size_t n, const unsigned short* pla
 void unregister_split_arena(const float* base);
 // fill the planes of the rows of W[n/K][K], which lies inside a registered arena (W - base and K multiples of 32)
 hipError_t split_registered(const float* W, size_t n, int K, hipStream_t s);
+// out[0] = max |x[i]| over n floats (one workgroup; load-time bounds of the plane-writing GEMM epilogues)
+hipError_t absmax(const float* x, size_t n, float* out, hipStream_t s);
 // dst[n/K][3][K] = exact bf16 split of the rows of src[n/K][K] (h = bf16(x), m = bf16(x-h), l = bf16(x-h-m))
 hipError_t split_planes(const float* src, unsigned short* dst, size_t n, int K, hipStream_t s);
 

@@ -809,6 +809,157 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mf(AttnArgs a) {
   }
 }
 
+// Swin-tower window attention (head dim 32: the dim-96 / dim-192 stages, 3 / 6 heads) on the exact-f32 MFMA, one
+// wave per (window, head), four per workgroup, no LDS in the forward. The scores are computed transposed,
+// S^T = k q^T (keys on the accumulator rows), so each lane (query li, lane group g) holds P[li][4g + r] in register r:
+// exactly the A operand of O = P v for k-step r (key 4g + r). Softmax over a query's 16 keys: 4 registers, then
+// lanes li, li + 16, li + 32, li + 48. Row operands (q, k for S^T; v, dO for dP^T) are loaded as float4 fragments
+// straight from global memory (lane group g: dims 8g .. 8g + 7); key-indexed operands (v, k, q, dO) as one float
+// per lane (16 consecutive columns of row 4g + s). The backward transposes dS through 1 KB of LDS per wave.
+__device__ __forceinline__ void awin_frag(const float* src, int ld, int li, int g, f4& a, f4& b) {
+  const float* r = src + (size_t)li * ld + 8 * g;
+  a = *reinterpret_cast<const f4*>(r);
+  b = *reinterpret_cast<const f4*>(r + 4);
+}
+__device__ __forceinline__ f4m awin_st(const f4& xa, const f4& xb, const f4& ya, const f4& yb) {
+  f4m acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], ya[e], acc, 0, 0, 0);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[e], yb[e], acc, 0, 0, 0);
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_attn_fwd_w32(AttnArgs a) {
+  constexpr int HD = 32;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, g = l >> 4;
+  const int item = blockIdx.x * 4 + w, win = item / a.heads, h = item - win * a.heads;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int C = a.C, ldq = 3 * C;
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * HD;
+  f4 qa, qb, ka, kb;
+  awin_frag(base, ldq, li, g, qa, qb);
+  awin_frag(base + C, ldq, li, g, ka, kb);
+  float vv[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) vv[nt][s] = base[2 * C + (size_t)(4 * g + s) * ldq + 16 * nt + li];
+  // bias table entries of (query li, key 4g + r): loaded with the rows
+  const int ri = li >> 2, ci = li & 3;
+  float bias[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = 4 * g + r, rj = j >> 2, cj = j & 3;
+    bias[r] = G.table[((ri - rj + 3) * 7 + (ci - cj + 3)) * a.heads + h];
+  }
+  const f4m st = awin_st(ka, kb, qa, qb);  // S^T: row = key 4g + r, column = query li
+  float sv[4], mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float b = bias[r];
+    if (a.shift > 0) {  // quirk Q1 (swinblock.py:240-258), as attn_bias_mask
+      const int wr = (win % (a.nWh * a.nWw)) / a.nWw, j = 4 * g + r;
+      const int yi = wr * 4 + ri, yj = wr * 4 + (j >> 2), H = a.H;
+      const int lbi = yi < H - 4 ? 0 : (yi < H - a.shift ? 1 : 2);
+      const int lbj = yj < H - 4 ? 0 : (yj < H - a.shift ? 1 : 2);
+      if (lbi != lbj) b += -100.0f;
+    }
+    sv[r] = st[r] * a.scale + b;
+    mx = fmaxf(mx, sv[r]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    sv[r] = expf(sv[r] - mx);
+    sum += sv[r];
+  }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.0f / sum;
+  f4 pv;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) pv[r] = sv[r] * inv;
+  *reinterpret_cast<f4*>(G.P + ((size_t)win * a.heads + h) * WN_ * WN_ + li * WN_ + 4 * g) = pv;
+  float* ob = G.o + (size_t)win * WN_ * C + h * HD;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    f4m acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pv[s], vv[nt][s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ob[(size_t)(4 * g + r) * C + 16 * nt + li] = acc[r];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_attn_bwd_w32(AttnArgs a) {
+  constexpr int HD = 32;
+  __shared__ float dsm[4][WN_ * 17];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, g = l >> 4;
+  const int item = blockIdx.x * 4 + w, win = item / a.heads, h = item - win * a.heads;
+  const AttnGroup G = a.g[blockIdx.z];
+  const int C = a.C, ldq = 3 * C;
+  const float* base = G.qkv + (size_t)win * WN_ * ldq + h * HD;
+  const float* dOg = G.dO + (size_t)win * WN_ * C + h * HD;
+  const float* Pg = G.P + ((size_t)win * a.heads + h) * WN_ * WN_;
+  f4 va, vb, oa, ob;
+  awin_frag(base + 2 * C, ldq, li, g, va, vb);
+  awin_frag(dOg, C, li, g, oa, ob);
+  const f4 pr = *reinterpret_cast<const f4*>(Pg + li * WN_ + 4 * g);  // P[li][4g + r]
+  float pt[4], kc[2][4], qc[2][4], oc[2][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    pt[s] = Pg[(4 * g + s) * WN_ + li];  // P[4g + s][li]
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const size_t rr = (size_t)(4 * g + s) * ldq + 16 * nt + li;
+      qc[nt][s] = base[rr];
+      kc[nt][s] = base[C + rr];
+      oc[nt][s] = dOg[(size_t)(4 * g + s) * C + 16 * nt + li];
+    }
+  }
+  const f4m dpt = awin_st(va, vb, oa, ob);  // dP^T: row = key 4g + r, column = query li
+  float rd = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rd += pr[r] * dpt[r];
+  rd += __shfl_xor(rd, 16);
+  rd += __shfl_xor(rd, 32);
+  f4 ds;  // dS[li][4g + r]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ds[r] = pr[r] * (dpt[r] - rd);
+    dsm[w][li * 17 + 4 * g + r] = ds[r];
+  }
+  __syncthreads();
+  float dt[4];  // dS[4g + s][li]
+#pragma unroll
+  for (int s = 0; s < 4; ++s) dt[s] = dsm[w][(4 * g + s) * 17 + li];
+  float* gb = G.dqkv + (size_t)win * WN_ * ldq + h * HD;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    f4m aq = {0.f, 0.f, 0.f, 0.f}, ak = aq, av = aq;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      aq = __builtin_amdgcn_mfma_f32_16x16x4f32(ds[s], kc[nt][s], aq, 0, 0, 0);
+      ak = __builtin_amdgcn_mfma_f32_16x16x4f32(dt[s], qc[nt][s], ak, 0, 0, 0);
+      av = __builtin_amdgcn_mfma_f32_16x16x4f32(pt[s], oc[nt][s], av, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float* row = gb + (size_t)(4 * g + r) * ldq + 16 * nt + li;
+      row[0] = aq[r] * a.scale;
+      row[C] = ak[r] * a.scale;
+      row[2 * C] = av[r];
+    }
+  }
+}
+
+static bool attn_w32_ok(const AttnArgs& a) {
+  return a.mfma && a.ws == 4 && a.heads > 0 && a.C == 32 * a.heads && (a.nwin * a.heads) % 4 == 0;
+}
+
 // the MFMA kernels serve one head of 192 per workgroup (the LG stage, 6 heads of 192) with 4x4 windows
 static bool attn_mf_ok(const AttnArgs& a) {
   return a.mfma && a.ws == 4 && a.heads > 0 && a.C == 192 * a.heads;
@@ -834,7 +985,9 @@ hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
   if (2 * kAttnThreads < hpb * 49) return hipErrorInvalidValue;  // the staged bias slice (ws = 4)
   const size_t lds = (3 * WN_ * st + hpb * WN_ * 17 + hpb * 49) * sizeof(float);
   const int ph = prof_begin(s);
-  if (attn_mf_ok(a)) {
+  if (attn_w32_ok(a)) {
+    hipLaunchKernelGGL(k_attn_fwd_w32, dim3(a.nwin * a.heads / 4, 1, a.ngroups), dim3(256), 0, s, a);
+  } else if (attn_mf_ok(a)) {
     const size_t lds_mf = (WN_ * 196 + 4 * WN_ * 17 + WN_ * kAmfP + 49) * sizeof(float);
     hipLaunchKernelGGL(k_attn_fwd_mf<192>, dim3(a.nwin, a.heads, a.ngroups), dim3(256), lds_mf, s, a);
   } else
@@ -848,7 +1001,9 @@ hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
   const int hpb = attn_hpb(a), st = hpb * (a.C / a.heads) + 4;
   const size_t lds = (4 * WN_ * st + 2 * hpb * WN_ * 17) * sizeof(float);
   const int ph = prof_begin(s);
-  if (attn_mf_ok(a)) {
+  if (attn_w32_ok(a)) {
+    hipLaunchKernelGGL(k_attn_bwd_w32, dim3(a.nwin * a.heads / 4, 1, a.ngroups), dim3(256), 0, s, a);
+  } else if (attn_mf_ok(a)) {
     const size_t lds_mf = (3 * WN_ * 196 + 4 * WN_ * 17 + 2 * WN_ * kAmfP) * sizeof(float);
     hipLaunchKernelGGL(k_attn_bwd_mf<192>, dim3(a.nwin, a.heads, a.ngroups), dim3(256), lds_mf, s, a);
   } else
