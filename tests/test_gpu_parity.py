@@ -553,14 +553,17 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
 
 
-def test_gelu_planes_vs_rowsplit(full_dec):
+@pytest.mark.parametrize("knob,extra", [("gelu_planes", {}), ("attn_planes", {"h4_small": 1})])
+def test_gelu_planes_vs_rowsplit(full_dec, knob, extra):
     """gelu_planes: the LG-stage fc1 (GELU) and fc2-input-gradient (gelu') GEMM epilogues write the fp16x3 planes of
     the K = 4608 GEMM that follows, with row scales from an a-priori bound (vv_kernels.h GemmArgs.opl), instead of
     fp32 C + a k_rowsplit pass. The scale only moves the planes' exponent, so the products match the split pass up to
     fp16 l parts that fall below the normal range (absolute error <= 2^-25 of the scaled row, far below fp32's
     rounding of the row maximum); the network then spreads those last-bit differences like any other change of
     rounding: the bounds of the other arithmetic variants (test_fused_tower_vs_unfused) hold -- decoder output and
-    input gradient 2e-6 of max, dJ/dz 1e-5, closure J 1e-7 (measured 1.0e-6 / 9.9e-7 / 5.9e-6 / 4.9e-8)."""
+    input gradient 2e-6 of max, dJ/dz 1e-5, closure J 1e-7 (measured 1.0e-6 / 9.9e-7 / 5.9e-6 / 4.9e-8).
+    attn_planes: the same for the LG-stage attention forward writing the planes of the proj GEMM (tile 48 with
+    h4_small), the row scale bounded through |o| <= max |v| over the window."""
     from vaevar.engine import DAProblem
     from vaevar.problem import make_problem
     from vaevar.synth import smooth_field, uniform_sym
@@ -570,10 +573,13 @@ def test_gelu_planes_vs_rowsplit(full_dec):
     prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
     zc = torch.from_numpy(0.3 * smooth_field(413, (1, 32, 128, 256))).cuda()
     res = []
-    default = full_dec.ctx.get_tuning("gelu_planes")
+    keys = [knob] + list(extra)
+    defaults = {k: full_dec.ctx.get_tuning(k) for k in keys}
     try:
+        for k, v in extra.items():
+            full_dec.ctx.set_tuning(k, v)
         for v in (0, 1):
-            full_dec.ctx.set_tuning("gelu_planes", v)
+            full_dec.ctx.set_tuning(knob, v)
             out = full_dec.forward_raw(z).clone()
             dz = torch.empty_like(z)
             full_dec.backward_raw(cot, dz)
@@ -581,10 +587,11 @@ def test_gelu_planes_vs_rowsplit(full_dec):
             jb, jo = prob.closure(zc, g)
             res.append((out, dz, jb, jo, g))
     finally:
-        full_dec.ctx.set_tuning("gelu_planes", default)
+        for k, v in defaults.items():
+            full_dec.ctx.set_tuning(k, v)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     e_o, e_d, e_g = rel(o1.cpu(), o0.cpu()), rel(d1.cpu(), d0.cpu()), rel(g1.cpu(), g0.cpu())
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
-    print(f"gelu_planes 1 vs 0: out rel {e_o:.2e} (bitwise {torch.equal(o0, o1)}) grad rel {e_d:.2e} "
+    print(f"{knob} 1 vs 0 {extra}: out rel {e_o:.2e} (bitwise {torch.equal(o0, o1)}) grad rel {e_d:.2e} "
           f"closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7

@@ -204,7 +204,7 @@ struct Planner {  // two-pass: first count bytes, then hand out pointers
 struct BlockW {
   const float *n1g, *n1b, *table, *qkvW, *qkvWT, *qkvb, *projW, *projWT, *projb, *n2g, *n2b, *fc1W, *fc1WT, *fc1b,
       *fc2W, *fc2WT, *fc2b;
-  const float *fc1Wmax, *fc1bmax, *fc2Wmax;  // device scalars max |w| (the plane-writing GEMM epilogues' bounds)
+  const float *fc1Wmax, *fc1bmax, *fc2Wmax, *qkvWmax, *qkvbmax;  // device scalars max |w| (the plane-writing GEMM epilogues' bounds)
 };
 
 struct Stage {
@@ -456,6 +456,8 @@ int bind_weights(Model& m) {
     b.fc1Wmax = wm(pre + ".mlp.fc1.weight");
     b.fc1bmax = wm(pre + ".mlp.fc1.bias");
     b.fc2Wmax = wm(pre + ".mlp.fc2.weight");
+    b.qkvWmax = wm(pre + ".attn.qkv.weight");
+    b.qkvbmax = wm(pre + ".attn.qkv.bias");
     return b;
   };
   for (int g = 0; g < c.G; ++g) {
@@ -522,6 +524,28 @@ bool gelu_feeds_planes(GemmArgs& p, GemmArgs& c, const float* wmax, const float*
   p.obb = bmax;
   c.apre = cc.apre;
   c.ascale = sc.rs2;
+  return true;
+}
+
+// the LG-stage attention forward writes the proj GEMM's fp16x3 A planes (into o's buffer) and row scales (rs2)
+// when that GEMM runs on tile 48 (AttnArgs.opl); q: the qkv GEMM whose output the attention reads (its A row scales
+// bound |v|)
+bool attn_feeds_planes(AttnArgs& at, GemmArgs& p, const GemmArgs& q, const BlockW& w, const Scratch& sc) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.attn_planes || !at.mfma || !w.qkvWmax || at.ngroups != 1 || at.ws != 4 || at.C != 192 * at.heads ||
+      !q.ascale || !sc.apl || p.ngroups != 1 || p.g[0].A != at.g[0].o)
+    return false;
+  GemmArgs pp = p;
+  pp.apre = reinterpret_cast<const unsigned short*>(at.g[0].o);
+  pp.ascale = sc.rs2;
+  if (vv::gemm_tile_of(pp) != 48) return false;
+  at.opl = reinterpret_cast<unsigned short*>(at.g[0].o);
+  at.ors = sc.rs2;
+  at.vrs = q.ascale;
+  at.vbw = w.qkvWmax;
+  at.vbb = w.qkvbmax;
+  p.apre = pp.apre;
+  p.ascale = sc.rs2;
   return true;
 }
 
@@ -689,13 +713,14 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     for (int g = 0; g < G; ++g)
       at.g[g] = {sv.qkv[b] + g * MC * 3, S.w[b][g].table, sc.t2 + g * MC,
                  sv.P[b] + (size_t)g * nwin * S.heads * 256, nullptr, nullptr};
-    CK(attn_fwd(at, st));
     // proj + window reverse + residual
     GemmArgs p = gemm_base(M, C, C, G, EPI_RESID, sc);
     p.crow = idx;
     for (int g = 0; g < G; ++g)
       p.g[g] = {sc.t2 + g * MC, nullptr, S.w[b][g].projW, S.w[b][g].projb, sv.x1[b] + g * MC, sv.x[b] + g * MC,
                 nullptr};
+    attn_feeds_planes(at, p, q, S.w[b][0], sc);
+    CK(attn_fwd(at, st));
     CK(gemm_nt(p, st, -1, sc.ws));
     }
     vv::MlpArgs ma;
@@ -1704,8 +1729,17 @@ int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
     if (it == m->W.end()) continue;
     VV_HIP(vv::transpose2d(m->W[p.name], const_cast<float*>(it->second), (int)p.shape[0], (int)p.shape[1], 0));
   }
-  for (size_t i = 0; i < m->params.size(); ++i)
-    VV_HIP(vv::absmax(m->pptr[i], numel(m->params[i].shape), const_cast<float*>(m->Wmax[m->params[i].name]), 0));
+  // max |param| of the tensors whose maxima bound a plane-writing GEMM epilogue (BlockW.fc1Wmax, ...)
+  auto ends = [](const std::string& n, const char* suf) {
+    const size_t l = strlen(suf);
+    return n.size() >= l && n.compare(n.size() - l, l, suf) == 0;
+  };
+  for (size_t i = 0; i < m->params.size(); ++i) {
+    const std::string& nm = m->params[i].name;
+    if (ends(nm, ".mlp.fc1.weight") || ends(nm, ".mlp.fc1.bias") || ends(nm, ".mlp.fc2.weight") ||
+        ends(nm, ".attn.qkv.weight") || ends(nm, ".attn.qkv.bias"))
+      VV_HIP(vv::absmax(m->pptr[i], numel(m->params[i].shape), const_cast<float*>(m->Wmax[nm]), 0));
+  }
   // split planes (bf16 and fp16) of every GEMM weight and its transpose (GEMM_SPLIT / GEMM_SPLIT16 B operands)
   for (auto& p : m->params) {
     auto it = m->W.find(p.name + "^T");

@@ -1968,6 +1968,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "fuse_attn") return &t.fuse_attn;
   if (k == "attn_mfma") return &t.attn_mfma;
   if (k == "gelu_planes") return &t.gelu_planes;
+  if (k == "attn_planes") return &t.attn_planes;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;

@@ -23,8 +23,10 @@ struct Tuning {
   int ln_scales = 1;            // fp16x3 row scales from the LayerNorm producer (0: k_rowscale everywhere)
   int h4 = 1;                   // the split-operand LDS-DMA fp16x3 kernel (tile 48) where the 256x128 tiles run
   int ln_planes = 1;            // LayerNorm writes the fp16x3 planes of the tile-48 GEMM it feeds (no split pass)
-  int h4_small = 0;             // tile 48 + whole-chip split-K also for 64..143 256-row tiles (1152 x 1152 at 2048 rows;
-                                // same-box config 2: 77.5 / 77.4 off vs 77.4 / 76.3 on, profiles/r03/ab_h4small)
+  int h4_small = 1;             // tile 48 + whole-chip split-K also for 64..143 256-row tiles (1152 x 1152 at 2048 rows):
+                                // neutral while the proj GEMM needed its own split pass (77.5 / 77.4 off vs 77.4 / 76.3 on,
+                                // profiles/r03/ab_h4small); with the attention writing its planes (attn_planes) 86.9 / 86.6
+                                // on vs 81.0 / 81.8 off, same box (profiles/r03/ab_attn_planes)
   int h4_split_minkt = 12;      // k-tiles per chunk at least, for that split of tile 48
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
@@ -32,6 +34,7 @@ struct Tuning {
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
   int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
   int attn_mfma = 1;            // LG-stage window attention (hd 192) on the exact-f32 MFMA (0: the VALU kernels)
+  int attn_planes = 1;          // the LG-stage attention forward writes the fp16x3 planes of a tile-48 proj GEMM
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
                                 // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
   int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
@@ -217,6 +220,16 @@ struct AttnArgs {
   float scale;
   int ngroups;
   int mfma;           // 1: the exact-f32 MFMA kernels where attn_mf_ok (one head of 192 per workgroup)
+  // forward, one head of 192 per workgroup, group 0 only: null, or write the output as the fp16x3 A planes of the
+  // tile-48 proj GEMM (opl: [row][2C], k_rowsplit's layout) with row scales ors instead of fp32 o. The scale of a
+  // window's rows comes from a bound: |o| <= max |v| over the window (P is a convex combination), and
+  // |v_j| <= C max|A_j| max|W_qkv| + max|b_qkv| with max|A_j| < 2^15 / vrs[j] (the qkv GEMM's A row scales, window
+  // order) and vbw / vbb device scalars (vbb may be null).
+  unsigned short* opl;
+  float* ors;
+  const float* vrs;
+  const float* vbw;
+  const float* vbb;
   AttnGroup g[kMaxGroups];
 };
 

@@ -703,6 +703,18 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mf(AttnArgs a) {
     attn_rows_all<1>(srcs, lds_, dsts, ST, HD);
   }
   if (tid < 49) tb[tid] = tv;
+  // plane output: one row scale for the window from the bound on |v| (loaded with the rows)
+  float so = 0.f;
+  if (a.opl) {
+    const float vr = a.vrs[(size_t)win * WN_ + li];  // 2^e_j: max|A_j| < 2^15 / vr
+    const float tw = *a.vbw, tbb = *(a.vbb ? a.vbb : a.vbw);
+    float ia = __uint_as_float((254u << 23) - __float_as_uint(vr));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) ia = fmaxf(ia, __shfl_xor(ia, o));
+    const unsigned mx = __float_as_uint(2.0f * ((float)C * tw * (32768.0f * ia) + (a.vbb ? tbb : 0.0f)));
+    so = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
+    if (h == 0 && tid < WN_) a.ors[(size_t)win * WN_ + tid] = so;
+  }
   amf_partial<HD>(qf, kf, part, w, li, g);
   __syncthreads();
   {
@@ -733,8 +745,21 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mf(AttnArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s], v[(4 * g + s) * ST + n0 + li], acc, 0, 0, 0);
+    if (a.opl) {
+      const int c = h * HD + n0 + li;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ob[(size_t)(4 * g + r) * C + n0 + li] = acc[r];
+      for (int r = 0; r < 4; ++r) {
+        const float x = acc[r] * so;
+        const _Float16 hv = (_Float16)x;
+        const _Float16 lv = (_Float16)(x - (float)hv);
+        unsigned short* pp = a.opl + ((size_t)win * WN_ + 4 * g + r) * 2 * C + 2 * (c & ~31) + (c & 31);
+        pp[0] = __builtin_bit_cast(unsigned short, hv);
+        pp[32] = __builtin_bit_cast(unsigned short, lv);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ob[(size_t)(4 * g + r) * C + n0 + li] = acc[r];
+    }
   }
 }
 
@@ -981,6 +1006,8 @@ static bool attn_ok(const AttnArgs& a) {
 
 hipError_t attn_fwd(const AttnArgs& a, hipStream_t s) {
   if (!attn_ok(a)) return hipErrorInvalidValue;
+  if (a.opl && (!attn_mf_ok(a) || attn_w32_ok(a) || a.ngroups != 1 || !a.ors || !a.vrs || !a.vbw))
+    return hipErrorInvalidValue;
   const int hpb = attn_hpb(a), st = hpb * (a.C / a.heads) + 4;
   if (2 * kAttnThreads < hpb * 49) return hipErrorInvalidValue;  // the staged bias slice (ws = 4)
   const size_t lds = (3 * WN_ * st + hpb * WN_ * 17 + hpb * 49) * sizeof(float);
