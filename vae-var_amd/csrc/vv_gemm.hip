@@ -2099,21 +2099,21 @@ hipError_t split_registered(const float* W, size_t n, int K, hipStream_t s) {
 }
 size_t gemm_ws_floats() { return kWsFloats + kScaleFloats; }
 
-__global__ __launch_bounds__(1024) void k_absmax(const float* __restrict__ x, size_t n, float* __restrict__ out) {
-  __shared__ unsigned red[16];
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, size_t n, unsigned* __restrict__ out) {
+  __shared__ unsigned red[4];
   unsigned mx = 0;
-  for (size_t i = threadIdx.x; i < n; i += 1024) mx = max(mx, __float_as_uint(fabsf(x[i])));
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    mx = max(mx, __float_as_uint(fabsf(x[i])));
   for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < 16; ++i) mx = max(mx, red[i]);
-    out[0] = __uint_as_float(mx);
-  }
+  if (threadIdx.x == 0) atomicMax(out, max(max(red[0], red[1]), max(red[2], red[3])));  // |x| bits order as floats
 }
 hipError_t absmax(const float* x, size_t n, float* out, hipStream_t s) {
   if (!x || !out || !n) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_absmax, dim3(1), dim3(1024), 0, s, x, n, out);
+  if (hipError_t e = hipMemsetAsync(out, 0, sizeof(float), s)) return e;
+  const unsigned g = (unsigned)std::min<size_t>(512, (n + 4095) / 4096);
+  hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, s, x, n, reinterpret_cast<unsigned*>(out));
   return hipGetLastError();
 }
 
