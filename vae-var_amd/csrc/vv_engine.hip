@@ -586,7 +586,10 @@ bool sync_check() { return g_sync_check.load(std::memory_order_relaxed) != 0; }
 // false where it does not apply (fp16x3 math only, dim 96, weights with fp16 planes): the unfused launches run
 bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, bool fwd, float* gx, vv::MlpArgs& ma) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  if (!T.fuse_mlp || sc.math != vv::GEMM_SPLIT16 || !vv::mlp_supported(S.C, S.M)) return false;
+  // fuse_mlp: bit 0 the dim-96 stages, bit 1 the dim-192 stages
+  if (!(T.fuse_mlp & (S.C == 96 ? 1 : S.C == 192 ? 2 : 0)) || sc.math != vv::GEMM_SPLIT16 ||
+      !vv::mlp_supported(S.C, S.M))
+    return false;
   memset(&ma, 0, sizeof(ma));
   const int M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;

@@ -32,7 +32,7 @@ struct Tuning {
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
   int win_mfma = 1;             // ... on the exact-f32 MFMA (0: the VALU kernel)
-  int fuse_mlp = 1;             // the fused Swin-tower MLP sub-block (vv_tower.hip) where mlp_supported
+  int fuse_mlp = 3;             // the fused Swin-tower MLP sub-block (vv_tower.hip): bit 0 at dim 96, bit 1 at dim 192
   int attn_mfma = 1;            // LG-stage window attention (hd 192) on the exact-f32 MFMA (0: the VALU kernels)
   int attn_planes = 1;          // the LG-stage attention forward writes the fp16x3 planes of a tile-48 proj GEMM
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of

@@ -46,7 +46,7 @@ __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * (q & 3))) & 3; 
 __device__ __forceinline__ int frag(int r, int q) { return r * 32 + ((q ^ hsw(r >> 2)) << 3); }
 
 template <int C, int NW, int HC, bool FWD>
-__global__ __launch_bounds__(64 * NW, 3) void k_mlp(MlpArgs a) {
+__global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
   constexpr int NT = 64 * NW, KS1 = C / 32, KS2 = HC / 32, NJ = HC / 16, NQ = C / 16, NC = 4 * C / HC;
   constexpr int CQ = C / 4;                  // channels per lane in the row phases (4 lanes per token)
   constexpr int A1W = KS1 * 2 * 16 * 32;     // halves of one wave's Y planes
@@ -1102,7 +1102,7 @@ hipError_t launch_ablk_fwd(const AblkArgs& a, hipStream_t s) {
 
 }  // namespace
 
-bool mlp_supported(int C, int M) { return C == 96 && M > 0 && M % 64 == 0; }
+bool mlp_supported(int C, int M) { return (C == 96 || C == 192) && M > 0 && M % 64 == 0; }
 
 static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
   if (!mlp_supported(a.C, a.M) || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
@@ -1113,7 +1113,8 @@ static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
     if (fwd ? (!G.beta || !G.b1 || !G.b2) : !G.dy) return hipErrorInvalidValue;
   }
   const int ph = prof_begin(s);
-  const hipError_t e = fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s);
+  const hipError_t e = a.C == 96 ? (fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s))
+                                  : (fwd ? launch_mlp<192, 4, 32, true>(a, s) : launch_mlp<192, 4, 32, false>(a, s));
   // 2 GEMMs of M x 4C x C per group; bytes: x1 / dx2 (+ out, + x1 bwd) and the 4C-wide pre-activation
   prof_end(ph, s, PC_TOWER, 4.0 * a.ngroups * a.M * 4.0 * a.C * a.C,
            (double)a.ngroups * a.M * 4.0 * (fwd ? 2.0 * a.C + 4.0 * a.C : 3.0 * a.C + 4.0 * a.C));
