@@ -215,7 +215,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    LN1 + qkv + window attention + proj + residual sub-block at dim 96: bit 0 forward, bit 1 backward, 1), "attn_mfma" (the window attention of
    the LG stage, head dim 192, and of the unfused tower stages, head dim 32, on the exact-f32 MFMA, 1), "gelu_planes" (the LG-stage GELU / gelu' GEMM
    epilogues write the fp16x3 planes of the K = 4C GEMM after them, 1), "attn_planes" (the LG-stage attention
-   forward writes the planes of a tile-48 proj GEMM, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
+   forward writes the planes of a tile-48 proj GEMM, 1), "fixup_ln" (that GEMM's split-K fixup fused into the LN2
+   after it, 1), "h4" (the split-operand LDS-DMA fp16x3 kernel, tile 48, where
    the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1), "gattn" (the
    LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1), "gattn_qf" (its 16-query blocks per
    wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1), "h4_small" (tile 48 with whole-chip split-K

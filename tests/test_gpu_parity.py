@@ -596,3 +596,34 @@ def test_gelu_planes_vs_rowsplit(full_dec, knob, extra):
     print(f"{knob} 1 vs 0 {extra}: out rel {e_o:.2e} (bitwise {torch.equal(o0, o1)}) grad rel {e_d:.2e} "
           f"closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
+
+
+def test_fixup_ln_bitwise(full_dec):
+    """fixup_ln: the LG-stage proj GEMM's split-K fixup fused into LN2 (vv::gemm_ln) repeats the fixup's chunk-order
+    sum + bias + residual and k_ln_fwd's reductions, so decoder output, input gradient, closure J and dJ/dz are
+    bit-identical with the separate fixup + LayerNorm launches."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field, uniform_sym
+
+    z = torch.from_numpy(0.5 * smooth_field(421, (1, 32, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(422, (1, 69, 128, 256), 1.0)).cuda()
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    zc = torch.from_numpy(0.3 * smooth_field(423, (1, 32, 128, 256))).cuda()
+    res = []
+    default = full_dec.ctx.get_tuning("fixup_ln")
+    try:
+        for v in (0, 1):
+            full_dec.ctx.set_tuning("fixup_ln", v)
+            out = full_dec.forward_raw(z).clone()
+            dz = torch.empty_like(z)
+            full_dec.backward_raw(cot, dz)
+            g = torch.empty_like(zc)
+            jb, jo = prob.closure(zc, g)
+            res.append((out, dz, jb, jo, g))
+    finally:
+        full_dec.ctx.set_tuning("fixup_ln", default)
+    (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
+    print(f"fixup_ln 1 vs 0: out max diff {(o1 - o0).abs().max().item():.1e}, grad {(d1 - d0).abs().max().item():.1e}, "
+          f"J {jb1 + jo1 - jb0 - jo0:.1e}, dJ/dz {(g1 - g0).abs().max().item():.1e}")
+    assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1) and jb0 == jb1 and jo0 == jo1

@@ -672,6 +672,30 @@ bool ablk_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, in
   return true;
 }
 
+// the LG-stage proj GEMM (RESID) with its split-K fixup fused into LN2 (vv::gemm_ln) when LN2 only has to write
+// fc1's tile-48 planes; hipErrorNotSupported where that does not apply (the caller runs gemm_nt + LayerNorm)
+hipError_t proj_ln2(const Stage& S, int b, const StageSave& sv, const Scratch& sc, const GemmArgs& p, hipStream_t st) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.fixup_ln || S.G != 1) return hipErrorNotSupported;
+  vv::MlpArgs ma;
+  if (mlp_args(S, b, sv, sc, true, nullptr, ma)) return hipErrorNotSupported;  // the fused MLP does its own LN2
+  GemmArgs f1 = gemm_base(S.M, 4 * S.C, S.C, 1, EPI_GELU, sc);
+  f1.ascale = sc.rs;
+  f1.g[0] = {sc.t1, nullptr, S.w[b][0].fc1W, S.w[b][0].fc1b, sc.h, nullptr, sv.h1[b]};
+  if (!ln_feeds_planes(f1, sc)) return hipErrorNotSupported;
+  vv::GemmLnArgs l;
+  memset(&l, 0, sizeof(l));
+  l.gmap = nullptr;
+  l.lo_x = 1;  // LN2 rows are the physical rows proj writes (through its crow)
+  l.gamma = S.w[b][0].n2g;
+  l.beta = S.w[b][0].n2b;
+  l.eps = 1e-5f;
+  l.pl = sc.apl;
+  l.rs = sc.rs;
+  l.stats = sv.st2[b];
+  return vv::gemm_ln(p, l, st, sc.ws);
+}
+
 int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st) {
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
@@ -679,6 +703,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
   for (int b = 0; b < S.depth; ++b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
+    bool ln2_done = false;
     vv::AblkArgs aa;
     if (ablk_args(S, b, sv, sc, ws, shift, idx, aa)) {
       CK(vv::ablk_fwd(aa, st));  // LN1 + qkv + window attention + proj + residual in one launch
@@ -724,7 +749,14 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                 nullptr};
     attn_feeds_planes(at, p, q, S.w[b][0], sc);
     CK(attn_fwd(at, st));
-    CK(gemm_nt(p, st, -1, sc.ws));
+    // proj's split-K fixup fused into LN2 where that LayerNorm feeds fc1's planes (gemm_ln)
+    const hipError_t pe = proj_ln2(S, b, sv, sc, p, st);
+    if (pe == hipSuccess)
+      ln2_done = true;
+    else if (pe == hipErrorNotSupported)
+      CK(gemm_nt(p, st, -1, sc.ws));
+    else
+      CK(pe);
     }
     vv::MlpArgs ma;
     if (mlp_args(S, b, sv, sc, true, nullptr, ma)) {  // LN2 + fc1 + GELU + fc2 + residual in one launch
@@ -744,7 +776,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
       ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, S.w[b][g].n2b, f1_pl ? nullptr : sc.t1 + g * MC,
                   sv.st2[b] + (size_t)g * M * 2, nullptr, nullptr, sc.rs + (size_t)g * M,
                   f1_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
-    CK(layernorm_fwd(ln2, st));
+    if (!ln2_done) CK(layernorm_fwd(ln2, st));
     if (f1_pl) f1.apre = sc.apl;
     // fc2 + residual (with tile 48, fc1's epilogue writes its A planes)
     GemmArgs f2 = gemm_base(M, C, 4 * C, G, EPI_RESID, sc);

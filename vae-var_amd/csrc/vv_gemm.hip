@@ -1870,7 +1870,7 @@ static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
                               const unsigned short* planes) {
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_h4<EPI>), grid, dim3(512), lds, s, a, sc, planes);
-  if (tail)  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
+  if (tail && !a.nofix)  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
     hipLaunchKernelGGL((k_gemm_fixup_sub16<256, 128, 4, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(512), 0, s, a);
   return hipGetLastError();
 }
@@ -1969,6 +1969,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "attn_mfma") return &t.attn_mfma;
   if (k == "gelu_planes") return &t.gelu_planes;
   if (k == "attn_planes") return &t.attn_planes;
+  if (k == "fixup_ln") return &t.fixup_ln;
   if (k == "h4") return &t.h4;
   if (k == "ln_planes") return &t.ln_planes;
   if (k == "gattn") return &t.gattn;
@@ -2186,8 +2187,8 @@ int gemm_tile_of(const GemmArgs& a_in, int tile_hint) {
   return resolve_tile(a, tile_hint);
 }
 
-hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
-  GemmArgs a = a_in;
+// validation, tile routing and the split / tile-order plan of one GEMM (gemm_nt, gemm_ln); t = the kernel's tile
+static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
   if (a.M <= 0 || a.N <= 0 || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
   if (a.K % KALIGN != 0 || a.ksplit % KALIGN != 0 || a.ksplit <= 0 || a.ksplit > a.K) return hipErrorInvalidValue;
   if ((a.lda & 3) || (a.lda2 & 3) || (a.K & 3) || (a.ldb & 3) || (a.ldb && a.ldb < a.K)) return hipErrorInvalidValue;
@@ -2204,7 +2205,7 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
     for (int g = 0; g < a.ngroups; ++g) ok = ok && !a.g[g].A2;
     a.ascale_phys = ok ? 1 : 0;
   }
-  const int t = resolve_tile(a, tile_hint);
+  t = resolve_tile(a, tile_hint);
   if (t < 0) return hipErrorInvalidValue;
   // producer planes are only read by tile 48; every other kernel reads A itself (which the producer then wrote)
   if (a.apre && t != 48) return hipErrorInvalidValue;
@@ -2255,6 +2256,14 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
       if (S > 1) a.tsplit = S;
     }
   }
+  return hipSuccess;
+}
+
+hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
+  GemmArgs a = a_in;
+  a.nofix = 0;
+  int t = -1;
+  if (hipError_t e = gemm_prepare(a, tile_hint, ws, t)) return e;
   const int ph = prof_begin(s);
   const hipError_t e = launch_variant(t, a, s);
   // algorithmic: 2MNK flops; bytes = A + B + C (+R/aux) once each
@@ -2262,6 +2271,24 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);
   if (a.epi == EPI_RESID || a.epi == EPI_GELU || a.epi == EPI_DGELU) bytes += 4.0 * G * (double)a.M * a.N;
   prof_end(ph, s, h3_tile(t) && h3_ready(a) ? PC_GEMM16 : PC_GEMM, 2.0 * G * a.M * a.N * a.K, bytes);
+  return e;
+}
+
+hipError_t gemm_ln(const GemmArgs& a_in, const GemmLnArgs& l, hipStream_t s, float* ws) {
+  GemmArgs a = a_in;
+  a.nofix = 0;
+  if (a.epi != EPI_RESID || a.ngroups != 1 || a.opl || a.N % 4 || a.N > 1280 || !ws || !l.gamma || !l.beta || !l.pl ||
+      !l.rs || !l.stats)
+    return hipErrorNotSupported;
+  int t = -1;
+  if (hipError_t e = gemm_prepare(a, -1, ws, t)) return e;
+  if (t != 48 || a.tsplit < 2 || a.tsplit > 4 || a.tdp != 0) return hipErrorNotSupported;
+  a.nofix = 1;
+  const int ph = prof_begin(s);
+  hipError_t e = launch_variant(t, a, s);
+  if (e == hipSuccess) e = fixup_ln_launch(a, l, s);
+  prof_end(ph, s, PC_GEMM16, 2.0 * a.M * a.N * a.K,
+           4.0 * ((double)a.M * a.K + (double)a.N * a.K + 3.0 * (double)a.M * a.N));
   return e;
 }
 

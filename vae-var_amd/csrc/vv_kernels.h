@@ -35,6 +35,7 @@ struct Tuning {
   int fuse_mlp = 3;             // the fused Swin-tower MLP sub-block (vv_tower.hip): bit 0 at dim 96, bit 1 at dim 192
   int attn_mfma = 1;            // LG-stage window attention (hd 192) on the exact-f32 MFMA (0: the VALU kernels)
   int attn_planes = 1;          // the LG-stage attention forward writes the fp16x3 planes of a tile-48 proj GEMM
+  int fixup_ln = 1;             // the proj GEMM's split-K fixup fused into the LG-stage LN2 (gemm_ln)
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
                                 // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
   int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
@@ -109,6 +110,7 @@ struct GemmArgs {
   const float* obw;
   const float* obb;
   const float* escale;  // set by the tile-48 launch: A's row scales in GEMM row order (what the kernel used)
+  int nofix;            // set by gemm_ln: the split-K partials are summed by the consumer (no fixup launch)
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   int h3_mink;         // > 0: this GEMM's own smallest K for the fp16x3 kernels (the forecast: Tuning.fc_h3_mink)
   GemmGroup g[kMaxGroups];
@@ -132,6 +134,26 @@ hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads,
 
 // ws: scratch of at least gemm_ws_floats() floats (may be null: no tail split)
 hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* ws = nullptr);
+
+// A residual GEMM whose split-K fixup is fused into the LayerNorm that consumes its output (tile 48 with every tile
+// split, EPI_RESID, one group, N <= 1280): one row per wave sums the S chunk partials in chunk order, adds bias and
+// residual (the fixup epilogue's arithmetic), stores the row x at its output row, then runs k_ln_fwd's LayerNorm
+// on it (the same reductions, so bit-identical to fixup + k_ln_fwd) and writes fp16x3 planes, row scales and stats.
+// LN row j reads GEMM row gmap[j] (null: j); its output row is the x row written (lo_x) or j.
+struct GemmLnArgs {
+  const int* gmap;
+  int lo_x;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  unsigned short* pl;  // planes [row][2N] (k_rowsplit's layout)
+  float* rs;           // row scales
+  float* stats;        // (mean, rstd) per row
+};
+// VV_E-style: hipErrorNotSupported when the GEMM does not take this form (the caller then runs gemm_nt + LayerNorm)
+hipError_t gemm_ln(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s, float* ws);
+// the LayerNorm half (vv_ops.hip), launched by gemm_ln with the GEMM's final arguments (tdp, tsplit, gm)
+hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s);
 // the kernel gemm_nt would run for `a` (tile hint -1: the routed choice, incl. the fallbacks), so a producer can
 // decide what form to write A in (tile 48: fp16x3 planes)
 int gemm_tile_of(const GemmArgs& a, int tile_hint = -1);

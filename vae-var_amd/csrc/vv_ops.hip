@@ -293,6 +293,111 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
   }
 }
 
+// gemm_ln's LayerNorm half: the fixup of a tile-48 split-K RESID GEMM (k_gemm_h4 with every tile split, partials
+// in ws as written by its part >= 0 path: tile tl, chunk c at ((tl S + c) 16 4 512 + ((a 4 + b) 4 + r) 512 + tid),
+// the thread / register of the 256 x 128 tile's 8 waves of 64 x 64 on 16x16 fragments) fused into k_ln_fwd<64, NV>:
+// one wave per LayerNorm row j. x = R + ((p0 + p1 + ...) + bias) is exactly k_gemm_fixup_sub16's arithmetic, the
+// LayerNorm exactly k_ln_fwd's, so the results are bit-identical to the two launches they replace.
+// 8 rows (waves) per workgroup: GEMM rows 8i .. 8i + 7 are fragment rows r = 0..3 of two lane quarters, so each
+// 128-B line of a partial (rows r and r + 4 of one 16-column block) is consumed inside one workgroup
+template <int NV, int S>
+__global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
+  const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
+  if (j >= args.M) return;
+  const GemmGroup G = args.g[0];
+  const int N = args.N, f4n = N >> 2;
+  const int gr = l.gmap ? l.gmap[j] : j;
+  const int xo = args.crow ? args.crow[gr] : gr;
+  const int lo = l.lo_x ? xo : j;
+  const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
+  const int mb = gr >> 8, rr = gr & 255, wm = rr >> 6, a = (rr >> 4) & 3, hh = (rr >> 2) & 3, r = rr & 3;
+  const int GM = args.gm > 0 ? args.gm : 8;  // tile_mn's grouped order (gemm_nt always sets gm)
+  const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
+  const int rrow = args.rmod > 0 ? xo % args.rmod : xo;
+  f4 pv[S][NV], rv[NV], bv[NV], gv[NV], bb[NV];
+  bool ok[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int jv = sl + v * 64;
+    ok[v] = jv < f4n;
+    const int c4 = 4 * (ok[v] ? jv : f4n - 1);
+    const int nb = c4 >> 7, cc = c4 & 127, wn = cc >> 6, b = (cc >> 4) & 3, rin = cc & 15;
+    const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
+    const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + hh * 16 + rin);
+#pragma unroll
+    for (int c = 0; c < S; ++c)
+      pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+    rv[v] = *reinterpret_cast<const f4*>(G.R + (size_t)rrow * args.ldr + c4);
+    const f4 t = *reinterpret_cast<const f4*>(G.bias ? G.bias + c4 : G.R + c4);
+    bv[v] = G.bias ? t : f4{0.f, 0.f, 0.f, 0.f};
+    gv[v] = *reinterpret_cast<const f4*>(l.gamma + c4);
+    bb[v] = *reinterpret_cast<const f4*>(l.beta + c4);
+  }
+  // the fixup: chunk partials in chunk order, then + bias, then residual + (k_gemm_fixup_sub16 + epilogue)
+  f4 xv[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    f4 acc = pv[0][v];
+#pragma unroll
+    for (int c = 1; c < S; ++c) acc += pv[c][v];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = acc[e] + bv[v][e];
+      xv[v][e] = rv[v][e] + t;
+    }
+    if (ok[v]) *reinterpret_cast<f4*>(G.C + (size_t)xo * args.ldc + 4 * (sl + v * 64)) = xv[v];
+  }
+  // k_ln_fwd<64, NV> on the row
+  constexpr int L = 64;
+  const int C = N;
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const f4 x = ok[v] ? xv[v] : f4{0.f, 0.f, 0.f, 0.f};
+    s += (x[0] + x[1]) + (x[2] + x[3]);
+  }
+  const float mean = sub_sum<L>(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = ok[v] ? xv[v][e] - mean : 0.f;
+      q += d * d;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(sub_sum<L>(q) / (float)C + l.eps);
+  unsigned mx = 0;
+  f4 ov[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ov[v][e] = (xv[v][e] - mean) * rstd * gv[v][e] + bb[v][e];
+    if (ok[v]) mx = absmax4(mx, ov[v]);
+  }
+  mx = sub_max<L>(mx);
+  const float sc = row_scale_of(mx);
+  if (sl == 0) {
+    l.rs[lo] = sc;
+    l.stats[2 * lo] = mean;
+    l.stats[2 * lo + 1] = rstd;
+  }
+  store_planes<L, NV>(l.pl + (size_t)lo * 2 * C, C, sl, ok, ov, sc);
+}
+
+hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s) {
+  const int nv = (a.N / 4 + 63) / 64;
+  if (nv > 5 || a.N % 4) return hipErrorInvalidValue;
+  const dim3 grid((a.M + 7) / 8);
+  switch (a.tsplit) {
+    case 2: hipLaunchKernelGGL((k_fixup_ln<5, 2>), grid, dim3(512), 0, s, a, l); break;
+    case 3: hipLaunchKernelGGL((k_fixup_ln<5, 3>), grid, dim3(512), 0, s, a, l); break;
+    case 4: hipLaunchKernelGGL((k_fixup_ln<5, 4>), grid, dim3(512), 0, s, a, l); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 // lanes per row: <= 3 float4 per lane up to C = 384, then a full wave (C = 1152: 4.5 float4 per lane)
 static int ln_lanes(int C) {
   const int f4n = C / 4;
