@@ -696,14 +696,43 @@ hipError_t proj_ln2(const Stage& S, int b, const StageSave& sv, const Scratch& s
   return vv::gemm_ln(p, l, st, sc.ws);
 }
 
+// the LG-stage fc2 GEMM (RESID) of block b with its split-K fixup fused into block b + 1's LN1 (window gather:
+// LN row j reads GEMM row idx[j]) when that LayerNorm only has to write qkv's tile-48 planes
+hipError_t fc2_ln1(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, const GemmArgs& f2,
+                   hipStream_t st) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.fixup_ln || S.G != 1 || b + 1 >= S.depth) return hipErrorNotSupported;
+  const int nb = b + 1, shift = (nb % 2 == 0) ? 0 : ws / 2;
+  vv::AblkArgs aa;
+  if (ablk_args(S, nb, sv, sc, ws, shift, S.idx[shift ? 1 : 0], aa)) return hipErrorNotSupported;
+  GemmArgs q = gemm_base(S.M, 3 * S.C, S.C, 1, EPI_STORE, sc);
+  q.ascale = sc.rs;
+  q.g[0] = {sc.t1, nullptr, S.w[nb][0].qkvW, S.w[nb][0].qkvb, sv.qkv[nb], nullptr, nullptr};
+  if (!ln_feeds_planes(q, sc)) return hipErrorNotSupported;
+  vv::GemmLnArgs l;
+  memset(&l, 0, sizeof(l));
+  l.gmap = S.idx[shift ? 1 : 0];  // LN1 -> window order
+  l.lo_x = 0;
+  l.gamma = S.w[nb][0].n1g;
+  l.beta = S.w[nb][0].n1b;
+  l.eps = 1e-5f;
+  l.pl = sc.apl;
+  l.rs = sc.rs;
+  l.stats = sv.st1[nb];
+  return vv::gemm_ln(f2, l, st, sc.ws);
+}
+
 int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st) {
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
   const int nwin = M / 16;
+  bool ln1_done = false;  // block b's LN1 already ran, fused into block b - 1's fc2 fixup
   for (int b = 0; b < S.depth; ++b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
     bool ln2_done = false;
+    const bool ln1_fused = ln1_done;
+    ln1_done = false;
     vv::AblkArgs aa;
     if (ablk_args(S, b, sv, sc, ws, shift, idx, aa)) {
       CK(vv::ablk_fwd(aa, st));  // LN1 + qkv + window attention + proj + residual in one launch
@@ -721,7 +750,7 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
       ln.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, S.w[b][g].n1b, q_pl ? nullptr : sc.t1 + g * MC,
                  sv.st1[b] + (size_t)g * M * 2, nullptr, nullptr, sc.rs + (size_t)g * M,
                  q_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
-    CK(layernorm_fwd(ln, st));
+    if (!ln1_fused) CK(layernorm_fwd(ln, st));
     if (q_pl) q.apre = sc.apl;
     CK(gemm_nt(q, st, -1, sc.ws));
     // window attention
@@ -785,7 +814,14 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
                  nullptr};
     gelu_feeds_planes(f1, f2, S.w[b][0].fc1Wmax, S.w[b][0].fc1bmax, sc);
     CK(gemm_nt(f1, st, -1, sc.ws));
-    CK(gemm_nt(f2, st, -1, sc.ws));
+    // fc2's split-K fixup fused into the next block's LN1 where that LayerNorm feeds qkv's planes
+    const hipError_t fe = fc2_ln1(S, b, sv, sc, ws, f2, st);
+    if (fe == hipSuccess)
+      ln1_done = true;
+    else if (fe == hipErrorNotSupported)
+      CK(gemm_nt(f2, st, -1, sc.ws));
+    else
+      CK(fe);
   }
   return 0;
 }
