@@ -826,6 +826,28 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
   return 0;
 }
 
+// an input-gradient GEMM g (EPI_STORE into ln's dy) with its split-K fixup fused into the LayerNorm backward ln that
+// consumes it (vv::gemm_ln, bwd): dy never goes to HBM; hipErrorNotSupported where that does not apply
+hipError_t gemm_ln_bwd(const GemmArgs& g, const LnArgs& ln, const Scratch& sc, hipStream_t st) {
+  const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
+  if (!T.fixup_ln || ln.ngroups != 1 || g.ngroups != 1 || ln.mode != LN_ROWMAP || ln.rows != g.M || ln.C != g.N ||
+      ln.ldx != ln.C || ln.ldy != ln.C || ln.lddy != ln.C || ln.ldres != ln.C || ln.g[0].dy != g.g[0].C)
+    return hipErrorNotSupported;
+  vv::GemmLnArgs l;
+  memset(&l, 0, sizeof(l));
+  l.bwd = 1;
+  l.lmap = ln.map;
+  l.x = ln.g[0].x;
+  l.res = ln.g[0].res;
+  l.y = ln.g[0].y;
+  l.gamma = ln.g[0].gamma;
+  l.stats = ln.g[0].stats;
+  l.rs = ln.g[0].rs;
+  l.pl = ln.g[0].pl;
+  l.eps = ln.eps;
+  return vv::gemm_ln(g, l, st, sc.ws);
+}
+
 // gx: [G][M][C] gradient w.r.t. the stage output, overwritten in place with the input gradient
 int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, float* gx, hipStream_t st) {
   const int G = S.G, M = S.M, C = S.C;
@@ -862,12 +884,17 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
         f1.g[g] = {sc.h + g * MC * 4, nullptr, S.w[b][g].fc1WT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
       gelu_feeds_planes(f2, f1, S.w[b][0].fc2Wmax, nullptr, sc);  // max |fc2^T| = max |fc2|
       CK(gemm_nt(f2, st, -1, sc.ws));
-      CK(gemm_nt(f1, st, -1, sc.ws));
       LnArgs ln2 = ln_base(M, C, G, 1e-5f);
       for (int g = 0; g < G; ++g)
         ln2.g[g] = {sv.x1[b] + g * MC, S.w[b][g].n2g, nullptr, gx + g * MC, sv.st2[b] + (size_t)g * M * 2,
                     sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, p_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
-      CK(layernorm_bwd(ln2, st));
+      const hipError_t fe = gemm_ln_bwd(f1, ln2, sc, st);  // fc1^T with its fixup fused into the LN2 backward
+      if (fe == hipErrorNotSupported) {
+        CK(gemm_nt(f1, st, -1, sc.ws));
+        CK(layernorm_bwd(ln2, st));
+      } else {
+        CK(fe);
+      }
     }
     if (p_pl) p.apre = sc.apl;  // planes in physical row order: the kernel gathers them through arow
     vv::AblkArgs ab;
@@ -896,14 +923,19 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     GemmArgs q = gemm_base(M, C, 3 * C, G, EPI_STORE, sc);
     for (int g = 0; g < G; ++g)
       q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
-    CK(gemm_nt(q, st, -1, sc.ws));
     LnArgs ln1 = ln_base(M, C, G, 1e-5f);
     ln1.map = idx;
     const bool l1_pl = f2_pl && b > 0;  // planes for the next block's fc2 input-gradient GEMM
     for (int g = 0; g < G; ++g)
       ln1.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, nullptr, gx + g * MC, sv.st1[b] + (size_t)g * M * 2,
                   sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, l1_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
-    CK(layernorm_bwd(ln1, st));
+    const hipError_t qe = gemm_ln_bwd(q, ln1, sc, st);  // qkv^T with its fixup fused into the LN1 backward
+    if (qe == hipErrorNotSupported) {
+      CK(gemm_nt(q, st, -1, sc.ws));
+      CK(layernorm_bwd(ln1, st));
+    } else {
+      CK(qe);
+    }
   }
   return 0;
 }

@@ -2277,8 +2277,9 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
 hipError_t gemm_ln(const GemmArgs& a_in, const GemmLnArgs& l, hipStream_t s, float* ws) {
   GemmArgs a = a_in;
   a.nofix = 0;
-  if (a.epi != EPI_RESID || a.ngroups != 1 || a.opl || a.N % 4 || a.N > 1280 || !ws || !l.gamma || !l.beta || !l.pl ||
-      !l.rs || !l.stats)
+  if (a.ngroups != 1 || a.opl || a.N % 4 || a.N > 1280 || !ws || !l.gamma || !l.stats) return hipErrorNotSupported;
+  if (!l.bwd && (a.epi != EPI_RESID || !l.beta || !l.pl || !l.rs)) return hipErrorNotSupported;
+  if (l.bwd && (a.epi != EPI_STORE || a.g[0].bias || a.crow || !l.x || !l.y || (l.pl && !l.rs)))
     return hipErrorNotSupported;
   int t = -1;
   if (hipError_t e = gemm_prepare(a, -1, ws, t)) return e;

@@ -148,7 +148,15 @@ struct GemmLnArgs {
   float eps;
   unsigned short* pl;  // planes [row][2N] (k_rowsplit's layout)
   float* rs;           // row scales
-  float* stats;        // (mean, rstd) per row
+  float* stats;        // (mean, rstd) per row (the backward reads them)
+  // backward (bwd = 1; the GEMM: EPI_STORE without bias, its output dy = C is not stored): k_ln_bwd on LN row j with
+  // dy = GEMM row j, x / res / y (in place allowed) and pl / rs at row lmap[j] (null: j), stats at j; y, x, res row
+  // stride N. pl may be null (no planes wanted), rs may be null with it.
+  int bwd;
+  const int* lmap;
+  const float* x;
+  const float* res;
+  float* y;
 };
 // VV_E-style: hipErrorNotSupported when the GEMM does not take this form (the caller then runs gemm_nt + LayerNorm)
 hipError_t gemm_ln(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s, float* ws);

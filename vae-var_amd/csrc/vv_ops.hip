@@ -385,10 +385,98 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   store_planes<L, NV>(l.pl + (size_t)lo * 2 * C, C, sl, ok, ov, sc);
 }
 
+// the backward form: dy = the fixup of a STORE GEMM without bias (chunk-order sum + 0, k_gemm_fixup_sub16's
+// value), then k_ln_bwd<64, NV> on the row (x, res, y and the planes at row lmap[j], stats at j)
+template <int NV, int S>
+__global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs l) {
+  const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
+  if (j >= args.M) return;
+  const int N = args.N, f4n = N >> 2, C = N;
+  const int gr = j;
+  const int pr = l.lmap ? l.lmap[j] : j;
+  const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
+  const int mb = gr >> 8, rr = gr & 255, wm = rr >> 6, a = (rr >> 4) & 3, hh = (rr >> 2) & 3, r = rr & 3;
+  const int GM = args.gm > 0 ? args.gm : 8;
+  const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
+  const float mean = l.stats[2 * j], rstd = l.stats[2 * j + 1];
+  const float* res = l.res ? l.res : l.x;  // dummy source when there is no residual (never added)
+  f4 pv[S][NV], xv[NV], gv[NV], rv[NV];
+  bool ok[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int jv = sl + v * 64;
+    ok[v] = jv < f4n;
+    const int c4 = 4 * (ok[v] ? jv : f4n - 1);
+    const int nb = c4 >> 7, cc = c4 & 127, wn = cc >> 6, b = (cc >> 4) & 3, rin = cc & 15;
+    const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
+    const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + hh * 16 + rin);
+#pragma unroll
+    for (int c = 0; c < S; ++c)
+      pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+    xv[v] = *reinterpret_cast<const f4*>(l.x + (size_t)pr * N + c4);
+    gv[v] = *reinterpret_cast<const f4*>(l.gamma + c4);
+    rv[v] = *reinterpret_cast<const f4*>(res + (size_t)pr * N + c4);
+  }
+  f4 dv[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    f4 acc = pv[0][v];
+#pragma unroll
+    for (int c = 1; c < S; ++c) acc += pv[c][v];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dv[v][e] = acc[e] + 0.0f;  // the STORE epilogue's v = acc + bias (none)
+  }
+  // k_ln_bwd<64, NV>
+  constexpr int L = 64;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const f4 d = ok[v] ? dv[v] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gd = gv[v][e] * d[e];
+      s1 += gd;
+      s2 += gd * ((xv[v][e] - mean) * rstd);
+    }
+  }
+  const float m1 = sub_sum<L>(s1) / (float)C;
+  const float m2 = sub_sum<L>(s2) / (float)C;
+  unsigned mx = 0;
+  f4 ov[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ov[v][e] = rstd * (gv[v][e] * dv[v][e] - m1 - ((xv[v][e] - mean) * rstd) * m2);
+    if (l.res) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ov[v][e] += rv[v][e];
+    }
+    if (ok[v]) {
+      *reinterpret_cast<f4*>(l.y + (size_t)pr * N + 4 * (sl + v * 64)) = ov[v];
+      mx = absmax4(mx, ov[v]);
+    }
+  }
+  if (l.rs) {
+    mx = sub_max<L>(mx);
+    const float sc = row_scale_of(mx);
+    if (sl == 0) l.rs[pr] = sc;
+    if (l.pl) store_planes<L, NV>(l.pl + (size_t)pr * 2 * C, C, sl, ok, ov, sc);
+  }
+}
+
 hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s) {
   const int nv = (a.N / 4 + 63) / 64;
   if (nv > 5 || a.N % 4) return hipErrorInvalidValue;
   const dim3 grid((a.M + 7) / 8);
+  if (l.bwd) {
+    switch (a.tsplit) {
+      case 2: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 2>), grid, dim3(512), 0, s, a, l); break;
+      case 3: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 3>), grid, dim3(512), 0, s, a, l); break;
+      case 4: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 4>), grid, dim3(512), 0, s, a, l); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (a.tsplit) {
     case 2: hipLaunchKernelGGL((k_fixup_ln<5, 2>), grid, dim3(512), 0, s, a, l); break;
     case 3: hipLaunchKernelGGL((k_fixup_ln<5, 3>), grid, dim3(512), 0, s, a, l); break;
