@@ -547,7 +547,8 @@ def main():
             out["cpu_baseline"] = cb
             out["cpu_wall_clock_to_convergence_s_extrapolated"] = cb.pop("wall_clock_to_convergence_s_extrapolated")
             out["speedup_vs_cpu"] = out["value"] / cb["value"]
-            if "value_all_cores" in cb:
+            if "value_all_cores" in cb and cb["value_all_cores"] > cb["value"]:
+                # only a faster all-cores run is a baseline; an oversubscribed (slower) one would inflate the ratio
                 out["speedup_vs_cpu_all_cores"] = out["value"] / cb["value_all_cores"]
             meas = cpu_convergence_measured() if args.config == 2 and args.batch == 1 else None
             if meas:
