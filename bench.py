@@ -267,11 +267,12 @@ class GpuAnalyses:
 
     def rebind(self, cfg_id: int):
         """Re-bind this rank to BASELINE config `cfg_id`'s problems (T from CONFIGS, T - 1 flow slots, the same decoder);
-        returns the analysis runner (used for the config-3 / config-4 sub-records)."""
+        returns the analysis runner (used for the config-3 / 4 / 5 sub-records)."""
         cfg = CONFIGS[cfg_id]
         T = cfg["T"]
         flow = self._LGUnet(self._C.FLOW, self.batch, T - 1, device=self.local).load_synthetic() if T > 1 else None
-        ps = [self._make_problem(nch=69, Hs=128, Ws=256, T=T, seed=20250620 + self.rank * self.batch + b)
+        Hs, Ws = cfg.get("grid", (128, 256))
+        ps = [self._make_problem(nch=69, Hs=Hs, Ws=Ws, T=T, seed=20250620 + self.rank * self.batch + b)
               for b in range(self.batch)]
         self.prob = self._DAProblem(self.dec, ps if self.batch > 1 else ps[0], flow=flow, device=self.local)
         self.prob_np = ps[0]
@@ -356,6 +357,7 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel-class profile")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (T=2) line section")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (T=6) line section")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (721x1440, T=2) line section")
     ap.add_argument("--no-exact-f32", action="store_true", help="skip the exact-f32 GEMM analysis")
     ap.add_argument("--no-sc4dvar", action="store_true", help="skip the sc4dvar (SURVEY §8 f4) section")
     ap.add_argument("--batch", type=int, default=1, help="independent analyses per GPU, evaluated in one batched "
@@ -418,11 +420,11 @@ def main():
         j_0 = w.prob.closure_batch(torch.zeros_like(res["z"]), None)
         j_info = (float(j_0[0][0] + j_0[1][0]), float(j_end[0][0] + j_end[1][0]))
 
-    # BASELINE configs 3 (T = 2) and 4 (T = 6) as sub-records of every line, each timed on its own after the main
+    # BASELINE configs 3 (T = 2), 4 (T = 6) and 5 (721x1440, T = 2) as sub-records of every line, each timed on its own after the main
     # region (warm-up analysis for the graph capture, then one timed analysis per rank + the gather)
     main_prob_np = getattr(w, "prob_np", None)
     subs = {}
-    for cid, skip in ((3, args.no_config3), (4, args.no_config4)):
+    for cid, skip in ((3, args.no_config3), (4, args.no_config4), (5, args.no_config5)):
         if skip or args.config == cid:
             continue
         subs[cid] = sub_record(w, cid, ensemble, dev, size, args.batch)
@@ -555,7 +557,7 @@ def main():
                 out["cpu_convergence_measured"] = meas
                 out["wall_clock_speedup_vs_cpu_measured"] = meas["wall_clock_s"] / per_analysis
         for cid, rec in subs.items():
-            if CONFIGS[cid]["T"] != 2 or rec.get("_prob_np") is None:
+            if CONFIGS[cid]["T"] != 2 or "grid" in CONFIGS[cid] or rec.get("_prob_np") is None:
                 continue
             epi = rec["evals"] / max(rec["iters"], 1)
             per_eval, cb = cpu_baseline(rec["_prob_np"], 2, epi, rec["evals"] / max(rec["analyses"], 1),

@@ -33,8 +33,9 @@ def test_bench_spawns_its_ranks():
     assert out["iters"] == 2 * (97 + 98) and out["evals"] == 2 * (110 + 111)
     assert out["gathered"] == [[69, 128, 256], [69, 128, 256]]
     assert out["value"] == out["iters"] / (out["ms_per_step"] * 1e-3 * out["steps"])
-    c4 = out["config4"]
-    assert c4["n_gpus"] == 2 and c4["gathered"] == [[69, 128, 256], [69, 128, 256]] and c4["iters"] == 97 + 98
+    for cid in (3, 4, 5):  # every BASELINE config other than the main one is a sub-record of the line
+        c = out[f"config{cid}"]
+        assert c["n_gpus"] == 2 and c["gathered"] == [[69, 128, 256], [69, 128, 256]] and c["iters"] == 97 + 98
     for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out
 
@@ -50,7 +51,7 @@ def test_bench_two_ranks_product_path():
     analysis on libvaevar (here both on the box's one GPU, over gloo since RCCL refuses two ranks per device), gather
     both analyses to rank 0, take the max time and sum the iterations."""
     p = _run("--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-profile", "--no-exact-f32",
-             "--no-config4", "--no-sc4dvar", env={"VAEVAR_DIST_BACKEND": "gloo"})
+             "--no-config4", "--no-config5", "--no-sc4dvar", env={"VAEVAR_DIST_BACKEND": "gloo"})
     assert p.returncode == 0, p.stderr[-3000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     print({k: out[k] for k in ("n_gpus", "iters", "evals", "value", "gathered", "J_start", "J_final")})

@@ -4,6 +4,6 @@ T=${1:-ab}
 shift || true
 mkdir -p gpurun_out/$T
 for i in 1 2; do
-  VAEVAR_LIB=$REF timeout -k 10 240 python bench.py --no-cpu-baseline --no-profile --no-exact-f32 --no-config4 --steps 2 "$@" > gpurun_out/$T/ref_$i.json 2>/dev/null
-  timeout -k 10 240 python bench.py --no-cpu-baseline --no-profile --no-exact-f32 --no-config4 --steps 2 "$@" > gpurun_out/$T/new_$i.json 2>/dev/null
+  VAEVAR_LIB=$REF timeout -k 10 240 python bench.py --no-cpu-baseline --no-profile --no-exact-f32 --no-config4 --no-config5 --steps 2 "$@" > gpurun_out/$T/ref_$i.json 2>/dev/null
+  timeout -k 10 240 python bench.py --no-cpu-baseline --no-profile --no-exact-f32 --no-config4 --no-config5 --steps 2 "$@" > gpurun_out/$T/new_$i.json 2>/dev/null
 done

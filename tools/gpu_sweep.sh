@@ -12,6 +12,6 @@ mkdir -p gpurun_out/$T
 for R in 1 2; do
   for V in "${VALS[@]}"; do
     env $ENVK=$V timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-exact-f32 --no-profile \
-      --no-config3 --no-config4 --no-sc4dvar "$@" >> gpurun_out/$T/c2_${KEY}_$V.json 2>> gpurun_out/$T/c2_${KEY}_$V.err
+      --no-config3 --no-config4 --no-config5 --no-sc4dvar "$@" >> gpurun_out/$T/c2_${KEY}_$V.json 2>> gpurun_out/$T/c2_${KEY}_$V.err
   done
 done

@@ -9,8 +9,8 @@ timeout -k 10 420 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 echo "bench done"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/rp -o run -- python bench.py --no-cpu-baseline > $OUT/rp.log 2>&1
 echo "rocprof done"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pf -o run -- python bench.py --steps 2 --no-cpu-baseline --no-profile > $OUT/pf.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pw -o run -- python bench.py --steps 2 --no-cpu-baseline --no-profile > $OUT/pw.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pf -o run -- python bench.py --steps 2 --no-cpu-baseline --no-profile --no-config5 > $OUT/pf.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pw -o run -- python bench.py --steps 2 --no-cpu-baseline --no-profile --no-config5 > $OUT/pw.log 2>&1
 echo "pmc done"
 python tools/pmc_traffic.py $(find $OUT/pf -name "*counter_collection.csv") $(find $OUT/pw -name "*counter_collection.csv") $OUT/gemm_traffic.json > /dev/null
 python tools/rocprof_gemm_summary.py $(find $OUT/rp -name "*kernel_stats.csv") $OUT/gemm_rocprof_summary.json > /dev/null
