@@ -1741,7 +1741,7 @@ int vv_ctx_create(int device, vv_ctx** out) {
   auto* c = new vv_ctx();
   c->device = device;
   VV_HIP(hipSetDevice(device));
-  VV_HIP(hipMalloc(&c->red, kRedBlocks * sizeof(double)));
+  VV_HIP(hipMalloc(&c->red, 2 * kRedBlocks * sizeof(double)));  // two halves: lbfgs_two_loop alternates
   VV_HIP(hipMalloc(&c->redf, kRedBlocks * sizeof(float)));
   VV_HIP(hipMalloc(&c->twoloop, kMaxHistory * sizeof(float)));
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));

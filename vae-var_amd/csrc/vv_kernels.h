@@ -399,7 +399,8 @@ hipError_t vec_axpby(float* out, const float* x, float a, const float* y, float 
 hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s);
 hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float* out, hipStream_t s);
 hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
-// q (= -g on entry) -> L-BFGS direction d (two-loop recursion, device scalars); al: >= m device floats
+// q (= -g on entry) -> L-BFGS direction d (two-loop recursion, device scalars); al: >= m device floats;
+// partial: 2 * nblk doubles
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,
                           int64_t n, double* partial, int nblk, float* al, hipStream_t s);
 hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,

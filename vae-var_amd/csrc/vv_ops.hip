@@ -1874,20 +1874,22 @@ hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s) {
   return hipGetLastError();
 }
 // L-BFGS two-loop recursion (torch/optim/lbfgs.py:404-442) with its scalars kept on the device: per history
-// pair one dot (k_dot partials) and one axpy whose blocks each finish the dot exactly as k_final_d does and form
-// the coefficient in fp32 as torch does on 0-d tensors; no host round trip. First loop (mode 0):
-// al[i] = f32(s_i . q) * ro[i], q += (-al[i]) y_i. Second loop (mode 1): be = f32(y_i . r) * ro[i],
-// r += (al[i] - be) s_i.
-// the coefficient step fused into the axpy: every block finishes the dot from the same partials in the same order
-// as k_final_d (so every block holds the same fp32 coefficient) and block 0 records al[i]; 2 launches per
-// history pair instead of 3
-constexpr int kTwoLoopBlocks = 256;
-__global__ __launch_bounds__(256) void k_twoloop_axpy(float* y, const float* x, const double* partial, int nblk,
-                                                      float ro, float* al, int i, int mode, int64_t n, int vec4) {
-  __shared__ double red[4];
+// pair one kernel whose blocks each finish the pending dot from its partials exactly as k_final_d does and form the
+// coefficient in fp32 as torch does on 0-d tensors (no host round trip), apply the axpy, and leave the partials of
+// the next pair's dot. First loop (mode 0): al[i] = f32(s_i . q) * ro[i], q += (-al[i]) y_i. Second loop (mode 1):
+// be = f32(y_i . r) * ro[i], r += (al[i] - be) s_i.
+// the axpy of history pair i fused with the dot of pair i -+ 1 on the updated q: grid = the k_dot grid (nblk blocks,
+// the same grid-stride element partition and accumulation order per thread, the same block_sum), so part_out holds
+// exactly the partials k_dot would write on the new q; the coefficient comes from part_in as in k_twoloop_axpy
+// (the two partial buffers alternate: blocks still reading part_in while others write part_out).
+// One launch and one pass over q per history pair instead of two.
+__global__ __launch_bounds__(256) void k_twoloop_axpy_dot(float* y, const float* x, const double* part_in, int nblk,
+                                                          float ro, float* al, int i, int mode, int64_t n,
+                                                          const float* next, double* part_out) {
+  __shared__ double red[4], red2[4];
   __shared__ float coef;
   double acc = 0.0;
-  for (int j = threadIdx.x; j < nblk; j += 256) acc += partial[j];
+  for (int j = threadIdx.x; j < nblk; j += 256) acc += part_in[j];
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) {
     const float v = (float)t * ro;
@@ -1900,48 +1902,33 @@ __global__ __launch_bounds__(256) void k_twoloop_axpy(float* y, const float* x, 
   }
   __syncthreads();
   const float a = coef;
-  if (vec4) {
-    // float4 view (n % 4 == 0, 16-B aligned; checked on the host), four float4 of y and x per thread in flight
-    // together: the scalar loop's stores to y kept every next load behind them (x and y may alias for the
-    // compiler), one memory round trip per element
-    f4* y4 = reinterpret_cast<f4*>(y);
-    const f4* x4 = reinterpret_cast<const f4*>(x);
-    const int64_t n4 = n >> 2, G = (int64_t)gridDim.x * 256;
-    for (int64_t b = blockIdx.x * 256 + threadIdx.x; b < n4; b += 4 * G) {
-      f4 xv[4], yv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t k = min(b + u * G, n4 - 1);
-        xv[u] = x4[k];
-        yv[u] = y4[k];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (b + u * G < n4) {
-          f4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = yv[u][e] + a * xv[u][e];
-          y4[b + u * G] = o;
-        }
-    }
-    return;
+  double d = 0.0;
+  for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+    const float v = y[k] + a * x[k];
+    y[k] = v;
+    if (next) d += (double)next[k] * (double)v;
   }
-  for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) y[k] = y[k] + a * x[k];
+  if (next) {
+    const double u = block_sum(d, red2);
+    if (threadIdx.x == 0) part_out[blockIdx.x] = u;
+  }
 }
+
+// partial: 2 * nblk doubles (the fused kernels alternate between its halves)
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,
                           int64_t n, double* partial, int nblk, float* al, hipStream_t s) {
-  auto v4 = [&](const float* x) { return (n % 4 == 0 && ((uintptr_t)q % 16) == 0 && ((uintptr_t)x % 16) == 0) ? 1 : 0; };
-  for (int i = m - 1; i >= 0; --i) {
-    hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, S[i], q, n, partial);
-    hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, Y[i], partial, nblk, ro[i], al, i, 0,
-                       n, v4(Y[i]));
-  }
+  double* pb[2] = {partial, partial + nblk};
+  int c = 0;
+  if (m > 0) hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, S[m - 1], q, n, pb[c]);
+  for (int i = m - 1; i >= 0; --i, c ^= 1)
+    hipLaunchKernelGGL(k_twoloop_axpy_dot, dim3(nblk), dim3(256), 0, s, q, Y[i], pb[c], nblk, ro[i], al, i, 0, n,
+                       i > 0 ? S[i - 1] : nullptr, pb[c ^ 1]);
   hipLaunchKernelGGL(k_scale, dim3(vgrid(n)), dim3(256), 0, s, q, H_diag, n);
-  for (int i = 0; i < m; ++i) {
-    hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, Y[i], q, n, partial);
-    hipLaunchKernelGGL(k_twoloop_axpy, dim3(kTwoLoopBlocks), dim3(256), 0, s, q, S[i], partial, nblk, ro[i], al, i, 1,
-                       n, v4(S[i]));
-  }
+  c = 0;
+  if (m > 0) hipLaunchKernelGGL(k_dot, dim3(nblk), dim3(256), 0, s, Y[0], q, n, pb[c]);
+  for (int i = 0; i < m; ++i, c ^= 1)
+    hipLaunchKernelGGL(k_twoloop_axpy_dot, dim3(nblk), dim3(256), 0, s, q, S[i], pb[c], nblk, ro[i], al, i, 1, n,
+                       i + 1 < m ? Y[i + 1] : nullptr, pb[c ^ 1]);
   return hipGetLastError();
 }
 hipError_t fill(float* p, float v, int64_t n, hipStream_t s) {
