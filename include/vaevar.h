@@ -242,8 +242,9 @@ int vv_attention_global(vv_ctx* ctx, const float* qkv, float* out, int N, int C,
 /* raw GEMM entry for kernel tests: C[M][N] = A[M][K] . B[N][K]^T (+bias), K a multiple of 32. tile = -1 picks the
    kernel as the engine does; otherwise one of the library kernels: 0 / 2 / 4 exact-f32 MFMA 128x128 / 64x64 /
    32x64, 24 / 34 bf16x6 split 64x64 / pipelined 128x128, 36 / 44 fp16x3 split 128x128 / 256x128 (32x32x16 MFMAs),
-   46 / 47 the same on 16x16x32 MFMAs. Any other tile: VV_E_ARG. An fp16x3 tile whose B has no fp16 planes (not
-   registered) runs tile 34. */
+   46 / 47 the same on 16x16x32 MFMAs, 48 fp16x3 256x128 on pre-split A planes staged by LDS-DMA (the engine's
+   default for the LG GEMMs). Any other tile: VV_E_ARG. An fp16x3 tile whose B has no fp16 planes (not registered)
+   runs tile 34. */
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
             int tile, void* stream);
 
