@@ -5,7 +5,9 @@ torch.optim.LBFGS and (b) as a fixed-step replay of G10's recorded line-search s
 mirror (vaevar.lbfgs.LBFGS with torch-CPU vector primitives). The relative J difference per outer pass against G10
 is the intrinsic sensitivity of the problem; tests/test_gpu_parity.py::test_config2_trajectory_g10 takes its
 tolerance from it (written to tests/golden/g10_sensitivity.npz). `--case g13` does the same for G13 (config 3:
-T = 2 with the flow stand-in) into tests/golden/g13_sensitivity.npz (test_config3_trajectory_g13).
+T = 2 with the flow stand-in) into tests/golden/g13_sensitivity.npz (test_config3_trajectory_g13); `--case g15`
+(config 5: 721x1440 state, T = 2, Nit 5, against the genuine one_step_DA of G15) and `--case g16` (config 4: T = 6,
+Nit 3) likewise (test_gpu_config4.py).
 
 Run:  PYTHONDONTWRITEBYTECODE=1 python -B oracle/g10_sensitivity.py [--threads 4] [--case g13]
 """
@@ -62,10 +64,13 @@ class CpuPrims:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=4)
-    ap.add_argument("--case", default="g10", choices=["g10", "g13"])
+    ap.add_argument("--case", default="g10", choices=["g10", "g13", "g15", "g16"])
     a = ap.parse_args()
-    T = 2 if a.case == "g13" else 1
-    g = np.load(os.path.join(GOLD, "g10_config2_trajectory.npz" if T == 1 else "g13_config3_trajectory.npz"))
+    T, Hs, Ws, nit, fx = {"g10": (1, 128, 256, 10, "g10_config2_trajectory.npz"),
+                          "g13": (2, 128, 256, 10, "g13_config3_trajectory.npz"),
+                          "g15": (2, 721, 1440, 5, "g15_config5_trajectory.npz"),
+                          "g16": (6, 128, 256, 3, "g16_config4_trajectory.npz")}[a.case]
+    g = np.load(os.path.join(GOLD, fx))
     Jr = g["J"].sum(1)
     torch.set_num_threads(a.threads)
     cwd = os.getcwd()
@@ -75,10 +80,10 @@ def main():
     fm = build_ref(tr, {k: v for k, v in C.FLOW.items() if k != "arch"})[0] if T > 1 else None
     for v in list(m.parameters()) + (list(fm.parameters()) if fm is not None else []):
         v.requires_grad_(False)
-    prob = make_problem(nch=69, Hs=128, Ws=256, T=T, seed=20250620)
+    prob = make_problem(nch=69, Hs=Hs, Ws=Ws, T=T, seed=20250620)
     rp = RefProblem(prob, m, C.DECODER["img_size"], fm) if fm is not None else RefProblem(prob, m, C.DECODER["img_size"])
     t0 = time.time()
-    _, _, js, _, _ = one_step_da_ref(rp, 10, (32, 128, 256))
+    _, _, js, _, _ = one_step_da_ref(rp, nit, (32, 128, 256))
     free = np.abs(np.array(js).sum(1) - Jr) / np.abs(Jr)
     print(f"free-running, {a.threads} threads ({time.time() - t0:.0f}s): J rel per pass {free.tolist()}", flush=True)
 
@@ -95,11 +100,11 @@ def main():
         return float(np.float32(float(r)) + np.float32(float(o)))
 
     jr = []
-    for kk in range(11):
+    for kk in range(nit + 1):
         with torch.no_grad():
             r, o = rp.loss_terms(z)
         jr.append(float(r) + float(o))
-        if kk < 10:
+        if kk < nit:
             opt.step(closure)
     rep = np.abs(np.array(jr) - Jr) / np.abs(Jr)
     print(f"replay, {a.threads} threads ({time.time() - t0:.0f}s): J rel per pass {rep.tolist()}", flush=True)

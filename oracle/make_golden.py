@@ -21,6 +21,12 @@ are stored):
   g9_metrics.npz        G9: the genuine utils.metrics.Metrics WRMSE / Bias as one_step_DA calls them
                         (da_4dvar.py:1256-1262) at 128x256 and 721x1440
   g7_tiny_lgunet1.npz   G7: tiny networks.LGUnet_all_1 (RoPE, -inf mask, global LG window, 3 levels): out
+  g14_sc4dvar_reference.npz  G14 (~2 min): the genuine sc4dvar get_static_info / transform / loss + backward / Nit=1
+                        L-BFGS pass with the oracle's float64 SHT as the torch_harmonics stub (float64 and float32 runs)
+  g15_config5_trajectory.npz  G15 (--g15, ~25 min): the genuine one_step_DA at 721x1440, T=2, Nit=5 (config 5's
+                        budget): J per pass, line-search steps, sampled xa
+  g16_config4_trajectory.npz  G16 (--g16, ~20 min): config 4 (T=6, decoder + flow stand-in) with torch.optim.LBFGS,
+                        Nit 3 at 128x256: J per pass, line-search steps, sampled xa
   g13_config3_trajectory.npz  G13 (--g13, ~30 min): config 3 (T=2, decoder + flow stand-in) with torch.optim.LBFGS,
                         Nit 10 at 128x256: J per pass, line-search steps, sampled xa
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
@@ -269,10 +275,10 @@ class LineSearchRecorder:
         return False
 
 
-def g6(tr):
-    """G6: run the reference's own one_step_DA vae4dvar branch (da_4dvar.py:1179-1306) on CPU at 721x1440 with
-    T=2 (flow stand-in), Nit=1, synthetic weights and the make_problem(seed=20250620) inputs (SURVEY §8 c2 iv:
-    object.__new__ + attributes, device 'cuda' rewritten to 'cpu')."""
+def genuine_one_step_da(tr, T, nit, seed, tag):
+    """Run the reference's own cyclic_4dvar.one_step_DA vae4dvar branch (da_4dvar.py:1179-1306) on CPU at 721x1440
+    (SURVEY §8 c2 iv: object.__new__ + attributes, device 'cuda' rewritten to 'cpu'), synthetic weights, flow
+    stand-in for T > 1, make_problem(seed) inputs. Returns (J per printed pass, xa, line-search steps, prob)."""
     import contextlib
     import importlib
     import io
@@ -297,19 +303,21 @@ def g6(tr):
     dec_p = synth_params(C.DECODER)
     missing, unexpected = vae.dec.load_state_dict(dec_p, strict=False)
     assert not unexpected and all(k.endswith(("relative_position_index", "attn_mask")) for k in missing)
-    flow_cfg = {k: v for k, v in C.FLOW.items() if k != "arch"}
-    flow = tr.LGUnet_all(rank=0, **flow_cfg)
-    missing, unexpected = flow.load_state_dict(synth_params(C.FLOW), strict=False)
-    assert not unexpected and all(k.endswith(("relative_position_index", "attn_mask")) for k in missing)
+    flow = None
+    if T > 1:
+        flow_cfg = {k: v for k, v in C.FLOW.items() if k != "arch"}
+        flow = tr.LGUnet_all(rank=0, **flow_cfg)
+        missing, unexpected = flow.load_state_dict(synth_params(C.FLOW), strict=False)
+        assert not unexpected and all(k.endswith(("relative_position_index", "attn_mask")) for k in missing)
     a = object.__new__(da.cyclic_4dvar)
     a.device = "cpu"
-    a.da_win, a.obs_type, a.obs_coeff, a.Nit, a.use_eval = 2, "synthetic", 1.0, 1, False
-    a.nchannel, a.nlev, a.nlat, a.nlon, a.current_time = 69, 13, 721, 1440, "G6"
+    a.da_win, a.obs_type, a.obs_coeff, a.Nit, a.use_eval = T, "synthetic", 1.0, nit, False
+    a.nchannel, a.nlev, a.nlat, a.nlon, a.current_time = 69, 13, 721, 1440, tag
     a.metric = metrics.Metrics()
     a.metrics_list = {"bg_wrmse": [], "bg_bias": [], "ana_wrmse": [], "ana_bias": []}
     a.model_mean, a.model_std, a.model_mean_gpu, a.model_std_gpu = a.get_model_mean_std()
     a.vae, a.flow_model = vae, flow
-    prob = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250620)
+    prob = make_problem(nch=69, Hs=721, Ws=1440, T=T, seed=seed)
     t = lambda k: torch.from_numpy(prob[k])
     old_cuda = torch.Tensor.cuda
     torch.Tensor.cuda = lambda self, *args, **kw: self
@@ -322,13 +330,30 @@ def g6(tr):
         torch.Tensor.cuda = old_cuda
     log = buf.getvalue()
     J = [(float(m.group(1)), float(m.group(2))) for m in re.finditer(r"loss reg: ([-0-9.e+]+) loss obs: ([-0-9.e+]+)", log)]
-    xa = xa.detach().numpy().astype(np.float32)
+    print(f"{tag} one_step_DA 721x1440 T={T} Nit={nit}: {time.time() - t0:.0f}s, J per pass {J}", flush=True)
+    return J, xa.detach().numpy().astype(np.float32), ls.steps, prob
+
+
+def g6(tr):
+    """G6: the genuine one_step_DA at 721x1440 with T=2 (flow stand-in), Nit=1, seed 20250620 (config 5's grid)."""
+    J, xa, steps, prob = genuine_one_step_da(tr, 2, 1, 20250620, "G6")
     idx = sample_idx(xa.size, 8192, 606)
     flat = xa.reshape(-1).astype(np.float64)
-    print(f"G6 one_step_DA 721x1440 T=2 Nit=1: {time.time() - t0:.0f}s, J per pass {J}")
     np.savez(os.path.join(GOLD, "g6_one_step_da_c5.npz"), J=np.array(J), idx_xa=idx, xa_sample=xa.reshape(-1)[idx],
-             ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]),
+             ls_t=np.array([x[0] for x in steps]), ls_evals=np.array([x[1] for x in steps]),
              xa_sum=flat.sum(), xa_sumsq=(flat * flat).sum(),
+             dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+
+
+def g15(tr):
+    """G15 (BASELINE config 5 at its budget): the genuine one_step_DA at 721x1440, T=2, Nit=5 (the bench's 50-iteration
+    budget), seed 20250620: J per printed pass (4 digits), every line search's (t, evals), sampled xa + sums."""
+    J, xa, steps, prob = genuine_one_step_da(tr, 2, 5, 20250620, "G15")
+    idx = sample_idx(xa.size, 8192, 1515)
+    flat = xa.reshape(-1).astype(np.float64)
+    np.savez(os.path.join(GOLD, "g15_config5_trajectory.npz"), J=np.array(J), idx_xa=idx,
+             xa_sample=xa.reshape(-1)[idx], ls_t=np.array([x[0] for x in steps]),
+             ls_evals=np.array([x[1] for x in steps]), xa_sum=flat.sum(), xa_sumsq=(flat * flat).sum(),
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
 
@@ -485,6 +510,206 @@ def g13(tr):
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
 
+class _RecordingLBFGS(torch.optim.LBFGS):
+    """torch.optim.LBFGS as da_4dvar.py:1119 builds it, recording every closure value; with `fixed` set, step()
+    instead puts the control variable at `fixed`, evaluates the reference's closure once and records J and dJ/dw
+    (one genuine loss + backward, da_4dvar.py:1099-1107)."""
+
+    fixed = None
+    log = None
+
+    def step(self, closure):
+        w = self.param_groups[0]["params"][0]
+        if _RecordingLBFGS.fixed is not None:
+            with torch.no_grad():
+                w.copy_(_RecordingLBFGS.fixed)
+            v = closure()
+            _RecordingLBFGS.log.append((float(v.detach()), w.grad.detach().clone()))
+            return v
+
+        def rec():
+            v = closure()
+            _RecordingLBFGS.log.append((float(v.detach()), None))
+            return v
+
+        out = super().step(rec)
+        _RecordingLBFGS.w = w.detach().clone()
+        return out
+
+
+G14_NIT = 2
+
+
+def g14(tr):
+    """G14: the reference's OWN sc4dvar code around the SHT — get_static_info (da_4dvar.py:608-638:
+    zonal kernel, its SHT, sph_scale, R), transform (:878-931: the 11/len^2 scaling, balance regression, std_sur,
+    vertical EOFs, partial_x / partial_y incl. torch.gradient, the 721x1440 interpolation, + xb), and the loss +
+    backward and L-BFGS pass of one_step_DA(..., 'sc4dvar') (:1064-1177) — with the oracle's float64 SHT installed as
+    torch_harmonics.RealSHT / InverseRealSHT (absent here; the SHT itself stays unpinned). B statistics: the
+    reference's dataset/bq_info_lr; obs_var from the genuine data_reader (:106-127, modify_tp 2), q_type -1.
+    Two runs: (a) float64 default dtype (the B statistics as float64) — the restatement must match it to float64
+    rounding; (b) the reference as it runs (float32; the SHT stub computes in float64 and rounds to float32) — the
+    GPU fixture."""
+    import contextlib
+    import importlib
+    import io
+
+    from oracle.sc4dvar_ref import SHT, Sc4dvarRef, load_bq
+
+    class RealSHTStub(torch.nn.Module):
+        def __init__(self, nlat, nlon, grid="equiangular"):
+            super().__init__()
+            assert grid == "equiangular"
+            self.s = SHT(nlat, nlon)
+
+        def forward(self, x):
+            y = self.s.forward(x.to(torch.float64))
+            return y.to(torch.complex128 if x.dtype == torch.float64 else torch.complex64)
+
+    class InverseRealSHTStub(RealSHTStub):
+        def forward(self, a):
+            y = self.s.inverse(a.to(torch.complex128))
+            return y.to(torch.float64 if a.dtype == torch.complex128 else torch.float32)
+
+    cwd = os.getcwd()
+    os.chdir(ref_harness.REF)
+    da = importlib.import_module("da_4dvar")
+    metrics = importlib.import_module("utils.metrics")
+    os.chdir(cwd)
+    da.RealSHT, da.InverseRealSHT = RealSHTStub, InverseRealSHTStub
+    da.Client = lambda *a, **k: None
+    lbfgs_orig = torch.optim.LBFGS
+    da.optim.LBFGS = _RecordingLBFGS  # da.optim is torch.optim: restored below
+    coeff_dir = os.path.join(ref_harness.REF, "dataset", "bq_info_lr")
+    # 3e-4 of the 721x1440 columns observed (~300, as the 1 % of a 128x256 grid): at 1 % the B-transformed problem is
+    # so stiff that the first line search ends at t ~ 7e-9 with J unchanged in fp32 and L-BFGS stops (tolerance_change)
+    prob = make_problem(nch=69, Hs=721, Ws=1440, T=1, seed=1414, obs_frac=3e-4)
+    ws = {"w1": uniform_sym(1401, (69, 128, 256), 0.5), "w2": 0.3 * smooth_field(1402, (69, 128, 256), sigma=3.0)}
+    old_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *args, **kw: self
+    idx = sample_idx(69 * 721 * 1440, 8192, 1414)
+    gidx = sample_idx(69 * 128 * 256, 8192, 1415)
+    st = lambda v, tag: v.astype(np.float32) if tag == "f32" else v  # the float32 run's values are float32
+    try:
+        res = {}
+        for tag, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            torch.set_default_dtype(dt)
+            a = object.__new__(da.cyclic_4dvar)
+            a.device, a.hpad, a.nchannel, a.nlev, a.nlat, a.nlon = "cpu", 112, 69, 13, 721, 1440
+            a.da_win, a.q_type, a.scale_factor, a.obs_coeff, a.obs_type, a.Nit = 1, -1, 1.0, 1.0, "synthetic", G14_NIT
+            a.use_eval, a.current_time = False, "G14"
+            a.metric = metrics.Metrics()
+            a.metrics_list = {"bg_wrmse": [], "bg_bias": [], "ana_wrmse": [], "ana_bias": []}
+            a.b_matrix = a.init_b_matrix(coeff_dir)
+            if dt == torch.float64:  # init_b_matrix's .float() kept out of the float64 run
+                a.b_matrix = {k: torch.from_numpy(np.load(os.path.join(coeff_dir, k + ".npy"))).double() for k in a.b_matrix}
+                a.b_matrix["len_scale"] = a.b_matrix["len_scale"] * a.scale_factor
+            a.q_matrix = a.init_q_matrix(coeff_dir)
+            a.model_mean, a.model_std, a.model_mean_gpu, a.model_std_gpu = a.get_model_mean_std()
+            a.obs_interp = da.obs_interpolater(13, 40)
+            a.data_reader = da.data_reader("synthetic", 0.005, a.model_std, 1, None, None, a.obs_interp, modify_tp=2)
+            with contextlib.redirect_stdout(io.StringIO()):
+                a.static_info = a.get_static_info()
+            R = a.static_info["R"]
+            r_ch = R[0, :, 0, 0].double().numpy()
+            assert torch.equal(R, R[:, :, :1, :1].expand_as(R)), "R is spatially constant"
+            xb = torch.from_numpy(prob["xb"]).to(dt)
+            t0 = time.time()
+            for wk in ("w1", "w2"):
+                w = torch.from_numpy(ws[wk]).to(dt)
+                with torch.no_grad():
+                    inc = a.transform(w, 0.0)
+                    x = a.transform(w, xb)
+                fi = inc.reshape(-1).double().numpy()
+                fx = x.reshape(-1).double().numpy()
+                res[f"{tag}_{wk}_inc"] = st(fi[idx], tag)
+                res[f"{tag}_{wk}_inc_sumsq"] = float((fi * fi).sum())
+                res[f"{tag}_{wk}_inc_sum"] = float(fi.sum())
+                if tag == "f32":
+                    res[f"{tag}_{wk}_x"] = st(fx[idx], tag)
+            print(f"G14 {tag}: genuine transform x2 at 721x1440 ({time.time() - t0:.1f}s)", flush=True)
+            # one genuine loss + backward at w1 (one_step_DA's own closure, T = 1)
+            g = {k: torch.from_numpy(prob[k]).to(dt) for k in ("gt", "yo", "H")}
+            _RecordingLBFGS.fixed, _RecordingLBFGS.log = torch.from_numpy(ws["w1"]).to(dt), []
+            with contextlib.redirect_stdout(io.StringIO()):
+                a.one_step_DA(g["gt"], xb, g["yo"], g["H"], R, "sc4dvar")
+            J, grad = _RecordingLBFGS.log[0]
+            gg = grad.reshape(-1).double().numpy()
+            res[f"{tag}_J"], res[f"{tag}_grad"] = J, st(gg[gidx], tag)
+            res[f"{tag}_grad_sumsq"] = float((gg * gg).sum())
+            print(f"G14 {tag}: genuine sc4dvar loss at w1 J {J:.10e} |g| {np.sqrt((gg * gg).sum()):.6e}", flush=True)
+            if tag == "f32":
+                # the genuine Nit = G14_NIT passes (LBFGS history 10, max_iter 5, strong Wolfe) from w = 0
+                _RecordingLBFGS.fixed, _RecordingLBFGS.log = None, []
+                with contextlib.redirect_stdout(io.StringIO()), LineSearchRecorder() as ls:
+                    xhat = a.one_step_DA(g["gt"], xb, g["yo"], g["H"], R, "sc4dvar")
+                fx = xhat.detach().reshape(-1).double().numpy()
+                xbf = prob["xb"].reshape(-1).astype(np.float64)
+                wf = _RecordingLBFGS.w.double()
+                jo_f = 0.5 * float(((g["H"][0].double() * (xhat.detach().double() - g["yo"][0].double()) ** 2)
+                                    / R[0].double()).sum())
+                res["J_final"] = (0.5 * float((wf * wf).sum()), jo_f)
+                res.update(lbfgs_J=np.array([v for v, _ in _RecordingLBFGS.log]),
+                           ls_t=np.array([t for t, _ in ls.steps]), ls_evals=np.array([n for _, n in ls.steps]),
+                           xa_inc=(fx - xbf)[idx].astype(np.float32), xa_dsumsq=float(((fx - xbf) ** 2).sum()))
+                print(f"G14 f32: genuine Nit={G14_NIT} passes: evals {len(_RecordingLBFGS.log)}, J {res['lbfgs_J'][0]:.6e} -> "
+                      f"final (J_b, J_o) {res['J_final']}, line searches {ls.steps}", flush=True)
+            res[f"{tag}_R"] = r_ch
+            # the restatement on the same inputs
+            torch.set_default_dtype(torch.float32)
+            p64 = dict(prob, R=R.double().numpy())
+            ref = Sc4dvarRef(load_bq(coeff_dir), p64, const_dtype=dt)
+            for wk in ("w1", "w2"):
+                w = torch.from_numpy(ws[wk]).double()
+                inc = ref.state(w) - ref.xb
+                e = rel(inc.reshape(-1).numpy()[idx], res[f"{tag}_{wk}_inc"])
+                print(f"G14 {tag} {wk}: restatement vs reference transform increment rel {e:.2e}", flush=True)
+                assert e < (1e-11 if tag == "f64" else 1e-5), e
+            wr = torch.from_numpy(ws["w1"]).double().requires_grad_(True)
+            lv = ref.loss(wr)
+            lv.backward()
+            ej = abs(float(lv) - res[f"{tag}_J"]) / abs(res[f"{tag}_J"])
+            eg = rel(wr.grad.reshape(-1).numpy()[gidx], res[f"{tag}_grad"])
+            print(f"G14 {tag}: restatement vs reference loss J rel {ej:.2e} grad rel {eg:.2e}", flush=True)
+            assert ej < (1e-11 if tag == "f64" else 1e-5) and eg < (1e-10 if tag == "f64" else 1e-4), (ej, eg)
+    finally:
+        torch.Tensor.cuda = old_cuda
+        torch.optim.LBFGS = lbfgs_orig
+        torch.set_default_dtype(torch.float32)
+    np.savez(os.path.join(GOLD, "g14_sc4dvar_reference.npz"), idx=idx, gidx=gidx, seed=1414, obs_frac=3e-4, nit=G14_NIT,
+             **res)
+
+
+def g16(tr):
+    """G16 (BASELINE config 4 at full size): the reference's networks_old.LGUnet_all decoder and the flow stand-in in
+    the restated 4D-Var closure with T = 6 (five integrate steps, da_4dvar.py:1183-1208, :666-681),
+    torch.optim.LBFGS(history 10, max_iter 10, strong Wolfe), Nit = 3 outer passes at 128x256, seed 20250620 (the
+    bench's config-4 rank-0 analysis): J per pass, every line search's (t, evals), sampled xa. Parameters frozen as
+    in G10/G13 (the unused weight gradients only cost time)."""
+    m, _ = build_ref(tr, C.DECODER)
+    fm, _ = build_ref(tr, {k: v for k, v in C.FLOW.items() if k != "arch"})
+    for v in list(m.parameters()) + list(fm.parameters()):
+        v.requires_grad_(False)
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=6, seed=20250620)
+    rp = RefProblem(prob, m, C.DECODER["img_size"], fm)
+    t0 = time.time()
+    with LineSearchRecorder() as ls:
+        xa, z, js, nev, nit = one_step_da_ref(rp, G16_NIT, (32, 128, 256),
+                                              log=lambda k, j: print(f"G16 pass {k}: J_b {j[0]:.6e} J_o {j[1]:.6e} "
+                                                                     f"({time.time() - t0:.0f}s)", flush=True))
+    xa = xa.numpy().astype(np.float32)
+    idx = sample_idx(xa.size, 8192, 1616)
+    flat = xa.reshape(-1).astype(np.float64)
+    print(f"G16 config-4 trajectory: {time.time() - t0:.0f}s, evals {nev}, iters {nit}, J {js}")
+    np.savez(os.path.join(GOLD, "g16_config4_trajectory.npz"), J=np.array(js, np.float64), n_eval=nev, n_iter=nit,
+             nit=G16_NIT, ls_t=np.array([x[0] for x in ls.steps]), ls_evals=np.array([x[1] for x in ls.steps]),
+             idx_xa=idx, xa_sample=xa.reshape(-1)[idx], xa_sum=flat.sum(),
+             dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
+
+
+G16_NIT = 3
+
+
 def g11():
     """G11: the reference's networks.LGUnet_all.LGUnet_all_1 at the full 0.25-degree
     configuration (training_options.yaml:64-119: 69ch 721x1440, 16,200-token global LG window), synthetic weights,
@@ -549,6 +774,8 @@ def main():
     ap.add_argument("--g10", action="store_true", help="also generate G10 (config-2 trajectory, Nit 10, ~10 min)")
     ap.add_argument("--g11", action="store_true", help="also generate G11 (0.25-deg LGUnet_all_1 forward, ~3 min)")
     ap.add_argument("--g13", action="store_true", help="also generate G13 (config-3 T=2 trajectory, Nit 10, ~30 min)")
+    ap.add_argument("--g15", action="store_true", help="also generate G15 (genuine one_step_DA, config 5, Nit 5, ~25 min)")
+    ap.add_argument("--g16", action="store_true", help="also generate G16 (config-4 T=6 trajectory, Nit 3, ~20 min)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.set_num_threads(8)
@@ -556,7 +783,7 @@ def main():
     tr, sb = ref_harness.import_reference()
     os.chdir(cwd)
     steps = {"g1": lambda: g1(tr), "g2": lambda: g2(sb), "g4": g4, "g5": lambda: g5(tr), "g5b": lambda: g5b(tr),
-             "g7": g7, "g9": g9, "g12": lambda: g12(tr)}
+             "g7": g7, "g9": g9, "g12": lambda: g12(tr), "g14": lambda: g14(tr)}
     if a.full:
         steps["g3"] = lambda: g3(tr)
     if a.g6:
@@ -569,6 +796,10 @@ def main():
         steps["g11"] = g11
     if a.g13:
         steps["g13"] = lambda: g13(tr)
+    if a.g15:
+        steps["g15"] = lambda: g15(tr)
+    if a.g16:
+        steps["g16"] = lambda: g16(tr)
     for k, f in steps.items():
         if a.only and k not in a.only.split(","):
             continue

@@ -94,3 +94,43 @@ def test_bq_fixture_is_the_reference_data():
     with np.load(BQ) as z:
         for k in ("len_scale", "reg_coeff", "std_sur", "vert_eig_value", "vert_eig_vec"):
             assert np.array_equal(z[k], np.load(os.path.join(src, k + ".npy")))
+
+
+def g14_inputs():
+    """The inputs of G14 (oracle/make_golden.py g14), regenerated from the counter-hash RNG: the 721x1440 problem
+    (T = 1, 3e-4 of the columns observed) with the genuine get_static_info R per channel, and the two w fields."""
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field, uniform_sym
+
+    g = np.load(os.path.join(GOLD, "g14_sc4dvar_reference.npz"))
+    p = make_problem(nch=69, Hs=721, Ws=1440, T=1, seed=int(g["seed"]), obs_frac=float(g["obs_frac"]))
+    ws = {"w1": uniform_sym(1401, (69, 128, 256), 0.5), "w2": 0.3 * smooth_field(1402, (69, 128, 256), sigma=3.0)}
+    return g, p, ws
+
+
+@pytest.mark.parametrize("run", ["f64", "f32"])
+def test_g14_oracle_vs_reference_code(run):
+    """G14 pins the restatement to the reference's OWN sc4dvar code (get_static_info, transform, the one_step_DA
+    loss + backward, da_4dvar.py:608-638, 878-931, 1064-1107) with the oracle's SHT injected as the torch_harmonics
+    stub: to float64 rounding against the reference run with float64 as its default dtype, to float32 rounding
+    against the reference as it runs (float32). The SHT itself stays unpinned (torch_harmonics absent)."""
+    from oracle.sc4dvar_ref import Sc4dvarRef, load_bq
+
+    g, p, ws = g14_inputs()
+    R = np.broadcast_to(g[f"{run}_R"][None, :, None, None], p["R"].shape)
+    ref = Sc4dvarRef(load_bq(npz=BQ), dict(p, R=R), const_dtype=torch.float64 if run == "f64" else torch.float32)
+    tol_x, tol_j, tol_g = (1e-11, 1e-11, 1e-10) if run == "f64" else (1e-5, 1e-5, 1e-4)
+    for wk in ("w1", "w2"):
+        inc = (ref.state(torch.from_numpy(ws[wk]).double()) - ref.xb).reshape(-1).numpy()
+        e = float(np.abs(inc[g["idx"]] - g[f"{run}_{wk}_inc"]).max() / np.abs(g[f"{run}_{wk}_inc"]).max())
+        e_s = abs(float((inc * inc).sum()) - float(g[f"{run}_{wk}_inc_sumsq"])) / float(g[f"{run}_{wk}_inc_sumsq"])
+        print(f"G14 {run} {wk}: transform increment rel {e:.2e}, sum of squares rel {e_s:.2e}")
+        assert e < tol_x and e_s < tol_x
+    w = torch.from_numpy(ws["w1"]).double().requires_grad_(True)
+    lv = ref.loss(w)
+    lv.backward()
+    gr = w.grad.reshape(-1).numpy()
+    e_j = abs(float(lv.detach()) - float(g[f"{run}_J"])) / float(g[f"{run}_J"])
+    e_g = float(np.abs(gr[g["gidx"]] - g[f"{run}_grad"]).max() / np.abs(g[f"{run}_grad"]).max())
+    print(f"G14 {run}: loss J rel {e_j:.2e}, dJ/dw rel {e_g:.2e}")
+    assert e_j < tol_j and e_g < tol_g
