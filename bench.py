@@ -158,6 +158,32 @@ def cpu_baseline(prob_np, T, evals_per_iter, gpu_evals_per_analysis, evals, thre
     return per_eval, out
 
 
+def grid_cost_s(prob_np, T, threads, reps=1):
+    """Seconds per oracle closure evaluation of everything that scales with the state grid (the decoder_hr / integrate
+    nearest interpolations, the misfit J_o over T x 69 x Hs x Ws and their backward) with the two networks replaced by
+    trivial maps of the same shapes: the grid-dependent part of one evaluation, for extrapolating a 721x1440 CPU
+    closure from a measured 128x256 one without a minutes-long oracle run."""
+    import torch
+
+    from oracle.da_ref import RefProblem
+
+    torch.set_num_threads(threads)
+    dec = lambda z: torch.cat([z, z, z[:, :5]], 1) * 0.01     # (1,32,128,256) -> (1,69,128,256)
+    flow = (lambda x: torch.cat([x, x], 1)) if T > 1 else None
+    rp = RefProblem(prob_np, dec, (128, 256), flow)
+    z = torch.zeros(1, 32, 128, 256, requires_grad=True)
+
+    def ev():
+        z.grad = None
+        rp.loss(z).backward()
+
+    ev()
+    t0 = time.time()
+    for _ in range(reps):
+        ev()
+    return (time.time() - t0) / reps
+
+
 def cpu_convergence_measured():
     """The measured full CPU convergence of config 2 (tools/cpu_convergence.py on the GPU box's host cores: the
     oracle restatement + torch.optim.LBFGS, Nit 10, weight grads on), committed under profiles/ (SURVEY §8 d)."""
@@ -307,6 +333,7 @@ def timed_analyses(w, ensemble, steps, dev):
     ensemble.barrier()
     w.sync()
     t0 = time.perf_counter()
+    c0 = time.process_time()
     iters = evals = 0
     shapes = None
     for _ in range(steps):
@@ -317,8 +344,10 @@ def timed_analyses(w, ensemble, steps, dev):
     w.sync()
     ensemble.barrier()
     el = time.perf_counter() - t0
+    cpu = time.process_time() - c0  # host CPU seconds of this rank (all its threads) over the timed region
     return (ensemble.reduce_scalar(el, "max", dev), ensemble.reduce_scalar(iters, "sum", dev),
-            ensemble.reduce_scalar(evals, "sum", dev), shapes)
+            ensemble.reduce_scalar(evals, "sum", dev), shapes,
+            (ensemble.reduce_scalar(cpu, "max", dev), ensemble.reduce_scalar(cpu, "sum", dev)))
 
 
 def sub_record(w, cid, ensemble, dev, size, batch):
@@ -382,7 +411,7 @@ def main():
 
     for _ in range(args.warmup):
         w.analysis()
-    t_max, iters, evals, shapes = timed_analyses(w, ensemble, args.steps, dev)
+    t_max, iters, evals, shapes, host_cpu = timed_analyses(w, ensemble, args.steps, dev)
 
     prof = None
     exact = None
@@ -463,11 +492,25 @@ def main():
         "ms_per_eval": 1e3 * t_max * size / max(evals, 1),
         "analyses_per_s": size * args.batch * args.steps / t_max,
         "gathered": [list(s) for s in shapes] if shapes else None,
+        # host CPU the ranks' Python drivers (L-BFGS mirror, launches, syncs) use in the timed region: at 8 ranks on
+        # one node, 8 x cpu_frac_max_rank CPUs against the box's CPU quota
+        "host_cpu": {"cpu_s_max_rank": host_cpu[0], "cpu_s_all_ranks": host_cpu[1],
+                     "cpu_frac_max_rank": host_cpu[0] / max(t_max, 1e-12),
+                     "cpus_busy_all_ranks": host_cpu[1] / max(t_max, 1e-12)},
         "timed_region": f"barrier + sync, {args.steps} step(s) of {args.batch} analyses per rank (z = 0, Nit = {cfg['nit']} outer lbfgs.step "
                         "calls, the analysis decode, at N > 1 the RCCL gather of every analysis to rank 0), sync + "
                         "barrier; max over ranks. The per-outer-pass logging evaluation cal_loss and WRMSE/Bias "
                         "(da_4dvar.py:1256-1269, SURVEY §8 a3; 1 forward per pass) is not run in it",
     }
+    out["headline_config"] = (f"BASELINE config {args.config} (" + {2: "vae4dvar, da_win=1: 3D-Var with the full VAE "
+                              "decoder, the da_4dvar_script.sh default window", 3: "vae4dvar, da_win=2: 4D-Var with the "
+                              "flow stand-in", 4: "vae4dvar, da_win=6", 5: "vae4dvar, da_win=2 at 721x1440"}[args.config]
+                              + "); `value` measures this config. The 4D-Var (da_win = 2) figure is `value_4dvar` "
+                              "(the config3 sub-record)")
+    if 3 in subs:
+        out["value_4dvar"] = subs[3]["iters_per_s"]
+    elif args.config == 3:
+        out["value_4dvar"] = out["value"]
     if j_info:
         out["J_start"], out["J_final"] = j_info
     if exact:
@@ -567,6 +610,25 @@ def main():
             rec["speedup_vs_cpu"] = rec["iters_per_s"] / cb["value"]
             rec["wall_clock_speedup_vs_cpu"] = (cb["wall_clock_to_convergence_s_extrapolated"] * rec["analyses"]
                                                 / rec["wall_clock_s"])
+        if 2 in per_eval_T and 5 in subs and subs[5].get("_prob_np") is not None:
+            # config 5 (721x1440, T = 2): the measured 128x256 T = 2 closure + the measured grid-dependent part at
+            # 721x1440 minus the same at 128x256 (grid_cost_s); one full oracle evaluation there takes minutes
+            rec = subs[5]
+            from vaevar.problem import make_problem
+
+            small = make_problem(nch=69, Hs=128, Ws=256, T=2, seed=20250620)
+            g_big, g_small = grid_cost_s(rec["_prob_np"], 2, threads), grid_cost_s(small, 2, threads)
+            s5 = per_eval_T[2] + g_big - g_small
+            epi = rec["evals"] / max(rec["iters"], 1)
+            rec["cpu_baseline"] = {"value": 1.0 / (s5 * epi), "unit": "L-BFGS iters/s", "cores": threads,
+                                   "kind": "port (extrapolated)", "s_per_eval": s5,
+                                   "wall_clock_to_convergence_s_extrapolated": s5 * rec["evals"] / max(rec["analyses"], 1),
+                                   "sample": f"not run at 721x1440: s/eval = s(T=2, 128x256, measured above) + grid "
+                                             f"part at 721x1440 - grid part at 128x256 = {per_eval_T[2]:.3f} + "
+                                             f"{g_big:.3f} - {g_small:.3f} (grid part: the oracle closure's nearest "
+                                             f"interpolations and misfit with the networks replaced by trivial maps, "
+                                             f"1 evaluation after 1 warm-up each, {threads} threads)"}
+            rec["speedup_vs_cpu"] = rec["iters_per_s"] / rec["cpu_baseline"]["value"]
         if 1 in per_eval_T and 2 in per_eval_T and 4 in subs:
             # per evaluation: decoder (T = 1) + (T - 1) flow steps, each step's cost = s(T=2) - s(T=1)
             a, b = per_eval_T[1], per_eval_T[2] - per_eval_T[1]

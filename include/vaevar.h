@@ -109,6 +109,14 @@ int vv_closure_async(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, vo
    ~540 kernel launches are captured once per kind (J only / J + gradient) and replayed as one graph launch, with z
    and grad_z copied through problem-owned buffers; results are bit-identical to the eager launches */
 int vv_set_closure_graph(vv_ctx* ctx, int enable);
+/* state of the closure graph of one kind (0: J only, 1: J + gradient) since the last bind / vv_set_closure_graph:
+   info[0] graphs enabled, info[1] graph instantiated, info[2] capture failed (this kind runs eagerly: a silent
+   slowdown otherwise, the results are identical), info[3] graph launches */
+int vv_get_closure_graph(vv_ctx* ctx, int kind, long long* info);
+/* process-wide host-side launch counters (monotonic; eager launches only, a graph replay does not count):
+   "rowsplit" (k_rowsplit passes building a GEMM's fp16x3 A planes), "fixup_ln" (split-K fixups fused into a
+   LayerNorm), "splitk_fixup" (stand-alone tile-48 split-K fixups). Tests use them to show a fused path ran. */
+int vv_get_counter(const char* name, long long* value);
 /* analysis states xa (B,C,Hs,Ws) */
 int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
 /* out = integrate(x, model, steps) (da_4dvar.py:666-681): z = (x - mean)/std (nearest to the model grid when

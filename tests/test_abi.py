@@ -140,3 +140,25 @@ def test_tuning_api_keys_and_rejection():
     assert lib.vv_set_debug_sync(0) == 0
     so = open(_lib.LIB_PATH, "rb").read()
     assert b"VAEVAR_" not in so and b"getenv" not in so
+
+
+def test_launch_counters_abi():
+    """vv_get_counter (host-side, no GPU needed): the named fused-path counters exist, unknown names fail cleanly."""
+    from vaevar import _lib
+    from vaevar.engine import Context
+
+    for name in ("rowsplit", "fixup_ln", "splitk_fixup"):
+        assert Context.counter(name) >= 0
+    with pytest.raises(_lib.VVError, match="unknown counter"):
+        Context.counter("nope")
+
+
+@pytest.mark.parametrize("var,val,msg", [("VAEVAR_GEMM_MATH", "fp8", "VAEVAR_GEMM_MATH"),
+                                         ("VAEVAR_H3_MINK", "big", "not an integer")])
+def test_context_env_validated_before_create(monkeypatch, var, val, msg):
+    """A bad VAEVAR_* value raises before the native context exists (no handle or device buffers leak)."""
+    from vaevar.engine import Context
+
+    monkeypatch.setenv(var, val)
+    with pytest.raises(ValueError, match=msg):
+        Context(0)

@@ -40,6 +40,28 @@ def test_bench_spawns_its_ranks():
         assert k in out
 
 
+def test_bench_spawns_eight_ranks():
+    """Config 4's layout (8 analyses, one per GPU of a node) on CPU: `bench.py --gpus 8` spawns 8 ranks over gloo;
+    rank 0 receives 8 (69, 128, 256) analyses per step, the iterations are summed over the ranks, the time is the
+    slowest rank's (the stand-in analysis of rank r sleeps 10 (1 + r) ms, so rank 7 sets it), and the host-CPU record
+    covers all ranks."""
+    p = _run("--gpus", "8", "--selftest", "--steps", "2", "--warmup", "1", env={"OMP_NUM_THREADS": "1"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8
+    assert out["iters"] == 2 * sum(97 + r for r in range(8)) and out["evals"] == 2 * sum(110 + r for r in range(8))
+    assert out["gathered"] == [[69, 128, 256]] * 8
+    assert out["ms_per_step"] >= 80.0  # max over ranks: rank 7's 80 ms stand-in
+    assert out["value"] == out["iters"] / (out["ms_per_step"] * 1e-3 * out["steps"])
+    c4 = out["config4"]
+    assert c4["n_gpus"] == 8 and c4["analyses"] == 8 and c4["gathered"] == [[69, 128, 256]] * 8
+    assert c4["iters"] == sum(97 + r for r in range(8)) and c4["wall_clock_s"] >= 0.08
+    hc = out["host_cpu"]
+    assert hc["cpu_s_all_ranks"] >= hc["cpu_s_max_rank"] > 0
+
+
 def test_bench_world_size_must_match():
     p = _run("--gpus", "2", "--selftest", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr

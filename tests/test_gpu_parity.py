@@ -405,10 +405,15 @@ def test_closure_graph_replay_bitwise():
         for mode in ("eager", "graph"):
             prob.ctx.set_closure_graph(mode == "graph")
             res = one_step_da(prob, nit=1)
-            out[mode] = (res["J"], res["xa"].cpu(), res["n_eval"])
+            out[mode] = (res["J"], res["xa"].cpu(), res["n_eval"], prob.ctx.closure_graph_state(1))
     finally:
         prob.ctx.set_closure_graph(True)
-    print("graph vs eager J", out["graph"][0], out["eager"][0], "evals", out["graph"][2], out["eager"][2])
+    print("graph vs eager J", out["graph"][0], out["eager"][0], "evals", out["graph"][2], out["eager"][2],
+          "graph state", out["graph"][3], "eager state", out["eager"][3])
+    # the graph path was actually taken (a failed capture would fall back to eager launches with equal results)
+    st = out["graph"][3]
+    assert st["enabled"] and st["instantiated"] and not st["eager_only"] and st["launches"] >= out["graph"][2] - 2
+    assert out["eager"][3]["launches"] == 0
     assert out["graph"][0] == out["eager"][0] and out["graph"][2] == out["eager"][2]
     assert torch.equal(out["graph"][1], out["eager"][1])
 
@@ -472,6 +477,7 @@ def test_ln_planes_bitwise(full_dec):
     prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
     z = torch.from_numpy(0.3 * smooth_field(11, (1, 32, 128, 256), sigma=2.0)).cuda()
     out = []
+    rowsplits = []
     try:
         for v in (1, 0):
             prob.ctx.set_tuning("ln_planes", v)
@@ -479,11 +485,16 @@ def test_ln_planes_bitwise(full_dec):
             jb, jo = prob.closure(z, g)
             jb2, jo2 = prob.closure(z, None)
             out.append((jb, jo, jb2, jo2, g.clone()))
+            # the fused path really runs: without LN-written planes every LN-fed tile-48 GEMM adds a k_rowsplit pass
+            c0 = prob.ctx.counter("rowsplit")
+            full_dec.forward_raw(z)
+            rowsplits.append(prob.ctx.counter("rowsplit") - c0)
     finally:
         prob.ctx.set_tuning("ln_planes", 1)
-    print(f"LN planes on/off: J {out[0][:2]} vs {out[1][:2]}")
+    print(f"LN planes on/off: J {out[0][:2]} vs {out[1][:2]}; k_rowsplit passes per decoder forward {rowsplits}")
     assert out[0][:4] == out[1][:4]
     assert torch.equal(out[0][4], out[1][4])
+    assert rowsplits[0] + 24 <= rowsplits[1], rowsplits  # qkv + fc1 of the 12 LG blocks read LN planes
 
 
 def test_ln_row_scales_bitwise(tmp_path):
@@ -611,18 +622,29 @@ def test_fixup_ln_bitwise(full_dec):
     prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
     zc = torch.from_numpy(0.3 * smooth_field(423, (1, 32, 128, 256))).cuda()
     res = []
+    ln_launches, fused = [], []
     default = full_dec.ctx.get_tuning("fixup_ln")
     try:
         for v in (0, 1):
             full_dec.ctx.set_tuning("fixup_ln", v)
+            full_dec.ctx.profile_start()
+            c0 = full_dec.ctx.counter("fixup_ln")
             out = full_dec.forward_raw(z).clone()
             dz = torch.empty_like(z)
             full_dec.backward_raw(cot, dz)
+            ln_launches.append(full_dec.ctx.profile_stop()["layernorm"]["launches"])
+            fused.append(full_dec.ctx.counter("fixup_ln") - c0)
             g = torch.empty_like(zc)
             jb, jo = prob.closure(zc, g)
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning("fixup_ln", default)
+    # the fused path really ran (gemm_ln falls back to separate launches when it returns hipErrorNotSupported):
+    # the LG-stage LayerNorms after split-K GEMMs (proj -> LN2, fc2 -> next LN1, and their backward) leave the
+    # LayerNorm class
+    print(f"fixup_ln 0 / 1: LayerNorm-class launches per forward + backward {ln_launches}, fused fixup + LayerNorm "
+          f"launches {fused}")
+    assert fused[0] == 0 and fused[1] >= 24 and ln_launches[1] <= ln_launches[0] - 24, (ln_launches, fused)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     print(f"fixup_ln 1 vs 0: out max diff {(o1 - o0).abs().max().item():.1e}, grad {(d1 - d0).abs().max().item():.1e}, "
           f"J {jb1 + jo1 - jb0 - jo0:.1e}, dJ/dz {(g1 - g0).abs().max().item():.1e}")

@@ -334,6 +334,7 @@ struct vv_ctx {
     hipGraphExec_t exec = nullptr;
     int eager_runs = 0;
     bool eager_only = false;  // capture or instantiation failed once: this kind runs eagerly until rebind
+    long long launches = 0;   // graph launches since the last rebind / vv_set_closure_graph (vv_get_closure_graph)
   } graphs[2];
   hipStream_t cap_stream = nullptr;
   bool use_graphs = true;  // vv_set_closure_graph / VAEVAR_GRAPH
@@ -1669,7 +1670,10 @@ int closure_graphed(vv_ctx* ctx, const float* z, float* grad_z, double* d_J, hip
         if (r2) return r2;
       }
     }
-    if (g.exec) VV_HIP(hipGraphLaunch(g.exec, st));
+    if (g.exec) {
+      VV_HIP(hipGraphLaunch(g.exec, st));
+      ++g.launches;
+    }
   }
   if (grad_z) VV_HIP(hipMemcpyAsync(grad_z, P.GZ, P.zn * sizeof(float), hipMemcpyDeviceToDevice, st));
   if (d_J) VV_HIP(hipMemcpyAsync(d_J, P.dJ, 2 * P.B * sizeof(double), hipMemcpyDeviceToDevice, st));
@@ -2262,6 +2266,27 @@ int vv_set_closure_graph(vv_ctx* ctx, int enable) {
   if (r) return r;
   drop_graphs(ctx);
   ctx->use_graphs = enable != 0;
+  return 0;
+}
+
+int vv_get_counter(const char* name, long long* value) {
+  if (!name || !value) return fail(VV_E_ARG, "null argument");
+  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup"};
+  for (int c = 0; c < vv::CNT_N; ++c)
+    if (!strcmp(name, names[c])) {
+      *value = vv::launch_count(c);
+      return 0;
+    }
+  return fail(VV_E_ARG, "unknown counter '%s'", name);
+}
+
+int vv_get_closure_graph(vv_ctx* ctx, int kind, long long* info) {
+  if (!ctx || !info || kind < 0 || kind > 1) return fail(VV_E_ARG, "null context / info or kind not 0 / 1");
+  const auto& g = ctx->graphs[kind];
+  info[0] = ctx->use_graphs ? 1 : 0;
+  info[1] = g.exec ? 1 : 0;
+  info[2] = g.eager_only ? 1 : 0;
+  info[3] = g.launches;
   return 0;
 }
 

@@ -1002,12 +1002,9 @@ hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st, co
     switch (hd * 8 + NT) {
 #define WM(D, T)                                                                                           \
   case D * 8 + T: {                                                                                        \
-    static bool init = false;                                                                              \
-    if (lds > 65536 && !init) { /* only past 64 KB: the attribute is not needed below */                  \
-      e = hipFuncSetAttribute((const void*)k_attn_win_mf<D, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                              (int)((3 * kWinMaxN * (kWinMaxHd + 1) + kWinMaxN) * 4));                     \
+    if (lds > 65536) { /* only past 64 KB: the attribute is not needed below */                            \
+      e = set_lds_limit((const void*)k_attn_win_mf<D, T>, (3 * kWinMaxN * (kWinMaxHd + 1) + kWinMaxN) * 4); \
       if (e != hipSuccess) return e;                                                                       \
-      init = true;                                                                                         \
     }                                                                                                      \
     hipLaunchKernelGGL((k_attn_win_mf<D, T>), grid, block, lds, st, a, *rope);                             \
     break;                                                                                                 \
@@ -1023,13 +1020,9 @@ hipError_t flash(const FlashArgs& a, int hd, int nwin, int G, hipStream_t st, co
   }
   if (a.N <= kWinMaxN && hd <= kWinMaxHd && hd % 4 == 0 && win_attn) {
     const size_t lds = (3 * (size_t)a.N * (hd + 4) + (size_t)a.N * (a.N + 1)) * sizeof(float);
-    static bool init = false;
-    if (!init) {
-      hipError_t e = hipFuncSetAttribute((const void*)k_attn_win, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)(3 * kWinMaxN * (kWinMaxHd + 4) + kWinMaxN * (kWinMaxN + 1)) * 4);
-      if (e != hipSuccess) return e;
-      init = true;
-    }
+    if (hipError_t e = set_lds_limit((const void*)k_attn_win,
+                                     (size_t)(3 * kWinMaxN * (kWinMaxHd + 4) + kWinMaxN * (kWinMaxN + 1)) * 4))
+      return e;
     hipLaunchKernelGGL(k_attn_win, dim3(nwin, a.heads, G), dim3(256), lds, st, a);
     return hipGetLastError();
   }

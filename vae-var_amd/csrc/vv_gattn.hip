@@ -357,6 +357,8 @@ hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads,
   const int hd = C / heads;
   hipLaunchKernelGGL(k_gattn_max, dim3(kVmaxBlocks, heads), dim3(256), 0, st, a, part);
   const size_t lp = 3 * 32 * (size_t)(hd + 1) * sizeof(float);
+  if (lp > 65536)  // head dim 192: 74 KB
+    if (hipError_t e = set_lds_limit((const void*)k_gattn_prep, 3 * 32 * (size_t)(192 + 1) * sizeof(float))) return e;
   hipLaunchKernelGGL(k_gattn_prep, dim3(a.Np / 32, heads), dim3(256), lp, st, a, (const unsigned*)part);
   const dim3 grid(a.Np / kQB, heads);
   const int qf = qf_per_wave == 1 ? 1 : 2;
@@ -364,13 +366,7 @@ hipError_t gattn(const float* qkv, float* out, int ldo, int N, int C, int heads,
 #define GA(KS, QF)                                                                                          \
   case KS * 4 + QF: {                                                                                       \
     constexpr size_t lds = 3 * (2 * KS * 2 + KS * 2 * 2) * 1024;                                            \
-    static bool init = false;                                                                               \
-    if (!init) {                                                                                            \
-      if (hipError_t e = hipFuncSetAttribute((const void*)k_gattn<KS, QF>,                                  \
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))        \
-        return e;                                                                                           \
-      init = true;                                                                                          \
-    }                                                                                                       \
+    if (hipError_t e = set_lds_limit((const void*)k_gattn<KS, QF>, lds)) return e;                         \
     hipLaunchKernelGGL((k_gattn<KS, QF>), grid, dim3(64 * 8 / QF), lds, st, a);                             \
     break;                                                                                                  \
   }

@@ -34,7 +34,7 @@ __device__ __forceinline__ float dgelu_f(float x) {
 constexpr int KALIGN = 32;  // K, ksplit granularity accepted by gemm_nt (covers every BK variant)
 
 // dynamic-LDS limit of a kernel, set once per (kernel, device): hipFuncSetAttribute acts on the current device
-static hipError_t set_lds_limit(const void* k, size_t lds) {
+hipError_t set_lds_limit(const void* k, size_t lds) {
   static std::mutex mu;
   static std::vector<std::pair<const void*, int>> done;
   int dev = 0;
@@ -1871,6 +1871,7 @@ static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_h4<EPI>), grid, dim3(512), lds, s, a, sc, planes);
   if (tail && !a.nofix)  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
+    count_launch(CNT_SPLITK_FIXUP);
     hipLaunchKernelGGL((k_gemm_fixup_sub16<256, 128, 4, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(512), 0, s, a);
   return hipGetLastError();
 }
@@ -1890,6 +1891,7 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s) {
   } else {
     const dim3 grid((a.M + 3) / 4, 1, a.ngroups);
     const int nv = (a.K + 255) / 256;
+    count_launch(CNT_ROWSPLIT);
     switch (nv <= 5 ? 5 : nv <= 9 ? 9 : nv <= 14 ? 14 : 18) {
       case 5: hipLaunchKernelGGL(k_rowsplit<5>, grid, dim3(256), 0, s, a, sc, a.apl); break;
       case 9: hipLaunchKernelGGL(k_rowsplit<9>, grid, dim3(256), 0, s, a, sc, a.apl); break;

@@ -126,6 +126,10 @@ struct GattnArgs {
   float* qs;                     // [heads][Np] score scale per query: 2^-eq 2^-ek
   float* vsc;                    // [heads] output scale 2^-ev 2^-14
 };
+// raise a kernel's dynamic-LDS limit to `lds` once per (kernel, device) (hipFuncSetAttribute acts on the current
+// device; locked, so concurrent contexts on several devices are safe). The first value set for a kernel stays: callers
+// whose LDS varies pass their maximum.
+hipError_t set_lds_limit(const void* k, size_t lds);
 bool gattn_supported(int C, int heads);
 size_t gattn_ws_bytes(int N, int C, int heads);
 // qf_per_wave: 16-query blocks per wave (2: 4 waves of 32 queries, one per SIMD; 1: 8 waves of 16, two per SIMD)
@@ -418,6 +422,11 @@ void prof_enable(bool on);
 bool prof_enabled();
 // sums since enable: ms, flops, bytes, launches per class (synchronises)
 void prof_read(double* ms, double* flops, double* bytes, int* n);
+// host-side launch counters of the fused-path alternatives (vv_get_counter): tests assert that a fused path really
+// ran, since every fused launcher falls back to the unfused launches with equal results when it does not apply
+enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_N = 3 };
+void count_launch(int c);
+long long launch_count(int c);
 
 hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStream_t s);
 

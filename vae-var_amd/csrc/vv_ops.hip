@@ -6,6 +6,7 @@
 #include "vv_kernels.h"
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 namespace vv {
@@ -30,6 +31,10 @@ void prof_enable(bool on) {
   g_used = 0;
   g_rec.clear();
 }
+static std::atomic<long long> g_counters[CNT_N];
+void count_launch(int c) { g_counters[c].fetch_add(1, std::memory_order_relaxed); }
+long long launch_count(int c) { return g_counters[c].load(std::memory_order_relaxed); }
+
 int prof_begin(hipStream_t s) {
   if (!g_prof_on) return -1;
   if (2 * g_used + 2 > g_ev.size()) {
@@ -468,6 +473,7 @@ hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s
   const int nv = (a.N / 4 + 63) / 64;
   if (nv > 5 || a.N % 4) return hipErrorInvalidValue;
   const dim3 grid((a.M + 7) / 8);
+  count_launch(CNT_FIXUP_LN);
   if (l.bwd) {
     switch (a.tsplit) {
       case 2: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 2>), grid, dim3(512), 0, s, a, l); break;
@@ -1395,10 +1401,8 @@ static int max_k(const PatchArgs& a, bool in) {
 template <typename K>
 static hipError_t patch_launch(K kern, const PatchArgs& a, size_t lds, hipStream_t s) {
   if (a.ngroups <= 0 || a.ngroups > kMaxGroups || lds > 160 * 1024) return hipErrorInvalidValue;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
+  if (lds > 64 * 1024)
+    if (hipError_t e = set_lds_limit((const void*)kern, 160 * 1024)) return e;
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   const int ph = prof_begin(s);
   hipLaunchKernelGGL(kern, dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);

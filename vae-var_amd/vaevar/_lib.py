@@ -104,6 +104,8 @@ _SIGS = {
     "vv_nearest_map": (c_int, [c_int, c_int, P(c_int)]),
     "vv_set_gemm_math": (c_int, [c_void_p, c_int]),
     "vv_set_closure_graph": (c_int, [c_void_p, c_int]),
+    "vv_get_closure_graph": (c_int, [c_void_p, c_int, P(ctypes.c_longlong)]),
+    "vv_get_counter": (c_int, [ctypes.c_char_p, P(ctypes.c_longlong)]),
     "vv_integrate": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                              c_int, c_void_p]),
     "vv_get_gemm_math": (c_int, [c_void_p, P(c_int)]),

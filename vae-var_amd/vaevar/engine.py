@@ -46,18 +46,33 @@ class Context:
     def __init__(self, device: int = 0):
         self.device = device
         self.h = ctypes.c_void_p()
-        check(lib.vv_ctx_create(device, ctypes.byref(self.h)), "ctx_create")
+        # the environment is parsed and validated before the native context exists (a bad value must not leak it)
         env = os.environ
-        if env.get("VAEVAR_GEMM_MATH"):
-            self.gemm_math = env["VAEVAR_GEMM_MATH"]
-        if env.get("VAEVAR_GRAPH", "1")[:1] == "0":
-            self.set_closure_graph(False)
-        if env.get("VAEVAR_SYNC_CHECK", "0")[:1] == "1":
-            check(lib.vv_set_debug_sync(1), "set_debug_sync")
+        math = env.get("VAEVAR_GEMM_MATH") or None
+        if math is not None and math not in self.GEMM_MATH:
+            raise ValueError(f"VAEVAR_GEMM_MATH={math!r}: expected one of {sorted(self.GEMM_MATH)}")
+        tuning = {}
         for k in self.TUNING_KEYS:
             v = env.get("VAEVAR_" + k.upper())
             if v is not None and v != "":
-                self.set_tuning(k, int(v))
+                try:
+                    tuning[k] = int(v)
+                except ValueError:
+                    raise ValueError(f"VAEVAR_{k.upper()}={v!r} is not an integer") from None
+        check(lib.vv_ctx_create(device, ctypes.byref(self.h)), "ctx_create")
+        try:
+            if math is not None:
+                self.gemm_math = math
+            if env.get("VAEVAR_GRAPH", "1")[:1] == "0":
+                self.set_closure_graph(False)
+            if env.get("VAEVAR_SYNC_CHECK", "0")[:1] == "1":
+                check(lib.vv_set_debug_sync(1), "set_debug_sync")
+            for k, v in tuning.items():
+                self.set_tuning(k, v)
+        except Exception:
+            lib.vv_ctx_destroy(self.h)
+            self.h = ctypes.c_void_p()
+            raise
 
     def set_tuning(self, key: str, value: int):
         """Set one dispatch knob of this context (keys: TUNING_KEYS; include/vaevar.h vv_set_tuning)."""
@@ -149,9 +164,28 @@ class Context:
         """Replay the closure from a captured hipGraph (default) or launch its kernels eagerly."""
         check(lib.vv_set_closure_graph(self.h, 1 if enable else 0), "set_closure_graph")
 
+    @staticmethod
+    def counter(name: str) -> int:
+        """vv_get_counter: process-wide eager launch count of a fused-path alternative ("rowsplit", "fixup_ln",
+        "splitk_fixup")."""
+        v = ctypes.c_longlong()
+        check(lib.vv_get_counter(name.encode(), ctypes.byref(v)), "get_counter")
+        return v.value
+
+    def closure_graph_state(self, kind: int = 1) -> dict:
+        """vv_get_closure_graph: whether the closure of this kind (0: J only, 1: J + gradient) runs from its graph."""
+        info = (ctypes.c_longlong * 4)()
+        check(lib.vv_get_closure_graph(self.h, kind, info), "get_closure_graph")
+        return {"enabled": bool(info[0]), "instantiated": bool(info[1]), "eager_only": bool(info[2]),
+                "launches": int(info[3])}
+
     def attention_global(self, qkv, heads: int):
         """softmax(q k^T) v per head over all N tokens of qkv [N, 3C] (vv_attention_global); returns out [N, C]."""
+        if not (qkv.is_cuda and qkv.dtype == torch.float32 and qkv.dim() == 2 and qkv.is_contiguous()):
+            raise ValueError("qkv must be a contiguous 2-D float32 CUDA tensor [N, 3C] (row stride 3C)")
         N, C3 = qkv.shape
+        if C3 % 3 or (C3 // 3) % heads:
+            raise ValueError(f"qkv width {C3} is not 3C with C divisible by heads={heads}")
         out = torch.empty(N, C3 // 3, device=qkv.device, dtype=torch.float32)
         check(lib.vv_attention_global(self.h, _ptr(qkv), _ptr(out), N, C3 // 3, heads, _stream()), "attention_global")
         return out
