@@ -1870,9 +1870,10 @@ static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
                               const unsigned short* planes) {
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_h4<EPI>), grid, dim3(512), lds, s, a, sc, planes);
-  if (tail && !a.nofix)  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
+  if (tail && !a.nofix) {  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
     count_launch(CNT_SPLITK_FIXUP);
     hipLaunchKernelGGL((k_gemm_fixup_sub16<256, 128, 4, 2, EPI>), dim3(tail, 4, a.ngroups), dim3(512), 0, s, a);
+  }
   return hipGetLastError();
 }
 
