@@ -150,6 +150,31 @@ def test_g13_fixture_consistent_and_oracle_pass0():
     assert abs(float(jo) - float(g["J"][0][1])) < 1e-5 * float(g["J"][0][1]), (float(jo), float(g["J"][0][1]))
 
 
+def test_g15_g16_fixtures_consistent_and_oracle_pass0():
+    """G15 (the genuine one_step_DA, config 5: 721x1440, T = 2, Nit 5) and G16 (config 4: T = 6, Nit 3, the reference
+    modules + torch.optim.LBFGS) are self-consistent, and the oracle restatement of the T = 6 closure (decoder + five
+    flow steps through integrate) reproduces G16's pass-0 J at z = 0."""
+    from oracle.da_ref import oracle_problem
+    from oracle.lgunet_ref import synth_params
+    from vaevar import config as C
+    from vaevar.problem import make_problem
+
+    g15 = gold("g15_config5_trajectory.npz")
+    J = g15["J"].sum(1)
+    assert len(J) == 6 and np.all(np.diff(J) < 0) and len(g15["ls_t"]) <= 50
+    g = gold("g16_config4_trajectory.npz")
+    J = g["J"].sum(1)
+    assert len(J) == int(g["nit"]) + 1 and np.all(np.diff(J) < 0)
+    assert len(g["ls_t"]) == int(g["n_iter"]) and int(g["ls_evals"].sum()) + int(g["nit"]) == int(g["n_eval"])
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    prob = make_problem(nch=69, Hs=128, Ws=256, T=6, seed=20250620)
+    ro = oracle_problem(prob, synth_params(C.DECODER), C.DECODER, synth_params(C.FLOW), C.FLOW)
+    with torch.no_grad():
+        jb, jo = ro.loss_terms(torch.zeros(1, 32, 128, 256))
+    assert float(jb) == 0.0
+    assert abs(float(jo) - float(g["J"][0][1])) < 1e-5 * float(g["J"][0][1]), (float(jo), float(g["J"][0][1]))
+
+
 def test_g5_tiny_lbfgs_trajectory():
     from oracle.da_ref import one_step_da_ref, oracle_problem
     from oracle.lgunet_ref import synth_params

@@ -518,7 +518,7 @@ bool gelu_feeds_planes(GemmArgs& p, GemmArgs& c, const float* wmax, const float*
   GemmArgs cc = c;
   cc.apre = reinterpret_cast<const unsigned short*>(p.g[0].C);
   cc.ascale = sc.rs2;
-  if (vv::gemm_tile_of(p) != 48 || vv::gemm_tile_of(cc) != 48) return false;
+  if (!vv::gemm_plane_tile(vv::gemm_tile_of(p)) || !vv::gemm_plane_tile(vv::gemm_tile_of(cc))) return false;
   p.opl = reinterpret_cast<unsigned short*>(p.g[0].C);
   p.ors = sc.rs2;
   p.obw = wmax;
@@ -539,7 +539,7 @@ bool attn_feeds_planes(AttnArgs& at, GemmArgs& p, const GemmArgs& q, const Block
   GemmArgs pp = p;
   pp.apre = reinterpret_cast<const unsigned short*>(at.g[0].o);
   pp.ascale = sc.rs2;
-  if (vv::gemm_tile_of(pp) != 48) return false;
+  if (!vv::gemm_plane_tile(vv::gemm_tile_of(pp))) return false;
   at.opl = reinterpret_cast<unsigned short*>(at.g[0].o);
   at.ors = sc.rs2;
   at.vrs = q.ascale;
@@ -552,7 +552,7 @@ bool attn_feeds_planes(AttnArgs& at, GemmArgs& p, const GemmArgs& q, const Block
 
 bool ln_feeds_planes(const GemmArgs& a, const Scratch& sc) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  return sc.apl && T.ln_planes && T.ln_scales && vv::gemm_tile_of(a) == 48;
+  return sc.apl && T.ln_planes && T.ln_scales && vv::gemm_plane_tile(vv::gemm_tile_of(a));
 }
 
 LnArgs ln_base(int rows, int C, int G, float eps) {

@@ -1828,6 +1828,265 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
     epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Tile 49: the tile-48 operands (fp16x3 planes, both by LDS-DMA through a 3-stage ring) on 256 x 144 tiles, so that
+// the N = 4608 GEMMs at 2048 rows (fc1 forward, the fc2 input gradient) are exactly 8 x 32 = 256 tiles: one round
+// on 256 CUs with no split-K tail and no fixup launch (tile 48: 288 tiles = 256 + a 32-tile tail split 3 ways + a
+// fixup). 8 waves of 32 rows x 144 columns (2 x 9 fragments of 16 x 16, 54 v_mfma_f32_16x16x32_f16 per k-tile).
+// Every accumulator receives l h, h l, h h of each k-tile in that order, as in tile 48, so C is bit-identical to
+// tile 48's data-parallel tiles.
+//
+// LDS stage = [A 256 rows | B 144 rows] x 128 B (h 32 | l 32 halfs per row and k-tile) = 51,200 B; 3 stages.
+// DMA pieces (1 KiB = 8 rows each): A 32 (4 per wave), B 18 (2 per wave, a third for waves 0 and 1).
+// Per k-tile t (frags of t: A in registers, B column blocks 0, 1 in registers):
+//   b = 0..6: fragment reads of B column block b + 2 (distance-two prefetch, 3-slot ring), the 6 MFMAs of block b;
+//             the 4 A pieces of k-tile t + 2 spread over them
+//   wait for my k-tile t + 1 pieces (vmcnt(4): only the 4 younger A pieces of t + 2 may stay in flight) and for my
+//   B block 8 reads, then s_barrier: everyone's t + 1 pieces landed, everyone's reads of buffer t % 3 retired
+//   b = 7, 8: MFMAs of blocks 7, 8 beside the reads of k-tile t + 1's A fragments and B blocks 0, 1, and the B
+//             pieces of k-tile t + 2
+// Buffer (t + 2) % 3 = (t - 1) % 3 was last read before the barrier of k-tile t - 1, so the DMA of t + 2 may start
+// anywhere in k-tile t.
+// VAR (schedule experiments, Tuning.h5_var): 0 reads of block b + 2 before block b's MFMAs; 1 after them; 2 no
+// scheduling barriers inside the block loop (the compiler interleaves reads and MFMAs); 3 as 1, the A pieces two
+// blocks later
+template <int EPI, int VAR = 0>
+__global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* __restrict__ ascale,
+                                                    const unsigned short* __restrict__ apl) {
+  constexpr int BM = 256, BN = 144, BK = 32, WM = 8, WN = 1, TM = 2, TN = 9;
+  constexpr int STG = (BM + BN) * 2 * BK;  // halfs per stage
+  typedef float accv __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds16[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const GemmGroup G = args.g[blockIdx.z];
+  const int M = args.M, N = args.N, K = args.K;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nk = K / BK;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const float* rs = ascale + (size_t)blockIdx.z * M;
+
+  const int prow = lane >> 3, pslot = lane & 7;
+  const unsigned short* asrc[4];
+  const unsigned short* bsrc[3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (wave + 8 * j) + prow;
+    int gr = min(m0 + row, M - 1);
+    if (args.apre && args.arow) gr = args.arow[gr];  // producer planes are in physical row order
+    asrc[j] = apl + ((size_t)blockIdx.z * M + gr) * 2 * K + 8 * (pslot ^ ((row >> 1) & 7));
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int row = 8 * min(wave + 8 * j, 17) + prow;  // pieces 16, 17: waves 0, 1 only
+    const int gn = min(n0 + row, N - 1);
+    bsrc[j] = G.Bh + (size_t)gn * 2 * K + 8 * (pslot ^ ((row >> 1) & 7));
+  }
+  const bool b3 = wave < 2;  // wave-uniform
+  auto apiece = [&](int kt, int buf, int j) {
+    unsigned short* S = lds16 + buf * STG;
+    __builtin_amdgcn_global_load_lds((const void*)(asrc[j] + 2 * kt * BK), (lds_ptr_t)(S + 8 * (wave + 8 * j) * 64), 16,
+                                     0, 0);
+  };
+  auto bpiece = [&](int kt, int buf, int j) {
+    unsigned short* S = lds16 + buf * STG;
+    __builtin_amdgcn_global_load_lds((const void*)(bsrc[j] + 2 * kt * BK),
+                                     (lds_ptr_t)(S + (BM + 8 * (wave + 8 * j)) * 64), 16, 0, 0);
+  };
+  auto bpieces = [&](int kt, int buf) {
+    bpiece(kt, buf, 0);
+    bpiece(kt, buf, 1);
+    if (b3) bpiece(kt, buf, 2);
+  };
+
+  const int rin = lane & 15, hh = lane >> 4;
+  const int ck0 = (hh ^ ((rin >> 1) & 7)) * 8, ck1 = ((4 + hh) ^ ((rin >> 1) & 7)) * 8;
+  const int aoff = (wave * TM * 16 + rin) * 64, boff = (BM + rin) * 64;
+  auto read_a = [&](int buf, h8v (&fa)[TM][2]) {
+    const unsigned short* S = lds16 + buf * STG;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      fa[a][1] = *reinterpret_cast<const h8v*>(S + aoff + a * 16 * 64 + ck1);
+      fa[a][0] = *reinterpret_cast<const h8v*>(S + aoff + a * 16 * 64 + ck0);
+    }
+  };
+  auto read_b = [&](int buf, int b, h8v (&fb)[2]) {
+    const unsigned short* S = lds16 + buf * STG;
+    fb[0] = *reinterpret_cast<const h8v*>(S + boff + b * 16 * 64 + ck0);
+    fb[1] = *reinterpret_cast<const h8v*>(S + boff + b * 16 * 64 + ck1);
+  };
+
+  accv acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.0f;
+
+  // the 6 MFMAs of column block b: (l h), (h l), (h h) for a = 0, 1 -- per accumulator tile 48's order
+  auto mfma_b = [&](const h8v (&fa)[TM][2], const h8v (&fb)[2], int b) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][1], fb[0], acc[a][b], 0, 0, 0);
+#pragma unroll
+    for (int a = 0; a < TM; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][0], fb[1], acc[a][b], 0, 0, 0);
+#pragma unroll
+    for (int a = 0; a < TM; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][0], fb[0], acc[a][b], 0, 0, 0);
+  };
+
+  h8v fb[3][2];  // B column block b of the current k-tile in slot b % 3 (9 % 3 == 0: the mapping runs on across k-tiles)
+  // VAR 4: B blocks read in groups of three, two groups ahead of use (6 slots: g0 / g2 of k-tile t and g1 of k-tile
+  // t + 1 in one half, the others in the other half); the reads of group g + 1 go out after the first MFMA block of
+  // group g, so the compiler's lgkmcnt waits before each group only find old reads outstanding
+  h8v gb[2][3][2];
+  auto step4 = [&](int t, const h8v (&fa)[TM][2], h8v (&na)[TM][2], int h) {  // h: half holding groups 0 and 2
+    const int cb = t % 3, nbuf = (t + 1) % 3, sb = (t + 2) % 3, sk = min(t + 2, nk - 1);
+    // group 0: blocks 0..2 in half h
+    mfma_b(fa, gb[h][0], 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) read_b(cb, 3 + i, gb[h ^ 1][i]);
+    apiece(sk, sb, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, gb[h][1], 1);
+    apiece(sk, sb, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, gb[h][2], 2);
+    apiece(sk, sb, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    // group 1: blocks 3..5 in half h ^ 1
+    mfma_b(fa, gb[h ^ 1][0], 3);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) read_b(cb, 6 + i, gb[h][i]);
+    apiece(sk, sb, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, gb[h ^ 1][1], 4);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, gb[h ^ 1][2], 5);
+    __builtin_amdgcn_sched_barrier(0);
+    // group 2: blocks 6..8 in half h; the barrier after block 6 (every read of buffer t % 3 has been waited for)
+    mfma_b(fa, gb[h][0], 6);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(nbuf, na);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) read_b(nbuf, i, gb[h ^ 1][i]);  // next k-tile's group 0 (its half is h ^ 1)
+    bpieces(sk, sb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, gb[h][1], 7);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, gb[h][2], 8);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto step = [&](int t, const h8v (&fa)[TM][2], h8v (&na)[TM][2]) {
+    const int cb = t % 3, nbuf = (t + 1) % 3, sb = (t + 2) % 3, sk = min(t + 2, nk - 1);
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+      if constexpr (VAR == 0 || VAR == 2) {
+        read_b(cb, b + 2, fb[(b + 2) % 3]);
+        if (b < 4) apiece(sk, sb, b);
+        if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
+        mfma_b(fa, fb[b % 3], b);
+        if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
+      } else {
+        if (b == 0) read_b(cb, 2, fb[2]);
+        if (VAR == 1 ? b < 4 : (b >= 2 && b < 6)) apiece(sk, sb, VAR == 1 ? b : b - 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_b(fa, fb[b % 3], b);
+        __builtin_amdgcn_sched_barrier(0);
+        if (b < 6) read_b(cb, b + 3, fb[(b + 3) % 3]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // block 7 beside the next k-tile's A fragments, block 8 beside its B blocks 0, 1 (slots 0, 1: blocks 7, 8 sit in
+    // slots 1, 2 -- block 7 is consumed before slot 1 is refilled)
+    read_a(nbuf, na);
+    bpieces(sk, sb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, fb[7 % 3], 7);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(nbuf, 0, fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_b(fa, fb[8 % 3], 8);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(nbuf, 1, fb[1]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: k-tiles 0 and 1 in flight, wait for 0, its A fragments and B blocks 0, 1
+  h8v fa0[TM][2], fa1[TM][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) apiece(0, 0, j);
+  bpieces(0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) apiece(min(1, nk - 1), 1, j);
+  bpieces(min(1, nk - 1), 1);
+  if (b3)
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read_a(0, fa0);
+  if constexpr (VAR == 4) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) read_b(0, i, gb[0][i]);
+  } else {
+    read_b(0, 0, fb[0]);
+    read_b(0, 1, fb[1]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  int t = 0;
+  if constexpr (VAR == 4) {
+    for (; t + 1 < nk; t += 2) {
+      step4(t, fa0, fa1, 0);
+      step4(t + 1, fa1, fa0, 1);
+    }
+    if (t < nk) step4(t, fa0, fa1, 0);
+  } else {
+    for (; t + 1 < nk; t += 2) {
+      step(t, fa0, fa1);
+      step(t + 1, fa1, fa0);
+    }
+    if (t < nk) step(t, fa0, fa1);
+  }
+  // drain the DMAs still in flight before the workgroup can exit (their LDS must not be reassigned under them)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  // undo the scales: rows of A (2^-e_a), rows of B = columns of C (2^-e_b); 16x16 fragment: row 4 hh + r, col rin
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = min(n0 + b * 16 + rin, N - 1);
+    const float sbv = G.Bs[(size_t)col * (K / 32)];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(m0 + wave * TM * 16 + a * 16 + 4 * hh + r, M - 1);
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));  // 2^-e_a
+        acc[a][b][r] *= ia * sbv;
+      }
+  }
+  if (m0 + BM <= M && n0 + BN <= N)
+    epilogue<BM, BN, WM, WN, EPI, 16, true>(args, G, acc, m0, n0, wave, 0, rin, hh);
+  else
+    epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wave, 0, rin, hh);
+}
+
 template <int EPI, int BM>
 static hipError_t launch_h3m_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc) {
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h3m<EPI, BM>, lds)) return e;
@@ -1877,8 +2136,30 @@ static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   return hipGetLastError();
 }
 
-static hipError_t launch_h4(const GemmArgs& a, hipStream_t s) {
+template <int EPI, int VAR>
+static hipError_t launch_h5_v(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, const float* sc,
+                              const unsigned short* planes) {
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_h5<EPI, VAR>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_h5<EPI, VAR>), grid, dim3(512), lds, s, a, sc, planes);
+  return hipGetLastError();
+}
+template <int EPI>
+static hipError_t launch_h5_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, const float* sc,
+                              const unsigned short* planes) {
+  const Tuning& T = a.tune ? *a.tune : kDefaultTuning;
+  switch (T.h5_var) {
+    case 1: return launch_h5_v<EPI, 1>(a, s, grid, lds, sc, planes);
+    case 2: return launch_h5_v<EPI, 2>(a, s, grid, lds, sc, planes);
+    case 3: return launch_h5_v<EPI, 3>(a, s, grid, lds, sc, planes);
+    case 4: return launch_h5_v<EPI, 4>(a, s, grid, lds, sc, planes);
+    default: return launch_h5_v<EPI, 0>(a, s, grid, lds, sc, planes);
+  }
+}
+
+// tiles 48 and 49 (t49: 256 x 144 tiles, data-parallel only)
+static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) {
   if (a.K % 32 || a.ksplit % 32 || !h3_ready(a) || !h4_ready(a)) return hipErrorInvalidValue;
+  if (t49 && (a.tsplit > 1 || a.nofix)) return hipErrorInvalidValue;
   float* sc = a.ws + kWsFloats;
   const unsigned short* planes = a.apl;
   if (a.apre) {
@@ -1900,12 +2181,27 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s) {
       default: hipLaunchKernelGGL(k_rowsplit<18>, grid, dim3(256), 0, s, a, sc, a.apl); break;
     }
   }
+  GemmArgs b = a;
+  b.escale = sc;  // the plane-writing epilogues bound |C| from the row scales the products used
+  if (t49) {
+    const size_t lds = 3 * (2 * (256 + 144) * 32) * sizeof(unsigned short);
+    const dim3 grid(((a.N + 143) / 144) * ((a.M + 255) / 256), 1, a.ngroups);
+    switch (a.epi) {
+      case EPI_STORE: return launch_h5_k<EPI_STORE>(b, s, grid, lds, sc, planes);
+      case EPI_GELU:
+        return a.opl ? launch_h5_k<EPI_GELU_PL>(b, s, grid, lds, sc, planes)
+                     : launch_h5_k<EPI_GELU>(b, s, grid, lds, sc, planes);
+      case EPI_RESID: return launch_h5_k<EPI_RESID>(b, s, grid, lds, sc, planes);
+      case EPI_DGELU:
+        return a.opl ? launch_h5_k<EPI_DGELU_PL>(b, s, grid, lds, sc, planes)
+                     : launch_h5_k<EPI_DGELU>(b, s, grid, lds, sc, planes);
+      default: return hipErrorInvalidValue;
+    }
+  }
   const size_t lds = 3 * (2 * (256 + 128) * 32) * sizeof(unsigned short);
   const int T = ((a.N + 127) / 128) * ((a.M + 255) / 256);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
   dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
-  GemmArgs b = a;
-  b.escale = sc;  // the plane-writing epilogues bound |C| from the row scales the products used
   switch (a.epi) {
     case EPI_STORE: return launch_h4_k<EPI_STORE>(b, s, grid, lds, tail, sc, planes);
     case EPI_GELU:
@@ -1952,7 +2248,8 @@ static hipError_t launch_h3(const GemmArgs& a, hipStream_t s) {
 //   exact f32 MFMA   0: 128x128   2: 64x64   4: 32x64            (GEMM_F32)
 //   bf16x6 split    24: 64x64    34: pipelined 128x128           (GEMM_SPLIT, short-K GEMMs of GEMM_SPLIT16)
 //   fp16x3 split    36: 128x128, 44: 256x128 (8 waves of 64x64); 46 / 47: the same on 16x16x32 MFMAs
-static bool h3_tile(int t) { return t == 36 || t == 44 || t == 46 || t == 47 || t == 48; }
+static bool h3_tile(int t) { return t == 36 || t == 44 || t == 46 || t == 47 || t == 48 || t == 49; }
+bool gemm_plane_tile(int t) { return t == 48 || t == 49; }
 const Tuning kDefaultTuning{};
 int* tuning_field(Tuning& t, const char* key) {
   if (!key) return nullptr;
@@ -1979,6 +2276,8 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "gattn_qf") return &t.gattn_qf;
   if (k == "h4_small") return &t.h4_small;
   if (k == "h4_split_minkt") return &t.h4_split_minkt;
+  if (k == "h5") return &t.h5;
+  if (k == "h5_var") return &t.h5_var;
   return nullptr;
 }
 
@@ -1996,6 +2295,7 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 46: return launch_h3<128, 16>(a, s);
     case 47: return launch_h3<256, 16>(a, s);
     case 48: return launch_h4(a, s);
+    case 49: return launch_h4(a, s, true);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2153,8 +2453,8 @@ static int pick_tile(const GemmArgs& a) {
 // tile edge of each variant (for the tail split)
 static void variant_tile(int t, int& bm, int& bn, int& bk) {
   bk = 32;
-  bm = t == 44 || t == 47 || t == 48 ? 256 : t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
-  bn = t == 0 || t >= 34 ? 128 : 64;
+  bm = t == 44 || t == 47 || t == 48 || t == 49 ? 256 : t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
+  bn = t == 49 ? 144 : t == 0 || t >= 34 ? 128 : 64;
 }
 
 // the routed tile plus the fallbacks gemm_nt applies (no fp16 B planes: bf16x6 34; no A-plane workspace: 47);
@@ -2180,7 +2480,13 @@ static int resolve_tile(GemmArgs& a, int tile_hint) {
   // pipelined bf16x6 kernel. Decided BEFORE the tile geometry: the split-K tail sizes its partials from the tile
   // edge of the kernel that actually runs (a 256-row tile count with 128-row fallback tiles overran ws).
   if (h3_tile(t) && !h3_ready(a)) t = 34;
-  if (t == 48 && !h4_ready(a)) t = 47;  // no plane workspace (or too small): the in-loop-split kernel, same geometry
+  if ((t == 48 || t == 49) && !h4_ready(a)) t = 47;  // no plane workspace (or too small): the in-loop-split kernel
+  // tile 49 (256 x 144) where its tiles fill whole rounds of the chip and tile 48's leave a split-K tail: N 4608 at
+  // 2048 rows = 256 tiles (tile 48: 288 = 256 + 32); same operands and per-element products as tile 48
+  if (t == 48 && tile_hint < 0 && TU.h5 && a.N % 144 == 0) {
+    const long P = device_cus(), t48 = tiles_of(a, 256, 128), t49 = tiles_of(a, 256, 144);
+    if (t48 % P != 0 && t49 % P == 0) t = 49;
+  }
   return t;
 }
 
@@ -2210,10 +2516,10 @@ static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
   }
   t = resolve_tile(a, tile_hint);
   if (t < 0) return hipErrorInvalidValue;
-  // producer planes are only read by tile 48; every other kernel reads A itself (which the producer then wrote)
-  if (a.apre && t != 48) return hipErrorInvalidValue;
-  // plane-writing epilogues: tile 48, GELU / DGELU, one group, output rows in GEMM order, N in whole k-tiles
-  if (a.opl && (t != 48 || (a.epi != EPI_GELU && a.epi != EPI_DGELU) || a.ngroups != 1 || a.crow || a.N % 32 ||
+  // producer planes are only read by tiles 48 / 49; every other kernel reads A itself (which the producer then wrote)
+  if (a.apre && !gemm_plane_tile(t)) return hipErrorInvalidValue;
+  // plane-writing epilogues: tiles 48 / 49, GELU / DGELU, one group, output rows in GEMM order, N in whole k-tiles
+  if (a.opl && (!gemm_plane_tile(t) || (a.epi != EPI_GELU && a.epi != EPI_DGELU) || a.ngroups != 1 || a.crow || a.N % 32 ||
                 !a.ors || !a.obw))
     return hipErrorInvalidValue;
   for (int g = 0; g < a.ngroups; ++g) {
@@ -2237,7 +2543,7 @@ static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
     const int T = ((a.N + bn - 1) / bn) * ((a.M + bm - 1) / bm);
     const int P = num_cu, nkt = a.K / bk;
     const int tdp = (T / P) * P, tail = T - tdp;
-    if (tdp > 0 && tail > 0 && tail <= P / 2) {
+    if (tdp > 0 && tail > 0 && tail <= P / 2 && t != 49) {
       // chunks of >= 12 k-tiles: below that the fixup launch and partial traffic cost more than the tail
       const int tail_minkt = std::max(1, TU.tail_minkt);  // k-tiles per tail chunk at least
       int S = std::min(P / tail, nkt / tail_minkt);
@@ -2247,7 +2553,7 @@ static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
         a.tdp = tdp;
         a.tsplit = S;
       }
-    } else if (tdp == 0 && h3_tile(t) && TU.small_split) {
+    } else if (tdp == 0 && h3_tile(t) && t != 49 && TU.small_split) {
       // fewer fp16x3 tiles than CUs (N = 1152 at 2048 tokens: 144 tiles): every tile split along K so that
       // two workgroups share most CUs (the co-resident pair overlaps one's staging with the other's MFMAs)
       // chunks of >= 24 k-tiles (K >= 2304 at S = 3): at K = 1152 the fixup costs more than the split gains

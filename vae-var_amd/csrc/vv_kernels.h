@@ -28,6 +28,8 @@ struct Tuning {
                                 // profiles/r03/ab_h4small); with the attention writing its planes (attn_planes) 86.9 / 86.6
                                 // on vs 81.0 / 81.8 off, same box (profiles/r03/ab_attn_planes)
   int h4_split_minkt = 12;      // k-tiles per chunk at least, for that split of tile 48
+  int h5 = 1;                   // tile 49 (256 x 144, k_gemm_h5) where its tiles fill whole rounds and tile 48's do not
+  int h5_var = 0;               // tile 49 schedule variant (experiments)
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
@@ -130,6 +132,8 @@ struct GattnArgs {
 // device; locked, so concurrent contexts on several devices are safe). The first value set for a kernel stays: callers
 // whose LDS varies pass their maximum.
 hipError_t set_lds_limit(const void* k, size_t lds);
+// the split-operand fp16x3 kernels that read producer planes (GemmArgs.apre) and write them (opl): tiles 48, 49
+bool gemm_plane_tile(int t);
 bool gattn_supported(int C, int heads);
 size_t gattn_ws_bytes(int N, int C, int heads);
 // qf_per_wave: 16-query blocks per wave (2: 4 waves of 32 queries, one per SIMD; 1: 8 waves of 16, two per SIMD)

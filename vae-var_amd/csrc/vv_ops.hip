@@ -1242,10 +1242,25 @@ hipError_t attn_bwd(const AttnArgs& a, hipStream_t s) {
 // ============================================================================
 // PatchEmbed (Conv2d k=s=2) + absolute_pos_embed   (transformer.py:41-49, 392-394)
 // ConvTranspose2d(k=s=2) + Dec_net mean/std reorder (transformer.py:593-623, quirk Q2)
-// Block = 64 consecutive tokens of one tower (blockIdx.y); the tower's weights and the block's token rows /
-// 2x2 pixel patches are staged in LDS so every global access is coalesced.
 // ============================================================================
-constexpr int PT = 64;  // tokens per block
+// PatchEmbed and ConvTranspose2d with k = s = 2 are per-token GEMMs (the im2col of a stride-2 2x2 patch is a plain
+// gather of 4 cin pixels): two kernels on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32: fp32 products and sums, as
+// torch's fp32 conv; only the summation order differs), one wave per 16 tokens, four waves per workgroup sharing the
+// tower's weights in LDS. Fragment layout of 16x16x4: lane l gives A[l % 16][k = l / 16] and B[k][l % 16] and holds
+// D[4 (l / 16) + r][l % 16]. A float4 read of 4 consecutive k per lane serves 4 k-steps when the k index of step i
+// in lane group g is kappa(i, g) = 16 (i / 4) + 4 g + i % 4 (the same permutation on both operands).
+//
+// k_p2t_mf (pixels -> token rows: PatchEmbed forward, ConvTranspose backward): D[t][c] = sum_j X[t][j] W[c][j] with
+//   X the 2x2xC patches of the 64 tokens staged in LDS by coalesced image-row loads ([t][KP], zero-padded), W[c][j]
+//   staged in LDS; lane (c, g) writes D[4 g + r][c]: 16 consecutive channels of a token row per 16 lanes.
+//   MODE 0: tok = (D + bias) + pos, x[t][ci 4 + 2 p + q] = img[cin_off + ci][2ho + p][2wo + q]
+//   MODE 1: dtok = D, x[t][co 4 + 2 p + q] = dout[ch(co)][2ho + p][2wo + q] (0 at channels >= climit)
+// k_t2p_mf (token rows -> pixels: PatchEmbed backward, ConvTranspose forward): D[j][t] = sum_c W[c][j] Y[t][c] with
+//   Y's rows read per lane as float4 from global memory and W transposed in LDS; lane (t, g) holds D[4 g + r][t], i.e.
+//   outputs j = 4 (4 mt + g) + 2 p + q of token t: two float2 stores (q = 0, 1) of horizontally adjacent pixels,
+//   consecutive lanes = consecutive pixels (needs Wo % 16 == 0).
+//   MODE 0: dimg = add + D; MODE 1: out[ch(co)] = D + bias[co] (ch < climit)
+constexpr int PT = 64;  // tokens per workgroup (4 waves x 16)
 
 __device__ __forceinline__ void tok_coords(int tok, int Ho, int Wo, int& b, int& ho, int& wo) {
   b = tok / (Ho * Wo);
@@ -1254,141 +1269,137 @@ __device__ __forceinline__ void tok_coords(int tok, int Ho, int Wo, int& b, int&
   wo = rem - ho * Wo;
 }
 
-// tok[t][co] = (sum_{ci,p,q} w[co][ci][p][q] * img[cin_off+ci][2ho+p][2wo+q] + bias[co]) + pos[t][co]
-__global__ __launch_bounds__(256) void k_patch_fwd(PatchArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const PatchGroup& G = a.g[blockIdx.y];
-  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = G.cin * 4, kcp = kc + 1, C = a.Ctok;
-  float* Ws = sm;              // [C][kc+1]
-  float* Xs = Ws + C * kcp;    // [PT][kc+1]
-  const int t0 = blockIdx.x * PT;
-  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i / kc) * kcp + i % kc] = G.w[i];
-  for (int i = threadIdx.x; i < PT * kc; i += 256) {
-    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;  // rest = ci*2 + p
-    const int ci = rest >> 1, p = rest & 1;
-    const int tok = t0 + t;
-    float v = 0.f;
-    if (tok < ntok) {
-      int b, ho, wo;
-      tok_coords(tok, Ho, Wo, b, ho, wo);
-      v = a.img[(((size_t)b * a.Cimg + G.cin_off + ci) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q];
-    }
-    Xs[t * kcp + ci * 4 + p * 2 + q] = v;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < PT * C; i += 256) {
-    const int t = i / C, co = i - t * C;
-    const int tok = t0 + t;
-    if (tok >= ntok) continue;
-    float acc = 0.f;
-    for (int j = 0; j < kc; ++j) acc += Ws[co * kcp + j] * Xs[t * kcp + j];
-    const int rem = tok % (Ho * Wo);
-    G.tok[(size_t)tok * C + co] = (acc + G.bias[co]) + G.pos[(size_t)rem * C + co];
-  }
-}
-
-// dimg[cin_off+ci][2ho+p][2wo+q] = add + sum_co dtok[t][co] * w[co][ci][p][q]
-__global__ __launch_bounds__(256) void k_patch_bwd(PatchArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const PatchGroup& G = a.g[blockIdx.y];
-  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = G.cin * 4, C = a.Ctok, Cp = C + 1;
-  float* Ws = sm;             // [kc][C+1]  (transposed: j-major)
-  float* Ds = Ws + kc * Cp;   // [PT][C+1]
-  const int t0 = blockIdx.x * PT;
-  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i % kc) * Cp + i / kc] = G.w[i];
-  for (int i = threadIdx.x; i < PT * C; i += 256) {
-    const int t = i / C, co = i - t * C;
-    Ds[t * Cp + co] = (t0 + t < ntok) ? G.dtok[(size_t)(t0 + t) * C + co] : 0.f;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < PT * kc; i += 256) {
-    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;
-    const int ci = rest >> 1, p = rest & 1;
-    const int tok = t0 + t;
-    if (tok >= ntok) continue;
-    const float* wr = Ws + (ci * 4 + p * 2 + q) * Cp;
-    const float* dr = Ds + t * Cp;
-    float acc = 0.f;
-    for (int co = 0; co < C; ++co) acc += dr[co] * wr[co];
-    int b, ho, wo;
-    tok_coords(tok, Ho, Wo, b, ho, wo);
-    const size_t o = (((size_t)b * a.Cimg + G.cin_off + ci) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q;
-    if (a.add_img) acc += a.add_img[o];
-    a.img_out[o] = acc;
-  }
-}
-
 __device__ __forceinline__ int unembed_ch(const PatchGroup& G, int co) {
   const int half = G.cout / 2;
   return co < half ? G.mean_off + co : G.std_off + co - half;
 }
 
-// out[ch(co)][2ho+p][2wo+q] = bias[co] + sum_ci tok[t][ci] * w[ci][co][p][q]   (channels < climit only)
-__global__ __launch_bounds__(256) void k_unembed_fwd(PatchArgs a) {
+constexpr int kPatchKmax = 112;  // patch taps per token (4 x channels), padded to 16
+constexpr int kPatchCmax = 128;  // token channels
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const PatchGroup& G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = G.cout * 4, C = a.Ctok, Cp = C + 1;
-  float* Ws = sm;            // [kc][C+1] (transposed)
-  float* Ts = Ws + kc * Cp;  // [PT][C+1]
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
+  const int KP = (kc + 15) / 16 * 16, KS = KP + 4;  // padded K; LDS row stride (floats)
+  float* Xs = sm;             // [64][KS]
+  float* Wsm = Xs + PT * KS;  // [C][KS]
   const int t0 = blockIdx.x * PT;
-  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i % kc) * Cp + i / kc] = G.w[i];
-  for (int i = threadIdx.x; i < PT * C; i += 256) {
-    const int t = i / C, ci = i - t * C;
-    Ts[t * Cp + ci] = (t0 + t < ntok) ? G.tok[(size_t)(t0 + t) * C + ci] : 0.f;
+  {
+    // thread (t, q) of one of two row phases: consecutive threads read consecutive pixels of an image row
+    const int q = threadIdx.x & 1, t = (threadIdx.x >> 1) & (PT - 1), half = threadIdx.x >> 7;
+    const int tok = t0 + t;
+    const bool okt = tok < ntok;
+    int b, ho, wo;
+    tok_coords(okt ? tok : 0, Ho, Wo, b, ho, wo);
+    const size_t plane = (size_t)a.Himg * a.Wimg;
+    const float* base = a.img + (size_t)b * a.Cimg * plane + (size_t)(2 * ho) * a.Wimg + 2 * wo + q;
+    for (int rest = half; rest < KP / 2; rest += 2) {  // rest = ci 2 + p (co 2 + p)
+      const int ci = rest >> 1, pp = rest & 1;
+      float v = 0.f;
+      if (okt && ci * 4 < kc) {
+        const int ch = MODE == 0 ? G.cin_off + ci : unembed_ch(G, ci);
+        if (MODE == 0 || ch < a.climit) v = base[(size_t)ch * plane + pp * a.Wimg];
+      }
+      Xs[t * KS + ci * 4 + pp * 2 + q] = v;
+    }
+  }
+  for (int i = threadIdx.x; i < C * KP; i += 256) {
+    const int c = i / KP, j = i - c * KP;
+    Wsm[c * KS + j] = j < kc ? G.w[(size_t)c * kc + j] : 0.f;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < PT * kc; i += 256) {
-    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;  // rest = co*2 + p
-    const int co = rest >> 1, p = rest & 1;
-    const int tok = t0 + t;
-    const int ch = unembed_ch(G, co);
-    if (tok >= ntok || ch >= a.climit) continue;
-    const float* wr = Ws + (co * 4 + p * 2 + q) * Cp;
-    const float* tr = Ts + t * Cp;
-    float acc = 0.f;
-    for (int ci = 0; ci < C; ++ci) acc += tr[ci] * wr[ci];
-    int b, ho, wo;
-    tok_coords(tok, Ho, Wo, b, ho, wo);
-    a.img_out[(((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q] = acc + G.bias[co];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int tb = wave * 16;  // this wave's 16 tokens within the workgroup
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  const int nt = (C + 15) / 16;
+  for (int n = 0; n < nt; ++n) {
+    fr4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int c = n * 16 + li;
+    const float* xr = Xs + (tb + li) * KS + 4 * g;
+    const float* wr = Wsm + min(c, C - 1) * KS + 4 * g;
+    for (int s4 = 0; s4 < KP; s4 += 16) {
+      const f4 xa = *reinterpret_cast<const f4*>(xr + s4);
+      const f4 wb = *reinterpret_cast<const f4*>(wr + s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], wb[e], acc, 0, 0, 0);
+    }
+    if (c < C) {
+      const float bias = MODE == 0 ? G.bias[c] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = t0 + tb + 4 * g + r;
+        if (tok >= ntok) continue;
+        if (MODE == 0) {
+          const int rem = tok % (Ho * Wo);
+          G.tok[(size_t)tok * C + c] = (acc[r] + bias) + G.pos[(size_t)rem * C + c];
+        } else {
+          G.tok[(size_t)tok * C + c] = acc[r];
+        }
+      }
+    }
   }
 }
 
-// dtok[t][ci] = sum_{co,p,q} dout[ch(co)][2ho+p][2wo+q] * w[ci][co][p][q]   (channels < climit only)
-__global__ __launch_bounds__(256) void k_unembed_bwd(PatchArgs a) {
+template <int MODE>
+__global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const PatchGroup& G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = G.cout * 4, kcp = kc + 1, C = a.Ctok;
-  float* Ws = sm;            // [C][kc+1]
-  float* Ds = Ws + C * kcp;  // [PT][kc+1]
-  const int t0 = blockIdx.x * PT;
-  for (int i = threadIdx.x; i < C * kc; i += 256) Ws[(i / kc) * kcp + i % kc] = G.w[i];
-  for (int i = threadIdx.x; i < PT * kc; i += 256) {
-    const int q = i & 1, t = (i >> 1) % PT, rest = (i >> 1) / PT;
-    const int co = rest >> 1, p = rest & 1;
-    const int tok = t0 + t;
-    const int ch = unembed_ch(G, co);
-    float v = 0.f;
-    if (tok < ntok && ch < a.climit) {
-      int b, ho, wo;
-      tok_coords(tok, Ho, Wo, b, ho, wo);
-      v = a.img[(((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho + p) * a.Wimg + 2 * wo + q];
-    }
-    Ds[t * kcp + co * 4 + p * 2 + q] = v;
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
+  const int CP = (C + 15) / 16 * 16, CS = CP + 4;
+  float* Wt = sm;  // [KP][CS]: W[c][j] at Wt[j][c]
+  const int KP = (kc + 15) / 16 * 16;
+  for (int i = threadIdx.x; i < KP * CP; i += 256) {  // coalesced over W's rows, transposed into LDS
+    const int c = i / KP, j = i - c * KP;
+    Wt[j * CS + c] = (j < kc && c < C) ? G.w[(size_t)c * kc + j] : 0.f;
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int tok = blockIdx.x * PT + wave * 16 + li;
+  const bool ok = tok < ntok;
+  const float* yr = (MODE == 0 ? G.dtok : G.tok) + (size_t)(ok ? tok : 0) * C + 4 * g;
+  f4 y[kPatchCmax / 16];
+#pragma unroll
+  for (int s = 0; s < kPatchCmax / 16; ++s) {
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (16 * s + 4 * g < C) v = *reinterpret_cast<const f4*>(yr + 16 * s);
+    y[s] = v;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < PT * C; i += 256) {
-    const int t = i / C, ci = i - t * C;
-    const int tok = t0 + t;
-    if (tok >= ntok) continue;
-    const float* wr = Ws + ci * kcp;
-    const float* dr = Ds + t * kcp;
-    float acc = 0.f;
-    for (int j = 0; j < kc; ++j) acc += dr[j] * wr[j];
-    G.tok[(size_t)tok * C + ci] = acc;
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  int b, ho, wo;
+  tok_coords(ok ? tok : 0, Ho, Wo, b, ho, wo);
+  for (int mt = 0; mt < KP / 16; ++mt) {
+    fr4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wr = Wt + (mt * 16 + li) * CS + 4 * g;
+#pragma unroll
+    for (int s = 0; s < kPatchCmax / 16; ++s) {
+      if (16 * s < CP) {
+        const f4 wa = *reinterpret_cast<const f4*>(wr + 16 * s);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[e], y[s][e], acc, 0, 0, 0);
+      }
+    }
+    // rows 4 g + r of output tile mt: channel o = 4 mt + g, p = r / 2, q = r % 2
+    const int o = 4 * mt + g;
+    if (!ok || o * 4 >= kc) continue;
+    const int ch = MODE == 0 ? G.cin_off + o : unembed_ch(G, o);
+    if (MODE == 1 && ch >= a.climit) continue;
+    const float bias = MODE == 1 ? G.bias[o] : 0.f;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const size_t off = (((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho + pp) * a.Wimg + 2 * wo;
+      float2 v;
+      if (MODE == 0) {
+        const float2 ad = a.add_img ? *reinterpret_cast<const float2*>(a.add_img + off) : make_float2(0.f, 0.f);
+        v = make_float2(acc[2 * pp] + ad.x, acc[2 * pp + 1] + ad.y);
+      } else {
+        v = make_float2(acc[2 * pp] + bias, acc[2 * pp + 1] + bias);
+      }
+      *reinterpret_cast<float2*>(a.img_out + off) = v;
+    }
   }
 }
 
@@ -1398,33 +1409,66 @@ static int max_k(const PatchArgs& a, bool in) {
   return m;
 }
 
-template <typename K>
-static hipError_t patch_launch(K kern, const PatchArgs& a, size_t lds, hipStream_t s) {
-  if (a.ngroups <= 0 || a.ngroups > kMaxGroups || lds > 160 * 1024) return hipErrorInvalidValue;
-  if (lds > 64 * 1024)
-    if (hipError_t e = set_lds_limit((const void*)kern, 160 * 1024)) return e;
+template <int MODE>
+static hipError_t p2t_launch(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
-  const int ph = prof_begin(s);
-  hipLaunchKernelGGL(kern, dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
-  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
+  const int KS = (kc + 15) / 16 * 16 + 4;
+  const size_t lds = (size_t)(PT + a.Ctok) * KS * sizeof(float);
+  if (lds > 64 * 1024)
+    if (hipError_t e = set_lds_limit((const void*)k_p2t_mf<MODE>, (size_t)(PT + kPatchCmax) * (kPatchKmax + 4) * 4))
+      return e;
+  hipLaunchKernelGGL((k_p2t_mf<MODE>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t t2p_launch(const PatchArgs& a, int kc, hipStream_t s) {
+  const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
+  const size_t lds = (size_t)((kc + 15) / 16 * 16) * ((a.Ctok + 15) / 16 * 16 + 4) * sizeof(float);
+  hipLaunchKernelGGL((k_t2p_mf<MODE>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+// preconditions: 2x2 patches, 16 tokens of a wave in one image row (Wo % 16), at most kPatchKmax taps per token and
+// kPatchCmax token channels (LDS: <= 64 KB)
+static hipError_t patch_check(const PatchArgs& a, int kc) {
+  if (a.ngroups <= 0 || a.ngroups > kMaxGroups || (a.Himg | a.Wimg) & 1 || (a.Wimg / 2) % 16 || a.Ctok <= 0 ||
+      a.Ctok > kPatchCmax || a.Ctok % 4 || kc <= 0 || kc > kPatchKmax)
+    return hipErrorInvalidValue;
+  return hipSuccess;
 }
 
 hipError_t patch_embed_fwd(const PatchArgs& a, hipStream_t s) {
   const int kc = max_k(a, true);
-  return patch_launch(k_patch_fwd, a, (size_t)(a.Ctok + PT) * (kc + 1) * sizeof(float), s);
+  if (hipError_t e = patch_check(a, kc)) return e;
+  const int ph = prof_begin(s);
+  const hipError_t e = p2t_launch<0>(a, kc, s);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
+  return e;
 }
 hipError_t patch_embed_bwd(const PatchArgs& a, hipStream_t s) {
   const int kc = max_k(a, true);
-  return patch_launch(k_patch_bwd, a, (size_t)(kc + PT) * (a.Ctok + 1) * sizeof(float), s);
+  if (hipError_t e = patch_check(a, kc)) return e;
+  const int ph = prof_begin(s);
+  const hipError_t e = t2p_launch<0>(a, kc, s);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
+  return e;
 }
 hipError_t patch_unembed_fwd(const PatchArgs& a, hipStream_t s) {
   const int kc = max_k(a, false);
-  return patch_launch(k_unembed_fwd, a, (size_t)(kc + PT) * (a.Ctok + 1) * sizeof(float), s);
+  if (hipError_t e = patch_check(a, kc)) return e;
+  const int ph = prof_begin(s);
+  const hipError_t e = t2p_launch<1>(a, kc, s);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
+  return e;
 }
 hipError_t patch_unembed_bwd(const PatchArgs& a, hipStream_t s) {
   const int kc = max_k(a, false);
-  return patch_launch(k_unembed_bwd, a, (size_t)(a.Ctok + PT) * (kc + 1) * sizeof(float), s);
+  if (hipError_t e = patch_check(a, kc)) return e;
+  const int ph = prof_begin(s);
+  const hipError_t e = p2t_launch<1>(a, kc, s);
+  prof_end(ph, s, PC_PATCH, 0.0, 0.0);
+  return e;
 }
 
 // ============================================================================
