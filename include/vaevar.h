@@ -228,7 +228,10 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    the 256x128 tiles run, 1), "ln_planes" (the LayerNorm writes that kernel's fp16 A planes, 1), "gattn" (the
    LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1), "gattn_qf" (its 16-query blocks per
    wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1), "h4_small" (tile 48 with whole-chip split-K
-   also for 64..143 256-row tiles, 1), "h4_split_minkt" (k-tiles per chunk of that split, 12). Results stay fp32-level for every value; a change drops the
+   also for 64..143 256-row tiles, 1), "h4_split_minkt" (k-tiles per chunk of that split, 12), "h5" (tile 49, 256x144, where its
+   tiles fill whole rounds of the chip and tile 48's leave a split-K tail: the N = 4608 GEMMs at 2048 rows, 1), "h5_var"
+   (tile 49's schedule variant, experiments), "fc_conv_mf" (LGUnet_all_1's PatchEmbed / ConvTranspose2d as direct
+   exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key: VV_E_ARG. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);
@@ -251,7 +254,7 @@ int vv_attention_global(vv_ctx* ctx, const float* qkv, float* out, int N, int C,
    kernel as the engine does; otherwise one of the library kernels: 0 / 2 / 4 exact-f32 MFMA 128x128 / 64x64 /
    32x64, 24 / 34 bf16x6 split 64x64 / pipelined 128x128, 36 / 44 fp16x3 split 128x128 / 256x128 (32x32x16 MFMAs),
    46 / 47 the same on 16x16x32 MFMAs, 48 fp16x3 256x128 on pre-split A planes staged by LDS-DMA (the engine's
-   default for the LG GEMMs). Any other tile: VV_E_ARG. An fp16x3 tile whose B has no fp16 planes (not registered)
+   default for the LG GEMMs), 49 the same operands on 256x144 tiles (data-parallel only). Any other tile: VV_E_ARG. An fp16x3 tile whose B has no fp16 planes (not registered)
    runs tile 34. */
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
             int tile, void* stream);

@@ -175,18 +175,38 @@ def test_gemm_h4_bitwise_h3m(ctx, M, N, K):
     _keep.append(B)
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 4608, 4608), (777, 300, 96), (2100, 4464, 1152)])
+def test_gemm_h5_bitwise_h4(ctx, M, N, K):
+    """Tile 49 (256 x 144 tiles) computes every element with tile 48's products in tile 48's order: C bit-identical to
+    tile 48 run data-parallel (split-K off), including ragged edges; and the router sends the N = 4608 GEMMs at 2048
+    rows (256 tiles of 256 x 144 = one round on 256 CUs; tile 48: 288) to it."""
+    from vaevar.engine import Context
+
+    g = torch.Generator().manual_seed(M + 5 * N + 3 * K)
+    A = (torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-4, 4, generator=g))).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.03).cuda()
+    c = Context(0)
+    c.set_tuning("small_split", 0)
+    c.set_tuning("tail_minkt", 1 << 20)
+    c.gemm_register_weight(B)
+    c48 = c.gemm(A, B, tile=48)
+    c49 = c.gemm(A, B, tile=49)
+    assert torch.equal(c48, c49), float((c48 - c49).abs().max())
+    _keep.append(B)
+
+
 def test_gemm_rejects_non_library_tiles(ctx):
-    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47, 48): any other hint, e.g. the r01
-    timing experiments 37-39, returns VV_E_ARG instead of running something."""
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47, 48, 49): any other hint, e.g. the
+    r01 timing experiments 37-39, returns VV_E_ARG instead of running something."""
     from vaevar._lib import VVError
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 49, 1000):
+    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 50, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
-    for t in (0, 2, 4, 24, 34, 36, 44, 46, 47, 48):
+    for t in (0, 2, 4, 24, 34, 36, 44, 46, 47, 48, 49):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
 

@@ -525,6 +525,200 @@ __global__ void k_col2im(ConvArgs a, const float* Y0, int ldy, size_t gstride) {
   }
 }
 
+// PatchEmbed and ConvTranspose2d of LGUnet_all_1 (patch (kh, 2), stride (2, 2)) on the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32, fp32 products and sums; only the summation order differs from torch's conv), reading the
+// image / writing the pixels directly: no im2col / col2im buffer (the 0.25-degree model's im2col rows were 600 MB).
+// Fragment layout and the k permutation of the float4 reads as the decoder's k_p2t_mf / k_t2p_mf (vv_ops.hip).
+//
+// k_fc_patch_mf: 64 tokens per workgroup (4 waves x 16); their kh x 2 x cin patches staged in LDS ([t][KP],
+// k = (ci kh + ky) 2 + kx as the im2col rows), each thread loading the two horizontally adjacent pixels of a patch
+// row for its token (all of a thread's loads in flight before its LDS stores); Wp [C0][Kp] staged in LDS;
+// tok[t][c] = (sum_k X[t][k] W[c][k] + bias[c]) + pos[t % (Ho Wo)][c].
+constexpr int kFcKP = 96;    // patch taps, padded to 16 (cin kh kw <= 96)
+// stage n floats f(i) into LDS at d(i) in batches of 16 loads in flight per thread (a load issued behind an LDS store
+// of the previous one would expose one memory latency per element)
+template <typename F, typename D>
+__device__ __forceinline__ void stage_batched(int n, F f, D d) {
+  for (int i0 = threadIdx.x; i0 < n; i0 += 256 * 16) {
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = i0 + 256 * r < n ? f(i0 + 256 * r) : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (i0 + 256 * r < n) d(i0 + 256 * r, v[r]);
+  }
+}
+
+template <int C0>
+__global__ __launch_bounds__(256) void k_fc_patch_mf(ConvArgs a, int Kp) {  // a.w[g]: Wp [C0][Kp]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int kFcC0 = C0, C = C0;
+  const int g = blockIdx.y;
+  const int ntok = a.B * a.Ho * a.Wo, K = a.cin[g] * a.kh * 2;
+  const int KP = (K + 15) / 16 * 16, KS = KP + 4;
+  float* Xs = sm;            // [64][KS]
+  float* Wsm = Xs + 64 * KS; // [C][KS]
+  const int t0 = blockIdx.x * 64;
+  {
+    const int q = threadIdx.x & 1, t = (threadIdx.x >> 1) & 63, half = threadIdx.x >> 7;
+    const int tok = min(t0 + t, ntok - 1);
+    const int b = tok / (a.Ho * a.Wo), rem = tok - b * a.Ho * a.Wo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    const size_t plane = (size_t)a.Himg * a.Wimg;
+    const float* base = a.img + ((size_t)b * a.Cimg + a.cin_off[g]) * plane + (size_t)(oy * a.sh) * a.Wimg + ox * 2 + q;
+    constexpr int NR = kFcKP / 4;  // patch rows (ci, ky) per thread at most
+    float v[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int rest = half + 2 * r;  // = ci kh + ky
+      const int ci = rest / a.kh, ky = rest - ci * a.kh;
+      v[r] = (rest * 2 < K && t0 + t < ntok) ? base[(size_t)ci * plane + (size_t)ky * a.Wimg] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int rest = half + 2 * r;
+      if (rest * 2 < KP) Xs[t * KS + rest * 2 + q] = v[r];
+    }
+  }
+  {
+    const float* W = a.w[g];
+    stage_batched(C * KP, [&](int i) { const int c = i / KP, j = i - c * KP; return j < K ? W[(size_t)c * Kp + j] : 0.f; },
+                  [&](int i, float v) { const int c = i / KP, j = i - c * KP; Wsm[c * KS + j] = v; });
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  constexpr int NTM = kFcC0 / 16;
+  const int nt = (C + 15) / 16;
+  fr4 acc[NTM];
+  const float* xr = Xs + (wave * 16 + li) * KS + 4 * gq;
+#pragma unroll
+  for (int n = 0; n < NTM; ++n) {
+    acc[n] = fr4{0.f, 0.f, 0.f, 0.f};
+    if (n < nt) {
+      const float* wr = Wsm + min(n * 16 + li, C - 1) * KS + 4 * gq;
+      for (int s4 = 0; s4 < KP; s4 += 16) {
+        const f4 xa = *reinterpret_cast<const f4*>(xr + s4);
+        const f4 wb = *reinterpret_cast<const f4*>(wr + s4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], wb[e], acc[n], 0, 0, 0);
+      }
+    }
+  }
+  const int tk0 = t0 + wave * 16 + 4 * gq;
+  float ex[NTM][4];
+#pragma unroll
+  for (int n = 0; n < NTM; ++n) {  // every epilogue load before the first store
+    const int c = min(n * 16 + li, C - 1);
+    const float bias = a.bias[g][c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = min(tk0 + r, ntok - 1);
+      ex[n][r] = n < nt ? a.pos[g][(size_t)(tok % (a.Ho * a.Wo)) * C + c] : 0.f;
+      acc[n][r] += bias;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NTM; ++n) {
+    const int c = n * 16 + li;
+    if (n >= nt || c >= C) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (tk0 + r < ntok) a.tok[g][(size_t)(tk0 + r) * C + c] = ex[n][r] + acc[n][r];
+  }
+}
+
+// k_fc_convT_mf: ConvTranspose2d (kernel (kh, 2), stride (2, 2)) gathered per OUTPUT pixel row y, so overlapping taps
+// (kh = 3: rows 2 iy + 2 = 2 (iy + 1) + 0) sum in registers without atomics: out[oc(co)][y][2 ix + kx] = bias[co] +
+// sum over (iy, ky) with y = 2 iy + ky of sum_c tok[iy][ix][c] W2[(co kh + ky) 2 + kx][c]. A workgroup (4 waves of 16
+// token columns) covers 8 output rows of one parity with the weights of that parity's taps staged in LDS as
+// [tap][j = co 2 + kx][c]; each wave: per row, one MFMA chain per 16 outputs j over the taps' K = C0 each; stores of
+// two horizontally adjacent pixels (kx = 0, 1) per lane, consecutive lanes = consecutive pixels.
+constexpr int kFcRows = 8;
+template <int C0>
+__global__ __launch_bounds__(256) void k_fc_convT_mf(ConvArgs a) {  // a.w[g]: W2 [(co kh + ky) kw + kx][C0]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int kFcC0 = C0, C = C0, CS = C0 + 4;
+  const int g = blockIdx.z, cout = a.cout[g];
+  const int par = blockIdx.y & 1, y0 = par + 2 * kFcRows * (blockIdx.y >> 1);
+  const int ntap = (a.kh - par + 1) / 2;  // taps ky = par, par + 2, ...
+  const int J = 2 * cout, JP = (J + 15) / 16 * 16;
+  // stage [tap][j][c] for ky = par + 2 tap: W2 row (co kh + ky) 2 + kx
+  const float* W = a.w[g];
+  stage_batched(ntap * JP * C,
+                [&](int i) {
+                  const int c = i % C, jj = (i / C) % JP, tap = i / (C * JP);
+                  return jj < J ? W[((size_t)((jj >> 1) * a.kh + par + 2 * tap) * 2 + (jj & 1)) * C + c] : 0.f;
+                },
+                [&](int i, float v) {
+                  const int c = i % C, r = i / C;  // r = tap JP + jj
+                  sm[r * CS + c] = v;
+                });
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
+  const int ix = (blockIdx.x * 4 + wave) * 16 + li;
+  if ((blockIdx.x * 4 + wave) * 16 >= a.Wo) return;
+  const bool okx = ix < a.Wo;
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  constexpr int NMT = 64 / 16;  // j tiles: 2 cout <= 64
+  const int nmt = JP / 16;
+  for (int yy = 0; yy < kFcRows; ++yy) {
+    const int y = y0 + 2 * yy;
+    if (y >= a.Himg) break;
+    for (int b = 0; b < a.B; ++b) {
+      fr4 acc[NMT];
+#pragma unroll
+      for (int m = 0; m < NMT; ++m) acc[m] = fr4{0.f, 0.f, 0.f, 0.f};
+      for (int tap = 0; tap < ntap; ++tap) {
+        const int ky = par + 2 * tap, iy2 = y - ky;
+        if (iy2 < 0 || iy2 >= 2 * a.Ho) continue;
+        const int iy = iy2 >> 1;
+        const float* tr = a.tok[g] + (((size_t)b * a.Ho + iy) * a.Wo + (okx ? ix : 0)) * C + 4 * gq;
+        f4 yv[kFcC0 / 16];
+#pragma unroll
+        for (int s = 0; s < kFcC0 / 16; ++s) {
+          f4 v = {0.f, 0.f, 0.f, 0.f};
+          if (16 * s < C) v = *reinterpret_cast<const f4*>(tr + 16 * s);
+          yv[s] = v;
+        }
+#pragma unroll
+        for (int m = 0; m < NMT; ++m) {
+          if (m < nmt) {
+            const float* wr = sm + (tap * JP + m * 16 + li) * CS + 4 * gq;
+#pragma unroll
+            for (int s = 0; s < kFcC0 / 16; ++s) {
+              if (16 * s < C) {
+                const f4 wa = *reinterpret_cast<const f4*>(wr + 16 * s);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[e], yv[s][e], acc[m], 0, 0, 0);
+              }
+            }
+          }
+        }
+      }
+      // lane holds j = 16 m + 4 gq + r: co = 8 m + 2 gq + r / 2, kx = r % 2
+      float bs[NMT][2];
+#pragma unroll
+      for (int m = 0; m < NMT; ++m)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bs[m][h] = a.bias[g][min(8 * m + 2 * gq + h, cout - 1)];
+      if (!okx) continue;
+#pragma unroll
+      for (int m = 0; m < NMT; ++m) {
+        if (m >= nmt) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int co = 8 * m + 2 * gq + h;
+          if (co >= cout) continue;
+          const int oc = co < cout / 2 ? a.mean_off[g] + co : a.std_off[g] + (co - cout / 2);
+          if (a.climit > 0 && oc >= a.climit) continue;
+          float* o = a.img_out + (((size_t)b * a.Ctot + oc) * a.Himg + y) * a.Wimg + 2 * ix;
+          *reinterpret_cast<float2*>(o) = make_float2(acc[m][2 * h] + bs[m][h], acc[m][2 * h + 1] + bs[m][h]);
+        }
+      }
+    }
+  }
+}
+
 // Global-window attention as GEMMs (LG layer 0, Hg*Wg tokens): V^T per head, zero-padded to Np columns
 __global__ void k_vt(const float* qkv, float* vt, int N, int Np, int C, int heads, int hd) {
   const size_t total = (size_t)heads * hd * Np;
@@ -1395,18 +1589,37 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     pa.cin_off[g] = off;
     pa.cin[g] = c.raw.inchans[g];
   }
-  // PatchEmbed = im2col + GEMM (+bias, +absolute_pos_embed in the epilogue)
-  const size_t colg = (size_t)M[0] * m->Kp;
+  const vv::Tuning& TU = m->tune ? *m->tune : vv::kDefaultTuning;
+  // the direct MFMA conv kernels: patch (kh, 2) / stride (2, 2), C0 32 or 96, <= kFcKP taps (LGUnet_all_1's configs)
+  const bool conv_mf = TU.fc_conv_mf && c.kw == 2 && c.sw == 2 && c.sh == 2 && c.kh <= 3 && m->Kp <= kFcKP &&
+                       (c.Cl[0] == 32 || c.Cl[0] == 96) && 2 * c.Wl[0] == c.Wimg && (c.Himg - c.kh) / 2 + 1 == c.Hl[0];
   int ph = prof_begin(st);
-  hipLaunchKernelGGL(k_im2col, dim3(grid_for(colg), G), dim3(256), 0, st, pa, m->h, m->Kp, colg);
-  FH(hipGetLastError());
-  prof_end(ph, st, PC_PATCH, 0.0, 8.0 * G * colg);
-  GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID, *m);
-  pe.rmod = c.Hl[0] * c.Wl[0];
-  pe.ldr = c.Cl[0];
-  for (int g = 0; g < G; ++g)
-    pe.g[g] = {m->h + g * colg, nullptr, m->Wp[g], pa.bias[g], pa.tok[g], pa.pos[g], nullptr};
-  FH(gemm_nt(pe, st, -1, m->ws));
+  if (conv_mf) {
+    ConvArgs pm = pa;
+    for (int g = 0; g < G; ++g) pm.w[g] = m->Wp[g];
+    const size_t lds = (size_t)(64 + c.Cl[0]) * (m->Kp + 4) * sizeof(float);
+    const dim3 grid((M[0] + 63) / 64, G);
+    if (c.Cl[0] == 96) {
+      FH(set_lds_limit((const void*)k_fc_patch_mf<96>, (64 + 96) * (kFcKP + 4) * sizeof(float)));
+      hipLaunchKernelGGL(k_fc_patch_mf<96>, grid, dim3(256), lds, st, pm, m->Kp);
+    } else {
+      hipLaunchKernelGGL(k_fc_patch_mf<32>, grid, dim3(256), lds, st, pm, m->Kp);
+    }
+    FH(hipGetLastError());
+    prof_end(ph, st, PC_PATCH, 2.0 * G * M[0] * c.Cl[0] * m->Kp, 4.0 * ((double)B * c.Cin * c.Himg * c.Wimg + 2.0 * G * M[0] * c.Cl[0]));
+  } else {
+    // PatchEmbed = im2col + GEMM (+bias, +absolute_pos_embed in the epilogue)
+    const size_t colg = (size_t)M[0] * m->Kp;
+    hipLaunchKernelGGL(k_im2col, dim3(grid_for(colg), G), dim3(256), 0, st, pa, m->h, m->Kp, colg);
+    FH(hipGetLastError());
+    prof_end(ph, st, PC_PATCH, 0.0, 8.0 * G * colg);
+    GemmArgs pe = gbase(M[0], c.Cl[0], m->Kp, G, EPI_RESID, *m);
+    pe.rmod = c.Hl[0] * c.Wl[0];
+    pe.ldr = c.Cl[0];
+    for (int g = 0; g < G; ++g)
+      pe.g[g] = {m->h + g * colg, nullptr, m->Wp[g], pa.bias[g], pa.tok[g], pa.pos[g], nullptr};
+    FH(gemm_nt(pe, st, -1, m->ws));
+  }
   for (int l = 0; l < L; ++l) {
     if (l > 0) {
       // PatchMerging (LGUnet_all.py:77-96): gather + LN(4C) + reduction, BEFORE the blocks (:236-246)
@@ -1514,6 +1727,25 @@ int forward(FModel* m, const float* in, float* out, int climit, hipStream_t st, 
     mo += co / 2;
     so += co - co / 2;
     maxc = std::max(maxc, co);
+  }
+  if (conv_mf && maxc <= 32) {
+    // ConvTranspose2d gathered per output row (overlapping taps summed in registers), no GEMM / col2im buffers
+    ConvArgs pm = pu;
+    for (int g = 0; g < G; ++g) pm.w[g] = m->W2[g];
+    const int JP = (2 * maxc + 15) / 16 * 16, ntap = (c.kh + 1) / 2;
+    const size_t lds = (size_t)ntap * JP * (c.Cl[0] + 4) * sizeof(float);
+    const dim3 grid((c.Wl[0] + 63) / 64, 2 * ((c.Himg + 2 * kFcRows - 1) / (2 * kFcRows)), G);
+    ph = prof_begin(st);
+    if (c.Cl[0] == 96) {
+      FH(set_lds_limit((const void*)k_fc_convT_mf<96>, (size_t)2 * 64 * (96 + 4) * sizeof(float)));
+      hipLaunchKernelGGL(k_fc_convT_mf<96>, grid, dim3(256), lds, st, pm);
+    } else {
+      hipLaunchKernelGGL(k_fc_convT_mf<32>, grid, dim3(256), lds, st, pm);
+    }
+    FH(hipGetLastError());
+    prof_end(ph, st, PC_PATCH, 2.0 * M[0] * c.Cl[0] * c.kh * c.kw * (double)c.Cout / 2,
+             4.0 * ((double)G * M[0] * c.Cl[0] + (double)B * c.Cout * c.Himg * c.Wimg));
+    return 0;
   }
   // ConvTranspose2d = GEMM (tokens x transposed weight) + col2im of the overlapping taps
   const size_t yg = (size_t)M[0] * m->NT;

@@ -2278,6 +2278,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h4_split_minkt") return &t.h4_split_minkt;
   if (k == "h5") return &t.h5;
   if (k == "h5_var") return &t.h5_var;
+  if (k == "fc_conv_mf") return &t.fc_conv_mf;
   return nullptr;
 }
 

@@ -29,7 +29,8 @@ struct Tuning {
                                 // on vs 81.0 / 81.8 off, same box (profiles/r03/ab_attn_planes)
   int h4_split_minkt = 12;      // k-tiles per chunk at least, for that split of tile 48
   int h5 = 1;                   // tile 49 (256 x 144, k_gemm_h5) where its tiles fill whole rounds and tile 48's do not
-  int h5_var = 0;               // tile 49 schedule variant (experiments)
+  int fc_conv_mf = 1;           // LGUnet_all_1 PatchEmbed / ConvTranspose2d as direct MFMA kernels (0: im2col / col2im + GEMM)
+  int h5_var = 4;               // tile 49 schedule variant (4: B blocks read in groups of three, two groups ahead)
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)

@@ -1296,50 +1296,90 @@ __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
     tok_coords(okt ? tok : 0, Ho, Wo, b, ho, wo);
     const size_t plane = (size_t)a.Himg * a.Wimg;
     const float* base = a.img + (size_t)b * a.Cimg * plane + (size_t)(2 * ho) * a.Wimg + 2 * wo + q;
-    for (int rest = half; rest < KP / 2; rest += 2) {  // rest = ci 2 + p (co 2 + p)
-      const int ci = rest >> 1, pp = rest & 1;
-      float v = 0.f;
-      if (okt && ci * 4 < kc) {
+    // all of this thread's pixel loads in flight before the first LDS store (one memory latency, not one per load)
+    constexpr int NR = kPatchKmax / 4;  // (ci, p) rows per thread at most
+    float v[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int rest = half + 2 * r, ci = rest >> 1, pp = rest & 1;  // rest = ci 2 + p (co 2 + p)
+      v[r] = 0.f;
+      if (rest < KP / 2 && okt && ci * 4 < kc) {
         const int ch = MODE == 0 ? G.cin_off + ci : unembed_ch(G, ci);
-        if (MODE == 0 || ch < a.climit) v = base[(size_t)ch * plane + pp * a.Wimg];
+        if (MODE == 0 || ch < a.climit) v[r] = base[(size_t)ch * plane + pp * a.Wimg];
       }
-      Xs[t * KS + ci * 4 + pp * 2 + q] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int rest = half + 2 * r;
+      if (rest < KP / 2) Xs[t * KS + (rest >> 1) * 4 + (rest & 1) * 2 + q] = v[r];
     }
   }
-  for (int i = threadIdx.x; i < C * KP; i += 256) {
-    const int c = i / KP, j = i - c * KP;
-    Wsm[c * KS + j] = j < kc ? G.w[(size_t)c * kc + j] : 0.f;
+  {
+    constexpr int NW = kPatchCmax * kPatchKmax / 256 / 2;  // two batches of loads
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[NW];
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
+        v[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
+        if (c < C) Wsm[c * KS + j] = v[r];
+      }
+    }
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tb = wave * 16;  // this wave's 16 tokens within the workgroup
   typedef float fr4 __attribute__((ext_vector_type(4)));
+  constexpr int NTM = kPatchCmax / 16;
   const int nt = (C + 15) / 16;
-  for (int n = 0; n < nt; ++n) {
-    fr4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int c = n * 16 + li;
-    const float* xr = Xs + (tb + li) * KS + 4 * g;
-    const float* wr = Wsm + min(c, C - 1) * KS + 4 * g;
-    for (int s4 = 0; s4 < KP; s4 += 16) {
-      const f4 xa = *reinterpret_cast<const f4*>(xr + s4);
-      const f4 wb = *reinterpret_cast<const f4*>(wr + s4);
+  fr4 acc[NTM];
+  const float* xr = Xs + (tb + li) * KS + 4 * g;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], wb[e], acc, 0, 0, 0);
-    }
-    if (c < C) {
-      const float bias = MODE == 0 ? G.bias[c] : 0.f;
+  for (int n = 0; n < NTM; ++n) {
+    acc[n] = fr4{0.f, 0.f, 0.f, 0.f};
+    if (n < nt) {
+      const float* wr = Wsm + min(n * 16 + li, C - 1) * KS + 4 * g;
+      for (int s4 = 0; s4 < KP; s4 += 16) {
+        const f4 xa = *reinterpret_cast<const f4*>(xr + s4);
+        const f4 wb = *reinterpret_cast<const f4*>(wr + s4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tok = t0 + tb + 4 * g + r;
-        if (tok >= ntok) continue;
-        if (MODE == 0) {
-          const int rem = tok % (Ho * Wo);
-          G.tok[(size_t)tok * C + c] = (acc[r] + bias) + G.pos[(size_t)rem * C + c];
-        } else {
-          G.tok[(size_t)tok * C + c] = acc[r];
-        }
+        for (int e = 0; e < 4; ++e) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], wb[e], acc[n], 0, 0, 0);
       }
     }
+  }
+  // epilogue: every load (bias, pos) issued before the first store (a load behind a store to a possibly aliasing
+  // address waits for it: one memory latency per element)
+  const int tk0 = t0 + tb + 4 * g;
+  if (MODE == 0) {
+    float ex[NTM][4];
+#pragma unroll
+    for (int n = 0; n < NTM; ++n) {
+      const int c = min(n * 16 + li, C - 1);
+      const float bias = G.bias[c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = min(tk0 + r, ntok - 1);
+        ex[n][r] = n < nt ? G.pos[(size_t)(tok % (Ho * Wo)) * C + c] : 0.f;
+        acc[n][r] += bias;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NTM; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[n][r] = acc[n][r] + ex[n][r];
+  }
+#pragma unroll
+  for (int n = 0; n < NTM; ++n) {
+    const int c = n * 16 + li;
+    if (n >= nt || c >= C) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (tk0 + r < ntok) G.tok[(size_t)(tk0 + r) * C + c] = acc[n][r];
   }
 }
 
@@ -1352,9 +1392,23 @@ __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
   const int CP = (C + 15) / 16 * 16, CS = CP + 4;
   float* Wt = sm;  // [KP][CS]: W[c][j] at Wt[j][c]
   const int KP = (kc + 15) / 16 * 16;
-  for (int i = threadIdx.x; i < KP * CP; i += 256) {  // coalesced over W's rows, transposed into LDS
-    const int c = i / KP, j = i - c * KP;
-    Wt[j * CS + c] = (j < kc && c < C) ? G.w[(size_t)c * kc + j] : 0.f;
+  {
+    // coalesced over W's rows, transposed into LDS; two batches of loads in flight before their LDS stores
+    constexpr int NW = kPatchCmax * kPatchKmax / 256 / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[NW];
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
+        v[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
+        if (c < CP) Wt[j * CS + c] = v[r];
+      }
+    }
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tok = blockIdx.x * PT + wave * 16 + li;
@@ -1369,37 +1423,55 @@ __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
   }
   __syncthreads();
   typedef float fr4 __attribute__((ext_vector_type(4)));
+  constexpr int NMT = kPatchKmax / 16;
   int b, ho, wo;
   tok_coords(ok ? tok : 0, Ho, Wo, b, ho, wo);
-  for (int mt = 0; mt < KP / 16; ++mt) {
-    fr4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wr = Wt + (mt * 16 + li) * CS + 4 * g;
+  const int nmt = KP / 16;
+  fr4 acc[NMT];
 #pragma unroll
-    for (int s = 0; s < kPatchCmax / 16; ++s) {
-      if (16 * s < CP) {
-        const f4 wa = *reinterpret_cast<const f4*>(wr + 16 * s);
+  for (int mt = 0; mt < NMT; ++mt) {
+    acc[mt] = fr4{0.f, 0.f, 0.f, 0.f};
+    if (mt < nmt) {
+      const float* wr = Wt + (mt * 16 + li) * CS + 4 * g;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[e], y[s][e], acc, 0, 0, 0);
+      for (int s = 0; s < kPatchCmax / 16; ++s) {
+        if (16 * s < CP) {
+          const f4 wa = *reinterpret_cast<const f4*>(wr + 16 * s);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[e], y[s][e], acc[mt], 0, 0, 0);
+        }
       }
     }
-    // rows 4 g + r of output tile mt: channel o = 4 mt + g, p = r / 2, q = r % 2
+  }
+  // rows 4 g + r of output tile mt: channel o = 4 mt + g, p = r / 2, q = r % 2. Every load (bias, the added image)
+  // is issued before the first store.
+  size_t off[NMT];
+  bool st[NMT];
+  float2 ex[NMT][2];
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
     const int o = 4 * mt + g;
-    if (!ok || o * 4 >= kc) continue;
-    const int ch = MODE == 0 ? G.cin_off + o : unembed_ch(G, o);
-    if (MODE == 1 && ch >= a.climit) continue;
-    const float bias = MODE == 1 ? G.bias[o] : 0.f;
+    const int oc = min(o, kc / 4 - 1);
+    const int ch = MODE == 0 ? G.cin_off + oc : unembed_ch(G, oc);
+    st[mt] = ok && mt < nmt && o * 4 < kc && (MODE == 0 || ch < a.climit);
+    off[mt] = (((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
+    if (MODE == 0) {
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      const size_t off = (((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho + pp) * a.Wimg + 2 * wo;
-      float2 v;
-      if (MODE == 0) {
-        const float2 ad = a.add_img ? *reinterpret_cast<const float2*>(a.add_img + off) : make_float2(0.f, 0.f);
-        v = make_float2(acc[2 * pp] + ad.x, acc[2 * pp + 1] + ad.y);
-      } else {
-        v = make_float2(acc[2 * pp] + bias, acc[2 * pp + 1] + bias);
-      }
-      *reinterpret_cast<float2*>(a.img_out + off) = v;
+      for (int pp = 0; pp < 2; ++pp)
+        ex[mt][pp] = (a.add_img && st[mt]) ? *reinterpret_cast<const float2*>(a.add_img + off[mt] + pp * a.Wimg)
+                                          : make_float2(0.f, 0.f);
+    } else {
+      const float bias = G.bias[oc];
+      ex[mt][0] = ex[mt][1] = make_float2(bias, bias);
     }
+  }
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    if (!st[mt]) continue;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp)
+      *reinterpret_cast<float2*>(a.img_out + off[mt] + pp * a.Wimg) =
+          make_float2(acc[mt][2 * pp] + ex[mt][pp].x, acc[mt][2 * pp + 1] + ex[mt][pp].y);
   }
 }
 
