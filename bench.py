@@ -222,7 +222,7 @@ def sc4dvar_line(dev_index: int):
 def gemm_rocprof(key="gemm16_avg_us_per_call"):
     """Average rocprofv3 --kernel-trace --stats duration per fp16x3 GEMM call (main kernel + row scales + split-K
     fixup, tools/rocprof_gemm_summary.py) from the latest committed profile of `bench.py` itself."""
-    for rnd in ("r03", "r02"):
+    for rnd in ("r04", "r03", "r02"):
         path = os.path.join(ROOT, "profiles", rnd, "gemm_rocprof_summary.json")
         try:
             with open(path) as f:
@@ -235,7 +235,7 @@ def gemm_rocprof(key="gemm16_avg_us_per_call"):
 def gemm_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes of `bench.py` (FETCH_SIZE x2 +
     WRITE_SIZE with the gfx950 corrections, tools/pmc_traffic.py); PMC counters cannot be read live."""
-    for rnd in ("r03", "r02", "r01"):
+    for rnd in ("r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, "gemm_traffic.json")
         try:
             with open(path) as f:
@@ -528,7 +528,7 @@ def main():
         allg = {k: g16[k] + g6[k] for k in ("ms", "flops", "bytes", "launches")}
         if math == "split16":
             dom, peak, tkey = g16, PEAK_SPLIT16_TFLOPS, "fp16x3"
-            kname = ("the fp16x3 GEMM class: k_gemm_h4 (tile 48, LDS-DMA on pre-split planes) / k_gemm_h3(m) with "
+            kname = ("the fp16x3 GEMM class: k_gemm_h4 / k_gemm_h5 (tiles 48 / 49, LDS-DMA on pre-split planes) / k_gemm_h3(m) with "
                      "their split-K fixups and the A split / row-scale passes: every GEMM launch that ran an fp16x3 "
                      "kernel in a HIP-event-profiled repeat of one timed analysis")
             desc = ("fp16x3 split: fp32 operands scaled per row by 2^e and split into 2 fp16 planes, 3 "

@@ -36,8 +36,10 @@ def summary(keys, what):
 out = {
     # one fp16x3 GEMM = its A pass (k_rowsplit / k_rowscale, or none when the LayerNorm wrote the planes / scales) +
     # the main kernel (k_gemm_h4 tile 48, k_gemm_h3(m)) + fixup: counted per main-kernel launch
-    "fp16x3": summary(("k_gemm_h4", "k_gemm_h3"), "fp16x3 main-kernel launches (k_gemm_h4 + k_gemm_h3(m))"),
+    "fp16x3": summary(("k_gemm_h4", "k_gemm_h5", "k_gemm_h3"),
+                      "fp16x3 main-kernel launches (k_gemm_h4 + k_gemm_h5 + k_gemm_h3(m))"),
     "k_gemm_h4": summary(("k_gemm_h4",), "k_gemm_h4 (tile 48) launches"),
+    "k_gemm_h5": summary(("k_gemm_h5",), "k_gemm_h5 (tile 49) launches"),
     "k_gemm_h3": summary(("k_gemm_h3",), "k_gemm_h3(m) launches"),
     "a_pass": summary(("k_rowsplit", "k_rowscale"), "A split / row-scale passes (k_rowsplit, k_rowscale)"),
     "all": summary(("k_gemm_nt", "k_gemm_bs", "k_gemm_h3", "k_gemm_h4"), "every GEMM main-kernel launch"),

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 --stats kernel_stats.csv for the GEMM classes as bench.py reports them (dev tool).
 
 One bench 'GEMM launch' = one gemm_nt call:
-  gemm16 (fp16x3): the A pass (k_rowsplit / k_rowscale / k_gather_scales) + k_gemm_h4 / k_gemm_h3(m) + their split-K
+  gemm16 (fp16x3): the A pass (k_rowsplit / k_rowscale / k_gather_scales) + k_gemm_h4 / k_gemm_h5 / k_gemm_h3(m) + their split-K
                    fixups (k_gemm_fixup_sub / _sub16); per call = sum / main-kernel calls
   all:             every GEMM kernel (main + fixups + k_rowscale); per call = sum / main-kernel calls
 Usage: rocprof_gemm_summary.py <run_kernel_stats.csv> [out.json]"""
@@ -13,7 +13,7 @@ main_n = main_ns = fix_ns = 0
 other = {}
 for r in rows:
     n, calls, tot = r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])
-    if "k_gemm_h3" in n or "k_gemm_h4" in n:
+    if "k_gemm_h3" in n or "k_gemm_h4" in n or "k_gemm_h5" in n:
         h3_n += calls
         h3_ns += tot
         main_n += calls
