@@ -231,7 +231,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    also for 64..143 256-row tiles, 1), "h4_split_minkt" (k-tiles per chunk of that split, 12), "h5" (tile 49, 256x144, where its
    tiles fill whole rounds of the chip and tile 48's leave a split-K tail: the N = 4608 GEMMs at 2048 rows, 1), "h5_var"
    (tile 49's schedule variant, experiments), "fc_conv_mf" (LGUnet_all_1's PatchEmbed / ConvTranspose2d as direct
-   exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1). Results stay fp32-level for every value; a change drops the
+   exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1), "mlp_hc" (the fused dim-192 MLP: 32 or 64 hidden units
+   per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key: VV_E_ARG. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);

@@ -569,13 +569,15 @@ def test_ln_row_scales_bitwise(tmp_path):
 
 
 @pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_mlp", 3), ("fuse_attn", 1), ("fuse_attn", 3),
-                                     ("attn_mfma", 1)])
+                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2)])
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient; 1 at dim 96, 3 also at dim 192) and fuse_attn (LN1 + qkv +
     window attention + proj + residual: 1 the forward, 3 also its input gradient); attn_mfma (the window attention of
     the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and backward on the exact-f32 MFMA instead of
-    the VALU kernels: fp32 products either way, only the summation order differs). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
+    the VALU kernels: fp32 products either way, only the summation order differs); mlp_hc 64 (the dim-192 fused MLP
+    in 64-unit hidden chunks, or 2: its hidden layer split over two waves per 16 tokens -- the hidden operand's
+    per-(token, chunk) scales and the order of the chunk sums change). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
     per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
     max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
     from vaevar.engine import DAProblem
@@ -605,6 +607,37 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     print(f"{knob} {on} vs 0: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert not torch.equal(o0, o1), "the fused kernel did not run"
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
+
+
+def test_h5_row_epilogue_bitwise(full_dec):
+    """Tile 49's full tiles go through the row-wise LDS epilogue (h5_var 4: accumulators -> LDS -> float4 rows: the
+    GELU / gelu' plane writers with their pre-activation stores and reads, bias) instead of the per-fragment one
+    (h5_var 5, same main loop): the same per-element arithmetic, so the config-2 decoder output, its input gradient and
+    the closure are bit-identical."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field, uniform_sym
+
+    z = torch.from_numpy(0.5 * smooth_field(411, (1, 32, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(412, (1, 69, 128, 256), 1.0)).cuda()
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    zc = torch.from_numpy(0.3 * smooth_field(413, (1, 32, 128, 256))).cuda()
+    res = []
+    default = full_dec.ctx.get_tuning("h5_var")
+    try:
+        for v in (5, 4):
+            full_dec.ctx.set_tuning("h5_var", v)
+            out = full_dec.forward_raw(z).clone()
+            dz = torch.empty_like(z)
+            full_dec.backward_raw(cot, dz)
+            g = torch.empty_like(zc)
+            jb, jo = prob.closure(zc, g)
+            res.append((out, dz, jb, jo, g))
+    finally:
+        full_dec.ctx.set_tuning("h5_var", default)
+    (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
+    assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1)
+    assert (jb0, jo0) == (jb1, jo1)
 
 
 @pytest.mark.parametrize("knob,extra", [("gelu_planes", {}), ("attn_planes", {"h4_small": 1})])

@@ -598,6 +598,7 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
   ma.C = C;
   ma.ngroups = S.G;
   ma.eps = 1e-5f;
+  ma.hc = T.mlp_hc;
   for (int g = 0; g < S.G; ++g) {
     const auto& w = S.w[b][g];
     vv::MlpGroup& G = ma.g[g];

@@ -1,0 +1,56 @@
+// GELU and its derivative for the epilogues (vv_gemm.hip) and the fused tower MLP (vv_tower.hip):
+// nn.GELU() (exact, erf form; networks_old/utils/swinblock.py:13-29 Mlp act_layer) at fp32 level, branch-free.
+//
+//   h(x)    = Phi(-|x|) = 0.5 erfc(|x| / sqrt 2) = 2^(u S(u) - 1),  u = min(|x|, 5.75)
+//   Phi(x)  = x >= 0 ? 1 - h : h
+//   GELU(x) = x Phi(x)  = x >= 0 ? x - x h : x h
+//   GELU'(x) = Phi(x) + x phi(x),  phi(x) = 2^(x^2 (-0.5 log2 e) + log2(1 / sqrt(2 pi)))
+//
+// S: degree-8 polynomial fitted to log2(2 h(u)) / u (tools/fit_erf.py, weights towards minimax on the GELU error
+// relative to |x|). In float32 (Horner fma chain, v_exp_f32): GELU within 8.7e-8 |x|, Phi and GELU' within 8.2e-8
+// absolute of float64 over [-9, 9] -- the rounding of the result itself; the libm erff path costs ~40 VALU
+// instructions per element with its two divergent ranges, this one 15 (GELU) / 19 (GELU').
+// Built with VV_GELU_ERFF: the erff forms (A/B builds only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+namespace vv {
+
+__device__ __forceinline__ float gelu_h(float x) {
+  const float u = fminf(fabsf(x), 5.75f);
+  float s = 5.128587759e-07f;
+  s = fmaf(s, u, -9.560183571e-06f);
+  s = fmaf(s, u, 7.497351908e-05f);
+  s = fmaf(s, u, -2.843466355e-04f);
+  s = fmaf(s, u, 1.498893471e-05f);
+  s = fmaf(s, u, 6.931121461e-03f);
+  s = fmaf(s, u, -5.243476480e-02f);
+  s = fmaf(s, u, -4.592214525e-01f);
+  s = fmaf(s, u, -1.151104212e+00f);
+  return __builtin_amdgcn_exp2f(fmaf(u, s, -1.0f));
+}
+
+#ifdef VV_GELU_ERFF
+__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float dgelu_fast(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+#else
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float xh = x * gelu_h(x);
+  return x >= 0.0f ? x - xh : xh;
+}
+__device__ __forceinline__ float dgelu_fast(float x) {
+  const float h = gelu_h(x);
+  const float cdf = x >= 0.0f ? 1.0f - h : h;
+  // phi(x) = 2^(-x^2 log2(e) / 2 - log2(sqrt(2 pi)))
+  const float pdf = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170f, -1.3257480647361593f));
+  return fmaf(x, pdf, cdf);
+}
+#endif
+
+}  // namespace vv

@@ -10,6 +10,7 @@
 // reads 4 consecutive k of its row with one ds_read_b128 (rows padded to 36 floats: conflict-free).
 // Double-buffered LDS, register-staged global prefetch of tile t+1 during the MFMAs of tile t,
 // one barrier per k-tile.
+#include "vv_gelu.h"
 #include "vv_kernels.h"
 
 #include <algorithm>
@@ -24,12 +25,8 @@ namespace vv {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float dgelu_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+__device__ __forceinline__ float gelu_f(float x) { return gelu_fast(x); }  // vv_gelu.h
+__device__ __forceinline__ float dgelu_f(float x) { return dgelu_fast(x); }
 
 constexpr int KALIGN = 32;  // K, ksplit granularity accepted by gemm_nt (covers every BK variant)
 
@@ -1828,6 +1825,85 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
     epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
 }
 
+// Row-wise epilogue of a full tile staged in LDS (tile 49): a wave's 32 x BN fp32 results, written to LDS from the
+// accumulators, are read back as float4 chunks of rows, so bias / aux are float4 loads, aux and C float4 stores and
+// the fp16x3 planes 8-byte stores of 4 halfs (the register epilogue stores 2 bytes per plane and element). Same
+// per-element arithmetic as epilogue() (results bit-identical); rows in GEMM order (no crow), no residual.
+template <int BN, int EPI_>
+__device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGroup& G, const float* E, int LS, int r0,
+                                              int n0, int lane) {
+  constexpr bool PL = EPI_ == EPI_GELU_PL || EPI_ == EPI_DGELU_PL;
+  constexpr int EPI = EPI_ == EPI_GELU_PL ? EPI_GELU : EPI_ == EPI_DGELU_PL ? EPI_DGELU : EPI_;
+  constexpr int CH = BN / 4, NCH = 32 * CH / 64, B6 = 6;  // float4 chunks per row / per lane; batch of loads
+  static_assert(NCH % B6 == 0, "chunk batches");
+  const int N = args.N;
+  float ubw = 0.f, ubb = 0.f;
+  if constexpr (PL) {
+    const float tw = *args.obw, tb = *(args.obb ? args.obb : args.obw);
+    constexpr float f = EPI == EPI_GELU ? 1.0f : 1.25f;
+    ubw = f * (float)args.K * tw;
+    ubb = args.obb ? f * tb : 0.0f;
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < NCH; i0 += B6) {
+    f4 v[B6], bv[B6], ex[B6];
+    float sc[B6];
+#pragma unroll
+    for (int j = 0; j < B6; ++j) {
+      const int e = lane + 64 * (i0 + j), rr = e / CH, col = 4 * (e - rr * CH);
+      const int gr = r0 + rr, gc = n0 + col;
+      v[j] = *reinterpret_cast<const f4*>(E + rr * LS + col);
+      const f4 t = *reinterpret_cast<const f4*>(G.bias ? G.bias + gc : G.A);  // unconditional (dummy address)
+      bv[j] = G.bias ? t : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_DGELU) ex[j] = *reinterpret_cast<const f4*>(G.aux + (size_t)gr * args.ldaux + gc);
+      if constexpr (PL) {
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(args.escale[gr]));
+        const unsigned mx = __float_as_uint(2.0f * (ubw * (32768.0f * ia) + ubb));
+        sc[j] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B6; ++j) {
+      const int e = lane + 64 * (i0 + j), rr = e / CH, col = 4 * (e - rr * CH);
+      const int gr = r0 + rr, gc = n0 + col;
+      f4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float x = v[j][q] + bv[j][q];
+        if constexpr (EPI == EPI_GELU) {
+          x = gelu_f(x);
+        } else if constexpr (EPI == EPI_DGELU) {
+          x = v[j][q] * dgelu_f(ex[j][q]);
+        }
+        o[q] = x;
+      }
+      if constexpr (EPI == EPI_GELU) {
+        if (G.aux) {
+          f4 pre;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pre[q] = v[j][q] + bv[j][q];
+          *reinterpret_cast<f4*>(G.aux + (size_t)gr * args.ldaux + gc) = pre;  // the pre-activation, for a backward
+        }
+      }
+      if constexpr (PL) {
+        h4v hv, lv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float x = o[q] * sc[j];
+          hv[q] = (_Float16)x;
+          lv[q] = (_Float16)(x - (float)hv[q]);
+        }
+        unsigned short* pp = args.opl + (size_t)gr * 2 * N + 2 * (gc & ~31) + (gc & 31);  // chunk-interleaved
+        *reinterpret_cast<h4v*>(pp) = hv;
+        *reinterpret_cast<h4v*>(pp + 32) = lv;
+        if (gc == 0) args.ors[gr] = sc[j];
+      } else {
+        *reinterpret_cast<f4*>(G.C + (size_t)gr * args.ldc + gc) = o;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // Tile 49: the tile-48 operands (fp16x3 planes, both by LDS-DMA through a 3-stage ring) on 256 x 144 tiles, so that
 // the N = 4608 GEMMs at 2048 rows (fc1 forward, the fc2 input gradient) are exactly 8 x 32 = 256 tiles: one round
@@ -2041,7 +2117,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   read_a(0, fa0);
-  if constexpr (VAR == 4) {
+  if constexpr (VAR == 4 || VAR == 5) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) read_b(0, i, gb[0][i]);
   } else {
@@ -2051,7 +2127,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int t = 0;
-  if constexpr (VAR == 4) {
+  if constexpr (VAR == 4 || VAR == 5) {
     for (; t + 1 < nk; t += 2) {
       step4(t, fa0, fa1, 0);
       step4(t + 1, fa1, fa0, 1);
@@ -2080,6 +2156,22 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
         const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));  // 2^-e_a
         acc[a][b][r] *= ia * sbv;
       }
+  }
+  if (VAR != 5 && EPI != EPI_RESID && !args.crow && m0 + BM <= M && n0 + BN <= N && (args.ldc & 3) == 0 &&
+      (args.ldaux & 3) == 0) {
+    // full tile: through LDS to a row-wise epilogue (every wave's fragment reads retired first; each wave then
+    // writes and reads back only its own 32 rows)
+    constexpr int LS = BN + 4;
+    __syncthreads();
+    float* E = reinterpret_cast<float*>(lds16) + wave * 32 * LS;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(a * 16 + 4 * hh + r) * LS + b * 16 + rin] = acc[a][b][r];
+    epilogue_rows<BN, EPI>(args, G, E, LS, m0 + wave * 32, n0, lane);
+    return;
   }
   if (m0 + BM <= M && n0 + BN <= N)
     epilogue<BM, BN, WM, WN, EPI, 16, true>(args, G, acc, m0, n0, wave, 0, rin, hh);
@@ -2152,6 +2244,7 @@ static hipError_t launch_h5_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
     case 2: return launch_h5_v<EPI, 2>(a, s, grid, lds, sc, planes);
     case 3: return launch_h5_v<EPI, 3>(a, s, grid, lds, sc, planes);
     case 4: return launch_h5_v<EPI, 4>(a, s, grid, lds, sc, planes);
+    case 5: return launch_h5_v<EPI, 5>(a, s, grid, lds, sc, planes);
     default: return launch_h5_v<EPI, 0>(a, s, grid, lds, sc, planes);
   }
 }
@@ -2265,6 +2358,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "win_attn") return &t.win_attn;
   if (k == "win_mfma") return &t.win_mfma;
   if (k == "fuse_mlp") return &t.fuse_mlp;
+  if (k == "mlp_hc") return &t.mlp_hc;
   if (k == "fuse_attn") return &t.fuse_attn;
   if (k == "attn_mfma") return &t.attn_mfma;
   if (k == "gelu_planes") return &t.gelu_planes;

@@ -30,7 +30,8 @@ struct Tuning {
   int h4_split_minkt = 12;      // k-tiles per chunk at least, for that split of tile 48
   int h5 = 1;                   // tile 49 (256 x 144, k_gemm_h5) where its tiles fill whole rounds and tile 48's do not
   int fc_conv_mf = 1;           // LGUnet_all_1 PatchEmbed / ConvTranspose2d as direct MFMA kernels (0: im2col / col2im + GEMM)
-  int h5_var = 4;               // tile 49 schedule variant (4: B blocks read in groups of three, two groups ahead)
+  int h5_var = 4;               // tile 49 schedule variant (4: B blocks read in groups of three, two groups ahead, full
+                                // tiles through the row-wise LDS epilogue; 5: the same with the per-fragment epilogue)
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
@@ -41,6 +42,8 @@ struct Tuning {
   int fixup_ln = 1;             // the proj GEMM's split-K fixup fused into the LG-stage LN2 (gemm_ln)
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
                                 // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
+  int mlp_hc = 2;               // the fused dim-192 MLP: hidden units per chunk (32 or 64: fewer chunk steps, 151 KB LDS),
+                                // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
   int fuse_attn = 1;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
                                 // the forward, bit 1 the backward (measured neutral, profiles/r03/ab_fuse_attn)
 };
@@ -457,6 +460,7 @@ struct MlpGroup {
 };
 struct MlpArgs {
   int M, C, ngroups;
+  int hc;  // C = 192: hidden units per chunk (32 or 64; 0 = 32), or 2 (32, hidden layer split over two waves)
   float eps;
   MlpGroup g[kMaxGroups];
 };

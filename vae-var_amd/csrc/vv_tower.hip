@@ -17,8 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
-#include <mutex>
 
+#include "vv_gelu.h"
 #include "vv_kernels.h"
 
 namespace vv {
@@ -30,12 +30,8 @@ typedef unsigned short u16;
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float gelu_t(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float dgelu_t(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+__device__ __forceinline__ float gelu_t(float x) { return gelu_fast(x); }  // vv_gelu.h
+__device__ __forceinline__ float dgelu_t(float x) { return dgelu_fast(x); }
 // fp16x3 row scale 2^(141 - E) of a row whose largest |value| has bit pattern mx, and its inverse 2^(E - 141)
 __device__ __forceinline__ float sc_of(unsigned mx) { return __uint_as_float((268u - max(mx >> 23, 15u)) << 23); }
 __device__ __forceinline__ float inv_of(unsigned mx) { return __uint_as_float((max(mx >> 23, 15u) - 14u) << 23); }
@@ -45,21 +41,30 @@ __device__ __forceinline__ unsigned amax(unsigned m, float v) { return max(m, __
 __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
 __device__ __forceinline__ int frag(int r, int q) { return r * 32 + ((q ^ hsw(r >> 2)) << 3); }
 
-template <int C, int NW, int HC, bool FWD>
-__global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
-  constexpr int NT = 64 * NW, KS1 = C / 32, KS2 = HC / 32, NJ = HC / 16, NQ = C / 16, NC = 4 * C / HC;
+// NH = 2 splits the hidden layer between two waves per 16 tokens (wave hh runs hidden units [hh 2C, hh 2C + 2C)):
+// twice the waves per CU for the same LDS weight stream, the two partial fc2 sums added through LDS at the end.
+template <int C, int NW, int HC, bool FWD, int NH>
+__global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
+  constexpr int NT = 64 * NW * NH, KS1 = C / 32, KS2 = HC / 32, NJ = HC / 16, NQ = C / 16, NC = 4 * C / (HC * NH);
+  constexpr int HH = 4 * C / NH;             // hidden units per wave half
   constexpr int CQ = C / 4;                  // channels per lane in the row phases (4 lanes per token)
   constexpr int A1W = KS1 * 2 * 16 * 32;     // halves of one wave's Y planes
   constexpr int W1S = KS1 * 2 * HC * 32;     // halves of a W1 chunk (HC rows x C)
-  static_assert(C % 32 == 0 && HC % 32 == 0 && (4 * C) % HC == 0 && CQ % 4 == 0, "shape");
+  constexpr int W2S = KS2 * 2 * C * 32;      // halves of a W2 chunk (C rows x HC)
+  static_assert(C % 32 == 0 && HC % 32 == 0 && HH % HC == 0 && CQ % 4 == 0 && (NH == 1 || NH == 2), "shape");
+  static_assert(NH == 1 || NW * NQ * 64 * 16 <= 2 * NH * (W1S + W2S), "fc2 partial sums fit the weight buffers");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
+  const int tg = wave % NW, hh = wave / NW;  // token group, hidden half
+  const int hoff = hh * HH;
   const MlpGroup G = a.g[blockIdx.z];
-  u16* A1 = lds + wave * A1W;
+  u16* A1 = lds + tg * A1W;
   u16* W1 = lds + NW * A1W;
-  u16* W2 = W1 + W1S;
+  u16* W2 = W1 + NH * W1S;
+  u16* W1w = W1 + hh * W1S;  // this wave's half of the chunk
+  u16* W2w = W2 + hh * W2S;
   // per-row tables: W1 row scales / fc1 bias [4C], W2 row scales / fc2 bias [C] (fwd; bwd: no biases)
-  float* T1s = reinterpret_cast<float*>(W2 + (HC / 32) * 2 * C * 32);
+  float* T1s = reinterpret_cast<float*>(W2 + NH * W2S);
   float* T1b = T1s + 4 * C;
   float* T2s = T1b + 4 * C;
   float* T2b = T2s + C;
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
         T2b[tid + i * NT] = c2[i];
       }
   }
-  const int t0 = blockIdx.x * 16 * NW + 16 * wave;  // this wave's first token
+  const int t0 = blockIdx.x * 16 * NW + 16 * tg;  // this wave's first token
 
   // ---- row phase: Y = LN2(x1) (fwd) or dx2 (bwd), scaled per token and split into planes ----
   const int tt = lane >> 2, qd = lane & 3;  // token, quarter of the row
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
       for (int v = 0; v < CQ / 4; ++v)
 #pragma unroll
         for (int e = 0; e < 4; ++e) yv[v][e] = (yv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
-      if (qd == 0) *reinterpret_cast<float2*>(G.stats + 2 * (size_t)(t0 + tt)) = make_float2(mean, rstd);
+      if (qd == 0 && hh == 0) *reinterpret_cast<float2*>(G.stats + 2 * (size_t)(t0 + tt)) = make_float2(mean, rstd);
     }
     unsigned mx = 0;
 #pragma unroll
@@ -143,6 +148,7 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
     typedef _Float16 h4t __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int v = 0; v < CQ / 4; ++v) {
+      if (hh != 0) continue;  // the other half's wave only needs the scale
       const int k = qd * CQ + 4 * v, ks = k >> 5, kk = k & 31;
       h4t hv, lv;
 #pragma unroll
@@ -164,8 +170,8 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
 
   // weight chunks: global -> registers one chunk ahead (every load of a chunk in flight at once, under the
   // previous chunk's MFMAs), registers -> LDS between two barriers
-  constexpr int P1 = HC * KS1 * 8 / NT, P2 = C * KS2 * 16 / NT;
-  static_assert(P1 * NT == HC * KS1 * 8 && P2 * NT == C * KS2 * 16, "staging split");
+  constexpr int P1 = NH * HC * KS1 * 8 / NT, P2 = NH * C * KS2 * 16 / NT;
+  static_assert(P1 * NT == NH * HC * KS1 * 8 && P2 * NT == NH * C * KS2 * 16, "staging split");
   u4v r1[P1];
   u2v r2[P2];
   // W1 chunk: rows c HC + r, the whole K = C; global row = KS1 x [h(32) | l(32)]. W2 chunk: rows n < C, hidden units
@@ -175,13 +181,15 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
 #define VV_MLP_LOAD(c)                                                                                            \
   {                                                                                                               \
     _Pragma("unroll") for (int i = 0; i < P1; ++i) {                                                             \
-      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8);                                     \
-      r1[i] = *reinterpret_cast<const u4v*>(G.w1h + (size_t)((c) * HC + r) * 2 * C + (rem >> 3) * 64 +          \
+      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8), rh = r / HC, rl = r - rh * HC;     \
+      r1[i] = *reinterpret_cast<const u4v*>(G.w1h + (size_t)(rh * HH + (c) * HC + rl) * 2 * C + (rem >> 3) * 64 + \
                                               ((rem >> 2) & 1) * 32 + (rem & 3) * 8);                             \
     }                                                                                                             \
     _Pragma("unroll") for (int i = 0; i < P2; ++i) {                                                             \
-      const int e = tid + i * NT, n = e / (KS2 * 16), rem = e - n * (KS2 * 16);                                   \
-      r2[i] = *reinterpret_cast<const u2v*>(G.w2h + (size_t)n * 2 * (4 * C) + ((c) * KS2 + (rem >> 4)) * 64 +   \
+      const int e0 = tid + i * NT, eh = e0 / (C * KS2 * 16), e = e0 - eh * (C * KS2 * 16), n = e / (KS2 * 16),   \
+                rem = e - n * (KS2 * 16);                                                                         \
+      r2[i] = *reinterpret_cast<const u2v*>(G.w2h + (size_t)n * 2 * (4 * C) +                                   \
+                                              (eh * (HH / 32) + (c) * KS2 + (rem >> 4)) * 64 +                   \
                                               ((rem >> 3) & 1) * 32 + 4 * ((rem >> 1) & 3) + 16 * (rem & 1));     \
     }                                                                                                             \
   }
@@ -193,26 +201,28 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
     if (!FWD) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        ex[j] = *reinterpret_cast<const f4*>(G.h1 + trow * (4 * C) + c * HC + 16 * j + 4 * g4);
+        ex[j] = *reinterpret_cast<const f4*>(G.h1 + trow * (4 * C) + hoff + c * HC + 16 * j + 4 * g4);
     }
     __syncthreads();  // the previous chunk's W1 / W2 fragment reads are done (and, at c = 0, the Y planes written)
 #pragma unroll
     for (int i = 0; i < P1; ++i) {
-      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8);
-      *reinterpret_cast<u4v*>(W1 + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * HC * 32 + frag(r, rem & 3)) = r1[i];
+      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8), rh = r / HC, rl = r - rh * HC;
+      *reinterpret_cast<u4v*>(W1 + rh * W1S + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * HC * 32 + frag(rl, rem & 3)) =
+          r1[i];
     }
 #pragma unroll
     for (int i = 0; i < P2; ++i) {
-      const int e = tid + i * NT, n = e / (KS2 * 16), rem = e - n * (KS2 * 16);
-      *reinterpret_cast<u2v*>(W2 + ((rem >> 4) * 2 + ((rem >> 3) & 1)) * C * 32 + frag(n, (rem >> 1) & 3) +
-                                4 * (rem & 1)) = r2[i];
+      const int e0 = tid + i * NT, eh = e0 / (C * KS2 * 16), e = e0 - eh * (C * KS2 * 16), n = e / (KS2 * 16),
+                rem = e - n * (KS2 * 16);
+      *reinterpret_cast<u2v*>(W2 + eh * W2S + ((rem >> 4) * 2 + ((rem >> 3) & 1)) * C * 32 +
+                                frag(n, (rem >> 1) & 3) + 4 * (rem & 1)) = r2[i];
     }
     __syncthreads();
     if (c + 1 < NC) VV_MLP_LOAD(c + 1)
     float s1[NJ][4];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int n = c * HC + 16 * j + 4 * g4;
+      const int n = hoff + c * HC + 16 * j + 4 * g4;
       const f4 sv = *reinterpret_cast<const f4*>(T1s + n);
 #pragma unroll
       for (int i = 0; i < 4; ++i) s1[j][i] = sv[i];
@@ -229,8 +239,8 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
       const h8v yl = *reinterpret_cast<const h8v*>(A1 + frag((ks * 2 + 1) * 16 + li, g4));
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const h8v wh = *reinterpret_cast<const h8v*>(W1 + (ks * 2 + 0) * HC * 32 + frag(16 * j + li, g4));
-        const h8v wl = *reinterpret_cast<const h8v*>(W1 + (ks * 2 + 1) * HC * 32 + frag(16 * j + li, g4));
+        const h8v wh = *reinterpret_cast<const h8v*>(W1w + (ks * 2 + 0) * HC * 32 + frag(16 * j + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(W1w + (ks * 2 + 1) * HC * 32 + frag(16 * j + li, g4));
         acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, yh, acc1[j], 0, 0, 0);
         acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yl, acc1[j], 0, 0, 0);
         acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yh, acc1[j], 0, 0, 0);
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
     unsigned mx = 0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int n = c * HC + 16 * j + 4 * g4;
+      const int n = hoff + c * HC + 16 * j + 4 * g4;
       if (FWD) {
         f4 v;
 #pragma unroll
@@ -274,8 +284,8 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
       }
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        const h8v wh = *reinterpret_cast<const h8v*>(W2 + (kk * 2 + 0) * C * 32 + frag(16 * q + li, g4));
-        const h8v wl = *reinterpret_cast<const h8v*>(W2 + (kk * 2 + 1) * C * 32 + frag(16 * q + li, g4));
+        const h8v wh = *reinterpret_cast<const h8v*>(W2w + (kk * 2 + 0) * C * 32 + frag(16 * q + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(W2w + (kk * 2 + 1) * C * 32 + frag(16 * q + li, g4));
         tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, tmp[q], 0, 0, 0);
         tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, tmp[q], 0, 0, 0);
         tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, tmp[q], 0, 0, 0);
@@ -285,6 +295,18 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc2[q][i] += tmp[q][i] * iu;
+  }
+  if (NH == 2) {  // half 1's fc2 partial sums through LDS (over the weight buffers) to half 0, which finishes
+    f4* R = reinterpret_cast<f4*>(W1);
+    __syncthreads();
+    if (hh == 1) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) R[(tg * NQ + q) * 64 + lane] = acc2[q];
+    }
+    __syncthreads();
+    if (hh == 1) return;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc2[q] += R[(tg * NQ + q) * 64 + lane];
   }
 
   // ---- epilogue 2 (lane: token li, channels 16 q + 4 g4 + i) ----
@@ -357,25 +379,12 @@ __global__ __launch_bounds__(64 * NW, C == 96 ? 3 : 1) void k_mlp(MlpArgs a) {
 
 #undef VV_MLP_LOAD
 
-template <int C, int NW, int HC, bool FWD>
+template <int C, int NW, int HC, bool FWD, int NH = 1>
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
-  constexpr size_t lds = 2 * ((size_t)NW * (C / 32) * 2 * 16 * 32 + (size_t)(C / 32) * 2 * HC * 32 +
-                              (size_t)(HC / 32) * 2 * C * 32) + 4 * (8 * C + 2 * C);
-  static std::mutex mu;
-  static bool init[64] = {false};
-  int dev = 0;
-  if (hipError_t e = hipGetDevice(&dev)) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (!init[dev]) {
-      if (hipError_t e = hipFuncSetAttribute((const void*)k_mlp<C, NW, HC, FWD>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
-        return e;
-      init[dev] = true;
-    }
-  }
-  hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD>), dim3(a.M / (16 * NW), 1, a.ngroups), dim3(64 * NW), lds, s, a);
+  constexpr size_t lds = 2 * ((size_t)NW * (C / 32) * 2 * 16 * 32 + (size_t)NH * (C / 32) * 2 * HC * 32 +
+                              (size_t)NH * (HC / 32) * 2 * C * 32) + 4 * (8 * C + 2 * C);
+  if (hipError_t e = set_lds_limit((const void*)k_mlp<C, NW, HC, FWD, NH>, lds)) return e;
+  hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD, NH>), dim3(a.M / (16 * NW), 1, a.ngroups), dim3(64 * NW * NH), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1059,20 +1068,7 @@ hipError_t launch_ablk_bwd(const AblkArgs& a, hipStream_t s) {
   constexpr int NW = 4, KS = C / 32;
   constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
                          4 * ((size_t)NW * (3 * 16 * 36 + 2 * 16 * 17) + 2 * C);
-  static std::mutex mu;
-  static bool init[64] = {false};
-  int dev = 0;
-  if (hipError_t e = hipGetDevice(&dev)) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (!init[dev]) {
-      if (hipError_t e = hipFuncSetAttribute((const void*)k_ablk_bwd<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds))
-        return e;
-      init[dev] = true;
-    }
-  }
+  if (hipError_t e = set_lds_limit((const void*)k_ablk_bwd<C>, lds)) return e;
   hipLaunchKernelGGL(k_ablk_bwd<C>, dim3(a.M / (16 * NW), 1, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
@@ -1082,20 +1078,7 @@ hipError_t launch_ablk_fwd(const AblkArgs& a, hipStream_t s) {
   constexpr int NW = 4, KS = C / 32, H = C / 32;
   constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
                          4 * ((size_t)NW * (16 * 36 + 16 * 16) + H * 49 + 8 * C);
-  static std::mutex mu;
-  static bool init[64] = {false};
-  int dev = 0;
-  if (hipError_t e = hipGetDevice(&dev)) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (!init[dev]) {
-      if (hipError_t e = hipFuncSetAttribute((const void*)k_ablk_fwd<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds))
-        return e;
-      init[dev] = true;
-    }
-  }
+  if (hipError_t e = set_lds_limit((const void*)k_ablk_fwd<C>, lds)) return e;
   hipLaunchKernelGGL(k_ablk_fwd<C>, dim3(a.M / (16 * NW), 1, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
@@ -1106,6 +1089,7 @@ bool mlp_supported(int C, int M) { return (C == 96 || C == 192) && M > 0 && M % 
 
 static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
   if (!mlp_supported(a.C, a.M) || a.ngroups <= 0 || a.ngroups > kMaxGroups) return hipErrorInvalidValue;
+  if (a.hc != 0 && a.hc != 32 && a.hc != 64 && a.hc != 2) return hipErrorInvalidValue;
   for (int g = 0; g < a.ngroups; ++g) {
     const MlpGroup& G = a.g[g];
     if (!G.x || !G.gamma || !G.stats || !G.w1h || !G.w1s || !G.w2h || !G.w2s || !G.h1 || !G.out)
@@ -1113,8 +1097,11 @@ static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
     if (fwd ? (!G.beta || !G.b1 || !G.b2) : !G.dy) return hipErrorInvalidValue;
   }
   const int ph = prof_begin(s);
-  const hipError_t e = a.C == 96 ? (fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s))
-                                  : (fwd ? launch_mlp<192, 4, 32, true>(a, s) : launch_mlp<192, 4, 32, false>(a, s));
+  const hipError_t e =
+      a.C == 96    ? (fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s))
+      : a.hc == 64 ? (fwd ? launch_mlp<192, 4, 64, true>(a, s) : launch_mlp<192, 4, 64, false>(a, s))
+      : a.hc == 2  ? (fwd ? launch_mlp<192, 4, 32, true, 2>(a, s) : launch_mlp<192, 4, 32, false, 2>(a, s))
+                   : (fwd ? launch_mlp<192, 4, 32, true>(a, s) : launch_mlp<192, 4, 32, false>(a, s));
   // 2 GEMMs of M x 4C x C per group; bytes: x1 / dx2 (+ out, + x1 bwd) and the 4C-wide pre-activation
   prof_end(ph, s, PC_TOWER, 4.0 * a.ngroups * a.M * 4.0 * a.C * a.C,
            (double)a.ngroups * a.M * 4.0 * (fwd ? 2.0 * a.C + 4.0 * a.C : 3.0 * a.C + 4.0 * a.C));
