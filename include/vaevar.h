@@ -174,6 +174,13 @@ int vv_state_ptr(vv_ctx* ctx, const float** x);
 int vv_dot(vv_ctx* ctx, const float* a, const float* b, int64_t n, double* out, void* stream);
 int vv_abssum(vv_ctx* ctx, const float* a, int64_t n, double* out, void* stream);
 int vv_absmax(vv_ctx* ctx, const float* a, int64_t n, float* out, void* stream);
+/* Several of the reductions above in one host round trip: op i = 0 dot(a[i], b[i]), 1 abssum(a[i]), 2 absmax(a[i])
+   over n floats each (count <= 8), with the same kernels and partial layouts as vv_dot / vv_abssum / vv_absmax (the
+   same values); then n_extra (<= 16) device doubles at dev_extra (e.g. the J of a vv_closure_async) are appended:
+   out[count + n_extra], one synchronisation. The L-BFGS mirror (vaevar/lbfgs.py) asks for the scalars of an
+   iteration together instead of one synchronising call each (torch/optim/lbfgs.py computes them one by one). */
+int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
+                    const double* dev_extra, int n_extra, double* out, void* stream);
 int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream);
 int vv_axpby(vv_ctx* ctx, float* out, const float* x, float a, const float* y, float b, int64_t n, void* stream);
 int vv_scale(vv_ctx* ctx, float* y, float alpha, int64_t n, void* stream);
@@ -220,7 +227,7 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "win_mfma" (that kernel on the exact-f32 MFMA, 1),
    "fc_h3_mink" (smallest K of the forecast network's fp16x3 GEMMs, 192), "fuse_mlp" (the fused Swin-tower
    LN2 + fc1 + GELU + fc2 + residual sub-block and its backward: bit 0 at dim 96, bit 1 at dim 192, 3), "fuse_attn" (the fused Swin-tower
-   LN1 + qkv + window attention + proj + residual sub-block at dim 96: bit 0 forward, bit 1 backward, 1), "attn_mfma" (the window attention of
+   LN1 + qkv + window attention + proj + residual sub-block at dim 96: bit 0 forward, bit 1 backward, 3), "attn_mfma" (the window attention of
    the LG stage, head dim 192, and of the unfused tower stages, head dim 32, on the exact-f32 MFMA, 1), "gelu_planes" (the LG-stage GELU / gelu' GEMM
    epilogues write the fp16x3 planes of the K = 4C GEMM after them, 1), "attn_planes" (the LG-stage attention
    forward writes the planes of a tile-48 proj GEMM, 1), "fixup_ln" (that GEMM's split-K fixup fused into the LN2

@@ -48,6 +48,10 @@ class CpuPrims:
     def absmax(self, a):
         return float(a.abs().max())
 
+    def reduce_batch(self, reqs, extra=None):
+        out = [self.dot(a, b) if op == 0 else self.abssum(a) if op == 1 else self.absmax(a) for op, a, b in reqs]
+        return out + (extra.tolist() if extra is not None else [])
+
     def axpy(self, y, x, alpha):
         y.add_(x, alpha=alpha)
 

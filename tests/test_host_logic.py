@@ -16,6 +16,10 @@ class CpuPrims:
     def absmax(self, a):
         return float(a.abs().max())
 
+    def reduce_batch(self, reqs, extra=None):
+        out = [self.dot(a, b) if op == 0 else self.abssum(a) if op == 1 else self.absmax(a) for op, a, b in reqs]
+        return out + (extra.tolist() if extra is not None else [])
+
     def axpy(self, y, x, alpha):
         y.add_(x, alpha=alpha)
 
@@ -91,6 +95,61 @@ def test_lbfgs_mirror_matches_torch():
         assert mir.state["func_evals"] == st["func_evals"]
         # same branches taken; iterates agree to fp32 reduction-order noise
         assert torch.allclose(zm, zt.detach(), rtol=1e-4, atol=1e-4), (zm - zt.detach()).abs().max()
+
+
+def test_lbfgs_batched_scalars_identical():
+    """The batched scalar fetches (vv_reduce_batch: gtd_new, |g|_max, |d|_max and the speculative ys, yy after an
+    evaluation; gtd and d_norm after the direction) give exactly the iterates, losses and counts of one call per
+    scalar, with far fewer host round trips."""
+    from vaevar.lbfgs import LBFGS
+
+    class Counting(CpuPrims):
+        def __init__(self):
+            self.calls = 0
+
+        def dot(self, a, b):
+            self.calls += 1
+            return super().dot(a, b)
+
+        def abssum(self, a):
+            self.calls += 1
+            return super().abssum(a)
+
+        def absmax(self, a):
+            self.calls += 1
+            return super().absmax(a)
+
+        def reduce_batch(self, reqs, extra=None):
+            c = self.calls
+            out = super().reduce_batch(reqs, extra)
+            self.calls = c + 1  # one round trip
+            return out
+
+        def lbfgs_two_loop(self, q, stps, dirs, ro, H_diag):
+            c = self.calls
+            super().lbfgs_two_loop(q, stps, dirs, ro, H_diag)
+            self.calls = c  # on the device: no round trip
+
+    def closure_m(z, g):
+        zz = z.clone().requires_grad_(True)
+        f = objective(zz)
+        f.backward()
+        g.copy_(zz.grad)
+        return float(f.detach())
+
+    runs = []
+    for batch in (False, True):
+        prims = Counting()
+        zm = torch.zeros(4096)
+        mir = LBFGS(prims, zm, history_size=10, max_iter=10, line_search_fn="strong_wolfe")
+        mir.batch_scalars = batch
+        losses = [mir.step(closure_m) for _ in range(3)]
+        runs.append((zm, losses, dict(mir.state), prims.calls))
+    (z0, l0, s0, c0), (z1, l1, s1, c1) = runs
+    assert torch.equal(z0, z1) and l0 == l1
+    assert s0["n_iter"] == s1["n_iter"] and s0["func_evals"] == s1["func_evals"]
+    print(f"scalar round trips: {c0} one at a time, {c1} batched ({s1['n_iter']} iterations)")
+    assert c1 * 2 < c0
 
 
 def test_adam_mirror_matches_torch():

@@ -318,6 +318,8 @@ struct vv_ctx {
   float* redf = nullptr;
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
+  double* redb = nullptr;   // vv_reduce_batch: kMaxBatch reduction scratch areas
+  double* doutb = nullptr;  // ... and its device results (kMaxBatch + kMaxExtra doubles)
   float* twoloop = nullptr;  // L-BFGS two-loop scalars: al[kMaxHistory]
   char* metric_ws = nullptr;  // vv_metrics partial sums + latitude weights
   size_t metric_cap = 0;
@@ -343,6 +345,7 @@ struct vv_ctx {
 namespace {
 
 constexpr int kRedBlocks = 1024;
+constexpr int kMaxBatch = 8, kMaxExtra = 16;  // vv_reduce_batch
 constexpr int kMaxHistory = 256;  // L-BFGS history pairs accepted by vv_lbfgs_two_loop
 
 int set_dev(vv_ctx* ctx) {
@@ -1751,6 +1754,8 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipMalloc(&c->twoloop, kMaxHistory * sizeof(float)));
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
+  VV_HIP(hipMalloc(&c->redb, (size_t)kMaxBatch * kRedBlocks * sizeof(double)));
+  VV_HIP(hipMalloc(&c->doutb, (size_t)(kMaxBatch + kMaxExtra) * sizeof(double)));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
   *out = c;
   return 0;
@@ -1777,6 +1782,8 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   (void)hipFree(ctx->redf);
   (void)hipFree(ctx->dout);
   (void)hipFree(ctx->doutf);
+  (void)hipFree(ctx->redb);
+  (void)hipFree(ctx->doutb);
   (void)hipFree(ctx->gemm_ws);
   if (ctx->apl) (void)hipFree(ctx->apl);
   if (ctx->gattn_ws) (void)hipFree(ctx->gattn_ws);
@@ -2166,6 +2173,45 @@ int vv_absmax(vv_ctx* ctx, const float* a, int64_t n, float* out, void* stream) 
   VV_HIP(vv::vec_absmax(a, n, ctx->redf, kRedBlocks, ctx->doutf, st));
   VV_HIP(hipMemcpyAsync(out, ctx->doutf, sizeof(float), hipMemcpyDeviceToHost, st));
   VV_HIP(hipStreamSynchronize(st));
+  return 0;
+}
+int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
+                    const double* dev_extra, int n_extra, double* out, void* stream) {
+  if (!ctx || count < 0 || count > kMaxBatch || n_extra < 0 || n_extra > kMaxExtra || (count && (!ops || !a)) ||
+      (n_extra && !dev_extra) || !out || n < 0)
+    return fail(VV_E_ARG, "reduce_batch: bad arguments");
+  for (int i = 0; i < count; ++i)
+    if (ops[i] < 0 || ops[i] > 2 || !a[i] || (ops[i] == 0 && (!b || !b[i])))
+      return fail(VV_E_ARG, "reduce_batch: bad op %d", i);
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  // the same kernels, grids and partial layouts as vv_dot / vv_abssum / vv_absmax: identical values
+  for (int i = 0; i < count; ++i) {
+    double* part = ctx->redb + (size_t)i * kRedBlocks;
+    if (ops[i] == 0)
+      VV_HIP(vv::vec_dot(a[i], b[i], n, part, kRedBlocks, ctx->doutb + i, st));
+    else if (ops[i] == 1)
+      VV_HIP(vv::vec_abssum(a[i], n, part, kRedBlocks, ctx->doutb + i, st));
+    else
+      VV_HIP(vv::vec_absmax(a[i], n, reinterpret_cast<float*>(part), kRedBlocks,
+                            reinterpret_cast<float*>(ctx->doutb + i), st));
+  }
+  if (n_extra)
+    VV_HIP(hipMemcpyAsync(ctx->doutb + count, dev_extra, n_extra * sizeof(double), hipMemcpyDeviceToDevice, st));
+  double h[kMaxBatch + kMaxExtra];
+  VV_HIP(hipMemcpyAsync(h, ctx->doutb, (count + n_extra) * sizeof(double), hipMemcpyDeviceToHost, st));
+  VV_HIP(hipStreamSynchronize(st));
+  for (int i = 0; i < count; ++i) {
+    if (ops[i] == 2) {
+      float f;
+      memcpy(&f, &h[i], sizeof(float));
+      out[i] = f;
+    } else {
+      out[i] = h[i];
+    }
+  }
+  for (int i = 0; i < n_extra; ++i) out[count + i] = h[count + i];
   return 0;
 }
 int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream) {

@@ -32,6 +32,24 @@ __device__ __forceinline__ float gelu_h(float x) {
   return __builtin_amdgcn_exp2f(fmaf(u, s, -1.0f));
 }
 
+// four at a time, each Horner step over the four before the next, so the four dependent chains interleave
+__device__ __forceinline__ void gelu_h4(const float (&x)[4], float (&h)[4]) {
+  float u[4], s[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u[i] = fminf(fabsf(x[i]), 5.75f);
+    s[i] = fmaf(5.128587759e-07f, u[i], -9.560183571e-06f);
+  }
+  constexpr float c[7] = {7.497351908e-05f, -2.843466355e-04f, 1.498893471e-05f, 6.931121461e-03f,
+                          -5.243476480e-02f, -4.592214525e-01f, -1.151104212e+00f};
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = fmaf(s[i], u[i], c[k]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h[i] = __builtin_amdgcn_exp2f(fmaf(u[i], s[i], -1.0f));
+}
+
 #ifdef VV_GELU_ERFF
 __device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float dgelu_fast(float x) {
@@ -50,6 +68,37 @@ __device__ __forceinline__ float dgelu_fast(float x) {
   // phi(x) = 2^(-x^2 log2(e) / 2 - log2(sqrt(2 pi)))
   const float pdf = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170f, -1.3257480647361593f));
   return fmaf(x, pdf, cdf);
+}
+#endif
+
+#ifdef VV_GELU_ERFF
+__device__ __forceinline__ void gelu4(const float (&x)[4], float (&y)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = gelu_fast(x[i]);
+}
+__device__ __forceinline__ void dgelu4(const float (&x)[4], float (&y)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = dgelu_fast(x[i]);
+}
+#else
+__device__ __forceinline__ void gelu4(const float (&x)[4], float (&y)[4]) {
+  float h[4];
+  gelu_h4(x, h);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float xh = x[i] * h[i];
+    y[i] = x[i] >= 0.0f ? x[i] - xh : xh;
+  }
+}
+__device__ __forceinline__ void dgelu4(const float (&x)[4], float (&y)[4]) {
+  float h[4];
+  gelu_h4(x, h);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float cdf = x[i] >= 0.0f ? 1.0f - h[i] : h[i];
+    const float pdf = __builtin_amdgcn_exp2f(fmaf(x[i] * x[i], -0.72134752044448170f, -1.3257480647361593f));
+    y[i] = fmaf(x[i], pdf, cdf);
+  }
 }
 #endif
 

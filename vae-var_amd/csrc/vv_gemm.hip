@@ -1867,16 +1867,14 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGr
       const int e = lane + 64 * (i0 + j), rr = e / CH, col = 4 * (e - rr * CH);
       const int gr = r0 + rr, gc = n0 + col;
       f4 o;
+      float xs[4], ys[4];  // GELU / GELU' four at a time (vv_gelu.h gelu4: the four chains interleave)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float x = v[j][q] + bv[j][q];
-        if constexpr (EPI == EPI_GELU) {
-          x = gelu_f(x);
-        } else if constexpr (EPI == EPI_DGELU) {
-          x = v[j][q] * dgelu_f(ex[j][q]);
-        }
-        o[q] = x;
-      }
+      for (int q = 0; q < 4; ++q) xs[q] = EPI == EPI_DGELU ? ex[j][q] : v[j][q] + bv[j][q];
+      if constexpr (EPI == EPI_GELU) gelu4(xs, ys);
+      if constexpr (EPI == EPI_DGELU) dgelu4(xs, ys);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        o[q] = EPI == EPI_GELU ? ys[q] : EPI == EPI_DGELU ? v[j][q] * ys[q] : v[j][q] + bv[j][q];
       if constexpr (EPI == EPI_GELU) {
         if (G.aux) {
           f4 pre;

@@ -195,6 +195,7 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   }
   VV_MLP_LOAD(0)
 
+#pragma unroll 2
   for (int c = 0; c < NC; ++c) {
     // bwd: this chunk's pre-activations, in flight before the next chunk's weight loads (vmcnt is in order)
     f4 ex[NJ];
@@ -257,11 +258,14 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc1[j][i] * (iy * s1[j][i]) + ex[j][i];
         *reinterpret_cast<f4*>(G.h1 + trow * (4 * C) + n) = v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) u[j][i] = gelu_t(v[i]);
+        const float vv[4] = {v[0], v[1], v[2], v[3]};
+        gelu4(vv, u[j]);
       } else {
+        const float xv[4] = {ex[j][0], ex[j][1], ex[j][2], ex[j][3]};
+        float dg[4];
+        dgelu4(xv, dg);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) u[j][i] = acc1[j][i] * (iy * s1[j][i]) * dgelu_t(ex[j][i]);
+        for (int i = 0; i < 4; ++i) u[j][i] = acc1[j][i] * (iy * s1[j][i]) * dg[i];
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) mx = amax(mx, u[j][i]);

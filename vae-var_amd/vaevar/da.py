@@ -35,6 +35,8 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
         raise ValueError(optimizer)
 
     def closure(zz, g):
+        if optimizer == "lbfgs":  # queued: the loss is fetched with the mirror's next scalars (vaevar/lbfgs.py)
+            return prob.closure_lazy(zz, g)
         jb, jo = prob.closure(zz, g)
         return prob.loss_f32(jb, jo)
 

@@ -106,6 +106,26 @@ class Context:
         check(lib.vv_absmax(self.h, _ptr(a), a.numel(), ctypes.byref(out), _stream()), "absmax")
         return out.value
 
+    def reduce_batch(self, reqs, extra=None) -> list:
+        """vv_reduce_batch: reqs = [(op, a, b)] with op 0 dot(a, b), 1 abssum(a), 2 absmax(a) (equal-length vectors,
+        <= 8), plus the float64 device tensor `extra` (<= 16 values) appended: one synchronisation for all of them,
+        the values of the one-call-each vv_dot / vv_abssum / vv_absmax."""
+        k = len(reqs)
+        n = reqs[0][1].numel() if k else 0
+        for op, a, b in reqs:
+            if a.numel() != n or (op == 0 and b.numel() != n):
+                raise ValueError("reduce_batch: vectors of different lengths")
+        ops = (ctypes.c_int * max(k, 1))(*[int(r[0]) for r in reqs])
+        A = (ctypes.c_void_p * max(k, 1))(*[_ptr(r[1]).value for r in reqs])
+        B = (ctypes.c_void_p * max(k, 1))(*[(_ptr(r[2]).value if r[0] == 0 else None) for r in reqs])
+        ne = extra.numel() if extra is not None else 0
+        if extra is not None and (extra.dtype != torch.float64 or not extra.is_cuda or not extra.is_contiguous()):
+            raise ValueError("reduce_batch: extra must be a contiguous float64 CUDA tensor")
+        out = (ctypes.c_double * max(k + ne, 1))()
+        check(lib.vv_reduce_batch(self.h, k, ops, A, B, n, _ptr(extra) if ne else None, ne, out, _stream()),
+              "reduce_batch")
+        return list(out[:k + ne])
+
     def axpy(self, y, x, alpha: float):
         check(lib.vv_axpy(self.h, _ptr(y), _ptr(x), float(alpha), y.numel(), _stream()), "axpy")
 
@@ -356,6 +376,21 @@ def resample_nearest(ctx: Context, x: torch.Tensor, size) -> torch.Tensor:
     return _Resample.apply(x, ctx, tuple(int(v) for v in size))
 
 
+class LazyLoss:
+    """A queued closure's loss: `dev` holds (J_b, J_o) on the device; `resolve(values)` turns the fetched pair into
+    the loss. `float()` fetches it on its own (one synchronisation)."""
+
+    def __init__(self, dev: torch.Tensor, finish):
+        self.dev, self.finish = dev, finish
+
+    def resolve(self, values) -> float:
+        return self.finish(values)
+
+    def __float__(self) -> float:
+        v = self.dev.cpu().tolist()
+        return float(self.finish(v))
+
+
 class DAProblem:
     """The vae4dvar closure (da_4dvar.py:1183-1208) bound to device buffers; evaluated by libvaevar.
 
@@ -420,6 +455,19 @@ class DAProblem:
         check(lib.vv_closure(self.ctx.h, _ptr(z), gp, jb, jo, _stream()), "closure")
         self.n_evals += 1
         return np.array(jb[:], np.float64), np.array(jo[:], np.float64)
+
+    def closure_lazy(self, z: torch.Tensor, grad: torch.Tensor | None) -> "LazyLoss":
+        """The closure queued without a host round trip (vv_closure_async): J_b, J_o stay in a device buffer until
+        the L-BFGS mirror fetches them together with its reductions (vaevar.lbfgs, vv_reduce_batch). Single
+        analysis (B = 1); the loss is loss_f32 of the fetched pair."""
+        if self.B != 1:
+            raise ValueError("batched problem: use closure_batch")
+        if getattr(self, "_dJ", None) is None:
+            self._dJ = torch.empty(2, device=self.xb.device, dtype=torch.float64)
+        gp = _ptr(grad) if grad is not None else None
+        check(lib.vv_closure_async(self.ctx.h, _ptr(z), gp, _ptr(self._dJ), _stream()), "closure_async")
+        self.n_evals += 1
+        return LazyLoss(self._dJ, lambda v: self.loss_f32(v[0], v[1]))
 
     def closure(self, z: torch.Tensor, grad: torch.Tensor | None):
         """Returns (J_b, J_o) as Python floats (double sums); grad <- dJ/dz if given. Single analysis (B = 1)."""

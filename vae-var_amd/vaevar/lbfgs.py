@@ -12,6 +12,15 @@ Python floats as weak scalars exactly like torch), the loss is a Python float.
 Every closure evaluation is a `yield (z, grad_out)` of the generator `step_gen()` that receives the loss, so B
 independent optimisers can be advanced in lockstep over one batched closure (vaevar.da.one_step_da_batch);
 `step(closure)` drives the same generator with a plain closure.
+
+Host round trips (r04, `batch_scalars`): torch computes an iteration's scalars one synchronising call at a time
+(the loss, gtd_new, |g|_max, |d|_max, ys, yy, gtd, d_norm: eight per iteration). Here the scalars that are
+known to be asked for next are computed together, in one vv_reduce_batch round trip: after an evaluation the
+loss (a vaevar.engine.LazyLoss from a queued closure), gtd_new = g_new.d, |g_new|_max, |d|_max and -- for the
+next iteration, should this step be accepted -- y = g_new - prev_flat_grad, s = t d and their ys, yy; after the
+direction, gtd and d_norm. A value is used only if the statement that needs it meets the same tensors (and t):
+every scalar is the one the one-at-a-time path computes (same kernels, same inputs), so the trajectory is
+unchanged; a speculative y / s that is not used costs two axpby and two dots.
 """
 from __future__ import annotations
 
@@ -19,6 +28,11 @@ import numpy as np
 import torch
 
 f32 = np.float32
+
+
+def _is_lazy(res):
+    # a queued closure's loss (vaevar.engine.LazyLoss): a device (J_b, J_o) to fetch with the next scalars
+    return hasattr(res, "dev") and hasattr(res, "resolve")
 
 
 def _cubic_interpolate(x1, f1, g1, x2, f2, g2, bounds=None):
@@ -58,16 +72,71 @@ class LBFGS:
         # _strong_wolfe calls; each line search then takes the recorded step and eval count instead of searching
         self.replay = None
         self.state = {"func_evals": 0, "n_iter": 0}
+        self.batch_scalars = hasattr(ctx, "reduce_batch")  # False: one synchronising call per scalar, as torch
+        self._cache = []           # [(op, a, b, value)] from the last vv_reduce_batch
+        self._spec = None          # (g, prev_flat_grad, d, t, y, s): y, s computed speculatively
+        self._prev_flat_grad = None
 
     # --- vector helpers ---------------------------------------------------
+    def _cached(self, op, a, b):
+        for e in self._cache:
+            if e[0] == op and e[1] is a and e[2] is b:
+                return e[3]
+        return None
+
     def _dot(self, a, b):
-        return f32(self.ctx.dot(a.view(-1), b.view(-1)))
+        v = self._cached(0, a, b)
+        return f32(v) if v is not None else f32(self.ctx.dot(a.view(-1), b.view(-1)))
 
     def _absmax(self, a):
-        return f32(self.ctx.absmax(a.view(-1)))
+        v = self._cached(2, a, None)
+        return f32(v) if v is not None else f32(self.ctx.absmax(a.view(-1)))
+
+    def _prefetch(self, reqs, lazy=None):
+        """One vv_reduce_batch for reqs [(op, a, b)] (+ the lazy loss's J pair); fills the cache; returns the loss
+        (float) if lazy was given."""
+        vals = self.ctx.reduce_batch([(op, a.view(-1), b.view(-1) if b is not None else None) for op, a, b in reqs],
+                                     extra=lazy.dev if lazy is not None else None)
+        self._cache = [(op, a, b, v) for (op, a, b), v in zip(reqs, vals)]
+        return lazy.resolve(vals[len(reqs):]) if lazy is not None else None
+
+    def _loss_of(self, res):
+        """The loss a closure returned: a float, or a LazyLoss fetched on its own."""
+        return float(res)
+
+    def _after_eval(self, res, g, d, t):
+        """The evaluation at z = x + t d returned res (loss) and g: fetch the loss with gtd_new, |g|_max, |d|_max and
+        the next iteration's ys, yy (speculative y, s) in one round trip."""
+        if not self.batch_scalars:
+            return float(res)
+        reqs = [(0, g, d), (2, g, None), (2, d, None)]
+        self._spec = None
+        if self._prev_flat_grad is not None:
+            y, s = self._new(), self._new()
+            self.ctx.axpby(y, g, 1.0, self._prev_flat_grad, -1.0)
+            self.ctx.axpby(s, d, float(t), None, 0.0)
+            self._spec = (g, self._prev_flat_grad, d, t, y, s)
+            reqs += [(0, y, s), (0, y, y)]
+        lazy = res if _is_lazy(res) else None
+        loss = self._prefetch(reqs, lazy)
+        return loss if lazy is not None else float(res)
+
+    def _y_s(self, flat_grad, prev_flat_grad, d, t):
+        """y = flat_grad - prev_flat_grad, s = t d (lbfgs.py:397-398): the speculative pair if it was made from the
+        same tensors and t."""
+        sp = self._spec
+        self._spec = None
+        if sp is not None and sp[0] is flat_grad and sp[1] is prev_flat_grad and sp[2] is d and sp[3] == t:
+            return sp[4], sp[5]
+        y = self._new()
+        self.ctx.axpby(y, flat_grad, 1.0, prev_flat_grad, -1.0)
+        s = self._new()
+        self.ctx.axpby(s, d, float(t), None, 0.0)
+        return y, s
 
     def _abssum(self, a):
-        return f32(self.ctx.abssum(a.view(-1)))
+        v = self._cached(1, a, None)
+        return f32(v) if v is not None else f32(self.ctx.abssum(a.view(-1)))
 
     def _new(self):
         return torch.empty_like(self.z)
@@ -79,7 +148,8 @@ class LBFGS:
         # lbfgs.py:325-331 (a generator: the evaluation is a yield)
         self._add_grad(t, d)
         g = self._new()
-        loss = float((yield self.z, g))
+        res = yield self.z, g
+        loss = self._after_eval(res, g, d, t)
         self.ctx.copy(self.z, x)
         return loss, g
 
@@ -178,7 +248,15 @@ class LBFGS:
         tolerance_grad, tolerance_change = self.tolerance_grad, self.tolerance_change
         state = self.state
         flat_grad = self._new()
-        orig_loss = yield self.z, flat_grad
+        res = yield self.z, flat_grad
+        if self.batch_scalars:
+            lazy = res if _is_lazy(res) else None
+            orig_loss = self._prefetch([(2, flat_grad, None)], lazy) if lazy is not None else res
+            if lazy is None:
+                self._prefetch([(2, flat_grad, None)])
+        else:
+            orig_loss = res
+        orig_loss = float(orig_loss)
         loss = float(orig_loss)
         current_evals = 1
         state["func_evals"] += 1
@@ -198,10 +276,7 @@ class LBFGS:
                 old_dirs, old_stps, ro = [], [], []
                 H_diag = 1
             else:
-                y = self._new()
-                self.ctx.axpby(y, flat_grad, 1.0, prev_flat_grad, -1.0)
-                s = self._new()
-                self.ctx.axpby(s, d, float(t), None, 0.0)
+                y, s = self._y_s(flat_grad, prev_flat_grad, d, t)
                 ys = self._dot(y, s)
                 if ys > 1e-10:
                     if len(old_dirs) == self.history_size:
@@ -235,7 +310,11 @@ class LBFGS:
                 prev_flat_grad = flat_grad.clone()
             else:
                 self.ctx.copy(prev_flat_grad, flat_grad)
+            self._prev_flat_grad = prev_flat_grad
             prev_loss = loss
+            if self.batch_scalars:  # gtd and the line search's d_norm (and the first step's |g|_1) together
+                reqs = [(0, flat_grad, d), (2, d, None)] + ([(1, flat_grad, None)] if state["n_iter"] == 1 else [])
+                self._prefetch(reqs)
             if state["n_iter"] == 1:
                 t = min(1.0, 1.0 / self._abssum(flat_grad)) * lr
             else:
@@ -260,7 +339,7 @@ class LBFGS:
                 self._add_grad(t, d)
                 if n_iter != max_iter:
                     flat_grad = self._new()
-                    loss = float((yield self.z, flat_grad))
+                    loss = self._loss_of((yield self.z, flat_grad))
                     opt_cond = self._absmax(flat_grad) <= tolerance_grad
                     ls_func_evals = 1
             current_evals += ls_func_evals
