@@ -227,7 +227,7 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "win_mfma" (that kernel on the exact-f32 MFMA, 1),
    "fc_h3_mink" (smallest K of the forecast network's fp16x3 GEMMs, 192), "fuse_mlp" (the fused Swin-tower
    LN2 + fc1 + GELU + fc2 + residual sub-block and its backward: bit 0 at dim 96, bit 1 at dim 192, 3), "fuse_attn" (the fused Swin-tower
-   LN1 + qkv + window attention + proj + residual sub-block at dim 96: bit 0 forward, bit 1 backward, 3), "attn_mfma" (the window attention of
+   LN1 + qkv + window attention + proj + residual sub-block: bits 0 / 1 forward / backward at dim 96, bits 2 / 3 at dim 192, 3), "attn_mfma" (the window attention of
    the LG stage, head dim 192, and of the unfused tower stages, head dim 32, on the exact-f32 MFMA, 1), "gelu_planes" (the LG-stage GELU / gelu' GEMM
    epilogues write the fp16x3 planes of the K = 4C GEMM after them, 1), "attn_planes" (the LG-stage attention
    forward writes the planes of a tile-48 proj GEMM, 1), "fixup_ln" (that GEMM's split-K fixup fused into the LN2

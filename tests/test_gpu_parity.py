@@ -569,11 +569,12 @@ def test_ln_row_scales_bitwise(tmp_path):
 
 
 @pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_mlp", 3), ("fuse_attn", 1), ("fuse_attn", 3),
-                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2)])
+                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2),
+                                     ("fuse_attn", 12)])
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient; 1 at dim 96, 3 also at dim 192) and fuse_attn (LN1 + qkv +
-    window attention + proj + residual: 1 the forward, 3 also its input gradient); attn_mfma (the window attention of
+    window attention + proj + residual: 1 the forward, 3 also its input gradient, 12 both at dim 192 only); attn_mfma (the window attention of
     the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and backward on the exact-f32 MFMA instead of
     the VALU kernels: fp32 products either way, only the summation order differs); mlp_hc 64 (the dim-192 fused MLP
     in 64-unit hidden chunks, or 2: its hidden layer split over two waves per 16 tokens -- the hidden operand's

@@ -632,8 +632,9 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
 bool ablk_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, int shift, const int* idx,
                vv::AblkArgs& aa, float* gx = nullptr) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  // fuse_attn: bit 0 the forward, bit 1 the backward
-  if (!(T.fuse_attn & (gx ? 2 : 1)) || sc.math != vv::GEMM_SPLIT16 || !vv::ablk_supported(S.C, S.heads, ws, S.M))
+  // fuse_attn: bit 0 the forward, bit 1 the backward at dim 96; bits 2, 3 the same at dim 192
+  if (!(T.fuse_attn & ((gx ? 2 : 1) << (S.C == 192 ? 2 : 0))) || sc.math != vv::GEMM_SPLIT16 ||
+      !vv::ablk_supported(S.C, S.heads, ws, S.M))
     return false;
   memset(&aa, 0, sizeof(aa));
   const int M = S.M, C = S.C;

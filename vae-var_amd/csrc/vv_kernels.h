@@ -45,7 +45,7 @@ struct Tuning {
   int mlp_hc = 2;               // the fused dim-192 MLP: hidden units per chunk (32 or 64: fewer chunk steps, 151 KB LDS),
                                 // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
   int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
-                                // the forward, bit 1 the backward (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box,
+                                // the forward, bit 1 the backward at dim 96, bits 2 / 3 at dim 192 (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box,
                                 // profiles/r04/ab_r04j)
 };
 extern const Tuning kDefaultTuning;

@@ -404,7 +404,7 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
 // accumulator (exact). No O buffer, and the scores come from q / k fragments in registers (fp16x3 MFMA): 54 KB of
 // LDS, three workgroups per CU.
 template <int C>
-__global__ __launch_bounds__(256, 3) void k_ablk_fwd(AblkArgs a) {
+__global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
   constexpr int NW = 4, NT = 256, KS = C / 32, H = C / 32, CQ = C / 4, NQ = C / 16;
   constexpr int YW = KS * 2 * 16 * 32;        // halves of one wave's Y planes
   constexpr int WCH = 8 * C * 8;              // halves of a weight chunk (8 C 16-B pieces)
@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256, 3) void k_ablk_fwd(AblkArgs a) {
 //   dY = dqkv W_qkv                                 (qkvW^T k-chunks of q_h, k_h, v_h, rescaled per k-step)
 //   gx[window rows] += LN1-backward(dY)             (full rows in registers, k_ln_bwd's formula), in place.
 template <int C>
-__global__ __launch_bounds__(256, 2) void k_ablk_bwd(AblkArgs a) {
+__global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   constexpr int NW = 4, NT = 256, KS = C / 32, H = C / 32, CQ = C / 4, NQ = C / 16;
   constexpr int YW = KS * 2 * 16 * 32;        // halves of one wave's gx planes
   constexpr int WCH = 8 * C * 8;              // halves of a weight chunk
@@ -1113,7 +1113,9 @@ static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
 }
 hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, true); }
 
-bool ablk_supported(int C, int heads, int ws, int M) { return C == 96 && heads == 3 && ws == 4 && M > 0 && M % 64 == 0; }
+bool ablk_supported(int C, int heads, int ws, int M) {
+  return ((C == 96 && heads == 3) || (C == 192 && heads == 6)) && ws == 4 && M > 0 && M % 64 == 0;
+}
 
 hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s) {
   if (!ablk_supported(a.C, a.heads, a.ws, a.M) || a.ngroups <= 0 || a.ngroups > kMaxGroups || !a.map)
@@ -1125,7 +1127,7 @@ hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s) {
       return hipErrorInvalidValue;
   }
   const int ph = prof_begin(s);
-  const hipError_t e = launch_ablk_fwd<96>(a, s);
+  const hipError_t e = a.C == 96 ? launch_ablk_fwd<96>(a, s) : launch_ablk_fwd<192>(a, s);
   // qkv + proj GEMMs (2 M 4C C) and the window attention (4 M 16 C); bytes: x in, qkv + P + stats + x1 out
   prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 64.0 * a.M * a.C),
            (double)a.ngroups * a.M * 4.0 * (a.C + 3 * a.C + 16 * a.heads + 2 + a.C));
@@ -1141,7 +1143,7 @@ hipError_t ablk_bwd(const AblkArgs& a, hipStream_t s) {
       return hipErrorInvalidValue;
   }
   const int ph = prof_begin(s);
-  const hipError_t e = launch_ablk_bwd<96>(a, s);
+  const hipError_t e = a.C == 96 ? launch_ablk_bwd<96>(a, s) : launch_ablk_bwd<192>(a, s);
   // proj^T and qkv^T GEMMs (2 M 4C C), the attention backward (8 M 16 C); bytes: gx in / out, qkv, P, x
   prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 128.0 * a.M * a.C),
            (double)a.ngroups * a.M * 4.0 * (2 * a.C + 3 * a.C + 16 * a.heads + 2 + a.C));
