@@ -195,7 +195,9 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   }
   VV_MLP_LOAD(0)
 
-#pragma unroll 2
+  // two chunks per loop trip where the registers allow (the hidden-split dim-192 backward spills at 2)
+  constexpr int UNR = (NH == 2 && !FWD) ? 1 : 2;
+#pragma unroll UNR
   for (int c = 0; c < NC; ++c) {
     // bwd: this chunk's pre-activations, in flight before the next chunk's weight loads (vmcnt is in order)
     f4 ex[NJ];

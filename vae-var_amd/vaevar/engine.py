@@ -122,7 +122,8 @@ class Context:
         if extra is not None and (extra.dtype != torch.float64 or not extra.is_cuda or not extra.is_contiguous()):
             raise ValueError("reduce_batch: extra must be a contiguous float64 CUDA tensor")
         out = (ctypes.c_double * max(k + ne, 1))()
-        check(lib.vv_reduce_batch(self.h, k, ops, A, B, n, _ptr(extra) if ne else None, ne, out, _stream()),
+        check(lib.vv_reduce_batch(self.h, k, ops, A, B, n, ctypes.c_void_p(extra.data_ptr()) if ne else None, ne, out,
+                                  _stream()),
               "reduce_batch")
         return list(out[:k + ne])
 
@@ -465,7 +466,8 @@ class DAProblem:
         if getattr(self, "_dJ", None) is None:
             self._dJ = torch.empty(2, device=self.xb.device, dtype=torch.float64)
         gp = _ptr(grad) if grad is not None else None
-        check(lib.vv_closure_async(self.ctx.h, _ptr(z), gp, _ptr(self._dJ), _stream()), "closure_async")
+        check(lib.vv_closure_async(self.ctx.h, _ptr(z), gp, ctypes.c_void_p(self._dJ.data_ptr()), _stream()),
+              "closure_async")
         self.n_evals += 1
         return LazyLoss(self._dJ, lambda v: self.loss_f32(v[0], v[1]))
 
