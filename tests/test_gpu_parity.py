@@ -177,6 +177,22 @@ def test_tiny_lbfgs_trajectory_g5():
     assert np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]) < 1e-3
 
 
+def test_lbfgs_batched_scalars_bitwise():
+    """The mirror's batched scalar round trips (queued closure + vv_reduce_batch, vaevar/lbfgs.py) against one
+    synchronising call per scalar on the GPU: the same analysis bit for bit (latent, J per pass, counts)."""
+    from vaevar import config as C
+    from vaevar.da import one_step_da
+    from vaevar.engine import DAProblem, LGUnet
+
+    dec = LGUnet(C.TINY, 1, 1).load_synthetic()
+    prob = DAProblem(dec, _tiny_problem(1))
+    r0 = one_step_da(prob, nit=2, batch_scalars=False)
+    r1 = one_step_da(prob, nit=2, batch_scalars=True)
+    assert r0["n_eval"] == r1["n_eval"] and r0["n_iter"] == r1["n_iter"]
+    assert r0["J"] == r1["J"]
+    assert torch.equal(r0["z"], r1["z"]) and torch.equal(r0["xa"], r1["xa"])
+
+
 def test_torch_lbfgs_dropin():
     """torch.optim.LBFGS drives the HIP closure unchanged through the autograd wrapper."""
     from vaevar import config as C

@@ -18,7 +18,8 @@ from .lbfgs import LBFGS, Adam
 
 
 def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10, optimizer: str = "lbfgs",
-                lr: float | None = None, log_terms: bool = True, log=None, gt=None, metrics=None, replay=None):
+                lr: float | None = None, log_terms: bool = True, log=None, gt=None, metrics=None, replay=None,
+                batch_scalars: bool = True):
     """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, seconds); with gt (T,C,Hs,Ws) and a
     vaevar.metrics.Metrics also metrics=[(wrmse[C], bias[C]) per outer pass] of xhat against gt[0] — the
     reference's bg_* (pass 0) and ana_* (pass Nit) entries of metrics_list (:1285-1291)."""
@@ -29,13 +30,14 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
         opt = LBFGS(ctx, z, lr=1 if lr is None else lr, history_size=history_size, max_iter=max_iter,
                     line_search_fn="strong_wolfe")
         opt.replay = list(replay) if replay is not None else None  # fixed-step replay of a reference run
+        opt.batch_scalars = batch_scalars  # False: one synchronising call per scalar (vaevar/lbfgs.py)
     elif optimizer == "adam":
         opt = Adam(ctx, z, lr=1e-3 if lr is None else lr)
     else:
         raise ValueError(optimizer)
 
     def closure(zz, g):
-        if optimizer == "lbfgs":  # queued: the loss is fetched with the mirror's next scalars (vaevar/lbfgs.py)
+        if optimizer == "lbfgs" and batch_scalars:  # queued: the loss comes with the mirror's next scalars
             return prob.closure_lazy(zz, g)
         jb, jo = prob.closure(zz, g)
         return prob.loss_f32(jb, jo)
