@@ -115,7 +115,8 @@ int vv_set_closure_graph(vv_ctx* ctx, int enable);
 int vv_get_closure_graph(vv_ctx* ctx, int kind, long long* info);
 /* process-wide host-side launch counters (monotonic; eager launches only, a graph replay does not count):
    "rowsplit" (k_rowsplit passes building a GEMM's fp16x3 A planes), "fixup_ln" (split-K fixups fused into a
-   LayerNorm), "splitk_fixup" (stand-alone tile-48 split-K fixups). Tests use them to show a fused path ran. */
+   LayerNorm), "splitk_fixup" (stand-alone tile-48 split-K fixups), "gather_scales" (k_gather_scales passes of tile 48).
+   Tests use them to show a fused path ran. */
 int vv_get_counter(const char* name, long long* value);
 /* analysis states xa (B,C,Hs,Ws) */
 int vv_decode(vv_ctx* ctx, const float* z, float* xa, void* stream);
@@ -239,7 +240,9 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    tiles fill whole rounds of the chip and tile 48's leave a split-K tail: the N = 4608 GEMMs at 2048 rows, 1), "h5_var"
    (tile 49's schedule variant, experiments), "fc_conv_mf" (LGUnet_all_1's PatchEmbed / ConvTranspose2d as direct
    exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1), "mlp_hc" (the fused dim-192 MLP: 32 or 64 hidden units
-   per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2). Results stay fp32-level for every value; a change drops the
+   per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
+   (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
+   launch, 1). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key: VV_E_ARG. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);

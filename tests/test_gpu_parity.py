@@ -626,11 +626,13 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
 
 
-def test_h5_row_epilogue_bitwise(full_dec):
-    """Tile 49's full tiles go through the row-wise LDS epilogue (h5_var 4: accumulators -> LDS -> float4 rows: the
+@pytest.mark.parametrize("knob,ref,on", [("h5_var", 5, 4), ("h4_gather", 0, 1)])
+def test_bitwise_knobs(full_dec, knob, ref, on):
+    """h5_var: tile 49's full tiles go through the row-wise LDS epilogue (4: accumulators -> LDS -> float4 rows: the
     GELU / gelu' plane writers with their pre-activation stores and reads, bias) instead of the per-fragment one
-    (h5_var 5, same main loop): the same per-element arithmetic, so the config-2 decoder output, its input gradient and
-    the closure are bit-identical."""
+    (5, same main loop). h4_gather: tile 48 reads a gathered A's producer row scales through the row map itself
+    instead of a k_gather_scales pass (the counter shows the pass is gone). The same per-element arithmetic either
+    way, so the config-2 decoder output, its input gradient and the closure are bit-identical."""
     from vaevar.engine import DAProblem
     from vaevar.problem import make_problem
     from vaevar.synth import smooth_field, uniform_sym
@@ -639,22 +641,29 @@ def test_h5_row_epilogue_bitwise(full_dec):
     cot = torch.from_numpy(uniform_sym(412, (1, 69, 128, 256), 1.0)).cuda()
     prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
     zc = torch.from_numpy(0.3 * smooth_field(413, (1, 32, 128, 256))).cuda()
-    res = []
-    default = full_dec.ctx.get_tuning("h5_var")
+    from vaevar.engine import Context
+
+    res, gathers = [], []
+    default = full_dec.ctx.get_tuning(knob)
     try:
-        for v in (5, 4):
-            full_dec.ctx.set_tuning("h5_var", v)
+        for v in (ref, on):
+            full_dec.ctx.set_tuning(knob, v)
+            c0 = Context.counter("gather_scales")
             out = full_dec.forward_raw(z).clone()
             dz = torch.empty_like(z)
             full_dec.backward_raw(cot, dz)
             g = torch.empty_like(zc)
             jb, jo = prob.closure(zc, g)
+            gathers.append(Context.counter("gather_scales") - c0)
             res.append((out, dz, jb, jo, g))
     finally:
-        full_dec.ctx.set_tuning("h5_var", default)
+        full_dec.ctx.set_tuning(knob, default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
+    print(f"{knob}: k_gather_scales passes {gathers[0]} -> {gathers[1]}")
     assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1)
     assert (jb0, jo0) == (jb1, jo1)
+    if knob == "h4_gather":
+        assert gathers[0] > 0 and gathers[1] == 0
 
 
 @pytest.mark.parametrize("knob,extra", [("gelu_planes", {}), ("attn_planes", {"h4_small": 1})])

@@ -1646,6 +1646,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const float* rs = ascale + (size_t)blockIdx.z * M;
+  // this lane's 16 A row scales, loaded before the k loop (gathered through arow from the producer's physical-row
+  // scales when agather: no k_gather_scales launch); the prologue's vmcnt waits retire them with the first pieces
+  float rsv[4][4];
+  {
+    const int wm_ = (threadIdx.x >> 6) / 2, hh_ = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(m0 + wm_ * 64 + a * 16 + 4 * hh_ + r, M - 1);
+        rsv[a][r] = rs[args.agather ? args.arow[row] : row];
+      }
+  }
 
   // Planes are chunk-interleaved in memory (per row and 32-deep k-tile: h 64 B | l 64 B, one 128-B line) and in
   // LDS ([row][128 B], A rows then B rows). One DMA instruction fills 8 rows: lane i writes LDS bytes 16 i, row
@@ -1803,8 +1816,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = min(m0 + wm * TM * 16 + a * 16 + 4 * hh + r, M - 1);
-        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));   // 2^-e_a
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rsv[a][r]));   // 2^-e_a
         acc[a][b][r] *= ia * sb;
       }
   }
@@ -2253,14 +2265,21 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
   if (t49 && (a.tsplit > 1 || a.nofix)) return hipErrorInvalidValue;
   float* sc = a.ws + kWsFloats;
   const unsigned short* planes = a.apl;
+  bool agather = false;
   if (a.apre) {
     // planes and scales from the producer (physical rows); the kernel gathers plane rows through arow itself
     planes = a.apre;
-    if (!a.arow)
+    const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+    if (!a.arow) {
       sc = const_cast<float*>(a.ascale);
-    else
+    } else if (!t49 && !a.opl && TU.h4_gather) {  // tile 48 reads ascale[arow[r]] itself (no plane epilogue here)
+      sc = const_cast<float*>(a.ascale);
+      agather = true;
+    } else {
+      count_launch(CNT_GATHER_SCALES);
       hipLaunchKernelGGL(k_gather_scales, dim3((a.M + 255) / 256, 1, a.ngroups), dim3(256), 0, s, a.ascale, a.arow,
                          sc, a.M);
+    }
   } else {
     const dim3 grid((a.M + 3) / 4, 1, a.ngroups);
     const int nv = (a.K + 255) / 256;
@@ -2274,6 +2293,7 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
   }
   GemmArgs b = a;
   b.escale = sc;  // the plane-writing epilogues bound |C| from the row scales the products used
+  b.agather = agather ? 1 : 0;
   if (t49) {
     const size_t lds = 3 * (2 * (256 + 144) * 32) * sizeof(unsigned short);
     const dim3 grid(((a.N + 143) / 144) * ((a.M + 255) / 256), 1, a.ngroups);
@@ -2370,6 +2390,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h4_split_minkt") return &t.h4_split_minkt;
   if (k == "h5") return &t.h5;
   if (k == "h5_var") return &t.h5_var;
+  if (k == "h4_gather") return &t.h4_gather;
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
   return nullptr;
 }

@@ -42,6 +42,7 @@ struct Tuning {
   int fixup_ln = 1;             // the proj GEMM's split-K fixup fused into the LG-stage LN2 (gemm_ln)
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
                                 // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
+  int h4_gather = 1;            // tile 48 reads gathered producer row scales through arow itself (0: k_gather_scales)
   int mlp_hc = 2;               // the fused dim-192 MLP: hidden units per chunk (32 or 64: fewer chunk steps, 151 KB LDS),
                                 // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
   int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
@@ -101,6 +102,7 @@ struct GemmArgs {
   // row (arow[r] when gathered), z * M + row; the fp16x3 kernels then skip k_rowscale (no concat A2 allowed)
   const float* ascale;
   int ascale_phys;  // set by gemm_nt: the kernel indexes its row scales by physical row
+  int agather;      // set by launch_h4 (tile 48, producer planes, gathered rows): ascale[arow[r]] read in the kernel
   // GEMM_SPLIT16 tile 48: workspace for A's fp16 planes in GEMM row order (groups x M x 2K halfs), or null
   unsigned short* apl;
   size_t apl_halfs;
@@ -433,7 +435,7 @@ bool prof_enabled();
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 // host-side launch counters of the fused-path alternatives (vv_get_counter): tests assert that a fused path really
 // ran, since every fused launcher falls back to the unfused launches with equal results when it does not apply
-enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_N = 3 };
+enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_N = 4 };
 void count_launch(int c);
 long long launch_count(int c);
 
