@@ -195,8 +195,13 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   }
   VV_MLP_LOAD(0)
 
-  // two chunks per loop trip where the registers allow (the hidden-split dim-192 backward spills at 2)
-  constexpr int UNR = (NH == 2 && !FWD) ? 1 : 2;
+  // two chunks per loop trip for the dim-192 forward (the hidden-split backward spills at 2; dim 96 runs faster
+  // without: profiles/r04/ab_r04p)
+#ifdef VV_MLP_UNR
+  constexpr int UNR = VV_MLP_UNR;  // A/B builds only
+#else
+  constexpr int UNR = (C == 96 || (NH == 2 && !FWD)) ? 1 : 2;  // dim 96: 50.0 / 54.0 vs 53.2 / 55.3 us unrolled
+#endif
 #pragma unroll UNR
   for (int c = 0; c < NC; ++c) {
     // bwd: this chunk's pre-activations, in flight before the next chunk's weight loads (vmcnt is in order)
