@@ -1838,16 +1838,17 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
 }
 
 // Row-wise epilogue of a full tile staged in LDS (tile 49): a wave's 32 x BN fp32 results, written to LDS from the
-// accumulators, are read back as float4 chunks of rows, so bias / aux are float4 loads, aux and C float4 stores and
-// the fp16x3 planes 8-byte stores of 4 halfs (the register epilogue stores 2 bytes per plane and element). Same
-// per-element arithmetic as epilogue() (results bit-identical); rows in GEMM order (no crow), no residual.
+// accumulators, are read back as pairs of float4 chunks of rows (8 consecutive columns per lane and item), so bias /
+// aux are float4 loads, aux and C float4 stores and the fp16x3 planes 16-byte stores of 8 halfs (the register
+// epilogue stores 2 bytes per plane and element). Same per-element arithmetic as epilogue() (results bit-identical);
+// rows in GEMM order (no crow), no residual.
 template <int BN, int EPI_>
 __device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGroup& G, const float* E, int LS, int r0,
                                               int n0, int lane) {
   constexpr bool PL = EPI_ == EPI_GELU_PL || EPI_ == EPI_DGELU_PL;
   constexpr int EPI = EPI_ == EPI_GELU_PL ? EPI_GELU : EPI_ == EPI_DGELU_PL ? EPI_DGELU : EPI_;
-  constexpr int CH = BN / 4, NCH = 32 * CH / 64, B6 = 6;  // float4 chunks per row / per lane; batch of loads
-  static_assert(NCH % B6 == 0, "chunk batches");
+  constexpr int CP = BN / 8, NI = 32 * CP / 64, B3 = 3;  // 8-column items per row / per lane; batch of loads
+  static_assert(BN % 8 == 0 && NI % B3 == 0, "item batches");
   const int N = args.N;
   float ubw = 0.f, ubb = 0.f;
   if constexpr (PL) {
@@ -1857,17 +1858,21 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGr
     ubb = args.obb ? f * tb : 0.0f;
   }
 #pragma unroll
-  for (int i0 = 0; i0 < NCH; i0 += B6) {
-    f4 v[B6], bv[B6], ex[B6];
-    float sc[B6];
+  for (int i0 = 0; i0 < NI; i0 += B3) {
+    f4 v[B3][2], bv[B3][2], ex[B3][2];
+    float sc[B3];
 #pragma unroll
-    for (int j = 0; j < B6; ++j) {
-      const int e = lane + 64 * (i0 + j), rr = e / CH, col = 4 * (e - rr * CH);
+    for (int j = 0; j < B3; ++j) {
+      const int e = lane + 64 * (i0 + j), rr = e / CP, col = 8 * (e - rr * CP);
       const int gr = r0 + rr, gc = n0 + col;
-      v[j] = *reinterpret_cast<const f4*>(E + rr * LS + col);
-      const f4 t = *reinterpret_cast<const f4*>(G.bias ? G.bias + gc : G.A);  // unconditional (dummy address)
-      bv[j] = G.bias ? t : f4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_DGELU) ex[j] = *reinterpret_cast<const f4*>(G.aux + (size_t)gr * args.ldaux + gc);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        v[j][h] = *reinterpret_cast<const f4*>(E + rr * LS + col + 4 * h);
+        const f4 t = *reinterpret_cast<const f4*>(G.bias ? G.bias + gc + 4 * h : G.A);  // unconditional (dummy address)
+        bv[j][h] = G.bias ? t : f4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_DGELU)
+          ex[j][h] = *reinterpret_cast<const f4*>(G.aux + (size_t)gr * args.ldaux + gc + 4 * h);
+      }
       if constexpr (PL) {
         const float ia = __uint_as_float((254u << 23) - __float_as_uint(args.escale[gr]));
         const unsigned mx = __float_as_uint(2.0f * (ubw * (32768.0f * ia) + ubb));
@@ -1875,40 +1880,42 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGr
       }
     }
 #pragma unroll
-    for (int j = 0; j < B6; ++j) {
-      const int e = lane + 64 * (i0 + j), rr = e / CH, col = 4 * (e - rr * CH);
+    for (int j = 0; j < B3; ++j) {
+      const int e = lane + 64 * (i0 + j), rr = e / CP, col = 8 * (e - rr * CP);
       const int gr = r0 + rr, gc = n0 + col;
-      f4 o;
-      float xs[4], ys[4];  // GELU / GELU' four at a time (vv_gelu.h gelu4: the four chains interleave)
+      f4 o[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xs[q] = EPI == EPI_DGELU ? ex[j][q] : v[j][q] + bv[j][q];
-      if constexpr (EPI == EPI_GELU) gelu4(xs, ys);
-      if constexpr (EPI == EPI_DGELU) dgelu4(xs, ys);
+      for (int h = 0; h < 2; ++h) {
+        float xs[4], ys[4];  // GELU / GELU' four at a time (vv_gelu.h gelu4: the four chains interleave)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        o[q] = EPI == EPI_GELU ? ys[q] : EPI == EPI_DGELU ? v[j][q] * ys[q] : v[j][q] + bv[j][q];
-      if constexpr (EPI == EPI_GELU) {
-        if (G.aux) {
-          f4 pre;
+        for (int q = 0; q < 4; ++q) xs[q] = EPI == EPI_DGELU ? ex[j][h][q] : v[j][h][q] + bv[j][h][q];
+        if constexpr (EPI == EPI_GELU) gelu4(xs, ys);
+        if constexpr (EPI == EPI_DGELU) dgelu4(xs, ys);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) pre[q] = v[j][q] + bv[j][q];
-          *reinterpret_cast<f4*>(G.aux + (size_t)gr * args.ldaux + gc) = pre;  // the pre-activation, for a backward
+        for (int q = 0; q < 4; ++q)
+          o[h][q] = EPI == EPI_GELU ? ys[q] : EPI == EPI_DGELU ? v[j][h][q] * ys[q] : v[j][h][q] + bv[j][h][q];
+        if constexpr (EPI == EPI_GELU) {
+          if (G.aux) {
+            f4 pre;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pre[q] = v[j][h][q] + bv[j][h][q];
+            *reinterpret_cast<f4*>(G.aux + (size_t)gr * args.ldaux + gc + 4 * h) = pre;  // the pre-activation
+          }
         }
+        if constexpr (!PL) *reinterpret_cast<f4*>(G.C + (size_t)gr * args.ldc + gc + 4 * h) = o[h];
       }
       if constexpr (PL) {
-        h4v hv, lv;
+        h8v hv, lv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float x = o[q] * sc[j];
+        for (int q = 0; q < 8; ++q) {
+          const float x = o[q >> 2][q & 3] * sc[j];
           hv[q] = (_Float16)x;
           lv[q] = (_Float16)(x - (float)hv[q]);
         }
         unsigned short* pp = args.opl + (size_t)gr * 2 * N + 2 * (gc & ~31) + (gc & 31);  // chunk-interleaved
-        *reinterpret_cast<h4v*>(pp) = hv;
-        *reinterpret_cast<h4v*>(pp + 32) = lv;
+        *reinterpret_cast<h8v*>(pp) = hv;
+        *reinterpret_cast<h8v*>(pp + 32) = lv;
         if (gc == 0) args.ors[gr] = sc[j];
-      } else {
-        *reinterpret_cast<f4*>(G.C + (size_t)gr * args.ldc + gc) = o;
       }
     }
   }
