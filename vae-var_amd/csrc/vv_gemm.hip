@@ -1646,9 +1646,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const float* rs = ascale + (size_t)blockIdx.z * M;
-  // this lane's 16 A row scales, loaded before the k loop (gathered through arow from the producer's physical-row
-  // scales when agather: no k_gather_scales launch); the prologue's vmcnt waits retire them with the first pieces
+  // this lane's 16 A row scales (gathered through arow from the producer's physical-row scales when agather: no
+  // k_gather_scales launch), loaded after the k loop
   float rsv[4][4];
+#ifdef VV_H4_EARLY_SCALES  // A/B builds only: loaded before the k loop (+2 % kernel time, profiles/r04/ab_r04s)
   {
     const int wm_ = (threadIdx.x >> 6) / 2, hh_ = (threadIdx.x & 63) >> 4;
 #pragma unroll
@@ -1659,6 +1660,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
         rsv[a][r] = rs[args.agather ? args.arow[row] : row];
       }
   }
+#endif
 
   // Planes are chunk-interleaved in memory (per row and 32-deep k-tile: h 64 B | l 64 B, one 128-B line) and in
   // LDS ([row][128 B], A rows then B rows). One DMA instruction fills 8 rows: lane i writes LDS bytes 16 i, row
@@ -1807,6 +1809,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   // drain the DMAs still in flight before the workgroup can exit (their LDS must not be reassigned under them)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+#ifndef VV_H4_EARLY_SCALES
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = min(m0 + wm * TM * 16 + a * 16 + 4 * hh + r, M - 1);
+      rsv[a][r] = rs[args.agather ? args.arow[row] : row];
+    }
+#endif
   // undo the scales: rows of A (2^-e_a), rows of B = columns of C (2^-e_b); 16x16 tile: row 4 hh + r, col rin
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
