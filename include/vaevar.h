@@ -242,7 +242,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1), "mlp_hc" (the fused dim-192 MLP: 32 or 64 hidden units
    per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
    (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
-   launch, 1). Results stay fp32-level for every value; a change drops the
+   launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
+   inverse window map, 1). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key: VV_E_ARG. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);

@@ -211,6 +211,7 @@ struct Stage {
   int G, H, W, C, heads, depth, M, nWh, nWw;
   std::vector<std::array<BlockW, kMaxGroups>> w;  // [depth][G]
   const int* idx[2];                              // window maps, shift 0 / ws/2
+  const int* idxinv[2];                           // their inverses (fused fixup + LN1 walks GEMM rows in order)
 };
 
 struct StageSave {
@@ -405,8 +406,16 @@ int init_stage(Model& m, Stage& s, int G, int H, int W, int C, int heads, int de
   s.nWw = W / m.cfg.ws;
   s.w.assign(depth, {});
   int rc;
-  if ((rc = upload_map(m, window_map(m.B, H, W, m.cfg.ws, 0), &s.idx[0]))) return rc;
-  if ((rc = upload_map(m, window_map(m.B, H, W, m.cfg.ws, m.cfg.ws / 2), &s.idx[1]))) return rc;
+  for (int k = 0; k < 2; ++k) {
+    const std::vector<int> fwd = window_map(m.B, H, W, m.cfg.ws, k ? m.cfg.ws / 2 : 0);
+    std::vector<int> inv(fwd.size(), -1);
+    for (size_t j = 0; j < fwd.size(); ++j) {
+      if (fwd[j] < 0 || (size_t)fwd[j] >= fwd.size() || inv[fwd[j]] >= 0) return VV_E_STATE;  // not a permutation
+      inv[fwd[j]] = (int)j;
+    }
+    if ((rc = upload_map(m, fwd, &s.idx[k]))) return rc;
+    if ((rc = upload_map(m, inv, &s.idxinv[k]))) return rc;
+  }
   return 0;
 }
 
@@ -718,6 +727,7 @@ hipError_t fc2_ln1(const Stage& S, int b, const StageSave& sv, const Scratch& sc
   vv::GemmLnArgs l;
   memset(&l, 0, sizeof(l));
   l.gmap = S.idx[shift ? 1 : 0];  // LN1 -> window order
+  l.ginv = T.fixup_ln_rows ? S.idxinv[shift ? 1 : 0] : nullptr;
   l.lo_x = 0;
   l.gamma = S.w[nb][0].n1g;
   l.beta = S.w[nb][0].n1b;

@@ -2409,6 +2409,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h5") return &t.h5;
   if (k == "h5_var") return &t.h5_var;
   if (k == "h4_gather") return &t.h4_gather;
+  if (k == "fixup_ln_rows") return &t.fixup_ln_rows;
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
   return nullptr;
 }

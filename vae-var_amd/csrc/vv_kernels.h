@@ -42,6 +42,7 @@ struct Tuning {
   int fixup_ln = 1;             // the proj GEMM's split-K fixup fused into the LG-stage LN2 (gemm_ln)
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
                                 // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
+  int fixup_ln_rows = 1;        // the fused fixup + LN1 walks GEMM rows in order through the inverse window map
   int h4_gather = 1;            // tile 48 reads gathered producer row scales through arow itself (0: k_gather_scales)
   int mlp_hc = 2;               // the fused dim-192 MLP: hidden units per chunk (32 or 64: fewer chunk steps, 151 KB LDS),
                                 // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
@@ -157,6 +158,7 @@ hipError_t gemm_nt(const GemmArgs& a, hipStream_t s, int tile_hint = -1, float* 
 // LN row j reads GEMM row gmap[j] (null: j); its output row is the x row written (lo_x) or j.
 struct GemmLnArgs {
   const int* gmap;
+  const int* ginv;  // the inverse of gmap (or null): workgroups then walk GEMM rows in order (partial lines stay local)
   int lo_x;
   const float* gamma;
   const float* beta;

@@ -307,11 +307,14 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
 // 128-B line of a partial (rows r and r + 4 of one 16-column block) is consumed inside one workgroup
 template <int NV, int S>
 __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
-  const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
-  if (j >= args.M) return;
+  // wave = GEMM row gr (ginv) or LN row j: with a gather, walking GEMM rows keeps each 128-B line of a partial
+  // (two GEMM rows of one wave quarter) inside one workgroup
+  const int w = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
+  if (w >= args.M) return;
   const GemmGroup G = args.g[0];
   const int N = args.N, f4n = N >> 2;
-  const int gr = l.gmap ? l.gmap[j] : j;
+  const int j = l.ginv ? l.ginv[w] : w;
+  const int gr = l.ginv ? w : l.gmap ? l.gmap[j] : j;
   const int xo = args.crow ? args.crow[gr] : gr;
   const int lo = l.lo_x ? xo : j;
   const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
