@@ -116,6 +116,11 @@ def test_new_entry_points_reject_bad_arguments():
     assert lib.vv_metrics(None, None, None, None, None, None, 1, 69, 8, 8, None, None, None) == 1001
     ro = (ctypes.c_float * 1)(1.0)
     assert lib.vv_lbfgs_two_loop(None, None, None, None, ro, 1, 1.0, 16, None) == 1001
+    out = (ctypes.c_double * 4)()
+    ops = (ctypes.c_int * 1)(0)
+    ptrs = (ctypes.c_void_p * 1)(None)
+    assert lib.vv_reduce_batch(None, 1, ops, ptrs, ptrs, 16, None, 0, out, None) == 1001
+    assert lib.vv_closure_async(None, None, None, None, None) == 1001
     buf = ctypes.create_string_buffer(256)
     lib.vv_last_error(buf, 256)
     assert buf.value  # a message describes the failure
@@ -147,7 +152,7 @@ def test_launch_counters_abi():
     from vaevar import _lib
     from vaevar.engine import Context
 
-    for name in ("rowsplit", "fixup_ln", "splitk_fixup"):
+    for name in ("rowsplit", "fixup_ln", "splitk_fixup", "gather_scales"):
         assert Context.counter(name) >= 0
     with pytest.raises(_lib.VVError, match="unknown counter"):
         Context.counter("nope")

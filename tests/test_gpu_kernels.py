@@ -195,6 +195,26 @@ def test_gemm_h5_bitwise_h4(ctx, M, N, K):
     _keep.append(B)
 
 
+def test_reduce_batch_matches_single_calls(ctx):
+    """vv_reduce_batch (the L-BFGS mirror's batched scalars): every op equals the one-call-each vv_dot / vv_abssum /
+    vv_absmax on the same vectors (same kernels, partial layouts and final reductions), and the appended device doubles
+    come back unchanged; bad op codes and too many ops are rejected."""
+    from vaevar._lib import VVError
+
+    g = torch.Generator().manual_seed(7)
+    n = 1 << 20
+    a, b, c = (torch.randn(n, generator=g).cuda() for _ in range(3))
+    extra = torch.tensor([1.25, -3.5e7], dtype=torch.float64, device="cuda")
+    reqs = [(0, a, b), (1, c, None), (2, b, None), (0, c, c), (2, a, None)]
+    got = ctx.reduce_batch(reqs, extra=extra)
+    want = [ctx.dot(a, b), ctx.abssum(c), ctx.absmax(b), ctx.dot(c, c), ctx.absmax(a)]
+    assert got[:5] == want and got[5:] == [1.25, -3.5e7]
+    with pytest.raises(VVError):
+        ctx.reduce_batch([(3, a, None)])
+    with pytest.raises(VVError):
+        ctx.reduce_batch([(1, a, None)] * 9)
+
+
 def test_gemm_rejects_non_library_tiles(ctx):
     """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47, 48, 49): any other hint, e.g. the
     r01 timing experiments 37-39, returns VV_E_ARG instead of running something."""
