@@ -182,6 +182,10 @@ int vv_absmax(vv_ctx* ctx, const float* a, int64_t n, float* out, void* stream);
    iteration together instead of one synchronising call each (torch/optim/lbfgs.py computes them one by one). */
 int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
                     const double* dev_extra, int n_extra, double* out, void* stream);
+/* The same reductions queued without a host round trip: the results stay in the caller's device doubles dev_out[count]
+   (absmax widened exactly), to be fetched later as another call's dev_extra. */
+int vv_reduce_enqueue(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
+                      double* dev_out, void* stream);
 int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream);
 int vv_axpby(vv_ctx* ctx, float* out, const float* x, float a, const float* y, float b, int64_t n, void* stream);
 int vv_scale(vv_ctx* ctx, float* y, float alpha, int64_t n, void* stream);

@@ -20,6 +20,10 @@ class CpuPrims:
         out = [self.dot(a, b) if op == 0 else self.abssum(a) if op == 1 else self.absmax(a) for op, a, b in reqs]
         return out + (extra.tolist() if extra is not None else [])
 
+    def reduce_enqueue(self, reqs, out):
+        for i, (op, a, b) in enumerate(reqs):
+            out[i] = self.dot(a, b) if op == 0 else self.abssum(a) if op == 1 else self.absmax(a)
+
     def axpy(self, y, x, alpha):
         y.add_(x, alpha=alpha)
 
@@ -150,6 +154,53 @@ def test_lbfgs_batched_scalars_identical():
     assert s0["n_iter"] == s1["n_iter"] and s0["func_evals"] == s1["func_evals"]
     print(f"scalar round trips: {c0} one at a time, {c1} batched ({s1['n_iter']} iterations)")
     assert c1 * 2 < c0
+
+
+def test_lbfgs_speculative_line_search_identical():
+    """With queued closures (vaevar.engine.LazyLoss) the mirror also defers gtd / d_norm to the line search's first
+    evaluation and discards that evaluation where the reference stops first (gtd > -tolerance_change): iterates,
+    losses and every count equal the one-call-per-scalar run; the discarded evaluations are uncounted."""
+    from vaevar.lbfgs import LBFGS
+
+    class Lazy:
+        def __init__(self, f, counter):
+            self.dev = torch.tensor([f, 0.0], dtype=torch.float64)
+            self.counter = counter
+
+        def resolve(self, v):
+            return float(v[0])
+
+        def discard(self):
+            self.counter[0] -= 1
+
+        def __float__(self):
+            return float(self.dev[0])
+
+    def make_closure(lazy, counter):
+        def closure_m(z, g):
+            zz = z.clone().requires_grad_(True)
+            f = objective(zz)
+            f.backward()
+            g.copy_(zz.grad)
+            counter[0] += 1
+            return Lazy(float(f.detach()), counter) if lazy else float(f.detach())
+        return closure_m
+
+    runs = []
+    for batch in (False, True):
+        cnt = [0]
+        zm = torch.zeros(4096)
+        mir = LBFGS(CpuPrims(), zm, history_size=10, max_iter=10, line_search_fn="strong_wolfe")
+        mir.batch_scalars = batch
+        losses = [float(mir.step(make_closure(batch, cnt))) for _ in range(4)]
+        # the reference's gtd > -tolerance_change exit (taken before the line search): the speculative run has
+        # already evaluated at x + t d and must drop that evaluation
+        mir.tolerance_change = 1e9
+        losses.append(float(mir.step(make_closure(batch, cnt))))
+        runs.append((zm, losses, dict(mir.state), cnt[0]))
+    (z0, l0, s0, c0), (z1, l1, s1, c1) = runs
+    assert torch.equal(z0, z1) and l0 == l1
+    assert s0["n_iter"] == s1["n_iter"] and s0["func_evals"] == s1["func_evals"] and c0 == c1
 
 
 def test_adam_mirror_matches_torch():

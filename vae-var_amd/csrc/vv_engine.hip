@@ -2225,6 +2225,28 @@ int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* 
   for (int i = 0; i < n_extra; ++i) out[count + i] = h[count + i];
   return 0;
 }
+int vv_reduce_enqueue(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
+                      double* dev_out, void* stream) {
+  if (!ctx || count <= 0 || count > kMaxBatch || !ops || !a || !dev_out || n < 0)
+    return fail(VV_E_ARG, "reduce_enqueue: bad arguments");
+  for (int i = 0; i < count; ++i)
+    if (ops[i] < 0 || ops[i] > 2 || !a[i] || (ops[i] == 0 && (!b || !b[i])))
+      return fail(VV_E_ARG, "reduce_enqueue: bad op %d", i);
+  int r = set_dev(ctx);
+  if (r) return r;
+  hipStream_t st = (hipStream_t)stream;
+  // vv_reduce_batch's kernels and partial layouts (the same values), results left in dev_out (doubles), no sync
+  for (int i = 0; i < count; ++i) {
+    double* part = ctx->redb + (size_t)i * kRedBlocks;
+    if (ops[i] == 0)
+      VV_HIP(vv::vec_dot(a[i], b[i], n, part, kRedBlocks, dev_out + i, st));
+    else if (ops[i] == 1)
+      VV_HIP(vv::vec_abssum(a[i], n, part, kRedBlocks, dev_out + i, st));
+    else
+      VV_HIP(vv::vec_absmax_d(a[i], n, reinterpret_cast<float*>(part), kRedBlocks, dev_out + i, st));
+  }
+  return 0;
+}
 int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream) {
   if (!ctx || !y || !x) return fail(VV_E_ARG, "null argument");
   VV_HIP(vv::vec_axpy(y, x, alpha, n, (hipStream_t)stream));

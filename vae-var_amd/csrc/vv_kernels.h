@@ -415,6 +415,7 @@ hipError_t vec_axpy(float* y, const float* x, float alpha, int64_t n, hipStream_
 hipError_t vec_axpby(float* out, const float* x, float a, const float* y, float b, int64_t n, hipStream_t s);
 hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s);
 hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float* out, hipStream_t s);
+hipError_t vec_absmax_d(const float* x, int64_t n, float* partial, int nblk, double* out, hipStream_t s);
 hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
 // q (= -g on entry) -> L-BFGS direction d (two-loop recursion, device scalars); al: >= m device floats;
 // partial: 2 * nblk doubles

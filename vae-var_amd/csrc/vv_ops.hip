@@ -1945,6 +1945,24 @@ __global__ __launch_bounds__(256) void k_final_max(const float* partial, int n, 
   if (threadIdx.x == 0) out[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// k_final_max with the result widened to double (vv_reduce_enqueue's device outputs are all doubles; exact)
+__global__ __launch_bounds__(256) void k_final_max_d(const float* partial, int n, double* out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, partial[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (double)fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+hipError_t vec_absmax_d(const float* x, int64_t n, float* partial, int nblk, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_absmax, dim3(nblk), dim3(256), 0, s, x, n, partial);
+  hipLaunchKernelGGL(k_final_max_d, dim3(1), dim3(256), 0, s, partial, nblk, out);
+  return hipGetLastError();
+}
+
 hipError_t reduce_sumsq(const float* x, int64_t n, double* partial, int nblk, hipStream_t s) {
   hipLaunchKernelGGL(k_sumsq, dim3(nblk), dim3(256), 0, s, x, n, partial);
   return hipGetLastError();

@@ -93,6 +93,7 @@ _SIGS = {
     "vv_absmax": (c_int, [c_void_p, c_void_p, c_int64, P(c_float), c_void_p]),
     "vv_reduce_batch": (c_int, [c_void_p, c_int, P(c_int), P(c_void_p), P(c_void_p), c_int64, c_void_p, c_int,
                                 P(c_double), c_void_p]),
+    "vv_reduce_enqueue": (c_int, [c_void_p, c_int, P(c_int), P(c_void_p), P(c_void_p), c_int64, c_void_p, c_void_p]),
     "vv_axpy": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_int64, c_void_p]),
     "vv_axpby": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_float, c_int64, c_void_p]),
     "vv_scale": (c_int, [c_void_p, c_void_p, c_float, c_int64, c_void_p]),

@@ -127,6 +127,22 @@ class Context:
               "reduce_batch")
         return list(out[:k + ne])
 
+    def reduce_enqueue(self, reqs, out: torch.Tensor):
+        """vv_reduce_enqueue: reqs as in reduce_batch, queued; the values land in the float64 device tensor `out`
+        (len(reqs) entries) without a synchronisation — fetch them later as reduce_batch's `extra`."""
+        k = len(reqs)
+        n = reqs[0][1].numel()
+        for op, a, b in reqs:
+            if a.numel() != n or (op == 0 and b.numel() != n):
+                raise ValueError("reduce_enqueue: vectors of different lengths")
+        if out.dtype != torch.float64 or not out.is_cuda or not out.is_contiguous() or out.numel() < k:
+            raise ValueError("reduce_enqueue: out must be a contiguous float64 CUDA tensor of len(reqs) entries")
+        ops = (ctypes.c_int * k)(*[int(r[0]) for r in reqs])
+        A = (ctypes.c_void_p * k)(*[_ptr(r[1]).value for r in reqs])
+        B = (ctypes.c_void_p * k)(*[(_ptr(r[2]).value if r[0] == 0 else None) for r in reqs])
+        check(lib.vv_reduce_enqueue(self.h, k, ops, A, B, n, ctypes.c_void_p(out.data_ptr()), _stream()),
+              "reduce_enqueue")
+
     def axpy(self, y, x, alpha: float):
         check(lib.vv_axpy(self.h, _ptr(y), _ptr(x), float(alpha), y.numel(), _stream()), "axpy")
 
@@ -381,11 +397,16 @@ class LazyLoss:
     """A queued closure's loss: `dev` holds (J_b, J_o) on the device; `resolve(values)` turns the fetched pair into
     the loss. `float()` fetches it on its own (one synchronisation)."""
 
-    def __init__(self, dev: torch.Tensor, finish):
-        self.dev, self.finish = dev, finish
+    def __init__(self, dev: torch.Tensor, finish, discard=None):
+        self.dev, self.finish, self._discard = dev, finish, discard
 
     def resolve(self, values) -> float:
         return self.finish(values)
+
+    def discard(self):
+        """The evaluation is dropped (the mirror speculated past an exit the reference takes before it): uncount it."""
+        if self._discard is not None:
+            self._discard()
 
     def __float__(self) -> float:
         v = self.dev.cpu().tolist()
@@ -469,7 +490,10 @@ class DAProblem:
         check(lib.vv_closure_async(self.ctx.h, _ptr(z), gp, ctypes.c_void_p(self._dJ.data_ptr()), _stream()),
               "closure_async")
         self.n_evals += 1
-        return LazyLoss(self._dJ, lambda v: self.loss_f32(v[0], v[1]))
+        def uncount():
+            self.n_evals -= 1
+
+        return LazyLoss(self._dJ, lambda v: self.loss_f32(v[0], v[1]), uncount)
 
     def closure(self, z: torch.Tensor, grad: torch.Tensor | None):
         """Returns (J_b, J_o) as Python floats (double sums); grad <- dJ/dz if given. Single analysis (B = 1)."""

@@ -24,6 +24,8 @@ unchanged; a speculative y / s that is not used costs two axpby and two dots.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -76,6 +78,14 @@ class LBFGS:
         self._cache = []           # [(op, a, b, value)] from the last vv_reduce_batch
         self._spec = None          # (g, prev_flat_grad, d, t, y, s): y, s computed speculatively
         self._prev_flat_grad = None
+        # after the direction (n_iter > 1, queued closures): gtd and d_norm queued on the device instead of fetched,
+        # and the line search's first evaluation started before they are known; they come back with that
+        # evaluation's scalars, and where the reference would have stopped before it (gtd > -tolerance_change) the
+        # evaluation is discarded -- same trajectory, same counts, one round trip less per iteration
+        self.speculate = os.environ.get("VAEVAR_LBFGS_SPECULATE", "1") != "0"  # A/B switch
+        self._lazy_seen = False
+        self._deferred = None      # [(op, a, b)] whose values are queued in self._xbuf[2:]
+        self._xbuf = None
 
     # --- vector helpers ---------------------------------------------------
     def _cached(self, op, a, b):
@@ -100,6 +110,13 @@ class LBFGS:
         self._cache = [(op, a, b, v) for (op, a, b), v in zip(reqs, vals)]
         return lazy.resolve(vals[len(reqs):]) if lazy is not None else None
 
+    def _enqueue(self, reqs):
+        if self._xbuf is None:
+            self._xbuf = torch.empty(2 + 8, dtype=torch.float64, device=self.z.device)
+        self.ctx.reduce_enqueue([(op, a.view(-1), b.view(-1) if b is not None else None) for op, a, b in reqs],
+                                self._xbuf[2:2 + len(reqs)])
+        self._deferred = reqs
+
     def _loss_of(self, res):
         """The loss a closure returned: a float, or a LazyLoss fetched on its own."""
         return float(res)
@@ -118,8 +135,19 @@ class LBFGS:
             self._spec = (g, self._prev_flat_grad, d, t, y, s)
             reqs += [(0, y, s), (0, y, y)]
         lazy = res if _is_lazy(res) else None
-        loss = self._prefetch(reqs, lazy)
-        return loss if lazy is not None else float(res)
+        if self._deferred is None:
+            loss = self._prefetch(reqs, lazy)
+            return loss if lazy is not None else float(res)
+        # the queued gtd / d_norm come back with this evaluation's scalars (and its J pair, copied beside them)
+        dq, self._deferred = self._deferred, None
+        k = len(dq)
+        self._xbuf[:2].copy_(lazy.dev)
+        vals = self.ctx.reduce_batch([(op, a.view(-1), b.view(-1) if b is not None else None) for op, a, b in reqs],
+                                     extra=self._xbuf[:2 + k])
+        n = len(reqs)
+        self._cache = [(op, a, b, v) for (op, a, b), v in zip(reqs, vals[:n])]
+        self._cache += [(op, a, b, v) for (op, a, b), v in zip(dq, vals[n + 2:n + 2 + k])]
+        return lazy.resolve(vals[n:n + 2])
 
     def _y_s(self, flat_grad, prev_flat_grad, d, t):
         """y = flat_grad - prev_flat_grad, s = t d (lbfgs.py:397-398): the speculative pair if it was made from the
@@ -149,15 +177,25 @@ class LBFGS:
         self._add_grad(t, d)
         g = self._new()
         res = yield self.z, g
+        self._last_res = res
         loss = self._after_eval(res, g, d, t)
         self.ctx.copy(self.z, x)
         return loss, g
 
-    def _strong_wolfe(self, x, t, d, f, g, gtd, c1=1e-4, c2=0.9, tolerance_change=1e-9, max_ls=25):
-        # lbfgs.py:40-209
-        d_norm = self._absmax(d)
+    def _strong_wolfe(self, x, t, d, f, g, gtd, c1=1e-4, c2=0.9, tolerance_change=1e-9, max_ls=25, exit_tol=None):
+        # lbfgs.py:40-209; gtd None: queued (speculate), resolved after the first evaluation, and None is returned
+        # where the reference's step() would have stopped on gtd > -exit_tol before calling this search
+        g_in = g
+        d_norm = self._absmax(d) if gtd is not None else None
         g = g.clone()
         f_new, g_new = yield from self._directional_evaluate(x, t, d)
+        if gtd is None:
+            gtd = self._dot(g_in, d)
+            if gtd > -exit_tol:
+                if hasattr(self._last_res, "discard"):
+                    self._last_res.discard()
+                return None
+            d_norm = self._absmax(d)
         ls_func_evals = 1
         gtd_new = self._dot(g_new, d)
         t_prev, f_prev, g_prev, gtd_prev = 0, f, g, gtd
@@ -251,6 +289,7 @@ class LBFGS:
         res = yield self.z, flat_grad
         if self.batch_scalars:
             lazy = res if _is_lazy(res) else None
+            self._lazy_seen = lazy is not None
             orig_loss = self._prefetch([(2, flat_grad, None)], lazy) if lazy is not None else res
             if lazy is None:
                 self._prefetch([(2, flat_grad, None)])
@@ -312,16 +351,22 @@ class LBFGS:
                 self.ctx.copy(prev_flat_grad, flat_grad)
             self._prev_flat_grad = prev_flat_grad
             prev_loss = loss
-            if self.batch_scalars:  # gtd and the line search's d_norm (and the first step's |g|_1) together
+            deferred = (self.batch_scalars and self.speculate and self._lazy_seen and state["n_iter"] > 1 and
+                        not self.replay and self.line_search_fn == "strong_wolfe")
+            if deferred:  # gtd and d_norm queued; fetched with the line search's first evaluation
+                self._enqueue([(0, flat_grad, d), (2, d, None)])
+            elif self.batch_scalars:  # gtd and the line search's d_norm (and the first step's |g|_1) together
                 reqs = [(0, flat_grad, d), (2, d, None)] + ([(1, flat_grad, None)] if state["n_iter"] == 1 else [])
                 self._prefetch(reqs)
             if state["n_iter"] == 1:
                 t = min(1.0, 1.0 / self._abssum(flat_grad)) * lr
             else:
                 t = lr
-            gtd = self._dot(flat_grad, d)
-            if gtd > -tolerance_change:
-                break
+            gtd = None
+            if not deferred:
+                gtd = self._dot(flat_grad, d)
+                if gtd > -tolerance_change:
+                    break
             ls_func_evals = 0
             if self.line_search_fn is not None:
                 if self.line_search_fn != "strong_wolfe":
@@ -331,8 +376,11 @@ class LBFGS:
                     t, ls_func_evals = self.replay.pop(0)
                     loss, flat_grad = yield from self._directional_evaluate(x_init, t, d)
                 else:
-                    loss, flat_grad, t, ls_func_evals = yield from self._strong_wolfe(
-                        x_init, t, d, loss, flat_grad, gtd, max_ls=max_eval - current_evals)
+                    out = yield from self._strong_wolfe(x_init, t, d, loss, flat_grad, gtd,
+                                                        max_ls=max_eval - current_evals, exit_tol=tolerance_change)
+                    if out is None:  # the queued gtd > -tolerance_change: the reference stopped before this search
+                        break
+                    loss, flat_grad, t, ls_func_evals = out
                 self._add_grad(t, d)
                 opt_cond = self._absmax(flat_grad) <= tolerance_grad
             else:
