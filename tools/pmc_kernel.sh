@@ -19,7 +19,8 @@ out = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        key = r["Kernel_Name"].split("(")[0][-40:] + " grid " + r.get("Grid_Size", "")
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        key = n.split("(")[0][-60:] + " grid " + r.get("Grid_Size", "")
         agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 with open(f"{out}/summary.txt", "w") as fh:
     for k, d in agg.items():
