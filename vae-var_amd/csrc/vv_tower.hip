@@ -40,6 +40,10 @@ __device__ __forceinline__ unsigned amax(unsigned m, float v) { return max(m, __
 // groups of a 16x16x32 fragment read (rows lane & 15, chunk lane >> 4) hit 16 distinct 16-B slots
 __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
 __device__ __forceinline__ int frag(int r, int q) { return r * 32 + ((q ^ hsw(r >> 2)) << 3); }
+#ifndef VV_MLP_BLOCK_PAD
+#define VV_MLP_BLOCK_PAD 32  // halves (64 B); 0 = the unpadded r03 layout (A/B builds)
+#endif
+constexpr int kMlpBlockPad = VV_MLP_BLOCK_PAD;
 
 // NH = 2 splits the hidden layer between two waves per 16 tokens (wave hh runs hidden units [hh 2C, hh 2C + 2C)):
 // twice the waves per CU for the same LDS weight stream, the two partial fc2 sums added through LDS at the end.
@@ -49,8 +53,13 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   constexpr int HH = 4 * C / NH;             // hidden units per wave half
   constexpr int CQ = C / 4;                  // channels per lane in the row phases (4 lanes per token)
   constexpr int A1W = KS1 * 2 * 16 * 32;     // halves of one wave's Y planes
-  constexpr int W1S = KS1 * 2 * HC * 32;     // halves of a W1 chunk (HC rows x C)
-  constexpr int W2S = KS2 * 2 * C * 32;      // halves of a W2 chunk (C rows x HC)
+  // plane blocks of a weight chunk (32 halves per row) padded by 64 B: unpadded they sit a multiple of 64 banks x 4 B
+  // apart, and the staging stores of one row (all its blocks at once) hit the same bank group (r04 PMC: ~1.1
+  // conflict cycles per LDS instruction); fragment reads stay inside one block (unchanged)
+  constexpr int BP = kMlpBlockPad;
+  constexpr int BLK1 = HC * 32 + BP, BLK2 = C * 32 + BP;
+  constexpr int W1S = KS1 * 2 * BLK1;        // halves of a W1 chunk (HC rows x C)
+  constexpr int W2S = KS2 * 2 * BLK2;        // halves of a W2 chunk (C rows x HC)
   static_assert(C % 32 == 0 && HC % 32 == 0 && HH % HC == 0 && CQ % 4 == 0 && (NH == 1 || NH == 2), "shape");
   static_assert(NH == 1 || NW * NQ * 64 * 16 <= 2 * NH * (W1S + W2S), "fc2 partial sums fit the weight buffers");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
@@ -215,14 +224,14 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
 #pragma unroll
     for (int i = 0; i < P1; ++i) {
       const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8), rh = r / HC, rl = r - rh * HC;
-      *reinterpret_cast<u4v*>(W1 + rh * W1S + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * HC * 32 + frag(rl, rem & 3)) =
+      *reinterpret_cast<u4v*>(W1 + rh * W1S + ((rem >> 3) * 2 + ((rem >> 2) & 1)) * BLK1 + frag(rl, rem & 3)) =
           r1[i];
     }
 #pragma unroll
     for (int i = 0; i < P2; ++i) {
       const int e0 = tid + i * NT, eh = e0 / (C * KS2 * 16), e = e0 - eh * (C * KS2 * 16), n = e / (KS2 * 16),
                 rem = e - n * (KS2 * 16);
-      *reinterpret_cast<u2v*>(W2 + eh * W2S + ((rem >> 4) * 2 + ((rem >> 3) & 1)) * C * 32 +
+      *reinterpret_cast<u2v*>(W2 + eh * W2S + ((rem >> 4) * 2 + ((rem >> 3) & 1)) * BLK2 +
                                 frag(n, (rem >> 1) & 3) + 4 * (rem & 1)) = r2[i];
     }
     __syncthreads();
@@ -247,8 +256,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
       const h8v yl = *reinterpret_cast<const h8v*>(A1 + frag((ks * 2 + 1) * 16 + li, g4));
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const h8v wh = *reinterpret_cast<const h8v*>(W1w + (ks * 2 + 0) * HC * 32 + frag(16 * j + li, g4));
-        const h8v wl = *reinterpret_cast<const h8v*>(W1w + (ks * 2 + 1) * HC * 32 + frag(16 * j + li, g4));
+        const h8v wh = *reinterpret_cast<const h8v*>(W1w + (ks * 2 + 0) * BLK1 + frag(16 * j + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(W1w + (ks * 2 + 1) * BLK1 + frag(16 * j + li, g4));
         acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, yh, acc1[j], 0, 0, 0);
         acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yl, acc1[j], 0, 0, 0);
         acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, yh, acc1[j], 0, 0, 0);
@@ -295,8 +304,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
       }
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        const h8v wh = *reinterpret_cast<const h8v*>(W2w + (kk * 2 + 0) * C * 32 + frag(16 * q + li, g4));
-        const h8v wl = *reinterpret_cast<const h8v*>(W2w + (kk * 2 + 1) * C * 32 + frag(16 * q + li, g4));
+        const h8v wh = *reinterpret_cast<const h8v*>(W2w + (kk * 2 + 0) * BLK2 + frag(16 * q + li, g4));
+        const h8v wl = *reinterpret_cast<const h8v*>(W2w + (kk * 2 + 1) * BLK2 + frag(16 * q + li, g4));
         tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, tmp[q], 0, 0, 0);
         tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, tmp[q], 0, 0, 0);
         tmp[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, tmp[q], 0, 0, 0);
@@ -392,8 +401,10 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
 
 template <int C, int NW, int HC, bool FWD, int NH = 1>
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
-  constexpr size_t lds = 2 * ((size_t)NW * (C / 32) * 2 * 16 * 32 + (size_t)NH * (C / 32) * 2 * HC * 32 +
-                              (size_t)NH * (HC / 32) * 2 * C * 32) + 4 * (8 * C + 2 * C);
+  constexpr size_t lds = 2 * ((size_t)NW * (C / 32) * 2 * 16 * 32 + (size_t)NH * (C / 32) * 2 * (HC * 32 + kMlpBlockPad) +
+                              (size_t)NH * (HC / 32) * 2 * (C * 32 + kMlpBlockPad)) + 4 * (8 * C + 2 * C);
+  static_assert(C != 96 || lds <= 163840 / 3, "three dim-96 workgroups per CU");
+  static_assert(lds <= 163840, "LDS");
   if (hipError_t e = set_lds_limit((const void*)k_mlp<C, NW, HC, FWD, NH>, lds)) return e;
   hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD, NH>), dim3(a.M / (16 * NW), 1, a.ngroups), dim3(64 * NW * NH), lds, s, a);
   return hipGetLastError();
