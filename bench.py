@@ -2,10 +2,12 @@
 """Benchmark of the VAE-Var 4D-Var inner loop on MI355X (BASELINE.json metric: inner-loop iterations/s and
 wall-clock to the converged analysis, 69ch 128x256 state).
 
-Workload (default): BASELINE config 2 — 3D-Var with the full VAE decoder (nf_model/parameters0_old.yaml, 216M
-parameters), 69-channel 128x256 state, L-BFGS(history 10, max_iter 10, strong Wolfe) as da_4dvar.py:1240, Nit = 10
-outer passes (the reference's budget: <= 100 iterations), synthetic weights and observations (no checkpoints ship
-with the reference). `--config 3|4|5` selects the other BASELINE configs (Nit 10 / 10 / 5).
+Workload (default, r05): BASELINE config 3 — the metric's own config: 4D-Var with a 2-step window (da_win = 2:
+the full VAE decoder, nf_model/parameters0_old.yaml, 216M parameters, plus one step of the LGUnet flow stand-in in
+the loss, da_4dvar.py:1183-1208), 69-channel 128x256 state, L-BFGS(history 10, max_iter 10, strong Wolfe) as
+da_4dvar.py:1240, Nit = 10 outer passes (the reference's budget: <= 100 iterations), synthetic weights and
+observations (no checkpoints ship with the reference). `--config 2|4|5` selects the other BASELINE configs
+(Nit 10 / 10 / 5); every line carries the others as sub-records (config2 = 3D-Var, the r01-r04 headline).
 
   step   = one converged analysis (one_step_DA 'vae4dvar', da_4dvar.py:1179-1306): z = 0, Nit outer lbfgs.step
            calls, the analysis decode; at N > 1 plus the RCCL gather of every rank's analysis to rank 0
@@ -37,6 +39,7 @@ PEAK_F32_TFLOPS = 157.3    # MI355X exact-f32 MFMA dense peak (MI355X_MICROARCH.
 PEAK_16_TFLOPS = 2500.0    # MI355X bf16 / fp16 MFMA dense peak
 PEAK_SPLIT16_TFLOPS = PEAK_16_TFLOPS / 3  # fp16x3 split: 3 fp16 MFMA products per fp32 product
 PEAK_SPLIT_TFLOPS = PEAK_16_TFLOPS / 6    # bf16x6 split: 6 bf16 MFMA products per fp32 product
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FLOPS_PER_EVAL = {1: 1787.8e9, 2: 3577.0e9, 6: 10733.7e9}  # SURVEY §8 d (input-grad only)
 METRIC = "4D-Var inner-loop iters/sec + wall-clock to convergence, 69ch 128×256 state"
 
@@ -222,7 +225,7 @@ def sc4dvar_line(dev_index: int):
 def gemm_rocprof(key="gemm16_avg_us_per_call"):
     """Average rocprofv3 --kernel-trace --stats duration per fp16x3 GEMM call (main kernel + row scales + split-K
     fixup, tools/rocprof_gemm_summary.py) from the latest committed profile of `bench.py` itself."""
-    for rnd in ("r04", "r03", "r02"):
+    for rnd in ("r05",):  # the profile of this round's default command (config 3); older rounds profiled config 2
         path = os.path.join(ROOT, "profiles", rnd, "gemm_rocprof_summary.json")
         try:
             with open(path) as f:
@@ -235,7 +238,7 @@ def gemm_rocprof(key="gemm16_avg_us_per_call"):
 def gemm_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes of `bench.py` (FETCH_SIZE x2 +
     WRITE_SIZE with the gfx950 corrections, tools/pmc_traffic.py); PMC counters cannot be read live."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05",):
         path = os.path.join(ROOT, "profiles", rnd, "gemm_traffic.json")
         try:
             with open(path) as f:
@@ -245,6 +248,33 @@ def gemm_traffic(kernel):
         except (OSError, KeyError, ValueError, TypeError):
             continue
     return None, None
+
+
+def grid_roofline(prof):
+    """Config 5's HBM roofline (SURVEY §8 d: 2.006 GB of state fields per evaluation at 721x1440, T = 2): the misfit
+    class of an event-profiled analysis (k_misfit_grid, one pass over xb / yo / H / R per slot, and its network-grid
+    adjoint k_misfit_net_bwd) — algorithmic bytes over the summed launch durations, against 8 TB/s — with the
+    rocprofv3 average of k_misfit_grid and its PMC traffic from the committed profile."""
+    pr, secs, evals = prof
+    m = pr["misfit"]
+    ach = m["bytes"] / max(m["ms"] * 1e-3, 1e-12) / 1e9
+    rec = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+           "kernel": "the config-5 state-grid misfit class: k_misfit_grid (x, J partials, the up-sampling adjoint of "
+                     "H(x-yo)/R onto the network grid, the next flow input, in one pass) + k_misfit_net_bwd",
+           "launches": m["launches"], "ms_per_eval": m["ms"] / max(evals, 1),
+           "algorithmic_bytes_per_eval": m["bytes"] / max(evals, 1),
+           "survey_bytes_per_eval": 2.006e9, "evals_profiled": evals,
+           "floor_ms_per_eval_at_peak": 2.006e9 / (PEAK_HBM_GBS * 1e9) * 1e3}
+    for rnd in ("r05",):
+        try:
+            with open(os.path.join(ROOT, "profiles", rnd, "grid_roofline.json")) as f:
+                d = json.load(f)
+            rec["rocprof"] = d.get("rocprof")
+            rec["traffic"] = d.get("traffic_bytes_per_eval")
+            rec["traffic_source"] = f"profiles/{rnd}/grid_roofline.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+        except (OSError, ValueError):
+            rec["traffic"] = None
+    return rec
 
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -291,6 +321,10 @@ class GpuAnalyses:
     def sync(self):
         self.torch.cuda.synchronize()
 
+    def discarded(self):
+        """speculative evaluations the L-BFGS mirror ran and discarded so far (vaevar/lbfgs.py; in the timed region)"""
+        return getattr(self.prob, "n_discarded", 0)
+
     def rebind(self, cfg_id: int):
         """Re-bind this rank to BASELINE config `cfg_id`'s problems (T from CONFIGS, T - 1 flow slots, the same decoder);
         returns the analysis runner (used for the config-3 / 4 / 5 sub-records)."""
@@ -324,6 +358,9 @@ class SelftestAnalyses:
     def sync(self):
         pass
 
+    def discarded(self):
+        return 0
+
     def rebind(self, cfg_id: int):
         return self.analysis
 
@@ -334,6 +371,7 @@ def timed_analyses(w, ensemble, steps, dev):
     w.sync()
     t0 = time.perf_counter()
     c0 = time.process_time()
+    d0 = w.discarded()
     iters = evals = 0
     shapes = None
     for _ in range(steps):
@@ -345,20 +383,24 @@ def timed_analyses(w, ensemble, steps, dev):
     ensemble.barrier()
     el = time.perf_counter() - t0
     cpu = time.process_time() - c0  # host CPU seconds of this rank (all its threads) over the timed region
+    disc = w.discarded() - d0
     return (ensemble.reduce_scalar(el, "max", dev), ensemble.reduce_scalar(iters, "sum", dev),
             ensemble.reduce_scalar(evals, "sum", dev), shapes,
-            (ensemble.reduce_scalar(cpu, "max", dev), ensemble.reduce_scalar(cpu, "sum", dev)))
+            (ensemble.reduce_scalar(cpu, "max", dev), ensemble.reduce_scalar(cpu, "sum", dev)),
+            ensemble.reduce_scalar(disc, "sum", dev))
 
 
-def sub_record(w, cid, ensemble, dev, size, batch):
+def sub_record(w, cid, ensemble, dev, size, batch, profile=False):
     """BASELINE config `cid` on this rank's GPU: a warm-up analysis (graph capture), then one timed analysis per rank
-    with the RCCL gather, max time over ranks (the same timed-region rules as the main line)."""
+    with the RCCL gather, max time over ranks (the same timed-region rules as the main line); with `profile` (rank 0)
+    one more analysis under the HIP-event profiler, outside the timed region."""
     run = w.rebind(cid)
     w.sync()
     run()
     ensemble.barrier()
     w.sync()
     t0 = time.perf_counter()
+    d0 = w.discarded()
     xa, it, ev = run()
     xs = ensemble.gather_analyses(xa)
     w.sync()
@@ -366,11 +408,20 @@ def sub_record(w, cid, ensemble, dev, size, batch):
     t = ensemble.reduce_scalar(time.perf_counter() - t0, "max", dev)
     it = ensemble.reduce_scalar(it, "sum", dev)
     ev = ensemble.reduce_scalar(ev, "sum", dev)
+    disc = ensemble.reduce_scalar(w.discarded() - d0, "sum", dev)
+    prof = None
+    if profile:
+        w.ctx.profile_start()
+        tp = time.perf_counter()
+        _, _, ev_p = run()
+        w.sync()
+        prof = (w.ctx.profile_stop(), time.perf_counter() - tp, ev_p)
     return {"workload": CONFIGS[cid]["name"], "T": CONFIGS[cid]["T"], "n_gpus": size, "analyses_per_gpu": batch,
             "analyses": size * batch, "analyses_per_s": size * batch / t, "iters_per_s": it / t,
             "wall_clock_s": t, "iters": it, "evals": ev, "ms_per_eval": 1e3 * t * size / max(ev, 1),
+            "discarded_speculative_evals": disc,
             "gathered": [list(x.shape) for x in xs] if xs is not None else None,
-            "_prob_np": getattr(w, "prob_np", None),
+            "_prob_np": getattr(w, "prob_np", None), "_prof": prof,
             "timed_region": f"barrier + sync, one config-{cid} analysis per rank, RCCL gather of the analyses to rank 0, "
                             "sync + barrier; max over ranks"}
 
@@ -380,10 +431,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3, help="timed analyses per rank (each = Nit outer L-BFGS passes)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed analyses per rank before the timed ones")
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-evals", type=int, default=None, help="timed CPU closure evaluations (default by config)")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel-class profile")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (T=1, 3D-Var) line section")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (T=2) line section")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (T=6) line section")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (721x1440, T=2) line section")
@@ -411,7 +463,7 @@ def main():
 
     for _ in range(args.warmup):
         w.analysis()
-    t_max, iters, evals, shapes, host_cpu = timed_analyses(w, ensemble, args.steps, dev)
+    t_max, iters, evals, shapes, host_cpu, discarded = timed_analyses(w, ensemble, args.steps, dev)
 
     prof = None
     exact = None
@@ -449,14 +501,16 @@ def main():
         j_0 = w.prob.closure_batch(torch.zeros_like(res["z"]), None)
         j_info = (float(j_0[0][0] + j_0[1][0]), float(j_end[0][0] + j_end[1][0]))
 
-    # BASELINE configs 3 (T = 2), 4 (T = 6) and 5 (721x1440, T = 2) as sub-records of every line, each timed on its own after the main
-    # region (warm-up analysis for the graph capture, then one timed analysis per rank + the gather)
+    # the other BASELINE configs (2: T = 1, 3: T = 2, 4: T = 6, 5: 721x1440, T = 2) as sub-records of every line, each
+    # timed on its own after the main region (warm-up analysis for the graph capture, then one timed analysis per rank
+    # + the gather); config 5 also gets an event-profiled repeat on rank 0 for its HBM roofline (the grid kernels)
     main_prob_np = getattr(w, "prob_np", None)
     subs = {}
-    for cid, skip in ((3, args.no_config3), (4, args.no_config4), (5, args.no_config5)):
+    for cid, skip in ((2, args.no_config2), (3, args.no_config3), (4, args.no_config4), (5, args.no_config5)):
         if skip or args.config == cid:
             continue
-        subs[cid] = sub_record(w, cid, ensemble, dev, size, args.batch)
+        subs[cid] = sub_record(w, cid, ensemble, dev, size, args.batch,
+                               profile=cid == 5 and rank == 0 and not args.selftest and not args.no_profile)
 
     sc4 = None
     if rank == 0 and not args.selftest and not args.no_sc4dvar:
@@ -487,6 +541,7 @@ def main():
         "wall_clock_to_convergence_s": per_analysis,
         "iters": iters,
         "evals": evals,
+        "discarded_speculative_evals": discarded,
         "iters_per_analysis": iters / (size * args.steps * args.batch),
         "evals_per_s": evals / t_max,
         "ms_per_eval": 1e3 * t_max * size / max(evals, 1),
@@ -504,13 +559,21 @@ def main():
     }
     out["headline_config"] = (f"BASELINE config {args.config} (" + {2: "vae4dvar, da_win=1: 3D-Var with the full VAE "
                               "decoder, the da_4dvar_script.sh default window", 3: "vae4dvar, da_win=2: 4D-Var with the "
-                              "flow stand-in", 4: "vae4dvar, da_win=6", 5: "vae4dvar, da_win=2 at 721x1440"}[args.config]
-                              + "); `value` measures this config. The 4D-Var (da_win = 2) figure is `value_4dvar` "
-                              "(the config3 sub-record)")
+                              "flow stand-in, 69ch 128x256: the config the metric names", 4: "vae4dvar, da_win=6",
+                              5: "vae4dvar, da_win=2 at 721x1440"}[args.config]
+                              + "); `value` measures this config. The 3D-Var (da_win = 1) figure is `value_3dvar` "
+                              "(the config2 sub-record, r01-r04's headline)")
+    out["discarded_speculative_evals_note"] = (
+        "evaluations the L-BFGS mirror started speculatively (the line search's first, queued before gtd is known) and "
+        "discarded where the reference stops on gtd > -tolerance_change: not in `evals`, their time is in the timed region")
     if 3 in subs:
         out["value_4dvar"] = subs[3]["iters_per_s"]
     elif args.config == 3:
         out["value_4dvar"] = out["value"]
+    if 2 in subs:
+        out["value_3dvar"] = subs[2]["iters_per_s"]
+    elif args.config == 2:
+        out["value_3dvar"] = out["value"]
     if j_info:
         out["J_start"], out["J_final"] = j_info
     if exact:
@@ -600,12 +663,18 @@ def main():
                 out["cpu_convergence_measured"] = meas
                 out["wall_clock_speedup_vs_cpu_measured"] = meas["wall_clock_s"] / per_analysis
         for cid, rec in subs.items():
-            if CONFIGS[cid]["T"] != 2 or "grid" in CONFIGS[cid] or rec.get("_prob_np") is None:
+            Tc = CONFIGS[cid]["T"]
+            if Tc > 2 or "grid" in CONFIGS[cid] or rec.get("_prob_np") is None:
                 continue
             epi = rec["evals"] / max(rec["iters"], 1)
-            per_eval, cb = cpu_baseline(rec["_prob_np"], 2, epi, rec["evals"] / max(rec["analyses"], 1),
-                                        args.cpu_evals or 2, threads, note)
-            per_eval_T[2] = per_eval
+            per_eval, cb = cpu_baseline(rec["_prob_np"], Tc, epi, rec["evals"] / max(rec["analyses"], 1),
+                                        args.cpu_evals or (3 if Tc == 1 else 2), threads, note)
+            per_eval_T[Tc] = per_eval
+            if cid == 2 and args.batch == 1:
+                meas = cpu_convergence_measured()
+                if meas:
+                    rec["cpu_convergence_measured"] = meas
+                    rec["wall_clock_speedup_vs_cpu_measured"] = meas["wall_clock_s"] / rec["wall_clock_s"] * rec["analyses"]
             rec["cpu_baseline"] = cb
             rec["speedup_vs_cpu"] = rec["iters_per_s"] / cb["value"]
             rec["wall_clock_speedup_vs_cpu"] = (cb["wall_clock_to_convergence_s_extrapolated"] * rec["analyses"]
@@ -642,8 +711,11 @@ def main():
                                              f"5 x {b:.3f} from the two measured oracle closures above (weight grads "
                                              f"on, {threads} threads)"}
             rec["speedup_vs_cpu"] = rec["iters_per_s"] / rec["cpu_baseline"]["value"]
+    if 5 in subs and subs[5].get("_prof") is not None:
+        subs[5]["roofline_hbm"] = grid_roofline(subs[5]["_prof"])
     for rec in subs.values():
         rec.pop("_prob_np", None)
+        rec.pop("_prof", None)
     print(json.dumps(out), flush=True)
     ensemble.barrier()
 

@@ -168,7 +168,10 @@ int vv_obs_augment(vv_ctx* ctx, const float* interp, int n_out, int n_in, const 
    pred, gt (B,C,H,W); mean, std_ (C) fp32; scale (C) fp64; wrmse, bias (C) fp64 device. Synchronises `stream`. */
 int vv_metrics(vv_ctx* ctx, const float* pred, const float* gt, const float* mean, const float* std_,
                const double* scale, int B, int C, int H, int W, double* wrmse, double* bias, void* stream);
-/* trajectories x_t (B,T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only) */
+/* trajectories x_t (B,T,C,Hs,Ws) of the last closure / forward evaluation (device pointer, read-only). On an
+   interpolated state grid with the one-pass misfit ("grid_fused", config 5) a gradient closure does not store x_t (the
+   state fields are read once and nothing is written at the state grid); a J-only evaluation (cal_loss, vv_closure with
+   grad_z = NULL) does, so the per-outer-pass logging of da_4dvar.py:1256-1262 sees the pass's x_t. */
 int vv_state_ptr(vv_ctx* ctx, const float** x);
 
 /* vector primitives (n floats). Host-returning ones synchronise `stream`. */
@@ -183,7 +186,9 @@ int vv_absmax(vv_ctx* ctx, const float* a, int64_t n, float* out, void* stream);
 int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
                     const double* dev_extra, int n_extra, double* out, void* stream);
 /* The same reductions queued without a host round trip: the results stay in the caller's device doubles dev_out[count]
-   (absmax widened exactly), to be fetched later as another call's dev_extra. */
+   (absmax widened exactly), to be fetched later as another call's dev_extra. The partial sums live in the context's
+   reduction scratch, which vv_reduce_batch and the next vv_reduce_enqueue reuse: every such call of one context must
+   go to the same stream (calls on two streams race on that scratch). */
 int vv_reduce_enqueue(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
                       double* dev_out, void* stream);
 int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream);
@@ -247,8 +252,14 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
    (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
    launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
-   inverse window map, 1). Results stay fp32-level for every value; a change drops the
-   context's captured closure graphs. Unknown key: VV_E_ARG. */
+   inverse window map, 1), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
+   the misfit reads each state field once per evaluation and its adjoint runs on the network grid, k_misfit_grid /
+   k_misfit_net_bwd; read by vv_bind_problem, 1), "mlp_w" (the fused Swin-tower MLP with its hidden layer split over
+   the four waves of a 64-token workgroup, per-wave LDS-DMA weight rings and one u scale per token, k_mlpw: bit 0 at
+   dim 96, bit 1 at dim 192, 2). Results stay fp32-level for every value; a change drops the
+   context's captured closure graphs. Unknown key, or a value the dispatch does not accept (switches 0 / 1; "mlp_hc"
+   0, 2, 32, 64; "h5_var" 0..5; "gattn_qf" 1, 2; "fuse_mlp" and "mlp_w" 0..3; "fuse_attn" 0..15; the k-tile floors >= 1; the
+   minimum K >= 0): VV_E_ARG, and the knob keeps its value. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);
 /* process-wide debug aid: synchronise after every library launch and report the first failing op (default 0) */
@@ -274,6 +285,14 @@ int vv_attention_global(vv_ctx* ctx, const float* qkv, float* out, int N, int C,
    runs tile 34. */
 int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
             int tile, void* stream);
+/* vv_gemm with the Mlp epilogues of the engine (kernel tests): epi 0 store; 1 GELU: C = gelu(acc + bias) and, when aux
+   is not null, aux = acc + bias (the fc1 forward, swinblock.py:23-29); 3 GELU': C = acc * gelu'(aux) (the fc1 input
+   gradient). Other epi values: VV_E_ARG. */
+int vv_gemm_epi(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
+                float* aux, int epi, int tile, void* stream);
+/* y = GELU(x), dy = GELU'(x) (nn.GELU(), exact erf form) by the device functions of every GEMM / fused-MLP epilogue
+   (vv_gelu.h): form 0 the one-value forms, 1 the four-value interleaved forms (kernel tests). */
+int vv_gelu_eval(vv_ctx* ctx, const float* x, float* y, float* dy, int64_t n, int form, void* stream);
 
 #ifdef __cplusplus
 }

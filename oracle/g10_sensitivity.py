@@ -69,13 +69,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--case", default="g10", choices=["g10", "g13", "g15", "g16"])
+    ap.add_argument("--part", default="both", choices=["both", "free", "replay"],
+                    help="free: run only the free-running trajectory and keep its J per pass in oracle/_ref/ (it needs "
+                         "no golden, so it can run beside make_golden.py); replay: read that file, run the replay and "
+                         "write the sensitivity fixture")
     a = ap.parse_args()
     T, Hs, Ws, nit, fx = {"g10": (1, 128, 256, 10, "g10_config2_trajectory.npz"),
                           "g13": (2, 128, 256, 10, "g13_config3_trajectory.npz"),
                           "g15": (2, 721, 1440, 5, "g15_config5_trajectory.npz"),
-                          "g16": (6, 128, 256, 3, "g16_config4_trajectory.npz")}[a.case]
-    g = np.load(os.path.join(GOLD, fx))
-    Jr = g["J"].sum(1)
+                          "g16": (6, 128, 256, 10, "g16_config4_trajectory.npz")}[a.case]
+    raw = os.path.join(HERE, "_ref", f"{a.case}_free_J_t{a.threads}.npy")
     torch.set_num_threads(a.threads)
     cwd = os.getcwd()
     tr, _ = ref_harness.import_reference()
@@ -87,9 +90,21 @@ def main():
     prob = make_problem(nch=69, Hs=Hs, Ws=Ws, T=T, seed=20250620)
     rp = RefProblem(prob, m, C.DECODER["img_size"], fm) if fm is not None else RefProblem(prob, m, C.DECODER["img_size"])
     t0 = time.time()
-    _, _, js, _, _ = one_step_da_ref(rp, nit, (32, 128, 256))
-    free = np.abs(np.array(js).sum(1) - Jr) / np.abs(Jr)
-    print(f"free-running, {a.threads} threads ({time.time() - t0:.0f}s): J rel per pass {free.tolist()}", flush=True)
+    if a.part == "replay":
+        jf = np.load(raw)
+    else:
+        _, _, js, _, _ = one_step_da_ref(rp, nit, (32, 128, 256))
+        jf = np.array(js).sum(1)
+        os.makedirs(os.path.dirname(raw), exist_ok=True)
+        np.save(raw, jf)
+        print(f"free-running, {a.threads} threads ({time.time() - t0:.0f}s): J per pass {jf.tolist()}", flush=True)
+        if a.part == "free":
+            return
+    g = np.load(os.path.join(GOLD, fx))
+    assert int(g["nit"]) == nit if "nit" in g else True, "golden and sensitivity budgets differ"
+    Jr = g["J"].sum(1)
+    free = np.abs(jf - Jr) / np.abs(Jr)
+    print(f"free-running, {a.threads} threads: J rel per pass {free.tolist()}", flush=True)
 
     # fixed-step replay of G10's line searches through the product's L-BFGS mirror
     z = torch.zeros(1, 32, 128, 256)

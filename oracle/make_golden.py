@@ -26,7 +26,7 @@ are stored):
   g15_config5_trajectory.npz  G15 (--g15, ~25 min): the genuine one_step_DA at 721x1440, T=2, Nit=5 (config 5's
                         budget): J per pass, line-search steps, sampled xa
   g16_config4_trajectory.npz  G16 (--g16, ~20 min): config 4 (T=6, decoder + flow stand-in) with torch.optim.LBFGS,
-                        Nit 3 at 128x256: J per pass, line-search steps, sampled xa
+                        Nit 10 at 128x256: J per pass, line-search steps, sampled xa
   g13_config3_trajectory.npz  G13 (--g13, ~30 min): config 3 (T=2, decoder + flow stand-in) with torch.optim.LBFGS,
                         Nit 10 at 128x256: J per pass, line-search steps, sampled xa
   g3_full_decoder.npz   G3 (--full): full parameters0_old decoder @128x256: sampled out/grad + sums,
@@ -683,9 +683,9 @@ def g14(tr):
 def g16(tr):
     """G16 (BASELINE config 4 at full size): the reference's networks_old.LGUnet_all decoder and the flow stand-in in
     the restated 4D-Var closure with T = 6 (five integrate steps, da_4dvar.py:1183-1208, :666-681),
-    torch.optim.LBFGS(history 10, max_iter 10, strong Wolfe), Nit = 3 outer passes at 128x256, seed 20250620 (the
-    bench's config-4 rank-0 analysis): J per pass, every line search's (t, evals), sampled xa. Parameters frozen as
-    in G10/G13 (the unused weight gradients only cost time)."""
+    torch.optim.LBFGS(history 10, max_iter 10, strong Wolfe), Nit = G16_NIT outer passes at 128x256 (r05: 10, the
+    bench's full budget; r04: 3), seed 20250620 (the bench's config-4 rank-0 analysis): J per pass, every line search's
+    (t, evals), sampled xa. Parameters frozen as in G10/G13 (the unused weight gradients only cost time)."""
     m, _ = build_ref(tr, C.DECODER)
     fm, _ = build_ref(tr, {k: v for k, v in C.FLOW.items() if k != "arch"})
     for v in list(m.parameters()) + list(fm.parameters()):
@@ -707,7 +707,7 @@ def g16(tr):
              dxa_sumsq=((flat - prob["xb"].reshape(-1).astype(np.float64)) ** 2).sum())
 
 
-G16_NIT = 3
+G16_NIT = int(os.environ.get("G16_NIT", "10"))
 
 
 def g11():
@@ -775,10 +775,10 @@ def main():
     ap.add_argument("--g11", action="store_true", help="also generate G11 (0.25-deg LGUnet_all_1 forward, ~3 min)")
     ap.add_argument("--g13", action="store_true", help="also generate G13 (config-3 T=2 trajectory, Nit 10, ~30 min)")
     ap.add_argument("--g15", action="store_true", help="also generate G15 (genuine one_step_DA, config 5, Nit 5, ~25 min)")
-    ap.add_argument("--g16", action="store_true", help="also generate G16 (config-4 T=6 trajectory, Nit 3, ~20 min)")
+    ap.add_argument("--g16", action="store_true", help="also generate G16 (config-4 T=6 trajectory, Nit 10, ~4 h on 8 threads)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
-    torch.set_num_threads(8)
+    torch.set_num_threads(int(os.environ.get("ORACLE_THREADS", "8")))
     cwd = os.getcwd()
     tr, sb = ref_harness.import_reference()
     os.chdir(cwd)

@@ -33,7 +33,8 @@ def test_bench_spawns_its_ranks():
     assert out["iters"] == 2 * (97 + 98) and out["evals"] == 2 * (110 + 111)
     assert out["gathered"] == [[69, 128, 256], [69, 128, 256]]
     assert out["value"] == out["iters"] / (out["ms_per_step"] * 1e-3 * out["steps"])
-    for cid in (3, 4, 5):  # every BASELINE config other than the main one is a sub-record of the line
+    assert out["config"]["T"] == 2  # the default workload is config 3, the metric's 4D-Var config (r05)
+    for cid in (2, 4, 5):  # every BASELINE config other than the main one is a sub-record of the line
         c = out[f"config{cid}"]
         assert c["n_gpus"] == 2 and c["gathered"] == [[69, 128, 256], [69, 128, 256]] and c["iters"] == 97 + 98
     for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
@@ -69,13 +70,14 @@ def test_bench_world_size_must_match():
 
 @pytest.mark.gpu
 def test_bench_two_ranks_product_path():
-    """The product path with two ranks: `bench.py --gpus 2` spawns two processes that each run a full config-2
-    analysis on libvaevar (here both on the box's one GPU, over gloo since RCCL refuses two ranks per device), gather
-    both analyses to rank 0, take the max time and sum the iterations."""
+    """The product path with two ranks: `bench.py --gpus 2` spawns two processes that each run a full config-3
+    analysis (the default workload: T = 2) on libvaevar (here both on the box's one GPU, over gloo since RCCL refuses
+    two ranks per device), gather both analyses to rank 0, take the max time and sum the iterations (G13: J falls to
+    0.41 of its start over the budget)."""
     p = _run("--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-profile", "--no-exact-f32",
-             "--no-config4", "--no-config5", "--no-sc4dvar", env={"VAEVAR_DIST_BACKEND": "gloo"})
+             "--no-config2", "--no-config4", "--no-config5", "--no-sc4dvar", env={"VAEVAR_DIST_BACKEND": "gloo"})
     assert p.returncode == 0, p.stderr[-3000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     print({k: out[k] for k in ("n_gpus", "iters", "evals", "value", "gathered", "J_start", "J_final")})
     assert out["n_gpus"] == 2 and out["gathered"] == [[69, 128, 256], [69, 128, 256]]
-    assert 150 <= out["iters"] <= 200 and out["J_final"] < 0.1 * out["J_start"]
+    assert 150 <= out["iters"] <= 200 and out["J_final"] < 0.5 * out["J_start"]

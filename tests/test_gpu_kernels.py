@@ -1,5 +1,7 @@
 """Kernel-level numerics on the GPU: the MFMA GEMM and the vector primitives against fp32/fp64
 torch CPU references (tolerances written per test)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -107,12 +109,19 @@ def test_tuning_knobs_per_context():
     c1, c2 = Context(0), Context(0)
     for k in Context.TUNING_KEYS:
         v = c1.get_tuning(k)
-        c1.set_tuning(k, v + 1)
-        assert c1.get_tuning(k) == v + 1
+        alt = {"mlp_hc": 32 if v != 32 else 64, "h5_var": 5 if v != 5 else 4, "gattn_qf": 3 - v,
+               "fuse_mlp": (v + 1) % 4, "fuse_attn": (v + 1) % 16}.get(k, v + 1 if v > 1 or "mink" in k else 1 - v)
+        c1.set_tuning(k, alt)
+        assert c1.get_tuning(k) == alt
         assert c2.get_tuning(k) == v
         c1.set_tuning(k, v)
     with pytest.raises(VVError):
         c1.set_tuning("no_such_knob", 1)
+    # values the dispatch does not accept are refused at vv_set_tuning, not inside a later closure
+    for k, bad in (("mlp_hc", 48), ("h5_var", 6), ("grid_fused", 2), ("gattn_qf", 0), ("tail_minkt", 0)):
+        with pytest.raises(VVError):
+            c1.set_tuning(k, bad)
+        assert c1.get_tuning(k) != bad
     M, N, K = 2048, 3456, 1152
     g = torch.Generator().manual_seed(99)
     A = (torch.rand(M, K, generator=g) * 2 - 1).cuda()
@@ -325,3 +334,66 @@ def test_resample_nearest_matches_interpolate(ctx, src, dst):
     torch.nn.functional.interpolate(xr, dst).backward(cot)
     assert float((xd.grad.cpu() - xr.grad).abs().max()) <= 1e-5 * float(xr.grad.abs().max())
 
+
+
+def _gelu_ref64(x):
+    """nn.GELU() (exact erf form, swinblock.py:13-29) and its derivative in float64."""
+    x = x.double()
+    cdf = 0.5 * (1.0 + torch.special.erf(x / math.sqrt(2.0)))
+    pdf = torch.exp(-0.5 * x * x) / math.sqrt(2.0 * math.pi)
+    return x * cdf, cdf + x * pdf
+
+
+@pytest.mark.parametrize("form", [0, 1])
+def test_gelu_device_dense_grid(ctx, form):
+    """The branch-free GELU / GELU' of every epilogue (vv_gelu.h: the fitted exp2 form of Phi, v_exp_f32 on the device)
+    over 2^21 + 1 points of [-10, 10] and the fitted range's edges, against float64 erf: GELU within 2e-7 max(|x|, 1),
+    GELU' within 2e-7 absolute (the verdict's bound; the fit's float32 emulation claims 8.7e-8 |x| / 8.2e-8). Form 0:
+    gelu_fast / dgelu_fast (GEMM epilogues), 1: gelu4 / dgelu4 (fused MLP, tile-49 row epilogue). Also +-inf and NaN."""
+    xs = torch.linspace(-10.0, 10.0, 2 ** 21 + 1, dtype=torch.float32)
+    edge = torch.tensor([0.0, -0.0, 5.75, -5.75, 5.7499995, -5.7500005, 1e-30, -1e-30, 29.9, 30.5, -31.0, 1e4, -1e4],
+                        dtype=torch.float32)
+    x = torch.cat([xs, edge]).cuda()
+    y, dy = ctx.gelu_eval(x, form)
+    torch.cuda.synchronize()
+    yr, dyr = _gelu_ref64(x.cpu())
+    ey = float(((y.cpu().double() - yr).abs() / x.cpu().double().abs().clamp(min=1.0)).max())
+    ed = float((dy.cpu().double() - dyr).abs().max())
+    print(f"GELU form {form}: max err / max(|x|,1) {ey:.2e}, GELU' max abs err {ed:.2e}")
+    assert ey <= 2e-7 and ed <= 2e-7
+    sp = torch.tensor([float("inf"), float("-inf"), float("nan")], device="cuda")
+    y, dy = ctx.gelu_eval(sp, form)
+    y, dy = y.cpu(), dy.cpu()
+    assert y[0] == float("inf") and abs(float(y[1])) < 2e-7 and torch.isnan(y[2])
+    assert dy[0] == 1.0 and abs(float(dy[1])) < 2e-7 and torch.isnan(dy[2])
+
+
+@pytest.mark.parametrize("tile", [0, 24, 36, 48])
+def test_gelu_gemm_epilogues_identity(ctx, tile):
+    """The GELU / GELU' GEMM epilogues (EPI_GELU: C = gelu(acc + bias), aux = acc + bias; EPI_DGELU: C = acc *
+    gelu'(aux)) through identity-B GEMMs over 1,048,576 points of [-10, 10]: GELU of the stored pre-activation within
+    2e-7 max(|x|, 1) of float64 erf, the pre-activation bit-identical to the EPI_STORE GEMM of the same tile, and with
+    A = 1 (acc = 1 exactly) GELU' of aux within 2e-7."""
+    from vaevar.engine import Context
+
+    c = Context(0)
+    c.gemm_math = "f32" if tile in (0,) else ("split" if tile == 24 else "split16")
+    n = 1024
+    eye = torch.eye(n, device="cuda")
+    c.gemm_register_weight(eye)
+    x = torch.linspace(-10.0, 10.0, n * n, dtype=torch.float32).reshape(n, n)
+    x = x[torch.randperm(n, generator=torch.Generator().manual_seed(5))].cuda()  # rows mix magnitudes
+    pre = c.gemm(x, eye, tile=tile)
+    aux = torch.empty_like(pre)
+    yg = c.gemm_epi(x, eye, "gelu", aux=aux, tile=tile)
+    ones = torch.ones(n, n, device="cuda")
+    yd = c.gemm_epi(ones, eye, "dgelu", aux=x, tile=tile)
+    torch.cuda.synchronize()
+    assert torch.equal(aux, pre)
+    yr, _ = _gelu_ref64(pre.cpu())
+    _, dyr = _gelu_ref64(x.cpu())
+    ey = float(((yg.cpu().double() - yr).abs() / pre.cpu().double().abs().clamp(min=1.0)).max())
+    ed = float((yd.cpu().double() - dyr).abs().max())
+    print(f"tile {tile}: GELU epilogue {ey:.2e} (pre-activation vs x {float((pre - x).abs().max()):.1e}), "
+          f"GELU' epilogue {ed:.2e}")
+    assert ey <= 2e-7 and ed <= 2e-7

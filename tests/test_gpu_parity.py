@@ -245,9 +245,12 @@ def test_oracle_on_box_tiny_adam():
     assert e < 1e-4
 
 
-def test_interpolated_grid_4dvar():
-    """State grid 45x90 != network grid 32x64 (non-integer ratio, like 721x1440 vs 128x256): decoder_hr
-    up-sampling, integrate down/up-sampling and their adjoints, T=2, against the oracle restatement."""
+@pytest.mark.parametrize("Hs,Ws,T", [(45, 90, 2), (45, 92, 2), (47, 100, 3)])
+def test_interpolated_grid_4dvar(Hs, Ws, T):
+    """State grid Hs x Ws != network grid 32x64 (non-integer ratio, like 721x1440 vs 128x256): decoder_hr
+    up-sampling, integrate down/up-sampling and their adjoints, against the oracle restatement. 45x90 runs the
+    per-element misfit kernels (Ws % 4 != 0); 45x92 (T = 2) and 47x100 (T = 3: the flow-input adjoint chained over
+    two flow steps) the one-pass k_misfit_grid + network-grid adjoint (grid_fused)."""
     from oracle.da_ref import oracle_problem
     from oracle.lgunet_ref import synth_params
     from vaevar import config as C
@@ -255,9 +258,9 @@ def test_interpolated_grid_4dvar():
     from vaevar.problem import make_problem
     from vaevar.synth import smooth_field
 
-    p = make_problem(nch=4, Hs=45, Ws=90, T=2, seed=778, obs_frac=0.2)
+    p = make_problem(nch=4, Hs=Hs, Ws=Ws, T=T, seed=778, obs_frac=0.2)
     dec = LGUnet(C.TINY, 1, 1).load_synthetic()
-    flow = LGUnet(C.TINY_FLOW, 1, 1).load_synthetic()
+    flow = LGUnet(C.TINY_FLOW, 1, T - 1).load_synthetic()
     prob = DAProblem(dec, p, flow=flow)
     z = torch.from_numpy(0.3 * smooth_field(304, (1, 4, 32, 64), sigma=2.0))
     g = torch.empty(1, 4, 32, 64, device="cuda")
@@ -271,8 +274,45 @@ def test_interpolated_grid_4dvar():
     xa = prob.analysis(z.cuda()).cpu().numpy()
     with torch.no_grad():
         e_x = rel(xa, ro.analysis(z).numpy())
-    print(f"interpolated grid T=2: J_o rel {e_j:.2e} grad rel {e_g:.2e} xa rel {e_x:.2e}")
-    assert e_j < 1e-5 and e_g < 1e-5 and e_x < 1e-6
+    # a J-only evaluation keeps the trajectory (the logging pass reads it) on either path
+    prob.closure(z.cuda(), None)
+    with torch.no_grad():
+        xr = ro.trajectory(z)
+    e_t = max(rel(prob.trajectory()[t].cpu(), xr[t]) for t in range(T))
+    print(f"interpolated grid {Hs}x{Ws} T={T}: J_o rel {e_j:.2e} grad rel {e_g:.2e} xa rel {e_x:.2e} x_t rel {e_t:.2e}")
+    assert e_j < 1e-5 and e_g < 1e-5 and e_x < 1e-6 and e_t < 1e-5
+
+
+def test_config5_grid_fused_vs_unfused():
+    """Config 5's state grid (69ch 721x1440, T = 2: decoder + one flow step): the one-pass misfit (grid_fused 1:
+    k_misfit_grid, the adjoint on the network grid) against the per-element kernels (grid_fused 0: k_misfit_fwd,
+    k_flow_input, k_misfit_bwd_gather, k_flow_input_adj) on the same problem — only the summation order of the
+    up-sampling adjoint differs — and the J-only evaluation's trajectory."""
+    from vaevar import config as C
+    from vaevar.engine import DAProblem, LGUnet
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field
+
+    p = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250621)
+    dec = LGUnet(C.DECODER, 1, 1).load_synthetic()
+    flow = LGUnet(C.FLOW, 1, 1).load_synthetic()
+    z = torch.from_numpy(0.3 * smooth_field(405, (1, 32, 128, 256))).cuda()
+    out = {}
+    for gf in (0, 1):
+        dec.ctx.set_tuning("grid_fused", gf)
+        prob = DAProblem(dec, p, flow=flow)
+        g = torch.empty(1, 32, 128, 256, device="cuda")
+        jb, jo = prob.closure(z, g)
+        jb2, jo2 = prob.closure(z, None)
+        out[gf] = (jo, g.cpu(), jo2, prob.trajectory().cpu())
+        del prob
+    dec.ctx.set_tuning("grid_fused", 1)
+    e_j = abs(out[1][0] - out[0][0]) / abs(out[0][0])
+    e_g = rel(out[1][1], out[0][1])
+    e_t = rel(out[1][3], out[0][3])
+    print(f"config-5 grid fused vs unfused: J_o {e_j:.2e} grad {e_g:.2e} J-only J_o {out[1][2]:.6e} vs "
+          f"{out[0][2]:.6e}, x_t {e_t:.2e}")
+    assert e_j < 1e-6 and e_g < 1e-5 and out[1][2] == out[1][0] and e_t == 0.0
 
 
 def test_config5_grid_closure():
@@ -586,7 +626,7 @@ def test_ln_row_scales_bitwise(tmp_path):
 
 @pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_mlp", 3), ("fuse_attn", 1), ("fuse_attn", 3),
                                      ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2),
-                                     ("fuse_attn", 12)])
+                                     ("fuse_attn", 12), ("mlp_w", 2), ("mlp_w", 1), ("mlp_w", 3)])
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient; 1 at dim 96, 3 also at dim 192) and fuse_attn (LN1 + qkv +
@@ -594,7 +634,9 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and backward on the exact-f32 MFMA instead of
     the VALU kernels: fp32 products either way, only the summation order differs); mlp_hc 64 (the dim-192 fused MLP
     in 64-unit hidden chunks, or 2: its hidden layer split over two waves per 16 tokens -- the hidden operand's
-    per-(token, chunk) scales and the order of the chunk sums change). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
+    per-(token, chunk) scales and the order of the chunk sums change); mlp_w (r05: the fused MLP as k_mlpw, the hidden
+    layer split over the waves with one bound-derived u scale per token, against r04's k_mlp; 2 at dim 192, 1 at
+    dim 96, 3 both; the mlp_hc cases run with mlp_w 0, the kernel they select). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
     per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
     max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
     from vaevar.engine import DAProblem
@@ -607,6 +649,9 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     zc = torch.from_numpy(0.3 * smooth_field(403, (1, 32, 128, 256))).cuda()
     res = []
     default = full_dec.ctx.get_tuning(knob)
+    w_default = full_dec.ctx.get_tuning("mlp_w")
+    if knob == "mlp_hc":
+        full_dec.ctx.set_tuning("mlp_w", 0)
     try:
         for v in (0, on):
             full_dec.ctx.set_tuning(knob, v)
@@ -618,6 +663,7 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning(knob, default)
+        full_dec.ctx.set_tuning("mlp_w", w_default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     e_o, e_d, e_g = rel(o1.cpu(), o0.cpu()), rel(d1.cpu(), d0.cpu()), rel(g1.cpu(), g0.cpu())
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
@@ -659,6 +705,7 @@ def test_bitwise_knobs(full_dec, knob, ref, on):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning(knob, default)
+        full_dec.ctx.set_tuning("mlp_w", w_default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     print(f"{knob}: k_gather_scales passes {gathers[0]} -> {gathers[1]}")
     assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1)

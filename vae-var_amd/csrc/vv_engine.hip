@@ -92,6 +92,15 @@ int parse_cfg(const vv_lgunet_config* c, Cfg& o) {
     o.Cin += c->inchans[g];
     o.Cout += c->outchans[g];
   }
+  // the PatchEmbed / ConvTranspose2d MFMA kernels (vv_ops.hip k_p2t_mf / k_t2p_mf, patch_check) take 16 tokens of
+  // one image row per wave, at most kPatchCmax token channels and kPatchKmax = 4 x 28 taps per token: refused here
+  // with a message instead of a failing first closure
+  if (o.W0 % 16) return fail(VV_E_ARG, "img_size[1] / 2 = %d must be a multiple of 16 (patch kernels)", o.W0);
+  if (o.C0 > 128) return fail(VV_E_ARG, "enc_dim %d > 128 (patch kernels)", o.C0);
+  for (int g = 0; g < o.G; ++g)
+    if (c->inchans[g] < 1 || c->inchans[g] > 28 || c->outchans[g] < 1 || c->outchans[g] > 28)
+      return fail(VV_E_ARG, "group %d: inchans %d / outchans %d outside 1..28 (patch kernels)", g, c->inchans[g],
+                  c->outchans[g]);
   o.lg_depth.assign(c->lg_depths, c->lg_depths + c->n_lg_layers);
   o.lg_heads.assign(c->lg_heads, c->lg_heads + c->n_lg_layers);
   for (int l = 0; l < c->n_lg_layers; ++l)
@@ -265,6 +274,12 @@ struct Problem {
   int *mi = nullptr, *mj = nullptr;    // state -> net (decoder_hr / integrate up-sampling)
   int *ri0 = nullptr, *rj0 = nullptr;  // net -> first state row/col mapping onto it (adjoint ranges)
   int *di = nullptr, *dj = nullptr;    // net -> state (integrate down-sampling)
+  // grid_fused (interpolated grids with Hs >= Hl, Ws >= Wl, synthetic observations): the misfit reads each state
+  // field once per evaluation (k_misfit_grid) and its adjoint runs on the network grid (k_misfit_net_bwd)
+  bool grid_fused = false;
+  int *rowinv = nullptr, *colinv = nullptr;  // [Hs] / [Ws]: inverse of di / dj, -1 off the sampled rows / columns
+  int *cr0 = nullptr, *cc0 = nullptr;        // [Hl+1] / [Wl+1]: ranges of mi[di[.]] / mj[dj[.]]
+  float* GON = nullptr;                      // (B,T,C,Hl,Wl): coeff * Up^T(H (x_t - yo_t) / R_t)
   const float *xb, *yo, *Hm, *R, *mean, *std_, *std_tr;
   float obs_coeff = 1.f;
   std::unique_ptr<Arena> arena;
@@ -611,6 +626,7 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
   ma.ngroups = S.G;
   ma.eps = 1e-5f;
   ma.hc = T.mlp_hc;
+  ma.w = T.mlp_w;
   for (int g = 0; g < S.G; ++g) {
     const auto& w = S.w[b][g];
     vv::MlpGroup& G = ma.g[g];
@@ -622,12 +638,15 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
       G.beta = w.n2b;
       vv::fp16_planes_of(w.fc1W, C, &G.w1h, &G.w1s);
       vv::fp16_planes_of(w.fc2W, 4 * C, &G.w2h, &G.w2s);
+      G.wmax = w.fc1Wmax;
+      G.bmax = w.fc1bmax;
       G.b1 = w.fc1b;
       G.b2 = w.fc2b;
       G.out = sv.x[b + 1] + g * MC;
     } else {
       vv::fp16_planes_of(w.fc2WT, C, &G.w1h, &G.w1s);
       vv::fp16_planes_of(w.fc1WT, 4 * C, &G.w2h, &G.w2s);
+      G.wmax = w.fc2Wmax;
       G.dy = gx + g * MC;
       G.out = gx + g * MC;
       G.rs = sc.rs + (size_t)g * M;
@@ -1391,6 +1410,8 @@ void set_maps(const Problem& P, MisfitArgs& m) {
   m.Wl = P.Wl;
   m.mi = P.interp ? P.mi : nullptr;
   m.mj = P.interp ? P.mj : nullptr;
+  m.ri0 = P.interp ? P.ri0 : nullptr;
+  m.rj0 = P.interp ? P.rj0 : nullptr;
 }
 
 // B analyses per evaluation (the decoder's batch): one decoder launch sequence over all B, one flow launch
@@ -1409,6 +1430,9 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   auto part = [&](int b, int t) { return P.partial + ((size_t)b * (T + 1) + t) * P.nblk; };
   auto X = [&](int b, int t) { return P.X + ((size_t)b * T + t) * CHW; };
   auto FI = [&](int t, int b) { return P.FI + ((size_t)t * B + b) * CHWl; };
+  // one pass over the state fields per slot (interpolated grids, synthetic observations): k_misfit_grid
+  const bool gf = P.grid_fused && !P.nout;
+  auto GON = [&](int b, int t) { return P.GON + ((size_t)b * T + t) * CHWl; };
   int r;
   // forward: x_0 = decoder(z)*stdTr*std + xb
   if ((r = model_fwd(D, 0, z, P.dec_out, C, st))) return r;
@@ -1423,6 +1447,11 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
   ma.mean = P.mean;
   ma.std_ = P.std_;
   ma.nblk = P.nblk;
+  if (gf) {
+    ma.rowinv = P.rowinv;
+    ma.colinv = P.colinv;
+    ma.coeff = P.obs_coeff;
+  }
   for (int b = 0; b < B; ++b) {
     MisfitArgs m0 = ma;
     m0.net = P.dec_out + b * DO;
@@ -1433,6 +1462,12 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     m0.x_out = X(b, 0);
     m0.flow_in = T > 1 ? FI(0, b) : nullptr;
     m0.partial = part(b, 0);
+    if (gf) {
+      m0.x_out = grad ? nullptr : X(b, 0);  // the state is kept for J-only (logging) evaluations only
+      m0.g_net_obs = grad ? GON(b, 0) : nullptr;
+      CK(misfit_grid_fwd(m0, st));
+      continue;
+    }
     CK(misfit_fwd(m0, st));
     CK(obs_term(P, b, 0, st));
     if (T > 1 && P.interp)
@@ -1454,6 +1489,12 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
       mt.x_out = X(b, t);
       mt.flow_in = t < T - 1 ? FI(t, b) : nullptr;
       mt.partial = part(b, t);
+      if (gf) {
+        mt.x_out = grad ? nullptr : X(b, t);
+        mt.g_net_obs = grad ? GON(b, t) : nullptr;
+        CK(misfit_grid_fwd(mt, st));
+        continue;
+      }
       CK(misfit_fwd(mt, st));
       CK(obs_term(P, b, t, st));
       if (t < T - 1 && P.interp)
@@ -1466,6 +1507,29 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     CK(reduce_final(part(b, T), P.nblk, P.dJ + 2 * b, st));
   }
   if (!grad) return 0;
+  if (gf) {
+    // backward on the network grid: g_net = (g_net_obs[t] + the flow-input adjoint of step t + 1) * scale
+    MisfitNetBwdArgs nb;
+    memset(&nb, 0, sizeof(nb));
+    nb.C = C;
+    nb.Hl = P.Hl;
+    nb.Wl = P.Wl;
+    nb.cr0 = P.cr0;
+    nb.cc0 = P.cc0;
+    nb.std_ = P.std_;
+    for (int t = T - 1; t >= 0; --t) {
+      for (int b = 0; b < B; ++b) {
+        MisfitNetBwdArgs n = nb;
+        n.g_net_obs = GON(b, t);
+        n.gfi = t < T - 1 ? P.GFI + b * CHWl : nullptr;
+        n.scale = t ? P.std_ : P.prod;
+        n.g_net = t ? P.GFO + b * FO : P.gdec + b * DO;
+        CK(misfit_net_bwd(n, st));
+      }
+      if (t && (r = model_bwd(*F, t - 1, P.GFO, P.GFI, nullptr, C, st))) return r;
+    }
+    return model_bwd(D, 0, P.gdec, grad, z, C, st);
+  }
   // backward
   MisfitBwdArgs mb0;
   memset(&mb0, 0, sizeof(mb0));
@@ -1958,6 +2022,13 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
   P.Hl = D->cfg.Himg;
   P.Wl = D->cfg.Wimg;
   P.interp = (Hs != P.Hl || Ws != P.Wl);
+  {
+    bool aligned = true;
+    for (const void* p : {(const void*)xb, (const void*)yo, (const void*)Hmask, (const void*)R})
+      aligned = aligned && !(reinterpret_cast<uintptr_t>(p) & 15);
+    P.grid_fused = P.interp && ctx->tune.grid_fused && Hs >= P.Hl && Ws >= P.Wl && Ws % 4 == 0 && Ws <= 16384 && aligned;
+    if (P.grid_fused) P.nblk = C * P.Hl;  // one J partial per (channel, network row) workgroup of k_misfit_grid
+  }
   const size_t CHW = (size_t)C * Hs * Ws;
   const size_t HWl = (size_t)P.Hl * P.Wl;
   const size_t CHWl = (size_t)C * HWl;
@@ -1974,22 +2045,27 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     P.FO = pl.f(B * fcout * HWl * std::max(T - 1, 1) + 1);
     P.GFO = pl.f(B * fcout * HWl + 1);
     P.GFI = pl.f(B * CHWl);
-    P.carry = pl.f(B * CHW);
+    P.carry = pl.f(P.grid_fused ? 1 : B * CHW);
+    P.GON = P.grid_fused ? pl.f(B * CHWl * T) : nullptr;
     P.zn = B * D->cfg.Cin * D->cfg.Himg * D->cfg.Wimg;
     P.Z = pl.f(P.zn);
     P.GZ = pl.f(P.zn);
-    float* maps = pl.f((size_t)Hs + Ws + 2 * (P.Hl + 1) + 2 * (P.Wl + 1));
+    float* maps = pl.f(2 * ((size_t)Hs + Ws) + 4 * (P.Hl + 1) + 4 * (P.Wl + 1) + 4);
     double* pd = reinterpret_cast<double*>(pl.f(2 * (B * P.nblk * (T + 1) + 2 * B + 8)));
     if (pass) {
       P.partial = pd;
       P.dJ = pd + B * P.nblk * (T + 1) + 2;
       int* mp = reinterpret_cast<int*>(maps);
       P.mi = mp;
-      P.mj = P.mi + Hs;
+      P.mj = P.mi + ((Hs + 3) & ~3);  // 16-B aligned: k_misfit_grid reads mj as int4
       P.ri0 = P.mj + Ws;
       P.rj0 = P.ri0 + P.Hl + 1;
       P.di = P.rj0 + P.Wl + 1;
       P.dj = P.di + P.Hl;
+      P.rowinv = P.dj + P.Wl;
+      P.colinv = P.rowinv + Hs;
+      P.cr0 = P.colinv + Ws;
+      P.cc0 = P.cr0 + P.Hl + 1;
     }
     if (!pass) {
       P.arena = std::make_unique<Arena>();
@@ -2010,8 +2086,22 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     for (size_t k = 1; k < mi.size(); ++k)
       if (mi[k] < mi[k - 1]) return fail(VV_E_ARG, "non-monotone nearest map");
     std::vector<int> ri0 = ranges(mi, P.Hl), rj0 = ranges(mj, P.Wl);
+    // grid_fused: the inverse of the (injective, Hs >= Hl) down-sampling maps, and for each network pixel the
+    // network pixels whose down-sampled source up-samples back onto it (mi[di[.]], mj[dj[.]] are monotone)
+    std::vector<int> rowinv(Hs, -1), colinv(Ws, -1), ci(P.Hl), cj(P.Wl);
+    for (int a = 0; a < P.Hl; ++a) {
+      rowinv[di[a]] = a;
+      ci[a] = mi[di[a]];
+    }
+    for (int b = 0; b < P.Wl; ++b) {
+      colinv[dj[b]] = b;
+      cj[b] = mj[dj[b]];
+    }
+    std::vector<int> cr0 = ranges(ci, P.Hl), cc0 = ranges(cj, P.Wl);
     std::vector<int> all;
-    for (auto* v : {&mi, &mj, &ri0, &rj0, &di, &dj}) all.insert(all.end(), v->begin(), v->end());
+    mi.resize((Hs + 3) & ~3, 0);  // the padding before mj (see the planner)
+    for (auto* v : {&mi, &mj, &ri0, &rj0, &di, &dj, &rowinv, &colinv, &cr0, &cc0})
+      all.insert(all.end(), v->begin(), v->end());
     VV_HIP(hipMemcpy(P.mi, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   hipLaunchKernelGGL(k_prod, dim3((C + 255) / 256), dim3(256), 0, 0, std_tr, std_, P.prod, C);
@@ -2322,6 +2412,7 @@ int vv_set_tuning(vv_ctx* ctx, const char* key, int value) {
   if (!ctx) return fail(VV_E_ARG, "null context");
   int* f = vv::tuning_field(ctx->tune, key);
   if (!f) return fail(VV_E_ARG, "unknown tuning key '%s'", key ? key : "(null)");
+  if (!vv::tuning_value_ok(key, value)) return fail(VV_E_ARG, "tuning key '%s': value %d not accepted", key, value);
   if (*f != value) drop_graphs(ctx);
   *f = value;
   return 0;
@@ -2460,15 +2551,17 @@ int vv_gemm_register_weight(vv_ctx* ctx, const float* B, int N, int K) {
   return 0;
 }
 
-int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C, int tile,
-            void* stream) {
+static int gemm_entry(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
+                      float* aux, int epi, int tile, void* stream) {
   if (!ctx || !A || !B || !C) return fail(VV_E_ARG, "null argument");
   if (tile >= 0 && !vv::valid_tile(tile)) return fail(VV_E_ARG, "tile hint %d is not a library kernel", tile);
   if (M <= 0 || N <= 0 || K <= 0 || K % 32) return fail(VV_E_ARG, "bad GEMM shape %dx%dx%d (K a multiple of 32)", M, N, K);
+  if (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_DGELU) return fail(VV_E_ARG, "epilogue %d", epi);
+  if (epi == EPI_DGELU && !aux) return fail(VV_E_ARG, "EPI_DGELU reads the pre-activation aux");
   int r = set_dev(ctx);
   if (r) return r;
-  GemmArgs a = gemm_base(M, N, K, 1, EPI_STORE, ctx->math, &ctx->tune);
-  a.g[0] = {A, nullptr, B, bias, C, nullptr, nullptr};
+  GemmArgs a = gemm_base(M, N, K, 1, epi, ctx->math, &ctx->tune);
+  a.g[0] = {A, nullptr, B, bias, C, nullptr, aux};
   if (ctx->math == vv::GEMM_SPLIT16) {
     // A-plane workspace of the split-operand kernel (tile 48), grown on demand (vv_gemm is never graph-captured)
     const size_t need = (size_t)M * 2 * K;
@@ -2484,6 +2577,24 @@ int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, co
     a.apl_halfs = ctx->apl_halfs;
   }
   VV_HIP(vv::gemm_nt(a, (hipStream_t)stream, tile, ctx->gemm_ws));
+  return 0;
+}
+
+int vv_gemm(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C, int tile,
+            void* stream) {
+  return gemm_entry(ctx, M, N, K, A, B, bias, C, nullptr, EPI_STORE, tile, stream);
+}
+
+int vv_gemm_epi(vv_ctx* ctx, int M, int N, int K, const float* A, const float* B, const float* bias, float* C,
+                float* aux, int epi, int tile, void* stream) {
+  return gemm_entry(ctx, M, N, K, A, B, bias, C, aux, epi, tile, stream);
+}
+
+int vv_gelu_eval(vv_ctx* ctx, const float* x, float* y, float* dy, int64_t n, int form, void* stream) {
+  if (!ctx || !x || !y || !dy || n < 0 || (form != 0 && form != 1)) return fail(VV_E_ARG, "bad argument");
+  int r = set_dev(ctx);
+  if (r) return r;
+  VV_HIP(vv::gelu_eval(x, y, dy, n, form, (hipStream_t)stream));
   return 0;
 }
 

@@ -11,6 +11,11 @@
 // absolute of float64 over [-9, 9] -- the rounding of the result itself; the libm erff path costs ~40 VALU
 // instructions per element with its two divergent ranges, this one 15 (GELU) / 19 (GELU').
 // Built with VV_GELU_ERFF: the erff forms (A/B builds only).
+// Infinities: GELU(+inf) = +inf (x - x h would be inf - inf), GELU(-inf) ~ 0 and GELU'(+-inf) = 1 / ~0
+// (x phi(x) would be inf * 0): the x that multiplies h and phi is clamped to +-30 by one v_med3_f32. For |x| <= 30
+// that is x itself; beyond it x h < 2^-25 x for x > 0, and the true x h and x phi(x) are below 1.4e-7 for x < -30.
+// A NaN stays NaN (GELU: the x - x h side of the select; GELU': phi from the unclamped x * x).
+// Checked on the device over a dense grid against float64 erf (tests/test_gpu_kernels.py::test_gelu_device_*).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -58,16 +63,19 @@ __device__ __forceinline__ float dgelu_fast(float x) {
   return cdf + x * pdf;
 }
 #else
+__device__ __forceinline__ float gelu_clamp(float x) { return __builtin_amdgcn_fmed3f(x, -30.0f, 30.0f); }
 __device__ __forceinline__ float gelu_fast(float x) {
-  const float xh = x * gelu_h(x);
-  return x >= 0.0f ? x - xh : xh;
+  const float h = gelu_h(x);
+  const float xh = gelu_clamp(x) * h;
+  return x < 0.0f ? xh : x - xh;  // NaN takes the x - xh side (v_med3 drops a NaN)
 }
 __device__ __forceinline__ float dgelu_fast(float x) {
   const float h = gelu_h(x);
   const float cdf = x >= 0.0f ? 1.0f - h : h;
   // phi(x) = 2^(-x^2 log2(e) / 2 - log2(sqrt(2 pi)))
+  // x * x (not xc * xc) in the exponent: a NaN x gives a NaN pdf and result, an infinite one pdf = 0
   const float pdf = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170f, -1.3257480647361593f));
-  return fmaf(x, pdf, cdf);
+  return fmaf(gelu_clamp(x), pdf, cdf);
 }
 #endif
 
@@ -86,8 +94,8 @@ __device__ __forceinline__ void gelu4(const float (&x)[4], float (&y)[4]) {
   gelu_h4(x, h);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float xh = x[i] * h[i];
-    y[i] = x[i] >= 0.0f ? x[i] - xh : xh;
+    const float xh = gelu_clamp(x[i]) * h[i];
+    y[i] = x[i] < 0.0f ? xh : x[i] - xh;
   }
 }
 __device__ __forceinline__ void dgelu4(const float (&x)[4], float (&y)[4]) {
@@ -97,7 +105,7 @@ __device__ __forceinline__ void dgelu4(const float (&x)[4], float (&y)[4]) {
   for (int i = 0; i < 4; ++i) {
     const float cdf = x[i] >= 0.0f ? 1.0f - h[i] : h[i];
     const float pdf = __builtin_amdgcn_exp2f(fmaf(x[i] * x[i], -0.72134752044448170f, -1.3257480647361593f));
-    y[i] = fmaf(x[i], pdf, cdf);
+    y[i] = fmaf(gelu_clamp(x[i]), pdf, cdf);
   }
 }
 #endif

@@ -2411,7 +2411,20 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h4_gather") return &t.h4_gather;
   if (k == "fixup_ln_rows") return &t.fixup_ln_rows;
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
+  if (k == "grid_fused") return &t.grid_fused;
+  if (k == "mlp_w") return &t.mlp_w;
   return nullptr;
+}
+bool tuning_value_ok(const char* key, int v) {
+  const std::string k(key ? key : "");
+  if (k == "h3_mink" || k == "fc_h3_mink") return v >= 0;
+  if (k == "small_split_minkt" || k == "tail_minkt" || k == "h4_split_minkt") return v >= 1;
+  if (k == "mlp_hc") return v == 0 || v == 2 || v == 32 || v == 64;  // vv_tower.hip mlp_run
+  if (k == "h5_var") return v >= 0 && v <= 5;
+  if (k == "gattn_qf") return v == 1 || v == 2;
+  if (k == "fuse_mlp" || k == "mlp_w") return v >= 0 && v <= 3;
+  if (k == "fuse_attn") return v >= 0 && v <= 15;
+  return v == 0 || v == 1;  // every other knob is a switch
 }
 
 bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || h3_tile(t); }

@@ -49,10 +49,17 @@ struct Tuning {
   int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
                                 // the forward, bit 1 the backward at dim 96, bits 2 / 3 at dim 192 (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box,
                                 // profiles/r04/ab_r04j)
+  int mlp_w = 2;                // the fused MLP as k_mlpw (hidden layer split over the waves, per-wave LDS-DMA weight
+                                // rings, one u scale per token): bit 0 at dim 96, bit 1 at dim 192 (0: k_mlp)
+  int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
+                                // adjoint k_misfit_net_bwd (0: k_misfit_fwd / k_misfit_bwd_gather / k_flow_input(_adj));
+                                // read by vv_bind_problem
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
 int* tuning_field(Tuning& t, const char* key);
+// whether `value` is one the dispatch of `key` accepts (vv_set_tuning rejects the others with VV_E_ARG)
+bool tuning_value_ok(const char* key, int value);
 
 // ---------------------------------------------------------------------------
 // GEMM: C[o(r)][n] = epi( sum_k A(r,k) * B[n][k] )      (B is [N][K] = nn.Linear weight)
@@ -337,9 +344,33 @@ struct MisfitArgs {
   const float* std_;
   double* partial;        // per-block partial sums of H(x-yo)^2/R
   int nblk;
+  // misfit_grid_fwd only (interpolated grids with Hs >= Hl, Ws >= Wl): the observation gradient reduced onto the
+  // network grid in the forward pass, and the next flow input written at the down-sampled pixels
+  const int* rowinv;      // [Hs] state row -> the network row that down-samples from it (integrate), or -1
+  const int* colinv;      // [Ws]
+  float* g_net_obs;       // null or (C,Hl,Wl): coeff * Up^T(H (x-yo)/R)
+  float coeff;
 };
 
 hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s);
+// one pass over the state fields per time slot (interpolated grids): x (only when x_out is set), the J partials (one
+// per (channel, network row): nblk must be C * Hl), g_net_obs, flow_in at the down-sampled pixels
+hipError_t misfit_grid_fwd(const MisfitArgs& a, hipStream_t s);
+// network-grid adjoint of misfit_grid_fwd: g_net[c][q] = (g_net_obs[c][q] + sum_{q' in S(q)} gfi[c][q'] / std[c])
+// * scale[c], S(q) = the network pixels whose down-sampled source pixel up-samples onto q (ranges cr0 / cc0)
+struct MisfitNetBwdArgs {
+  int C, Hl, Wl;
+  const float* g_net_obs; // (C,Hl,Wl)
+  const float* gfi;       // null or (C,Hl,Wl): gradient of the next flow step's input
+  const int* cr0;         // [Hl+1]
+  const int* cc0;         // [Wl+1]
+  const float* std_;
+  const float* scale;
+  float* g_net;           // (C',Hl,Wl) first C channels written
+};
+hipError_t misfit_net_bwd(const MisfitNetBwdArgs& a, hipStream_t s);
+// y = GELU(x), dy = GELU'(x) by the epilogues' device functions (vv_gelu.h); form 0 one-value, 1 four-value forms
+hipError_t gelu_eval(const float* x, float* y, float* dy, int64_t n, int form, hipStream_t s);
 // g_state = coeff*H*(x-yo)/R + g_carry ; g_net(net grid) = adjoint(g_state) * scale
 struct MisfitBwdArgs {
   int C, Hs, Ws, Hl, Wl;
@@ -463,10 +494,13 @@ struct MlpGroup {
   const float* dy;                   // bwd: dx2 [M][C]
   float* out;                        // fwd x2, bwd dx1 [M][C]
   float* rs;                         // bwd, optional: fp16x3 row scales of dx1 (k_rowscale's formula)
+  const float* wmax;                 // k_mlpw: device scalar max |w1h's weight| (fc1.weight fwd, fc2.weight bwd)
+  const float* bmax;                 //   and max |fc1.bias| (fwd; null bwd): the bound of the u scale
 };
 struct MlpArgs {
   int M, C, ngroups;
   int hc;  // C = 192: hidden units per chunk (32 or 64; 0 = 32), or 2 (32, hidden layer split over two waves)
+  int w;   // k_mlpw (hidden layer split over the 4 waves of a 64-token workgroup): bit 0 at dim 96, bit 1 at dim 192
   float eps;
   MlpGroup g[kMaxGroups];
 };

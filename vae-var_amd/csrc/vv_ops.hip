@@ -4,6 +4,7 @@
 //   PatchEmbed conv + absolute_pos_embed, ConvTranspose2d with the quirk-Q2 channel reorder
 //   misfit J_o and its adjoint, vector primitives of L-BFGS / Adam
 #include "vv_kernels.h"
+#include "vv_gelu.h"
 
 #include <algorithm>
 #include <atomic>
@@ -1280,65 +1281,80 @@ __device__ __forceinline__ int unembed_ch(const PatchGroup& G, int co) {
 constexpr int kPatchKmax = 112;  // patch taps per token (4 x channels), padded to 16
 constexpr int kPatchCmax = 128;  // token channels
 
-template <int MODE>
+template <int MODE, int KPM>
 __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const PatchGroup& G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
   const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
   const int KP = (kc + 15) / 16 * 16, KS = KP + 4;  // padded K; LDS row stride (floats)
+  const int OS = C + 4;                             // row stride of the per-wave output staging (floats)
   float* Xs = sm;             // [64][KS]
   float* Wsm = Xs + PT * KS;  // [C][KS]
+  float* Os = Wsm + C * KS;   // [4 waves][16][OS]: D + bias, rows = tokens, for whole-row float4 stores
   const int t0 = blockIdx.x * PT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int tb = wave * 16;  // this wave's 16 tokens within the workgroup: one contiguous [16][C] block of rows
+  const bool wok = t0 + tb < ntok;
+  constexpr int NO = kPatchCmax / 16;  // float4 of the wave's [16][C] block per lane (C / 16 used)
+  // every global load of the kernel is issued here, before any LDS store or MFMA: the pixels of the patches, the
+  // weights, and (MODE 0) the absolute_pos_embed rows and the bias -- one memory latency per workgroup, not three
+  f4 pv[NO];
+  if (MODE == 0) {
+    const size_t pbase = (size_t)((wok ? t0 + tb : 0) % (Ho * Wo)) * C;
+#pragma unroll
+    for (int i = 0; i < NO; ++i)
+      pv[i] = (i < C / 16 && wok) ? *reinterpret_cast<const f4*>(G.pos + pbase + 4 * (i * 64 + lane))
+                                  : f4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr int NTM = kPatchCmax / 16;
+  float bv[NTM];
+#pragma unroll
+  for (int n = 0; n < NTM; ++n) bv[n] = MODE == 0 ? G.bias[min(n * 16 + li, C - 1)] : 0.f;
+  constexpr int NR = KPM / 4;  // (ci, p) rows per thread at most (KPM: the padded K this instantiation serves)
+  float xv[NR];
+  // thread (t, q) of one of two row phases: consecutive threads read consecutive pixels of an image row
+  const int xq = threadIdx.x & 1, xt = (threadIdx.x >> 1) & (PT - 1), half = threadIdx.x >> 7;
   {
-    // thread (t, q) of one of two row phases: consecutive threads read consecutive pixels of an image row
-    const int q = threadIdx.x & 1, t = (threadIdx.x >> 1) & (PT - 1), half = threadIdx.x >> 7;
-    const int tok = t0 + t;
+    const int tok = t0 + xt;
     const bool okt = tok < ntok;
     int b, ho, wo;
     tok_coords(okt ? tok : 0, Ho, Wo, b, ho, wo);
     const size_t plane = (size_t)a.Himg * a.Wimg;
-    const float* base = a.img + (size_t)b * a.Cimg * plane + (size_t)(2 * ho) * a.Wimg + 2 * wo + q;
-    // all of this thread's pixel loads in flight before the first LDS store (one memory latency, not one per load)
-    constexpr int NR = kPatchKmax / 4;  // (ci, p) rows per thread at most
-    float v[NR];
+    const float* base = a.img + (size_t)b * a.Cimg * plane + (size_t)(2 * ho) * a.Wimg + 2 * wo + xq;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const int rest = half + 2 * r, ci = rest >> 1, pp = rest & 1;  // rest = ci 2 + p (co 2 + p)
-      v[r] = 0.f;
+      xv[r] = 0.f;
       if (rest < KP / 2 && okt && ci * 4 < kc) {
         const int ch = MODE == 0 ? G.cin_off + ci : unembed_ch(G, ci);
-        if (MODE == 0 || ch < a.climit) v[r] = base[(size_t)ch * plane + pp * a.Wimg];
+        if (MODE == 0 || ch < a.climit) xv[r] = base[(size_t)ch * plane + pp * a.Wimg];
       }
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const int rest = half + 2 * r;
-      if (rest < KP / 2) Xs[t * KS + (rest >> 1) * 4 + (rest & 1) * 2 + q] = v[r];
     }
   }
-  {
-    constexpr int NW = kPatchCmax * kPatchKmax / 256 / 2;  // two batches of loads
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[NW];
+  for (int r = 0; r < NR; ++r) {
+    const int rest = half + 2 * r;
+    if (rest < KP / 2) Xs[xt * KS + (rest >> 1) * 4 + (rest & 1) * 2 + xq] = xv[r];
+  }
+  // weights (L2-resident: every workgroup of the tower reads them) in batches of 16 loads
+  constexpr int NW = kPatchCmax * KPM / 256, NB = NW < 16 ? NW : 16;
 #pragma unroll
-      for (int r = 0; r < NW; ++r) {
-        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
-        v[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
-      }
+  for (int h = 0; h < NW; h += NB) {
+    float wv[NB];
 #pragma unroll
-      for (int r = 0; r < NW; ++r) {
-        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
-        if (c < C) Wsm[c * KS + j] = v[r];
-      }
+    for (int r = 0; r < NB; ++r) {
+      const int i = threadIdx.x + 256 * (h + r), c = i / KP, j = i - c * KP;
+      wv[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      const int i = threadIdx.x + 256 * (h + r), c = i / KP, j = i - c * KP;
+      if (c < C) Wsm[c * KS + j] = wv[r];
     }
   }
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-  const int tb = wave * 16;  // this wave's 16 tokens within the workgroup
   typedef float fr4 __attribute__((ext_vector_type(4)));
-  constexpr int NTM = kPatchCmax / 16;
   const int nt = (C + 15) / 16;
   fr4 acc[NTM];
   const float* xr = Xs + (tb + li) * KS + 4 * g;
@@ -1355,38 +1371,31 @@ __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
       }
     }
   }
-  // epilogue: every load (bias, pos) issued before the first store (a load behind a store to a possibly aliasing
-  // address waits for it: one memory latency per element)
-  const int tk0 = t0 + tb + 4 * g;
-  if (MODE == 0) {
-    float ex[NTM][4];
-#pragma unroll
-    for (int n = 0; n < NTM; ++n) {
-      const int c = min(n * 16 + li, C - 1);
-      const float bias = G.bias[c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tok = min(tk0 + r, ntok - 1);
-        ex[n][r] = n < nt ? G.pos[(size_t)(tok % (Ho * Wo)) * C + c] : 0.f;
-        acc[n][r] += bias;
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < NTM; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[n][r] = acc[n][r] + ex[n][r];
-  }
+  // lane (channel n 16 + li, g) holds tokens 4 g + r: (D + bias) into the wave's staging rows, then read back as the
+  // wave's contiguous [16][C] block, float4 per lane, + pos: whole 1-KB row runs per store instruction
+  float* O = Os + wave * 16 * OS;
 #pragma unroll
   for (int n = 0; n < NTM; ++n) {
     const int c = n * 16 + li;
     if (n >= nt || c >= C) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (tk0 + r < ntok) G.tok[(size_t)(tk0 + r) * C + c] = acc[n][r];
+    for (int r = 0; r < 4; ++r) O[(4 * g + r) * OS + c] = MODE == 0 ? acc[n][r] + bv[n] : acc[n][r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staging stores done (no other wave reads them)
+  __builtin_amdgcn_wave_barrier();
+  if (!wok) return;
+  float* out = G.tok + (size_t)(t0 + tb) * C;
+#pragma unroll
+  for (int i = 0; i < NO; ++i) {
+    if (i >= C / 16) break;
+    const int e = 4 * (i * 64 + lane), row = e / C, col = e - row * C;
+    f4 v = *reinterpret_cast<const f4*>(O + row * OS + col);
+    if (MODE == 0) v = v + pv[i];
+    *reinterpret_cast<f4*>(out + e) = v;
   }
 }
 
-template <int MODE>
+template <int MODE, int KPM>
 __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const PatchGroup& G = a.g[blockIdx.y];
@@ -1395,27 +1404,15 @@ __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
   const int CP = (C + 15) / 16 * 16, CS = CP + 4;
   float* Wt = sm;  // [KP][CS]: W[c][j] at Wt[j][c]
   const int KP = (kc + 15) / 16 * 16;
-  {
-    // coalesced over W's rows, transposed into LDS; two batches of loads in flight before their LDS stores
-    constexpr int NW = kPatchCmax * kPatchKmax / 256 / 2;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[NW];
-#pragma unroll
-      for (int r = 0; r < NW; ++r) {
-        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
-        v[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < NW; ++r) {
-        const int i = threadIdx.x + 256 * (h * NW + r), c = i / KP, j = i - c * KP;
-        if (c < CP) Wt[j * CS + c] = v[r];
-      }
-    }
-  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tok = blockIdx.x * PT + wave * 16 + li;
   const bool ok = tok < ntok;
+  constexpr int NMT = KPM / 16;
+  const int nmt = KP / 16;
+  int b, ho, wo;
+  tok_coords(ok ? tok : 0, Ho, Wo, b, ho, wo);
+  // every global load first (token rows, the added image / bias, the weights), then the LDS transposition: one
+  // memory latency per workgroup
   const float* yr = (MODE == 0 ? G.dtok : G.tok) + (size_t)(ok ? tok : 0) * C + 4 * g;
   f4 y[kPatchCmax / 16];
 #pragma unroll
@@ -1424,30 +1421,7 @@ __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
     if (16 * s + 4 * g < C) v = *reinterpret_cast<const f4*>(yr + 16 * s);
     y[s] = v;
   }
-  __syncthreads();
-  typedef float fr4 __attribute__((ext_vector_type(4)));
-  constexpr int NMT = kPatchKmax / 16;
-  int b, ho, wo;
-  tok_coords(ok ? tok : 0, Ho, Wo, b, ho, wo);
-  const int nmt = KP / 16;
-  fr4 acc[NMT];
-#pragma unroll
-  for (int mt = 0; mt < NMT; ++mt) {
-    acc[mt] = fr4{0.f, 0.f, 0.f, 0.f};
-    if (mt < nmt) {
-      const float* wr = Wt + (mt * 16 + li) * CS + 4 * g;
-#pragma unroll
-      for (int s = 0; s < kPatchCmax / 16; ++s) {
-        if (16 * s < CP) {
-          const f4 wa = *reinterpret_cast<const f4*>(wr + 16 * s);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[e], y[s][e], acc[mt], 0, 0, 0);
-        }
-      }
-    }
-  }
-  // rows 4 g + r of output tile mt: channel o = 4 mt + g, p = r / 2, q = r % 2. Every load (bias, the added image)
-  // is issued before the first store.
+  // rows 4 g + r of output tile mt: channel o = 4 mt + g, p = r / 2, q = r % 2
   size_t off[NMT];
   bool st[NMT];
   float2 ex[NMT][2];
@@ -1468,6 +1442,43 @@ __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
       ex[mt][0] = ex[mt][1] = make_float2(bias, bias);
     }
   }
+  {
+    // coalesced over W's rows, transposed into LDS, in batches of 16 loads
+    constexpr int NW = kPatchCmax * KPM / 256, NB = NW < 16 ? NW : 16;
+#pragma unroll
+    for (int h = 0; h < NW; h += NB) {
+      float v[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int i = threadIdx.x + 256 * (h + r), c = i / KP, j = i - c * KP;
+        v[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int i = threadIdx.x + 256 * (h + r), c = i / KP, j = i - c * KP;
+        if (c < CP) Wt[j * CS + c] = v[r];
+      }
+    }
+  }
+  __syncthreads();
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  fr4 acc[NMT];
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    acc[mt] = fr4{0.f, 0.f, 0.f, 0.f};
+    if (mt < nmt) {
+      const float* wr = Wt + (mt * 16 + li) * CS + 4 * g;
+#pragma unroll
+      for (int s = 0; s < kPatchCmax / 16; ++s) {
+        if (16 * s < CP) {
+          const f4 wa = *reinterpret_cast<const f4*>(wr + 16 * s);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[e], y[s][e], acc[mt], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // two float2 stores per tile: consecutive lanes = consecutive tokens = horizontally adjacent pixel pairs
 #pragma unroll
   for (int mt = 0; mt < NMT; ++mt) {
     if (!st[mt]) continue;
@@ -1484,31 +1495,43 @@ static int max_k(const PatchArgs& a, bool in) {
   return m;
 }
 
-template <int MODE>
-static hipError_t p2t_launch(const PatchArgs& a, int kc, hipStream_t s) {
+template <int MODE, int KPM>
+static hipError_t p2t_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   const int KS = (kc + 15) / 16 * 16 + 4;
-  const size_t lds = (size_t)(PT + a.Ctok) * KS * sizeof(float);
+  const size_t lds = ((size_t)(PT + a.Ctok) * KS + (size_t)PT * (a.Ctok + 4)) * sizeof(float);
   if (lds > 64 * 1024)
-    if (hipError_t e = set_lds_limit((const void*)k_p2t_mf<MODE>, (size_t)(PT + kPatchCmax) * (kPatchKmax + 4) * 4))
+    if (hipError_t e = set_lds_limit((const void*)k_p2t_mf<MODE, KPM>,
+                                     ((size_t)(PT + kPatchCmax) * (KPM + 4) + (size_t)PT * (kPatchCmax + 4)) * 4))
       return e;
-  hipLaunchKernelGGL((k_p2t_mf<MODE>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((k_p2t_mf<MODE, KPM>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
-
+// the instantiation whose padded K (32, 64 or 112 taps) covers kc: registers scale with it
 template <int MODE>
-static hipError_t t2p_launch(const PatchArgs& a, int kc, hipStream_t s) {
+static hipError_t p2t_launch(const PatchArgs& a, int kc, hipStream_t s) {
+  return kc <= 32 ? p2t_launch_k<MODE, 32>(a, kc, s) : kc <= 64 ? p2t_launch_k<MODE, 64>(a, kc, s)
+                                                                 : p2t_launch_k<MODE, kPatchKmax>(a, kc, s);
+}
+
+template <int MODE, int KPM>
+static hipError_t t2p_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   const size_t lds = (size_t)((kc + 15) / 16 * 16) * ((a.Ctok + 15) / 16 * 16 + 4) * sizeof(float);
-  hipLaunchKernelGGL((k_t2p_mf<MODE>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((k_t2p_mf<MODE, KPM>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
+}
+template <int MODE>
+static hipError_t t2p_launch(const PatchArgs& a, int kc, hipStream_t s) {
+  return kc <= 32 ? t2p_launch_k<MODE, 32>(a, kc, s) : kc <= 64 ? t2p_launch_k<MODE, 64>(a, kc, s)
+                                                                 : t2p_launch_k<MODE, kPatchKmax>(a, kc, s);
 }
 
 // preconditions: 2x2 patches, 16 tokens of a wave in one image row (Wo % 16), at most kPatchKmax taps per token and
-// kPatchCmax token channels (LDS: <= 64 KB)
+// kPatchCmax token channels, a multiple of 16 (LDS: <= 64 KB); parse_cfg refuses configs outside them
 static hipError_t patch_check(const PatchArgs& a, int kc) {
   if (a.ngroups <= 0 || a.ngroups > kMaxGroups || (a.Himg | a.Wimg) & 1 || (a.Wimg / 2) % 16 || a.Ctok <= 0 ||
-      a.Ctok > kPatchCmax || a.Ctok % 4 || kc <= 0 || kc > kPatchKmax)
+      a.Ctok > kPatchCmax || a.Ctok % 16 || kc <= 0 || kc > kPatchKmax)
     return hipErrorInvalidValue;
   return hipSuccess;
 }
@@ -1625,6 +1648,130 @@ __global__ __launch_bounds__(256) void k_misfit_bwd_gather(MisfitBwdArgs a) {
   }
 }
 
+// The misfit on an interpolated state grid in ONE pass over the state fields (config 5: 721x1440 state, 128x256
+// networks; da_4dvar.py:1184-1207 with decoder_hr's / integrate's nearest up-sampling, nf_model/vae.py:90,
+// da_4dvar.py:679). One workgroup per (channel c, network row ra) reads the preimage rows [ri0[ra], ri0[ra+1]) of
+// xb / yo / H / R once, as float4 along the row (a thread owns 4 columns for every row of the band), and produces:
+//  - x = net[mi[i]][mj[j]] * scale (* scale2) + xb (+ offset), stored only when x_out is set (J-only evaluations);
+//  - the J partial of its band (fp64, deterministic: one partial per workgroup);
+//  - the observation gradient already reduced onto the network grid (the adjoint of the up-sampling):
+//    g_net_obs[c][ra][cb] = sum over the preimage rectangle of coeff * H (x - yo) / R — column sums over the band in
+//    registers, then the columns [rj0[cb], rj0[cb+1]) summed from LDS;
+//  - the next flow step's input (integrate's down-sampling, da_4dvar.py:671) at the pixels it samples.
+// The backward pass then never reads a state field again (k_misfit_net_bwd runs on the network grid).
+template <int MR>
+__global__ __launch_bounds__(384) void k_misfit_grid(MisfitArgs a) {
+  extern __shared__ float colsum[];  // [Ws]
+  __shared__ double red[6];
+  const int c = blockIdx.x / a.Hl, ra = blockIdx.x - c * a.Hl;
+  const int r0 = a.ri0[ra], r1 = a.ri0[ra + 1];
+  const int W4 = a.Ws >> 2, HWl = a.Hl * a.Wl;
+  const float sc = a.scale[c];
+  const float sc2 = a.scale2 ? a.scale2[c] : 1.f;
+  const float off = a.offset ? a.offset[c] : 0.f;
+  const float mean = a.flow_in ? a.mean[c] : 0.f, sd = a.flow_in ? a.std_[c] : 1.f;
+  const float* __restrict__ netc = a.net + (size_t)c * HWl;
+  double acc = 0.0;
+  for (int j4 = threadIdx.x; j4 < W4; j4 += blockDim.x) {
+    const int j = 4 * j4;
+    const int4 q = *reinterpret_cast<const int4*>(a.mj + j);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int i0 = r0; i0 < r1; i0 += MR) {
+      float4 xv[MR], yv[MR], hv[MR], rv[MR], nv[MR];
+      // every load of the band first (the stores below cannot alias them, but the compiler does not know it)
+#pragma unroll
+      for (int k = 0; k < MR; ++k) {
+        const int i = min(i0 + k, r1 - 1);
+        const size_t e = ((size_t)c * a.Hs + i) * a.Ws + j;
+        xv[k] = a.xb ? *reinterpret_cast<const float4*>(a.xb + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        yv[k] = *reinterpret_cast<const float4*>(a.yo + e);
+        hv[k] = *reinterpret_cast<const float4*>(a.Hm + e);
+        rv[k] = *reinterpret_cast<const float4*>(a.R + e);
+        const float* nr = netc + (size_t)a.mi[i] * a.Wl;
+        nv[k] = make_float4(nr[q.x], nr[q.y], nr[q.z], nr[q.w]);
+      }
+#pragma unroll
+      for (int k = 0; k < MR; ++k) {
+        const int i = i0 + k;
+        if (i >= r1) break;
+        const float nn[4] = {nv[k].x, nv[k].y, nv[k].z, nv[k].w};
+        const float xx[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+        const float yy[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+        const float hh[4] = {hv[k].x, hv[k].y, hv[k].z, hv[k].w};
+        const float rr[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+        float v[4], g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          // k_misfit_fwd's arithmetic, element for element
+          float t = nn[u] * sc;
+          if (a.scale2) t = t * sc2;
+          if (a.xb) t = t + xx[u];
+          if (a.offset) t = t + off;
+          v[u] = t;
+          const float d = t - yy[u];
+          acc += (double)((hh[u] * (d * d)) / rr[u]);
+          g[u] = a.coeff * ((hh[u] * d) / rr[u]);
+        }
+        s0 += g[0];
+        s1 += g[1];
+        s2 += g[2];
+        s3 += g[3];
+        const size_t e = ((size_t)c * a.Hs + i) * a.Ws + j;
+        if (a.x_out) *reinterpret_cast<float4*>(a.x_out + e) = make_float4(v[0], v[1], v[2], v[3]);
+        if (a.flow_in) {
+          const int fr = a.rowinv[i];
+          if (fr >= 0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int fc = a.colinv[j + u];
+              if (fc >= 0) a.flow_in[(size_t)c * HWl + (size_t)fr * a.Wl + fc] = (v[u] - mean) / sd;
+            }
+          }
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(colsum + j) = make_float4(s0, s1, s2, s3);
+  }
+  // J partial of the band
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += red[k];
+    a.partial[blockIdx.x] = t;
+  }
+  if (!a.g_net_obs) return;
+  // the up-sampling adjoint along the row: network column cb sums its preimage columns
+  for (int cb = threadIdx.x; cb < a.Wl; cb += blockDim.x) {
+    float g = 0.f;
+    for (int j = a.rj0[cb]; j < a.rj0[cb + 1]; ++j) g += colsum[j];
+    a.g_net_obs[(size_t)c * HWl + (size_t)ra * a.Wl + cb] = g;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_misfit_net_bwd(MisfitNetBwdArgs a) {
+  const int HWl = a.Hl * a.Wl;
+  const int n = a.C * HWl;
+  for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
+    const int c = id / HWl, q = id - c * HWl;
+    float g = a.g_net_obs[id];
+    if (a.gfi) {
+      // the flow-input adjoint (integrate's down-sampling, k_flow_input_adj's gfi / std) followed by the up-sampling
+      // adjoint, composed on the network grid
+      const int ra = q / a.Wl, cb = q - ra * a.Wl;
+      const float sd = a.std_[c];
+      float s = 0.f;
+      for (int r = a.cr0[ra]; r < a.cr0[ra + 1]; ++r)
+        for (int k = a.cc0[cb]; k < a.cc0[cb + 1]; ++k) s += a.gfi[(size_t)c * HWl + (size_t)r * a.Wl + k] / sd;
+      g += s;
+    }
+    a.g_net[id] = g * a.scale[c];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_flow_input(const float* x, float* fi, const int* di, const int* dj,
                                                     const float* mean, const float* std_, int C, int Hs, int Ws,
                                                     int Hl, int Wl) {
@@ -1717,6 +1864,28 @@ hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
   const int ph = prof_begin(s);
   hipLaunchKernelGGL(k_misfit_fwd, dim3(a.nblk), dim3(256), 0, s, a);
   prof_end(ph, s, PC_MISFIT, 6.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * ((a.xb ? 6 : 5) + (a.flow_in ? 1 : 0)));
+  return hipGetLastError();
+}
+hipError_t misfit_grid_fwd(const MisfitArgs& a, hipStream_t s) {
+  if (!a.mi || !a.mj || !a.ri0 || !a.rj0 || !a.Hm || !a.yo || !a.R || (a.Ws & 3) || a.nblk != a.C * a.Hl ||
+      a.Ws > 16384 || (a.flow_in && (!a.rowinv || !a.colinv)))
+    return hipErrorInvalidValue;
+  for (const void* p : {(const void*)a.xb, (const void*)a.yo, (const void*)a.Hm, (const void*)a.R,
+                        (const void*)a.x_out, (const void*)a.mj})
+    if (reinterpret_cast<uintptr_t>(p) & 15) return hipErrorInvalidValue;
+  const int ph = prof_begin(s);
+  const size_t n = (size_t)a.C * a.Hs * a.Ws;
+  hipLaunchKernelGGL(k_misfit_grid<6>, dim3(a.C * a.Hl), dim3(384), a.Ws * sizeof(float), s, a);
+  // algorithmic bytes: the state fields once (xb, yo, H, R; x when stored)
+  prof_end(ph, s, PC_MISFIT, 8.0 * n, 4.0 * n * ((a.xb ? 4 : 3) + (a.x_out ? 1 : 0)));
+  return hipGetLastError();
+}
+hipError_t misfit_net_bwd(const MisfitNetBwdArgs& a, hipStream_t s) {
+  if (!a.g_net_obs || !a.g_net || !a.scale || (a.gfi && (!a.cr0 || !a.cc0 || !a.std_))) return hipErrorInvalidValue;
+  const int ph = prof_begin(s);
+  const int n = a.C * a.Hl * a.Wl;
+  hipLaunchKernelGGL(k_misfit_net_bwd, dim3(std::min((n + 255) / 256, 2048)), dim3(256), 0, s, a);
+  prof_end(ph, s, PC_MISFIT, 2.0 * n, 4.0 * n * (a.gfi ? 3 : 2));
   return hipGetLastError();
 }
 hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
@@ -2117,4 +2286,39 @@ hipError_t transpose2d(const float* in, float* out, int rows, int cols, hipStrea
   return hipGetLastError();
 }
 
+}  // namespace vv
+
+namespace vv {
+// the GELU / GELU' device functions every epilogue uses (vv_gelu.h), evaluated as they are compiled there: form 0 the
+// one-value forms (gelu_fast / dgelu_fast: the GEMM epilogues), 1 the four-value interleaved forms (gelu4 / dgelu4: the
+// fused tower MLP, the tile-49 row epilogue)
+__global__ __launch_bounds__(256) void k_gelu_eval(const float* __restrict__ x, float* __restrict__ y,
+                                                   float* __restrict__ dy, int64_t n, int form) {
+  for (int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x); i < n; i += 4 * (int64_t)gridDim.x * 256) {
+    float v[4], g[4], d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = i + u < n ? x[i + u] : 0.f;
+    if (form) {
+      gelu4(v, g);
+      dgelu4(v, d);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g[u] = gelu_fast(v[u]);
+        d[u] = dgelu_fast(v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u < n) {
+        y[i + u] = g[u];
+        dy[i + u] = d[u];
+      }
+  }
+}
+hipError_t gelu_eval(const float* x, float* y, float* dy, int64_t n, int form, hipStream_t s) {
+  const unsigned g = (unsigned)std::min<int64_t>((n + 1023) / 1024, 4096);
+  hipLaunchKernelGGL(k_gelu_eval, dim3(std::max(g, 1u)), dim3(256), 0, s, x, y, dy, n, form);
+  return hipGetLastError();
+}
 }  // namespace vv

@@ -118,6 +118,9 @@ _SIGS = {
     "vv_attention_global": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "vv_gemm_register_weight": (c_int, [c_void_p, c_void_p, c_int, c_int]),
     "vv_gemm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "vv_gemm_epi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                            c_int, c_void_p]),
+    "vv_gelu_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "vv_sc4dvar_bind": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_float, c_void_p, c_int, P(c_double), P(c_double), c_int,
                                 P(c_double), P(c_double), P(c_double), c_double, c_int]),

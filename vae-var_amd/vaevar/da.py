@@ -20,7 +20,8 @@ from .lbfgs import LBFGS, Adam
 def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10, optimizer: str = "lbfgs",
                 lr: float | None = None, log_terms: bool = True, log=None, gt=None, metrics=None, replay=None,
                 batch_scalars: bool = True):
-    """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, seconds); with gt (T,C,Hs,Ws) and a
+    """Returns dict(xa, z, J=[(J_b, J_o) per outer pass], n_eval, n_iter, n_discarded (speculative evaluations the
+    reference would not have made, not in n_eval but in seconds), seconds); with gt (T,C,Hs,Ws) and a
     vaevar.metrics.Metrics also metrics=[(wrmse[C], bias[C]) per outer pass] of xhat against gt[0] — the
     reference's bg_* (pass 0) and ana_* (pass Nit) entries of metrics_list (:1285-1291)."""
     dev = prob.xb.device
@@ -44,6 +45,7 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
 
     js, ms = [], []
     n0 = prob.n_evals
+    d0 = prob.n_discarded
     t0 = time.time()
     for kk in range(nit + 1):
         if log_terms:
@@ -62,7 +64,7 @@ def one_step_da(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int
     n_log = (nit + 1) if log_terms else 0
     n_iter = opt.state["n_iter"] if optimizer == "lbfgs" else opt.t
     return {"xa": xa, "z": z, "J": js, "n_eval": prob.n_evals - n0 - n_log, "n_iter": n_iter,
-            "seconds": time.time() - t0, "metrics": ms}
+            "n_discarded": prob.n_discarded - d0, "seconds": time.time() - t0, "metrics": ms}
 
 
 def one_step_da_batch(prob: DAProblem, nit: int, history_size: int = 10, max_iter: int = 10):

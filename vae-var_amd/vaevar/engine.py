@@ -42,7 +42,7 @@ class Context:
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
                    "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt",
                    "win_mfma", "fc_h3_mink", "fuse_mlp", "fuse_attn", "attn_mfma", "gelu_planes", "attn_planes", "fixup_ln", "h5", "h5_var", "fc_conv_mf",
-                   "mlp_hc", "h4_gather", "fixup_ln_rows")
+                   "mlp_hc", "h4_gather", "fixup_ln_rows", "grid_fused", "mlp_w")
 
     def __init__(self, device: int = 0):
         self.device = device
@@ -239,6 +239,25 @@ class Context:
         bp = _ptr(bias) if bias is not None else None
         check(lib.vv_gemm(self.h, M, N, K, _ptr(A), _ptr(B), bp, _ptr(C), tile, _stream()), "gemm")
         return C
+
+    EPI = {"store": 0, "gelu": 1, "dgelu": 3}
+
+    def gemm_epi(self, A, B, epi, aux=None, bias=None, tile=-1):
+        """vv_gemm_epi: C = gelu(A B^T + bias) (aux, if given, receives A B^T + bias) or C = (A B^T) * gelu'(aux)."""
+        M, K = A.shape
+        N = B.shape[0]
+        C = torch.empty(M, N, device=A.device, dtype=torch.float32)
+        bp = _ptr(bias) if bias is not None else None
+        ap = _ptr(aux) if aux is not None else None
+        check(lib.vv_gemm_epi(self.h, M, N, K, _ptr(A), _ptr(B), bp, _ptr(C), ap, self.EPI[epi], tile, _stream()),
+              "gemm_epi")
+        return C
+
+    def gelu_eval(self, x, form=0):
+        """(GELU(x), GELU'(x)) by the epilogues' device functions (vv_gelu_eval; form 1: the four-value forms)."""
+        y, dy = torch.empty_like(x), torch.empty_like(x)
+        check(lib.vv_gelu_eval(self.h, _ptr(x), _ptr(y), _ptr(dy), x.numel(), form, _stream()), "gelu_eval")
+        return y, dy
 
 
 class _NetFn(torch.autograd.Function):
@@ -469,6 +488,10 @@ class DAProblem:
         if self.interp is not None:
             check(lib.vv_set_obs_operator(self.ctx.h, n_out, n_in, _ptr(self.interp)), "set_obs_operator")
         self.n_evals = 0
+        # evaluations the speculative L-BFGS mirror ran and discarded (vaevar/lbfgs.py: the line search's first
+        # evaluation started before gtd is known, where the reference stops on gtd > -tolerance_change); their time is
+        # inside one_step_da's seconds and the bench's timed region
+        self.n_discarded = 0
 
     def closure_batch(self, z: torch.Tensor, grad: torch.Tensor | None):
         """One evaluation of all B analyses: (J_b[B], J_o[B]) as float64 arrays; grad <- dJ/dz (B,...) if given."""
@@ -490,8 +513,10 @@ class DAProblem:
         check(lib.vv_closure_async(self.ctx.h, _ptr(z), gp, ctypes.c_void_p(self._dJ.data_ptr()), _stream()),
               "closure_async")
         self.n_evals += 1
-        def uncount():
+
+        def uncount():  # a speculative evaluation the reference would not have made (counted, not hidden)
             self.n_evals -= 1
+            self.n_discarded += 1
 
         return LazyLoss(self._dJ, lambda v: self.loss_f32(v[0], v[1]), uncount)
 
