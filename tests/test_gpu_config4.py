@@ -106,10 +106,12 @@ def test_full_t6_closure_vs_oracle():
 @pytest.mark.parametrize("mode", ["free", "replay"])
 def test_config4_trajectory_g16(mode):
     """BASELINE config 4's window at full size (216M-parameter decoder + the flow stand-in, T = 6: five integrate steps
-    in the loss, 69x128x256) over Nit = 3 outer passes (27 L-BFGS iterations, 34 evaluations) against G16: the
-    reference's networks_old modules + torch.optim.LBFGS on CPU (oracle/make_golden.py --g16, da_4dvar.py:1183-1208,
-    :1238-1299). The reference's own summation-order drift on this trajectory is small (g16_sensitivity.npz: free
-    3.9e-5, replay 2.0e-7 in J), so J per pass and xa are held to SURVEY c6's 1e-3 both ways (xa rel-L2 1e-2 free)."""
+    in the loss, 69x128x256) over the bench's full budget, Nit = 10 outer passes (r05; 97 L-BFGS iterations, 111
+    evaluations; r04: Nit 3) against G16: the reference's networks_old modules + torch.optim.LBFGS on CPU
+    (oracle/make_golden.py --g16, da_4dvar.py:1183-1208, :1238-1299). Bounds: SURVEY c6's 1e-3 on J, or twice the
+    reference's own summation-order drift on this trajectory where that is larger (g16_sensitivity.npz: the same run
+    on 4 threads, free-running and replayed along G16's line searches, oracle/g10_sensitivity.py --case g16); xa
+    rel-L2 1e-2 free, 1e-3 replayed."""
     from vaevar import config as C
     from vaevar.da import one_step_da
     from vaevar.engine import DAProblem, LGUnet

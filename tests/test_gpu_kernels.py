@@ -118,7 +118,7 @@ def test_tuning_knobs_per_context():
     with pytest.raises(VVError):
         c1.set_tuning("no_such_knob", 1)
     # values the dispatch does not accept are refused at vv_set_tuning, not inside a later closure
-    for k, bad in (("mlp_hc", 48), ("h5_var", 6), ("grid_fused", 2), ("gattn_qf", 0), ("tail_minkt", 0)):
+    for k, bad in (("mlp_hc", 48), ("h5_var", 6), ("grid_fused", 3), ("gattn_qf", 0), ("tail_minkt", 0)):
         with pytest.raises(VVError):
             c1.set_tuning(k, bad)
         assert c1.get_tuning(k) != bad

@@ -705,7 +705,6 @@ def test_bitwise_knobs(full_dec, knob, ref, on):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning(knob, default)
-        full_dec.ctx.set_tuning("mlp_w", w_default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     print(f"{knob}: k_gather_scales passes {gathers[0]} -> {gathers[1]}")
     assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1)

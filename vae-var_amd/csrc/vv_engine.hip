@@ -277,6 +277,7 @@ struct Problem {
   // grid_fused (interpolated grids with Hs >= Hl, Ws >= Wl, synthetic observations): the misfit reads each state
   // field once per evaluation (k_misfit_grid) and its adjoint runs on the network grid (k_misfit_net_bwd)
   bool grid_fused = false;
+  int grid_mr = 6;                           // k_misfit_grid rows in flight per pass
   int *rowinv = nullptr, *colinv = nullptr;  // [Hs] / [Ws]: inverse of di / dj, -1 off the sampled rows / columns
   int *cr0 = nullptr, *cc0 = nullptr;        // [Hl+1] / [Wl+1]: ranges of mi[di[.]] / mj[dj[.]]
   float* GON = nullptr;                      // (B,T,C,Hl,Wl): coeff * Up^T(H (x_t - yo_t) / R_t)
@@ -1414,6 +1415,28 @@ void set_maps(const Problem& P, MisfitArgs& m) {
   m.rj0 = P.interp ? P.rj0 : nullptr;
 }
 
+// the problem's index maps in one block of ints (offsets): mj and colinv 16-B aligned (k_misfit_grid reads them as
+// int4), the rest packed
+struct MapLayout {
+  size_t mi, mj, ri0, rj0, di, dj, rowinv, colinv, cr0, cc0, n;
+};
+MapLayout map_layout(int Hs, int Ws, int Hl, int Wl) {
+  auto al4 = [](size_t v) { return (v + 3) & ~(size_t)3; };
+  MapLayout L;
+  L.mi = 0;
+  L.mj = al4(L.mi + Hs);
+  L.ri0 = L.mj + Ws;
+  L.rj0 = L.ri0 + Hl + 1;
+  L.di = L.rj0 + Wl + 1;
+  L.dj = L.di + Hl;
+  L.rowinv = L.dj + Wl;
+  L.colinv = al4(L.rowinv + Hs);
+  L.cr0 = L.colinv + Ws;
+  L.cc0 = L.cr0 + Hl + 1;
+  L.n = al4(L.cc0 + Wl + 1);
+  return L;
+}
+
 // B analyses per evaluation (the decoder's batch): one decoder launch sequence over all B, one flow launch
 // sequence per forecast step; the misfit / adjoint kernels run per analysis (each has its own J partials).
 // Layouts: X (B, T, C, Hs, Ws); decoder output / gradient (B, Cout, Hl, Wl); flow input FI[t] (B, C, Hl, Wl), flow
@@ -1451,6 +1474,7 @@ int closure_impl(vv_ctx* ctx, const float* z, float* grad, hipStream_t st) {
     ma.rowinv = P.rowinv;
     ma.colinv = P.colinv;
     ma.coeff = P.obs_coeff;
+    ma.mr = P.grid_mr;
   }
   for (int b = 0; b < B; ++b) {
     MisfitArgs m0 = ma;
@@ -2028,6 +2052,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
       aligned = aligned && !(reinterpret_cast<uintptr_t>(p) & 15);
     P.grid_fused = P.interp && ctx->tune.grid_fused && Hs >= P.Hl && Ws >= P.Wl && Ws % 4 == 0 && Ws <= 16384 && aligned;
     if (P.grid_fused) P.nblk = C * P.Hl;  // one J partial per (channel, network row) workgroup of k_misfit_grid
+    P.grid_mr = ctx->tune.grid_fused == 2 ? 3 : 6;
   }
   const size_t CHW = (size_t)C * Hs * Ws;
   const size_t HWl = (size_t)P.Hl * P.Wl;
@@ -2050,22 +2075,23 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     P.zn = B * D->cfg.Cin * D->cfg.Himg * D->cfg.Wimg;
     P.Z = pl.f(P.zn);
     P.GZ = pl.f(P.zn);
-    float* maps = pl.f(2 * ((size_t)Hs + Ws) + 4 * (P.Hl + 1) + 4 * (P.Wl + 1) + 4);
+    float* maps = pl.f(map_layout(Hs, Ws, P.Hl, P.Wl).n);
     double* pd = reinterpret_cast<double*>(pl.f(2 * (B * P.nblk * (T + 1) + 2 * B + 8)));
     if (pass) {
       P.partial = pd;
       P.dJ = pd + B * P.nblk * (T + 1) + 2;
       int* mp = reinterpret_cast<int*>(maps);
-      P.mi = mp;
-      P.mj = P.mi + ((Hs + 3) & ~3);  // 16-B aligned: k_misfit_grid reads mj as int4
-      P.ri0 = P.mj + Ws;
-      P.rj0 = P.ri0 + P.Hl + 1;
-      P.di = P.rj0 + P.Wl + 1;
-      P.dj = P.di + P.Hl;
-      P.rowinv = P.dj + P.Wl;
-      P.colinv = P.rowinv + Hs;
-      P.cr0 = P.colinv + Ws;
-      P.cc0 = P.cr0 + P.Hl + 1;
+      const MapLayout L = map_layout(Hs, Ws, P.Hl, P.Wl);
+      P.mi = mp + L.mi;
+      P.mj = mp + L.mj;
+      P.ri0 = mp + L.ri0;
+      P.rj0 = mp + L.rj0;
+      P.di = mp + L.di;
+      P.dj = mp + L.dj;
+      P.rowinv = mp + L.rowinv;
+      P.colinv = mp + L.colinv;
+      P.cr0 = mp + L.cr0;
+      P.cc0 = mp + L.cc0;
     }
     if (!pass) {
       P.arena = std::make_unique<Arena>();
@@ -2098,11 +2124,13 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
       cj[b] = mj[dj[b]];
     }
     std::vector<int> cr0 = ranges(ci, P.Hl), cc0 = ranges(cj, P.Wl);
-    std::vector<int> all;
-    mi.resize((Hs + 3) & ~3, 0);  // the padding before mj (see the planner)
-    for (auto* v : {&mi, &mj, &ri0, &rj0, &di, &dj, &rowinv, &colinv, &cr0, &cc0})
-      all.insert(all.end(), v->begin(), v->end());
-    VV_HIP(hipMemcpy(P.mi, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice));
+    const MapLayout L = map_layout(Hs, Ws, P.Hl, P.Wl);
+    std::vector<int> all(L.n, 0);
+    const std::pair<const std::vector<int>*, size_t> parts[] = {
+        {&mi, L.mi}, {&mj, L.mj}, {&ri0, L.ri0}, {&rj0, L.rj0}, {&di, L.di}, {&dj, L.dj},
+        {&rowinv, L.rowinv}, {&colinv, L.colinv}, {&cr0, L.cr0}, {&cc0, L.cc0}};
+    for (const auto& pv : parts) std::copy(pv.first->begin(), pv.first->end(), all.begin() + pv.second);
+    VV_HIP(hipMemcpy(P.mi - L.mi, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   hipLaunchKernelGGL(k_prod, dim3((C + 255) / 256), dim3(256), 0, 0, std_tr, std_, P.prod, C);
   VV_HIP(hipGetLastError());

@@ -2422,6 +2422,7 @@ bool tuning_value_ok(const char* key, int v) {
   if (k == "mlp_hc") return v == 0 || v == 2 || v == 32 || v == 64;  // vv_tower.hip mlp_run
   if (k == "h5_var") return v >= 0 && v <= 5;
   if (k == "gattn_qf") return v == 1 || v == 2;
+  if (k == "grid_fused") return v >= 0 && v <= 2;
   if (k == "fuse_mlp" || k == "mlp_w") return v >= 0 && v <= 3;
   if (k == "fuse_attn") return v >= 0 && v <= 15;
   return v == 0 || v == 1;  // every other knob is a switch

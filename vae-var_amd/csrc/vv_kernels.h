@@ -49,10 +49,12 @@ struct Tuning {
   int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
                                 // the forward, bit 1 the backward at dim 96, bits 2 / 3 at dim 192 (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box,
                                 // profiles/r04/ab_r04j)
-  int mlp_w = 2;                // the fused MLP as k_mlpw (hidden layer split over the waves, per-wave LDS-DMA weight
-                                // rings, one u scale per token): bit 0 at dim 96, bit 1 at dim 192 (0: k_mlp)
+  int mlp_w = 0;                // the fused MLP as k_mlpw (hidden layer split over the waves, per-wave LDS-DMA weight
+                                // rings, one u scale per token): bit 0 at dim 96, bit 1 at dim 192 (0: k_mlp). r05: correct
+                                // but not faster (dim 192: 64.7 / 72.5 vs 66.7 / 67.4 us; profiles/r05/knob_ab_*), off
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
                                 // adjoint k_misfit_net_bwd (0: k_misfit_fwd / k_misfit_bwd_gather / k_flow_input(_adj));
+                                // 1: 6 rows of a band in flight per pass, 2: 3 rows (two passes, more waves per SIMD);
                                 // read by vv_bind_problem
 };
 extern const Tuning kDefaultTuning;
@@ -350,6 +352,7 @@ struct MisfitArgs {
   const int* colinv;      // [Ws]
   float* g_net_obs;       // null or (C,Hl,Wl): coeff * Up^T(H (x-yo)/R)
   float coeff;
+  int mr;                 // rows in flight per pass (Tuning.grid_fused: 1 -> 6, 2 -> 3)
 };
 
 hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s);

@@ -1332,12 +1332,8 @@ __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
       }
     }
   }
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int rest = half + 2 * r;
-    if (rest < KP / 2) Xs[xt * KS + (rest >> 1) * 4 + (rest & 1) * 2 + xq] = xv[r];
-  }
-  // weights (L2-resident: every workgroup of the tower reads them) in batches of 16 loads
+  // weights (L2-resident: every workgroup of the tower reads them) in batches of 16 loads; the first batch is in
+  // flight with the pixels before the first LDS store
   constexpr int NW = kPatchCmax * KPM / 256, NB = NW < 16 ? NW : 16;
 #pragma unroll
   for (int h = 0; h < NW; h += NB) {
@@ -1346,6 +1342,13 @@ __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
     for (int r = 0; r < NB; ++r) {
       const int i = threadIdx.x + 256 * (h + r), c = i / KP, j = i - c * KP;
       wv[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+    }
+    if (h == 0) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int rest = half + 2 * r;
+        if (rest < KP / 2) Xs[xt * KS + (rest >> 1) * 4 + (rest & 1) * 2 + xq] = xv[r];
+      }
     }
 #pragma unroll
     for (int r = 0; r < NB; ++r) {
@@ -1659,7 +1662,7 @@ __global__ __launch_bounds__(256) void k_misfit_bwd_gather(MisfitBwdArgs a) {
 //    registers, then the columns [rj0[cb], rj0[cb+1]) summed from LDS;
 //  - the next flow step's input (integrate's down-sampling, da_4dvar.py:671) at the pixels it samples.
 // The backward pass then never reads a state field again (k_misfit_net_bwd runs on the network grid).
-template <int MR>
+template <int MR, bool XB>
 __global__ __launch_bounds__(384) void k_misfit_grid(MisfitArgs a) {
   extern __shared__ float colsum[];  // [Ws]
   __shared__ double red[6];
@@ -1670,67 +1673,81 @@ __global__ __launch_bounds__(384) void k_misfit_grid(MisfitArgs a) {
   const float sc2 = a.scale2 ? a.scale2[c] : 1.f;
   const float off = a.offset ? a.offset[c] : 0.f;
   const float mean = a.flow_in ? a.mean[c] : 0.f, sd = a.flow_in ? a.std_[c] : 1.f;
-  const float* __restrict__ netc = a.net + (size_t)c * HWl;
+  // every row i of the band up-samples from network row ra (mi[i] == ra by the definition of ri0), so the network
+  // values of a column are the same for the whole band: one gather per column, no per-row map lookup (a per-row
+  // mi[i] load put a dependent wait between the rows' field loads)
+  const float* __restrict__ nrow = a.net + (size_t)c * HWl + (size_t)ra * a.Wl;
+  // the column ranges of the final reduction, loaded up front (after the barrier they would be one more round trip)
+  int cb0[2], cb1[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int cb = min((int)threadIdx.x + u * (int)blockDim.x, a.Wl - 1);
+    cb0[u] = a.rj0[cb];
+    cb1[u] = a.rj0[cb + 1];
+  }
   double acc = 0.0;
   for (int j4 = threadIdx.x; j4 < W4; j4 += blockDim.x) {
     const int j = 4 * j4;
     const int4 q = *reinterpret_cast<const int4*>(a.mj + j);
+    // the flow-input sampling maps of this thread's columns (loaded with the others, not under a store)
+    const int4 fcv = a.flow_in ? *reinterpret_cast<const int4*>(a.colinv + j) : make_int4(-1, -1, -1, -1);
+    const int fcs[4] = {fcv.x, fcv.y, fcv.z, fcv.w};
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     for (int i0 = r0; i0 < r1; i0 += MR) {
-      float4 xv[MR], yv[MR], hv[MR], rv[MR], nv[MR];
-      // every load of the band first (the stores below cannot alias them, but the compiler does not know it)
+      int frs[MR];
+#pragma unroll
+      for (int k = 0; k < MR; ++k) frs[k] = a.flow_in ? a.rowinv[min(i0 + k, r1 - 1)] : -1;
+      // the band's field loads (streamed once: nontemporal), then the column's network values (they wait for mj
+      // only, the oldest load)
+      f4 xv[MR], yv[MR], hv[MR], rv[MR];
 #pragma unroll
       for (int k = 0; k < MR; ++k) {
         const int i = min(i0 + k, r1 - 1);
         const size_t e = ((size_t)c * a.Hs + i) * a.Ws + j;
-        xv[k] = a.xb ? *reinterpret_cast<const float4*>(a.xb + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-        yv[k] = *reinterpret_cast<const float4*>(a.yo + e);
-        hv[k] = *reinterpret_cast<const float4*>(a.Hm + e);
-        rv[k] = *reinterpret_cast<const float4*>(a.R + e);
-        const float* nr = netc + (size_t)a.mi[i] * a.Wl;
-        nv[k] = make_float4(nr[q.x], nr[q.y], nr[q.z], nr[q.w]);
+        if (XB) xv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a.xb + e));
+        yv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a.yo + e));
+        hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a.Hm + e));
+        rv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a.R + e));
+      }
+      const float nn[4] = {nrow[q.x], nrow[q.y], nrow[q.z], nrow[q.w]};
+      float base[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = nn[u] * sc;
+        if (a.scale2) t = t * sc2;
+        base[u] = t;
       }
 #pragma unroll
       for (int k = 0; k < MR; ++k) {
         const int i = i0 + k;
         if (i >= r1) break;
-        const float nn[4] = {nv[k].x, nv[k].y, nv[k].z, nv[k].w};
-        const float xx[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
-        const float yy[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
-        const float hh[4] = {hv[k].x, hv[k].y, hv[k].z, hv[k].w};
-        const float rr[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
         float v[4], g[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           // k_misfit_fwd's arithmetic, element for element
-          float t = nn[u] * sc;
-          if (a.scale2) t = t * sc2;
-          if (a.xb) t = t + xx[u];
+          float t = base[u];
+          if (XB) t = t + xv[k][u];
           if (a.offset) t = t + off;
           v[u] = t;
-          const float d = t - yy[u];
-          acc += (double)((hh[u] * (d * d)) / rr[u]);
-          g[u] = a.coeff * ((hh[u] * d) / rr[u]);
+          const float d = t - yv[k][u];
+          const float ri = 1.0f / rv[k][u];  // one division per element (k_misfit_fwd: two)
+          acc += (double)((hv[k][u] * (d * d)) * ri);
+          g[u] = a.coeff * ((hv[k][u] * d) * ri);
         }
         s0 += g[0];
         s1 += g[1];
         s2 += g[2];
         s3 += g[3];
         const size_t e = ((size_t)c * a.Hs + i) * a.Ws + j;
-        if (a.x_out) *reinterpret_cast<float4*>(a.x_out + e) = make_float4(v[0], v[1], v[2], v[3]);
-        if (a.flow_in) {
-          const int fr = a.rowinv[i];
-          if (fr >= 0) {
+        if (a.x_out) *reinterpret_cast<f4*>(a.x_out + e) = f4{v[0], v[1], v[2], v[3]};
+        if (frs[k] >= 0) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int fc = a.colinv[j + u];
-              if (fc >= 0) a.flow_in[(size_t)c * HWl + (size_t)fr * a.Wl + fc] = (v[u] - mean) / sd;
-            }
-          }
+          for (int u = 0; u < 4; ++u)
+            if (fcs[u] >= 0) a.flow_in[(size_t)c * HWl + (size_t)frs[k] * a.Wl + fcs[u]] = (v[u] - mean) / sd;
         }
       }
     }
-    *reinterpret_cast<float4*>(colsum + j) = make_float4(s0, s1, s2, s3);
+    *reinterpret_cast<f4*>(colsum + j) = f4{s0, s1, s2, s3};
   }
   // J partial of the band
 #pragma unroll
@@ -1745,9 +1762,12 @@ __global__ __launch_bounds__(384) void k_misfit_grid(MisfitArgs a) {
   }
   if (!a.g_net_obs) return;
   // the up-sampling adjoint along the row: network column cb sums its preimage columns
-  for (int cb = threadIdx.x; cb < a.Wl; cb += blockDim.x) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int cb = threadIdx.x + u * blockDim.x;
+    if (cb >= a.Wl) break;
     float g = 0.f;
-    for (int j = a.rj0[cb]; j < a.rj0[cb + 1]; ++j) g += colsum[j];
+    for (int j = cb0[u]; j < cb1[u]; ++j) g += colsum[j];
     a.g_net_obs[(size_t)c * HWl + (size_t)ra * a.Wl + cb] = g;
   }
 }
@@ -1871,11 +1891,22 @@ hipError_t misfit_grid_fwd(const MisfitArgs& a, hipStream_t s) {
       a.Ws > 16384 || (a.flow_in && (!a.rowinv || !a.colinv)))
     return hipErrorInvalidValue;
   for (const void* p : {(const void*)a.xb, (const void*)a.yo, (const void*)a.Hm, (const void*)a.R,
-                        (const void*)a.x_out, (const void*)a.mj})
+                        (const void*)a.x_out, (const void*)a.mj, (const void*)a.colinv})
     if (reinterpret_cast<uintptr_t>(p) & 15) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
   const size_t n = (size_t)a.C * a.Hs * a.Ws;
-  hipLaunchKernelGGL(k_misfit_grid<6>, dim3(a.C * a.Hl), dim3(384), a.Ws * sizeof(float), s, a);
+  if (a.Wl > 2 * 384) return hipErrorInvalidValue;  // two network columns per thread in the final reduction
+  // mr: rows of the band whose loads are in flight together (6: the whole 721 -> 128 band, 152 VGPRs, 3 waves per
+  // SIMD; 3: two passes per band, 5 waves per SIMD)
+  const dim3 g(a.C * a.Hl), b(384);
+  const size_t l = a.Ws * sizeof(float);
+  if (a.mr == 3) {
+    if (a.xb) hipLaunchKernelGGL((k_misfit_grid<3, true>), g, b, l, s, a);
+    else hipLaunchKernelGGL((k_misfit_grid<3, false>), g, b, l, s, a);
+  } else {
+    if (a.xb) hipLaunchKernelGGL((k_misfit_grid<6, true>), g, b, l, s, a);
+    else hipLaunchKernelGGL((k_misfit_grid<6, false>), g, b, l, s, a);
+  }
   // algorithmic bytes: the state fields once (xb, yo, H, R; x when stored)
   prof_end(ph, s, PC_MISFIT, 8.0 * n, 4.0 * n * ((a.xb ? 4 : 3) + (a.x_out ? 1 : 0)));
   return hipGetLastError();

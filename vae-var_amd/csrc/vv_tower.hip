@@ -37,6 +37,17 @@ __device__ __forceinline__ float dgelu_t(float x) { return dgelu_fast(x); }
 __device__ __forceinline__ float sc_of(unsigned mx) { return __uint_as_float((268u - max(mx >> 23, 15u)) << 23); }
 __device__ __forceinline__ float inv_of(unsigned mx) { return __uint_as_float((max(mx >> 23, 15u) - 14u) << 23); }
 __device__ __forceinline__ unsigned amax(unsigned m, float v) { return max(m, __float_as_uint(fabsf(v))); }
+// XCD-aware workgroup order (r05): the tower launches are 1-D over ngroups x nb workgroups, numbered tower-major,
+// and XCD x (workgroups are dealt round-robin to the 8 XCDs, each with its own 4 MB L2) gets a contiguous range of
+// them (vv_gemm.hip xcd_remap's formula), so an XCD streams the weights of at most two towers instead of all six
+// (the dim-192 MLP's fp16x3 weight planes are 1.18 MB per tower, 7.1 MB for six)
+__device__ __forceinline__ void tower_wg(int nb, int ng, int& blk, int& grp) {
+  const int n = nb * ng, bid = blockIdx.x;
+  const int q = n >> 3, r = n & 7, x = bid & 7, l = bid >> 3;
+  const int w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+  grp = w / nb;
+  blk = w - grp * nb;
+}
 // [rows][32 halves] plane blocks: 16-B chunk q of row r at q ^ h((r >> 2) & 3), h = {0, 2, 3, 1}, so the four lane
 // groups of a 16x16x32 fragment read (rows lane & 15, chunk lane >> 4) hit 16 distinct 16-B slots
 __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
@@ -67,7 +78,9 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
   const int tg = wave % NW, hh = wave / NW;  // token group, hidden half
   const int hoff = hh * HH;
-  const MlpGroup G = a.g[blockIdx.z];
+  int blk, grp;
+  tower_wg(a.M / (16 * NW), a.ngroups, blk, grp);
+  const MlpGroup G = a.g[grp];
   u16* A1 = lds + tg * A1W;
   u16* W1 = lds + NW * A1W;
   u16* W2 = W1 + NH * W1S;
@@ -106,7 +119,7 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
         T2b[tid + i * NT] = c2[i];
       }
   }
-  const int t0 = blockIdx.x * 16 * NW + 16 * tg;  // this wave's first token
+  const int t0 = blk * 16 * NW + 16 * tg;  // this wave's first token
 
   // ---- row phase: Y = LN2(x1) (fwd) or dx2 (bwd), scaled per token and split into planes ----
   const int tt = lane >> 2, qd = lane & 3;  // token, quarter of the row
@@ -425,7 +438,9 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
   static_assert(FT >= R && 2 * 64 * LS * 2 <= YB + 4 * RB, "ring / reduction buffers");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
-  const MlpGroup G = a.g[blockIdx.z];
+  int blk, grp;
+  tower_wg(a.M / 64, a.ngroups, blk, grp);
+  const MlpGroup G = a.g[grp];
   u16* Y = lds;
   u16* ring = lds + YB + wave * RB;
   float* T1s = reinterpret_cast<float*>(lds + YB + 4 * RB);
@@ -434,7 +449,7 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
   float* T2b = T2s + C;
   float* Tiy = T2b + C;   // [64] 2^-e of token t's Y row
   float* Tsu = Tiy + 64;  // [64] scale of token t's u values
-  const int t0 = blockIdx.x * 64;
+  const int t0 = blk * 64;
   const int hb = wave * C;  // this wave's hidden units [hb, hb + C)
 
   // fragment F (0..FT-1) of this wave's stream: chunk c = F / FC, then W1 (ks, j, p) and W2 (q, p); lane (row li,
@@ -583,26 +598,37 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int tg = 0; tg < TG; ++tg) acc1[j][tg] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS1; ++ks) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 4) : "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      h8v w[2][2], y[TG][2];
+    // the fragments of step ks + 1 are read under step ks's MFMAs (one exposed LDS latency per GEMM, not per step);
+    // a step's slots are refilled once its fragments are in registers
+    h8v w[2][2], y[TG][2];
+    auto rd1 = [&](int ks, int f0, h8v (&wv)[2][2], h8v (&yv)[TG][2]) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
-          w[j][p] = *reinterpret_cast<const h8v*>(ring + ((F + 2 * j + p) % R) * 512 + lane * 8);
+          wv[j][p] = *reinterpret_cast<const h8v*>(ring + ((f0 + 2 * j + p) % R) * 512 + lane * 8);
 #pragma unroll
       for (int tg = 0; tg < TG; ++tg)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
-          y[tg][p] = *reinterpret_cast<const h8v*>(Y + ((tg * KS1 + ks) * 2 + p) * 512 + lane * 8);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
+          yv[tg][p] = *reinterpret_cast<const h8v*>(Y + ((tg * KS1 + ks) * 2 + p) * 512 + lane * 8);
+    };
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 4) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    rd1(0, F, w, y);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) issue(F + R + k);
       F += 4;
+      h8v wn[2][2], yn[TG][2];
+      if (ks + 1 < KS1) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 4) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        rd1(ks + 1, F, wn, yn);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < 3; ++pr)
@@ -612,6 +638,19 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
           for (int tg = 0; tg < TG; ++tg)
             acc1[j][tg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[j][pr == 0 ? 1 : 0], y[tg][pr == 1 ? 1 : 0],
                                                                  acc1[j][tg], 0, 0, 0);
+      if (ks + 1 < KS1) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) w[j][p] = wn[j][p];
+#pragma unroll
+        for (int tg = 0; tg < TG; ++tg)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) y[tg][p] = yn[tg][p];
+      }
     }
     // epilogue 1: lane (token li of group tg, g4) holds hidden hc + 4 j + i in acc1[j][tg][i]
     const f4 s1a = *reinterpret_cast<const f4*>(T1s + hc), s1b = *reinterpret_cast<const f4*>(T1s + hc + 4);
@@ -652,25 +691,39 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
       }
     }
     // GEMM2^T: rows = output channels 16 q + 4 g4 + i, columns = tokens; acc2 += W2 . u
+    h8v w2c[2];
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) w2c[p] = *reinterpret_cast<const h8v*>(ring + ((F + p) % R) * 512 + lane * 8);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      h8v w[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) w[p] = *reinterpret_cast<const h8v*>(ring + ((F + p) % R) * 512 + lane * 8);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
       issue(F + R);
       issue(F + R + 1);
       F += 2;
+      h8v w2n[2];
+      if (q + 1 < NQ) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) w2n[p] = *reinterpret_cast<const h8v*>(ring + ((F + p) % R) * 512 + lane * 8);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < 3; ++pr)
 #pragma unroll
         for (int tg = 0; tg < TG; ++tg)
-          acc2[q][tg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[pr == 0 ? 1 : 0], ub[tg][pr == 1 ? 1 : 0], acc2[q][tg],
-                                                               0, 0, 0);
+          acc2[q][tg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2c[pr == 0 ? 1 : 0], ub[tg][pr == 1 ? 1 : 0],
+                                                               acc2[q][tg], 0, 0, 0);
+      if (q + 1 < NQ) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        w2c[0] = w2n[0];
+        w2c[1] = w2n[1];
+      }
     }
   }
 
@@ -771,7 +824,7 @@ hipError_t launch_mlpw(const MlpArgs& a, hipStream_t s) {
   constexpr size_t lds = 2 * ((size_t)4 * (C / 32) * 2 * 512 + 4 * 24 * 512) + 4 * (8 * C + 2 * C + 128);
   static_assert(lds <= 163840, "LDS");
   if (hipError_t e = set_lds_limit((const void*)k_mlpw<C, FWD>, lds)) return e;
-  hipLaunchKernelGGL((k_mlpw<C, FWD>), dim3(a.M / 64, 1, a.ngroups), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((k_mlpw<C, FWD>), dim3(a.M / 64 * a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
@@ -782,7 +835,7 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
   static_assert(C != 96 || lds <= 163840 / 3, "three dim-96 workgroups per CU");
   static_assert(lds <= 163840, "LDS");
   if (hipError_t e = set_lds_limit((const void*)k_mlp<C, NW, HC, FWD, NH>, lds)) return e;
-  hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD, NH>), dim3(a.M / (16 * NW), 1, a.ngroups), dim3(64 * NW * NH), lds, s, a);
+  hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD, NH>), dim3(a.M / (16 * NW) * a.ngroups), dim3(64 * NW * NH), lds, s, a);
   return hipGetLastError();
 }
 
@@ -809,7 +862,9 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
   static_assert(PC * NT == 8 * C, "staging split");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
-  const AblkGroup G = a.g[blockIdx.z];
+  int blk, grp;
+  tower_wg(a.M / 64, a.ngroups, blk, grp);
+  const AblkGroup G = a.g[grp];
   u16* Ypl = lds + wave * YW;
   u16* Wc = lds + NW * YW;
   float* fl = reinterpret_cast<float*>(Wc + WCH);
@@ -820,7 +875,7 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
   float* Tqb = Tqs + 3 * C;      // qkv bias [3C]
   float* Tps = Tqb + 3 * C;      // proj row scales [C]
   float* Tpb = Tps + C;          // proj bias [C]
-  const int win = blockIdx.x * NW + wave;  // this wave's window (over the batch)
+  const int win = blk * NW + wave;  // this wave's window (over the batch)
   const int r0 = win * 16;                 // its first window-order row
 
   {  // every table load issued before the first LDS store (one memory round trip)
@@ -1153,7 +1208,9 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   static_assert(PC * NT == 8 * C, "staging split");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
-  const AblkGroup G = a.g[blockIdx.z];
+  int blk, grp;
+  tower_wg(a.M / 64, a.ngroups, blk, grp);
+  const AblkGroup G = a.g[grp];
   u16* Dpl = lds + wave * YW;
   u16* Wc = lds + NW * YW;
   float* fl = reinterpret_cast<float*>(Wc + WCH);
@@ -1164,7 +1221,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   float* pb = sb + 16 * SS;        // [16][SS] P
   float* Tos = fl + NW * PWAVE;    // proj^T row scales [C]
   float* Tqs = Tos + C;            // qkv^T row scales [C]
-  const int win = blockIdx.x * NW + wave;
+  const int win = blk * NW + wave;
   const int r0 = win * 16;
   {
     constexpr int N1 = (C + NT - 1) / NT;
@@ -1467,7 +1524,7 @@ hipError_t launch_ablk_bwd(const AblkArgs& a, hipStream_t s) {
   constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
                          4 * ((size_t)NW * (3 * 16 * 36 + 2 * 16 * 17) + 2 * C);
   if (hipError_t e = set_lds_limit((const void*)k_ablk_bwd<C>, lds)) return e;
-  hipLaunchKernelGGL(k_ablk_bwd<C>, dim3(a.M / (16 * NW), 1, a.ngroups), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(k_ablk_bwd<C>, dim3(a.M / (16 * NW) * a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1477,7 +1534,7 @@ hipError_t launch_ablk_fwd(const AblkArgs& a, hipStream_t s) {
   constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
                          4 * ((size_t)NW * (16 * 36 + 16 * 16) + H * 49 + 8 * C);
   if (hipError_t e = set_lds_limit((const void*)k_ablk_fwd<C>, lds)) return e;
-  hipLaunchKernelGGL(k_ablk_fwd<C>, dim3(a.M / (16 * NW), 1, a.ngroups), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(k_ablk_fwd<C>, dim3(a.M / (16 * NW) * a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
