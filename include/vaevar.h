@@ -254,7 +254,7 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
    inverse window map, 1), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
    the misfit reads each state field once per evaluation and its adjoint runs on the network grid, k_misfit_grid /
-   k_misfit_net_bwd; 2 = the same with 3 rows of a band in flight per pass instead of 6; read by vv_bind_problem, 1), "mlp_w" (the fused Swin-tower MLP with its hidden layer split over
+   k_misfit_net_bwd, 3 rows of a band in flight per pass; 2 = the same with 6 rows; read by vv_bind_problem, 1), "mlp_w" (the fused Swin-tower MLP with its hidden layer split over
    the four waves of a 64-token workgroup, per-wave LDS-DMA weight rings and one u scale per token, k_mlpw: bit 0 at
    dim 96, bit 1 at dim 192, 0: correct, measured no faster than k_mlp). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key, or a value the dispatch does not accept (switches 0 / 1; "mlp_hc"

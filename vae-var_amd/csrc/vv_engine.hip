@@ -277,7 +277,7 @@ struct Problem {
   // grid_fused (interpolated grids with Hs >= Hl, Ws >= Wl, synthetic observations): the misfit reads each state
   // field once per evaluation (k_misfit_grid) and its adjoint runs on the network grid (k_misfit_net_bwd)
   bool grid_fused = false;
-  int grid_mr = 6;                           // k_misfit_grid rows in flight per pass
+  int grid_mr = 3;                           // k_misfit_grid rows in flight per pass
   int *rowinv = nullptr, *colinv = nullptr;  // [Hs] / [Ws]: inverse of di / dj, -1 off the sampled rows / columns
   int *cr0 = nullptr, *cc0 = nullptr;        // [Hl+1] / [Wl+1]: ranges of mi[di[.]] / mj[dj[.]]
   float* GON = nullptr;                      // (B,T,C,Hl,Wl): coeff * Up^T(H (x_t - yo_t) / R_t)
@@ -2052,7 +2052,7 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
       aligned = aligned && !(reinterpret_cast<uintptr_t>(p) & 15);
     P.grid_fused = P.interp && ctx->tune.grid_fused && Hs >= P.Hl && Ws >= P.Wl && Ws % 4 == 0 && Ws <= 16384 && aligned;
     if (P.grid_fused) P.nblk = C * P.Hl;  // one J partial per (channel, network row) workgroup of k_misfit_grid
-    P.grid_mr = ctx->tune.grid_fused == 2 ? 3 : 6;
+    P.grid_mr = ctx->tune.grid_fused == 2 ? 6 : 3;
   }
   const size_t CHW = (size_t)C * Hs * Ws;
   const size_t HWl = (size_t)P.Hl * P.Wl;

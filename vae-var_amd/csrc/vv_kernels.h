@@ -54,7 +54,8 @@ struct Tuning {
                                 // but not faster (dim 192: 64.7 / 72.5 vs 66.7 / 67.4 us; profiles/r05/knob_ab_*), off
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
                                 // adjoint k_misfit_net_bwd (0: k_misfit_fwd / k_misfit_bwd_gather / k_flow_input(_adj));
-                                // 1: 6 rows of a band in flight per pass, 2: 3 rows (two passes, more waves per SIMD);
+                                // 1: 3 rows of a band in flight per pass (more waves per SIMD), 2: 6 rows (r05: misfit
+                                // class 0.404 vs 0.480 ms / eval at 721x1440, profiles/r05/knob_ab_grid_mr_r05g.jsonl);
                                 // read by vv_bind_problem
 };
 extern const Tuning kDefaultTuning;
@@ -352,7 +353,7 @@ struct MisfitArgs {
   const int* colinv;      // [Ws]
   float* g_net_obs;       // null or (C,Hl,Wl): coeff * Up^T(H (x-yo)/R)
   float coeff;
-  int mr;                 // rows in flight per pass (Tuning.grid_fused: 1 -> 6, 2 -> 3)
+  int mr;                 // rows in flight per pass (Tuning.grid_fused: 1 -> 3, 2 -> 6)
 };
 
 hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s);
