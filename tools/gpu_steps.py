@@ -17,6 +17,7 @@ steps (one shell word each; arguments after ':' are split on whitespace):
                           ARGS containing --trace, as kernel_trace.csv)
   pmc:COUNTER[:ARGS]      rocprofv3 --pmc COUNTER of bench.py ARGS (one counter group per pass); keeps counter_collection.csv
   py:SCRIPT[:ARGS]        python SCRIPT ARGS (tools/quick_time.py, tools/h5_check.py, ...)
+  pyenv:K=V[,K=V]:SCRIPT[:ARGS]  the same with extra environment (e.g. VAEVAR_LIB=vae-var_amd/vaevar/ab/x.so)
 """
 from __future__ import annotations
 
@@ -27,7 +28,8 @@ import subprocess
 import sys
 import time
 
-LIMIT = {"tests": 1000, "smoke": 200, "bench": 420, "ab": 900, "env": 420, "rocprof": 420, "pmc": 300, "py": 420}
+LIMIT = {"tests": 1000, "smoke": 200, "bench": 420, "ab": 900, "env": 420, "rocprof": 420, "pmc": 300, "py": 420,
+         "pyenv": 420}
 
 
 def run(cmd, out, limit, env=None):
@@ -93,6 +95,11 @@ def main():
         elif kind == "py":
             script, _, args = rest.partition(":")
             rc = run([py, "-u", script] + args.split(), base + ".log", lim)
+        elif kind == "pyenv":
+            kv, _, r2 = rest.partition(":")
+            script, _, args = r2.partition(":")
+            env = dict(x.split("=", 1) for x in kv.split(",") if x)
+            rc = run([py, "-u", script] + args.split(), base + ".log", lim, env)
         else:
             sys.exit(f"unknown step {st!r}")
         if rc:
