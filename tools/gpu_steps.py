@@ -18,6 +18,10 @@ steps (one shell word each; arguments after ':' are split on whitespace):
   pmc:COUNTER[:ARGS]      rocprofv3 --pmc COUNTER of bench.py ARGS (one counter group per pass); keeps counter_collection.csv
   py:SCRIPT[:ARGS]        python SCRIPT ARGS (tools/quick_time.py, tools/h5_check.py, ...)
   pyenv:K=V[,K=V]:SCRIPT[:ARGS]  the same with extra environment (e.g. VAEVAR_LIB=vae-var_amd/vaevar/ab/x.so)
+  ktrace:SCRIPT[:ARGS]    rocprofv3 --kernel-trace of python SCRIPT ARGS, summarised per (kernel, grid) by tools/kstats.py
+                          into NN_ktrace.txt (the trace itself is not kept)
+  kseq:MARKER:SCRIPT[:ARGS]  the same, listed launch by launch after the second-to-last MARKER kernel
+                          (tools/ktrace_seq.py) into NN_kseq.txt
 """
 from __future__ import annotations
 
@@ -29,7 +33,7 @@ import sys
 import time
 
 LIMIT = {"tests": 1000, "smoke": 200, "bench": 420, "ab": 900, "env": 420, "rocprof": 420, "pmc": 300, "py": 420,
-         "pyenv": 420}
+         "pyenv": 420, "ktrace": 420, "kseq": 420}
 
 
 def run(cmd, out, limit, env=None):
@@ -91,6 +95,21 @@ def main():
                     ((("*kernel_trace.csv", "kernel_trace.csv"),) if "--trace" in args.split() else ()):
                 for f in glob.glob(os.path.join(d, "**", pat), recursive=True):
                     shutil.copy(f, f"{base}_{name}")
+            shutil.rmtree(d, ignore_errors=True)
+        elif kind in ("ktrace", "kseq"):
+            marker = None
+            if kind == "kseq":
+                marker, _, rest = rest.partition(":")
+            script, _, args = rest.partition(":")
+            d = base + "_rp"
+            cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--", py, "-u",
+                   script] + args.split()
+            rc = run(cmd, base + ".log", lim)
+            if rc == 0:
+                tr = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+                tool = [os.path.join(root, "tools", "kstats.py"), tr[0]] if tr and not marker else \
+                    [os.path.join(root, "tools", "ktrace_seq.py"), tr[0], marker, "700"] if tr else None
+                rc = run([py] + tool, base + ".txt", 120) if tool else 1
             shutil.rmtree(d, ignore_errors=True)
         elif kind == "py":
             script, _, args = rest.partition(":")

@@ -1291,7 +1291,9 @@ __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
   const int OS = C + 4;                             // row stride of the per-wave output staging (floats)
   float* Xs = sm;             // [64][KS]
   float* Wsm = Xs + PT * KS;  // [C][KS]
-  float* Os = Wsm + C * KS;   // [4 waves][16][OS]: D + bias, rows = tokens, for whole-row float4 stores
+  float* Os = sm;             // [4 waves][16][OS]: D + bias, rows = tokens, for whole-row float4 stores; over Xs / Wsm
+                              // once every wave's MFMAs are done (r05: separate, it cost the KPM 64 / 112 launches
+                              // a resident workgroup per CU -- 1.5 and 3 rounds of 768 workgroups)
   const int t0 = blockIdx.x * PT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tb = wave * 16;  // this wave's 16 tokens within the workgroup: one contiguous [16][C] block of rows
@@ -1376,6 +1378,7 @@ __global__ __launch_bounds__(256) void k_p2t_mf(PatchArgs a) {
   }
   // lane (channel n 16 + li, g) holds tokens 4 g + r: (D + bias) into the wave's staging rows, then read back as the
   // wave's contiguous [16][C] block, float4 per lane, + pos: whole 1-KB row runs per store instruction
+  __syncthreads();  // every wave's Xs / Wsm reads are done: the staging rows overlay them
   float* O = Os + wave * 16 * OS;
 #pragma unroll
   for (int n = 0; n < NTM; ++n) {
@@ -1502,10 +1505,10 @@ template <int MODE, int KPM>
 static hipError_t p2t_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   const int KS = (kc + 15) / 16 * 16 + 4;
-  const size_t lds = ((size_t)(PT + a.Ctok) * KS + (size_t)PT * (a.Ctok + 4)) * sizeof(float);
+  const size_t lds = std::max((size_t)(PT + a.Ctok) * KS, (size_t)PT * (a.Ctok + 4)) * sizeof(float);
   if (lds > 64 * 1024)
     if (hipError_t e = set_lds_limit((const void*)k_p2t_mf<MODE, KPM>,
-                                     ((size_t)(PT + kPatchCmax) * (KPM + 4) + (size_t)PT * (kPatchCmax + 4)) * 4))
+                                     std::max((size_t)(PT + kPatchCmax) * (KPM + 4), (size_t)PT * (kPatchCmax + 4)) * 4))
       return e;
   hipLaunchKernelGGL((k_p2t_mf<MODE, KPM>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
@@ -1589,12 +1592,57 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
   return t;
 }
 
+// V4 (r05): same-grid states (no maps) with HW % 4 == 0 and 16-B aligned fields, four consecutive elements per thread
+// and float4 accesses (the per-element arithmetic unchanged; the J partial sums its terms in a different order)
+template <bool V4>
 __global__ __launch_bounds__(256) void k_misfit_fwd(MisfitArgs a) {
   __shared__ double red[4];
   const int HW = a.Hs * a.Ws;
   const int n = a.C * HW;
   const int HWl = a.Hl * a.Wl;
   double acc = 0.0;
+  if (V4) {
+    for (int id = 4 * (blockIdx.x * 256 + threadIdx.x); id < n; id += gridDim.x * 1024) {
+      const int c = id / HW;
+      const int p = id - c * HW;
+      const f4 nv = *reinterpret_cast<const f4*>(a.net + (size_t)c * HWl + p);
+      const float s1 = a.scale[c], s2 = a.scale2 ? a.scale2[c] : 1.f, of = a.offset ? a.offset[c] : 0.f;
+      const f4 xb = a.xb ? *reinterpret_cast<const f4*>(a.xb + id) : f4{0.f, 0.f, 0.f, 0.f};
+      f4 yo, hm, rr;
+      if (a.Hm) {
+        yo = *reinterpret_cast<const f4*>(a.yo + id);
+        hm = *reinterpret_cast<const f4*>(a.Hm + id);
+        rr = *reinterpret_cast<const f4*>(a.R + id);
+      }
+      f4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = nv[e] * s1;
+        if (a.scale2) t = t * s2;
+        if (a.xb) t = t + xb[e];
+        if (a.offset) t = t + of;
+        v[e] = t;
+      }
+      *reinterpret_cast<f4*>(a.x_out + id) = v;
+      if (a.flow_in) {
+        const float mu = a.mean[c], sd = a.std_[c];
+        f4 fi;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) fi[e] = (v[e] - mu) / sd;
+        *reinterpret_cast<f4*>(a.flow_in + id) = fi;
+      }
+      if (a.Hm) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[e] - yo[e];
+          acc += (double)((hm[e] * (d * d)) / rr[e]);
+        }
+      }
+    }
+    const double t = block_sum(acc, red);
+    if (threadIdx.x == 0) a.partial[blockIdx.x] = t;
+    return;
+  }
   for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
     const int c = id / HW;
     const int p = id - c * HW;
@@ -1618,9 +1666,34 @@ __global__ __launch_bounds__(256) void k_misfit_fwd(MisfitArgs a) {
   if (threadIdx.x == 0) a.partial[blockIdx.x] = t;
 }
 
+template <bool V4>
 __global__ __launch_bounds__(256) void k_misfit_bwd(MisfitBwdArgs a) {
   const int HW = a.Hs * a.Ws;
   const int n = a.C * HW;
+  if (V4) {  // as k_misfit_fwd<true>: four consecutive elements per thread, float4 accesses, same arithmetic
+    for (int id = 4 * (blockIdx.x * 256 + threadIdx.x); id < n; id += gridDim.x * 1024) {
+      const int c = id / HW;
+      f4 g;
+      if (a.g_obs) {
+        g = *reinterpret_cast<const f4*>(a.g_obs + id);
+      } else {
+        const f4 hm = *reinterpret_cast<const f4*>(a.Hm + id), x = *reinterpret_cast<const f4*>(a.x + id),
+                 yo = *reinterpret_cast<const f4*>(a.yo + id), rr = *reinterpret_cast<const f4*>(a.R + id);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = a.coeff * ((hm[e] * (x[e] - yo[e])) / rr[e]);
+      }
+      if (a.g_carry) {
+        const f4 gc = *reinterpret_cast<const f4*>(a.g_carry + id);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] += gc[e];
+      }
+      const float sc = a.scale[c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g[e] = g[e] * sc;
+      *reinterpret_cast<f4*>(a.g_net + id) = g;
+    }
+    return;
+  }
   for (int id = blockIdx.x * 256 + threadIdx.x; id < n; id += gridDim.x * 256) {
     const int c = id / HW;
     const int p = id - c * HW;
@@ -1882,7 +1955,12 @@ hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
   if ((a.mi == nullptr) != (a.mj == nullptr)) return hipErrorInvalidValue;
   if (!a.mi && (a.Hs != a.Hl || a.Ws != a.Wl)) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
-  hipLaunchKernelGGL(k_misfit_fwd, dim3(a.nblk), dim3(256), 0, s, a);
+  bool v4 = !a.mi && (a.Hs * a.Ws) % 4 == 0;
+  for (const void* p : {(const void*)a.net, (const void*)a.xb, (const void*)a.yo, (const void*)a.Hm, (const void*)a.R,
+                        (const void*)a.x_out, (const void*)a.flow_in})
+    v4 = v4 && !(reinterpret_cast<uintptr_t>(p) & 15);
+  if (v4) hipLaunchKernelGGL(k_misfit_fwd<true>, dim3(a.nblk), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_misfit_fwd<false>, dim3(a.nblk), dim3(256), 0, s, a);
   prof_end(ph, s, PC_MISFIT, 6.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * ((a.xb ? 6 : 5) + (a.flow_in ? 1 : 0)));
   return hipGetLastError();
 }
@@ -1925,7 +2003,12 @@ hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_misfit_bwd_gather, dim3(1024), dim3(256), 0, s, a);
   } else {
     if (a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_misfit_bwd, dim3(1024), dim3(256), 0, s, a);
+    bool v4 = (a.Hs * a.Ws) % 4 == 0;
+    for (const void* p : {(const void*)a.g_obs, (const void*)a.Hm, (const void*)a.x, (const void*)a.yo, (const void*)a.R,
+                          (const void*)a.g_carry, (const void*)a.g_net})
+      v4 = v4 && !(reinterpret_cast<uintptr_t>(p) & 15);
+    if (v4) hipLaunchKernelGGL(k_misfit_bwd<true>, dim3(1024), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_misfit_bwd<false>, dim3(1024), dim3(256), 0, s, a);
   }
   prof_end(ph, s, PC_MISFIT, 5.0 * a.C * a.Hs * a.Ws, 4.0 * a.C * a.Hs * a.Ws * (a.g_carry ? 6 : 5));
   return hipGetLastError();
@@ -2229,6 +2312,19 @@ __global__ __launch_bounds__(256) void k_twoloop_axpy_dot(float* y, const float*
                                                           const float* next, double* part_out) {
   __shared__ double red[4], red2[4];
   __shared__ float coef;
+  // this thread's first PF elements are loaded before the pending dot is finished (they do not depend on the
+  // coefficient): the partials' reduction no longer sits in front of the vector loads (r05). Same elements, same
+  // order of the d accumulation as the plain grid-stride loop below.
+  constexpr int PF = 4;
+  const int64_t k0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  float yv[PF], xv[PF], nv[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int64_t k = k0 + j * stride;
+    yv[j] = k < n ? y[k] : 0.f;
+    xv[j] = k < n ? x[k] : 0.f;
+    nv[j] = next && k < n ? next[k] : 0.f;
+  }
   double acc = 0.0;
   for (int j = threadIdx.x; j < nblk; j += 256) acc += part_in[j];
   const double t = block_sum(acc, red);
@@ -2244,7 +2340,16 @@ __global__ __launch_bounds__(256) void k_twoloop_axpy_dot(float* y, const float*
   __syncthreads();
   const float a = coef;
   double d = 0.0;
-  for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int64_t k = k0 + j * stride;
+    if (k < n) {
+      const float v = yv[j] + a * xv[j];
+      y[k] = v;
+      if (next) d += (double)nv[j] * (double)v;
+    }
+  }
+  for (int64_t k = k0 + PF * stride; k < n; k += stride) {
     const float v = y[k] + a * x[k];
     y[k] = v;
     if (next) d += (double)next[k] * (double)v;

@@ -31,6 +31,31 @@ typedef unsigned u4v __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+#ifdef VV_TRACE
+// Development builds only (make EXTRA=-DVV_TRACE, tools/tower_trace.py): wave 0 of every workgroup records the shader
+// clock at fixed points of the tower kernels into vv_trace_buf[region][workgroup][64] (slot 0..2: realtime at entry,
+// HW_ID, XCC_ID; the rest s_memtime), vector stores from lane 0; the product build has none of it.
+__device__ unsigned long long* vv_trace_buf;
+#define VV_TR(region, slot)                                                                                       \
+  do {                                                                                                            \
+    unsigned long long* tb_ = vv_trace_buf;                                                                       \
+    if (tb_ && threadIdx.x == 0) {                                                                                \
+      tb_ += ((size_t)(region) * 2048 + blockIdx.x) * 64;                                                         \
+      if ((slot) == 3) {                                                                                          \
+        tb_[0] = __builtin_amdgcn_s_memrealtime();                                                                \
+        tb_[1] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                             \
+        tb_[2] = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));                                            \
+      }                                                                                                           \
+      tb_[slot] = __builtin_readcyclecounter();                                                                   \
+      if ((slot) == 63) tb_[62] = __builtin_amdgcn_s_memrealtime();                                               \
+    }                                                                                                             \
+  } while (0)
+#else
+#define VV_TR(region, slot) \
+  do {                      \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float gelu_t(float x) { return gelu_fast(x); }  // vv_gelu.h
 __device__ __forceinline__ float dgelu_t(float x) { return dgelu_fast(x); }
 // fp16x3 row scale 2^(141 - E) of a row whose largest |value| has bit pattern mx, and its inverse 2^(E - 141)
@@ -56,6 +81,9 @@ __device__ __forceinline__ int frag(int r, int q) { return r * 32 + ((q ^ hsw(r 
 #define VV_MLP_BLOCK_PAD 32  // halves (64 B); 0 = the unpadded r03 layout (A/B builds)
 #endif
 constexpr int kMlpBlockPad = VV_MLP_BLOCK_PAD;
+// k_ablk_fwd's per-wave v buffer row stride (floats): 32, not 36, so that three dim-96 workgroups fit a CU's LDS (the v
+// rows are read as broadcasts, 4 addresses per instruction; only the 6 row stores per wave take a 4-way conflict)
+constexpr int kAblkHBS = 32;
 
 // NH = 2 splits the hidden layer between two waves per 16 tokens (wave hh runs hidden units [hh 2C, hh 2C + 2C)):
 // twice the waves per CU for the same LDS weight stream, the two partial fc2 sums added through LDS at the end.
@@ -75,6 +103,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   static_assert(C % 32 == 0 && HC % 32 == 0 && HH % HC == 0 && CQ % 4 == 0 && (NH == 1 || NH == 2), "shape");
   static_assert(NH == 1 || NW * NQ * 64 * 16 <= 2 * NH * (W1S + W2S), "fc2 partial sums fit the weight buffers");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  constexpr int TRR = (C == 96 ? 0 : 4) + (FWD ? 0 : 1);  // trace region (VV_TRACE builds)
+  VV_TR(TRR, 3);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
   const int tg = wave % NW, hh = wave / NW;  // token group, hidden half
   const int hoff = hh * HH;
@@ -91,6 +121,46 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   float* T1b = T1s + 4 * C;
   float* T2s = T1b + 4 * C;
   float* T2b = T2s + C;
+  const int t0 = blk * 16 * NW + 16 * tg;  // this wave's first token
+
+  // prologue (r05): the token rows, then chunk 0's weights, then the tables, all in flight together (r04 order:
+  // tables, rows, weights -- three memory round trips before the first chunk; tools/tower_trace.py)
+  const int tt = lane >> 2, qd = lane & 3;  // token, quarter of the row
+  f4 yv[CQ / 4];
+  {
+    const f4* src = reinterpret_cast<const f4*>((FWD ? G.x : G.dy) + (size_t)(t0 + tt) * C + qd * CQ);
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
+  }
+  // weight chunks: global -> registers one chunk ahead (every load of a chunk in flight at once, under the
+  // previous chunk's MFMAs), registers -> LDS between two barriers
+  constexpr int P1 = NH * HC * KS1 * 8 / NT, P2 = NH * C * KS2 * 16 / NT;
+  static_assert(P1 * NT == NH * HC * KS1 * 8 && P2 * NT == NH * C * KS2 * 16, "staging split");
+  u4v r1[P1];
+  u2v r2[P2];
+  // W1 chunk: rows c HC + r, the whole K = C; global row = KS1 x [h(32) | l(32)]. W2 chunk: rows n < C, hidden units
+  // [c HC, c HC + HC) in the order of the u fragments: position 8 g + e of k-step kk holds hidden
+  // 32 kk + (e < 4 ? 4 g + e : 16 + 4 g + e - 4). (Plain unrolled loops, no lambdas: the staging registers must
+  // not become a stack array.)
+#define VV_MLP_LOAD(c)                                                                                            \
+  {                                                                                                               \
+    _Pragma("unroll") for (int i = 0; i < P1; ++i) {                                                             \
+      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8), rh = r / HC, rl = r - rh * HC;     \
+      r1[i] = *reinterpret_cast<const u4v*>(G.w1h + (size_t)(rh * HH + (c) * HC + rl) * 2 * C + (rem >> 3) * 64 + \
+                                              ((rem >> 2) & 1) * 32 + (rem & 3) * 8);                             \
+    }                                                                                                             \
+    _Pragma("unroll") for (int i = 0; i < P2; ++i) {                                                             \
+      const int e0 = tid + i * NT, eh = e0 / (C * KS2 * 16), e = e0 - eh * (C * KS2 * 16), n = e / (KS2 * 16),   \
+                rem = e - n * (KS2 * 16);                                                                         \
+      r2[i] = *reinterpret_cast<const u2v*>(G.w2h + (size_t)n * 2 * (4 * C) +                                   \
+                                              (eh * (HH / 32) + (c) * KS2 + (rem >> 4)) * 64 +                   \
+                                              ((rem >> 3) & 1) * 32 + 4 * ((rem >> 1) & 3) + 16 * (rem & 1));     \
+    }                                                                                                             \
+  }
+  // (the forward loads chunk 0's weights after its row phase: at dim 192 they would spill beside gamma / beta, at dim 96
+  // the earlier issue measured 2.7 K cycles slower, tools/tower_trace.py)
+  constexpr bool kEarlyW = !FWD;
+  if (kEarlyW) VV_MLP_LOAD(0)
   {  // every table load issued before the first LDS store (one memory round trip)
     constexpr int N1 = (4 * C + NT - 1) / NT, N2 = (C + NT - 1) / NT;
     float a1[N1], c1[N1], a2[N2], c2[N2];
@@ -119,16 +189,9 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
         T2b[tid + i * NT] = c2[i];
       }
   }
-  const int t0 = blk * 16 * NW + 16 * tg;  // this wave's first token
-
   // ---- row phase: Y = LN2(x1) (fwd) or dx2 (bwd), scaled per token and split into planes ----
-  const int tt = lane >> 2, qd = lane & 3;  // token, quarter of the row
   float iy_own;                             // 2^-e of token tt's Y row
   {
-    const f4* src = reinterpret_cast<const f4*>((FWD ? G.x : G.dy) + (size_t)(t0 + tt) * C + qd * CQ);
-    f4 yv[CQ / 4];
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
     if (FWD) {
       f4 gv[CQ / 4], bv[CQ / 4];
 #pragma unroll
@@ -190,33 +253,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
   f4 acc2[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) acc2[q] = f4{0.f, 0.f, 0.f, 0.f};
-
-  // weight chunks: global -> registers one chunk ahead (every load of a chunk in flight at once, under the
-  // previous chunk's MFMAs), registers -> LDS between two barriers
-  constexpr int P1 = NH * HC * KS1 * 8 / NT, P2 = NH * C * KS2 * 16 / NT;
-  static_assert(P1 * NT == NH * HC * KS1 * 8 && P2 * NT == NH * C * KS2 * 16, "staging split");
-  u4v r1[P1];
-  u2v r2[P2];
-  // W1 chunk: rows c HC + r, the whole K = C; global row = KS1 x [h(32) | l(32)]. W2 chunk: rows n < C, hidden units
-  // [c HC, c HC + HC) in the order of the u fragments: position 8 g + e of k-step kk holds hidden
-  // 32 kk + (e < 4 ? 4 g + e : 16 + 4 g + e - 4). (Plain unrolled loops, no lambdas: the staging registers must
-  // not become a stack array.)
-#define VV_MLP_LOAD(c)                                                                                            \
-  {                                                                                                               \
-    _Pragma("unroll") for (int i = 0; i < P1; ++i) {                                                             \
-      const int e = tid + i * NT, r = e / (KS1 * 8), rem = e - r * (KS1 * 8), rh = r / HC, rl = r - rh * HC;     \
-      r1[i] = *reinterpret_cast<const u4v*>(G.w1h + (size_t)(rh * HH + (c) * HC + rl) * 2 * C + (rem >> 3) * 64 + \
-                                              ((rem >> 2) & 1) * 32 + (rem & 3) * 8);                             \
-    }                                                                                                             \
-    _Pragma("unroll") for (int i = 0; i < P2; ++i) {                                                             \
-      const int e0 = tid + i * NT, eh = e0 / (C * KS2 * 16), e = e0 - eh * (C * KS2 * 16), n = e / (KS2 * 16),   \
-                rem = e - n * (KS2 * 16);                                                                         \
-      r2[i] = *reinterpret_cast<const u2v*>(G.w2h + (size_t)n * 2 * (4 * C) +                                   \
-                                              (eh * (HH / 32) + (c) * KS2 + (rem >> 4)) * 64 +                   \
-                                              ((rem >> 3) & 1) * 32 + 4 * ((rem >> 1) & 3) + 16 * (rem & 1));     \
-    }                                                                                                             \
-  }
-  VV_MLP_LOAD(0)
+  if (!kEarlyW) VV_MLP_LOAD(0)
+  VV_TR(TRR, 4);
 
   // two chunks per loop trip for the dim-192 forward (the hidden-split backward spills at 2; dim 96 runs faster
   // without: profiles/r04/ab_r04p)
@@ -249,6 +287,7 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
                                 frag(n, (rem >> 1) & 3) + 4 * (rem & 1)) = r2[i];
     }
     __syncthreads();
+    VV_TR(TRR, 5 + 2 * (c & 15));
     if (c + 1 < NC) VV_MLP_LOAD(c + 1)
     float s1[NJ][4];
 #pragma unroll
@@ -329,7 +368,9 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc2[q][i] += tmp[q][i] * iu;
+    VV_TR(TRR, 6 + 2 * (c & 15));
   }
+  VV_TR(TRR, 40);
   if (NH == 2) {  // half 1's fc2 partial sums through LDS (over the weight buffers) to half 0, which finishes
     f4* R = reinterpret_cast<f4*>(W1);
     __syncthreads();
@@ -409,6 +450,7 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
       if (g4 == 0) G.rs[trow] = sc_of(omx);
     }
   }
+  VV_TR(TRR, 63);
 }
 
 #undef VV_MLP_LOAD
@@ -832,7 +874,7 @@ template <int C, int NW, int HC, bool FWD, int NH = 1>
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
   constexpr size_t lds = 2 * ((size_t)NW * (C / 32) * 2 * 16 * 32 + (size_t)NH * (C / 32) * 2 * (HC * 32 + kMlpBlockPad) +
                               (size_t)NH * (HC / 32) * 2 * (C * 32 + kMlpBlockPad)) + 4 * (8 * C + 2 * C);
-  static_assert(C != 96 || lds <= 163840 / 3, "three dim-96 workgroups per CU");
+  static_assert(C != 96 || lds <= 53760, "three dim-96 workgroups per CU (k_ablk_fwd launch: LDS granules)");
   static_assert(lds <= 163840, "LDS");
   if (hipError_t e = set_lds_limit((const void*)k_mlp<C, NW, HC, FWD, NH>, lds)) return e;
   hipLaunchKernelGGL((k_mlp<C, NW, HC, FWD, NH>), dim3(a.M / (16 * NW) * a.ngroups), dim3(64 * NW * NH), lds, s, a);
@@ -855,12 +897,14 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
   constexpr int NW = 4, NT = 256, KS = C / 32, H = C / 32, CQ = C / 4, NQ = C / 16;
   constexpr int YW = KS * 2 * 16 * 32;        // halves of one wave's Y planes
   constexpr int WCH = 8 * C * 8;              // halves of a weight chunk (8 C 16-B pieces)
-  constexpr int HBS = 36;                     // fp32 row stride of the per-wave q / k / v head buffers
+  constexpr int HBS = kAblkHBS;               // fp32 row stride of the per-wave v head buffers
   constexpr int PBS = 16;                     // fp32 row stride of the per-wave P buffer
   constexpr int NSC = 4 * H;                  // chunks: q, k, v rows and proj columns per head
   constexpr int PC = 8 * C / NT;              // 16-B staging pieces per thread and chunk
   static_assert(PC * NT == 8 * C, "staging split");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  constexpr int TRR = C == 96 ? 2 : 6;
+  VV_TR(TRR, 3);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
   int blk, grp;
   tower_wg(a.M / 64, a.ngroups, blk, grp);
@@ -870,14 +914,45 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
   float* fl = reinterpret_cast<float*>(Wc + WCH);
   float* hb = fl + wave * 16 * HBS;                       // [16][HBS]: v of the head
   float* pb = fl + NW * 16 * HBS + wave * 16 * PBS;       // [16][PBS]: P of the head
-  float* tb = fl + NW * (16 * HBS + 16 * PBS);            // [H][49]
-  float* Tqs = tb + H * 49;      // qkv row scales [3C]
+  float* tb = fl + NW * (16 * HBS + 16 * PBS);            // [H][49], padded to 16 B
+  float* Tqs = tb + ((H * 49 + 3) & ~3);  // qkv row scales [3C]
   float* Tqb = Tqs + 3 * C;      // qkv bias [3C]
   float* Tps = Tqb + 3 * C;      // proj row scales [C]
   float* Tpb = Tps + C;          // proj bias [C]
   const int win = blk * NW + wave;  // this wave's window (over the batch)
   const int r0 = win * 16;                 // its first window-order row
 
+  // prologue (r05): the window's token rows, then chunks 0 and 1, then the tables, all in flight together (r04:
+  // tables, weights, rows -- the rows a round trip after the rest; tools/tower_trace.py)
+  const int tt = lane >> 2, qd = lane & 3;
+  f4 yv[CQ / 4];
+  {
+    const size_t prow = (size_t)a.map[r0 + tt];
+    const f4* src = reinterpret_cast<const f4*>(G.x + prow * C + qd * CQ);
+#pragma unroll
+    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
+  }
+  // weight chunk sc = 4 h + part: part < 3 -> rows part C + 32 h + r (r < 32) of the qkv weight, the whole K = C
+  // ([ks][plane][32 rows][32]); part 3 -> k-chunk h of every proj row n < C ([plane][C rows][32])
+  u4v rw[2][PC];
+#define VV_ABLK_LOAD(buf, sc)                                                                                    \
+  {                                                                                                              \
+    const int h_ = (sc) >> 2, part_ = (sc)&3;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < PC; ++i) {                                                            \
+      const int e = tid + i * NT;                                                                                \
+      if (part_ < 3) {                                                                                           \
+        const int r = e / (KS * 8), rem = e - r * (KS * 8);                                                      \
+        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wqh + (size_t)(part_ * C + 32 * h_ + r) * 2 * C +            \
+                                                   (rem >> 3) * 64 + ((rem >> 2) & 1) * 32 + (rem & 3) * 8);     \
+      } else {                                                                                                   \
+        const int n = e >> 3, rem = e & 7;                                                                       \
+        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wph + (size_t)n * 2 * C + h_ * 64 + (rem >> 2) * 32 +         \
+                                                   (rem & 3) * 8);                                               \
+      }                                                                                                          \
+    }                                                                                                            \
+  }
+  VV_ABLK_LOAD(0, 0)
+  VV_ABLK_LOAD(1, 1)
   {  // every table load issued before the first LDS store (one memory round trip)
     constexpr int NB = (H * 49 + NT - 1) / NT, N1 = (3 * C + NT - 1) / NT, N2 = (C + NT - 1) / NT;
     float tv[NB], a1[N1], c1[N1], a2[N2], c2[N2];
@@ -915,38 +990,14 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
       }
   }
 
-  // weight chunk sc = 4 h + part: part < 3 -> rows part C + 32 h + r (r < 32) of the qkv weight, the whole K = C
-  // ([ks][plane][32 rows][32]); part 3 -> k-chunk h of every proj row n < C ([plane][C rows][32])
-  u4v rw[2][PC];
-#define VV_ABLK_LOAD(buf, sc)                                                                                    \
-  {                                                                                                              \
-    const int h_ = (sc) >> 2, part_ = (sc)&3;                                                                    \
-    _Pragma("unroll") for (int i = 0; i < PC; ++i) {                                                            \
-      const int e = tid + i * NT;                                                                                \
-      if (part_ < 3) {                                                                                           \
-        const int r = e / (KS * 8), rem = e - r * (KS * 8);                                                      \
-        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wqh + (size_t)(part_ * C + 32 * h_ + r) * 2 * C +            \
-                                                   (rem >> 3) * 64 + ((rem >> 2) & 1) * 32 + (rem & 3) * 8);     \
-      } else {                                                                                                   \
-        const int n = e >> 3, rem = e & 7;                                                                       \
-        rw[buf][i] = *reinterpret_cast<const u4v*>(G.wph + (size_t)n * 2 * C + h_ * 64 + (rem >> 2) * 32 +         \
-                                                   (rem & 3) * 8);                                               \
-      }                                                                                                          \
-    }                                                                                                            \
-  }
-  VV_ABLK_LOAD(0, 0)
-  VV_ABLK_LOAD(1, 1)
+  VV_TR(TRR, 4);
 
   // ---- LN1 of the window's 16 rows (gathered through the window map), planes in LDS ----
-  const int tt = lane >> 2, qd = lane & 3;
   float iy_own;
   {
-    const size_t prow = (size_t)a.map[r0 + tt];
-    const f4* src = reinterpret_cast<const f4*>(G.x + prow * C + qd * CQ);
-    f4 yv[CQ / 4], gv[CQ / 4], bv[CQ / 4];
+    f4 gv[CQ / 4], bv[CQ / 4];
 #pragma unroll
     for (int v = 0; v < CQ / 4; ++v) {
-      yv[v] = src[v];
       gv[v] = reinterpret_cast<const f4*>(G.n1g + qd * CQ)[v];
       bv[v] = reinterpret_cast<const f4*>(G.n1b + qd * CQ)[v];
     }
@@ -1033,6 +1084,7 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
       VV_ABLK_STORE(0)
     }
     __syncthreads();
+    VV_TR(TRR, 5 + 2 * sc);
     if (sc + 2 < NSC) {
       if (sc & 1) {
         VV_ABLK_LOAD(1, sc + 2)
@@ -1168,6 +1220,7 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
         for (int i = 0; i < 4; ++i) pacc[q][i] += t[i] * io;
       }
     }
+    VV_TR(TRR, 6 + 2 * sc);
   }
 #undef VV_ABLK_STORE
 #undef VV_ABLK_LOAD
@@ -1186,6 +1239,7 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
     for (int i = 0; i < 4; ++i) v[i] = xv[q][i] + (pacc[q][i] * sv[i] + bv[i]);
     *reinterpret_cast<f4*>(G.out + tphys * C + n) = v;
   }
+  VV_TR(TRR, 63);
 }
 
 // Backward of the attention sub-block (the input gradient only, quirk Q5), one wave per window:
@@ -1207,6 +1261,8 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   constexpr int PC = 8 * C / NT;
   static_assert(PC * NT == 8 * C, "staging split");
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  constexpr int TRR = C == 96 ? 3 : 7;
+  VV_TR(TRR, 3);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
   int blk, grp;
   tower_wg(a.M / 64, a.ngroups, blk, grp);
@@ -1223,22 +1279,32 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   float* Tqs = Tos + C;            // qkv^T row scales [C]
   const int win = blk * NW + wave;
   const int r0 = win * 16;
+  // prologue (r05): the window's gx rows, then chunks 0 and 1, then the tables, all in flight together
+  const int tt = lane >> 2, qd = lane & 3;
+  f4 yv[CQ / 4];
   {
-    constexpr int N1 = (C + NT - 1) / NT;
-    float a1[N1], c1[N1];
+    const size_t prow = (size_t)a.map[r0 + tt];
+    const f4* src = reinterpret_cast<const f4*>(G.out + prow * C + qd * CQ);
 #pragma unroll
-    for (int i = 0; i < N1; ++i) {
-      const int r = min(tid + i * NT, C - 1);
-      a1[i] = G.wpts[(size_t)r * (C / 32)];
-      c1[i] = G.wqts[(size_t)r * (3 * C / 32)];
-    }
-#pragma unroll
-    for (int i = 0; i < N1; ++i)
-      if (tid + i * NT < C) {
-        Tos[tid + i * NT] = a1[i];
-        Tqs[tid + i * NT] = c1[i];
-      }
+    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
   }
+  const size_t trow = (size_t)(r0 + li);  // this lane's token, window order
+  // the saved q, k, v rows and P of a head (HBM), loaded three chunks before the head's dO GEMM needs them (r05:
+  // loaded at that chunk, they cost an exposed HBM round trip per head, 40 % of the workgroup's cycles)
+  f4 sq[2], sk[2], sv3[2];
+  float sp[4];
+#define VV_ABWD_SAVED(h_)                                                                                         \
+  {                                                                                                               \
+    const float* qr_ = G.qkv + trow * (3 * C) + (h_)*32;                                                          \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                              \
+      sq[j] = *reinterpret_cast<const f4*>(qr_ + 16 * j + 4 * g4);                                               \
+      sk[j] = *reinterpret_cast<const f4*>(qr_ + C + 16 * j + 4 * g4);                                           \
+      sv3[j] = *reinterpret_cast<const f4*>(qr_ + 2 * C + 16 * j + 4 * g4);                                      \
+    }                                                                                                             \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) sp[i] =                                                        \
+        G.P[(((size_t)win * a.heads + (h_)) * 16 + 4 * g4 + i) * 16 + li];                                       \
+  }
+  VV_ABWD_SAVED(0)
   // chunk sc = 4 h + part: part 0 -> proj^T rows 32 h + r, the whole K = C ([ks][plane][32][32]); part 1..3 ->
   // k-chunk (part - 1) KS + h of every qkv^T row c < C ([plane][C][32])
   u4v rw[2][PC];
@@ -1260,16 +1326,27 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   }
   VV_ABWD_LOAD(0, 0)
   VV_ABWD_LOAD(1, 1)
+  {
+    constexpr int N1 = (C + NT - 1) / NT;
+    float a1[N1], c1[N1];
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      const int r = min(tid + i * NT, C - 1);
+      a1[i] = G.wpts[(size_t)r * (C / 32)];
+      c1[i] = G.wqts[(size_t)r * (3 * C / 32)];
+    }
+#pragma unroll
+    for (int i = 0; i < N1; ++i)
+      if (tid + i * NT < C) {
+        Tos[tid + i * NT] = a1[i];
+        Tqs[tid + i * NT] = c1[i];
+      }
+  }
+  VV_TR(TRR, 4);
 
   // ---- gx rows of the window (gathered), scaled per token and split into planes ----
-  const int tt = lane >> 2, qd = lane & 3;
   float id_own;
   {
-    const size_t prow = (size_t)a.map[r0 + tt];
-    const f4* src = reinterpret_cast<const f4*>(G.out + prow * C + qd * CQ);
-    f4 yv[CQ / 4];
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
     unsigned mx = 0;
 #pragma unroll
     for (int v = 0; v < CQ / 4; ++v)
@@ -1295,7 +1372,6 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
     }
   }
   const float idx1 = __shfl(id_own, li << 2);
-  const size_t trow = (size_t)(r0 + li);
   const size_t tphys = (size_t)a.map[r0 + li];
 
   f4 yacc[NQ];
@@ -1303,6 +1379,13 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   for (int q = 0; q < NQ; ++q) yacc[q] = f4{0.f, 0.f, 0.f, 0.f};
   h8v fh[3], fl8[3];  // dq, dk, dv planes of the head (token li, 8 consecutive channels of the k-step)
   float fi[3] = {0.f, 0.f, 0.f};
+  // fully unrolled at dim 96 (r05): as a loop, the two staging register sets were swapped by copies at the back
+  // edge, which waited for every load in flight (vmcnt(0)) once per chunk (dim 192 unrolled spills)
+  constexpr int ABU = C == 96 ? NSC : 1;
+  constexpr bool kEpf = C == 96;  // epilogue operands prefetched inside the (unrolled) loop
+  f4 exv[NQ], edv[NQ];
+  float2 est = make_float2(0.f, 0.f);
+#pragma unroll ABU
   for (int sc = 0; sc < NSC; ++sc) {
     const int h = sc >> 2, part = sc & 3;
     __syncthreads();
@@ -1323,6 +1406,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
       VV_ABWD_STORE(0)
     }
     __syncthreads();
+    VV_TR(TRR, 5 + 2 * (sc & 15));
     if (sc + 2 < NSC) {
       if (sc & 1) {
         VV_ABWD_LOAD(1, sc + 2)
@@ -1332,17 +1416,16 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
     }
     if (part == 0) {
       // this head's saved q, k, v rows and P (HBM), issued ahead of the dO GEMM
-      const float* qr = G.qkv + trow * (3 * C) + h * 32;
       f4 qv[2], kv[2], vv[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        qv[j] = *reinterpret_cast<const f4*>(qr + 16 * j + 4 * g4);
-        kv[j] = *reinterpret_cast<const f4*>(qr + C + 16 * j + 4 * g4);
-        vv[j] = *reinterpret_cast<const f4*>(qr + 2 * C + 16 * j + 4 * g4);
-      }
       float pv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) pv[i] = G.P[(((size_t)win * a.heads + h) * 16 + 4 * g4 + i) * 16 + li];
+      for (int j = 0; j < 2; ++j) {
+        qv[j] = sq[j];
+        kv[j] = sk[j];
+        vv[j] = sv3[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = sp[i];
       // dO^T rows c = 32 h + 16 j + 4 g4 + i, columns = tokens
       f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -1452,6 +1535,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
         }
       }
     } else {
+      if (part == 1 && h + 1 < H) VV_ABWD_SAVED(h + 1)
       // dY^T k-step (part - 1, h): rows c = 16 q + 4 g4 + i, columns = tokens
       const int p3 = part - 1;
       const h8v bh = p3 == 0 ? fh[0] : (p3 == 1 ? fh[1] : fh[2]);
@@ -1469,11 +1553,23 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
         for (int i = 0; i < 4; ++i) yacc[q][i] += t[i] * bi;
       }
     }
+    VV_TR(TRR, 6 + 2 * (sc & 15));
+    if (kEpf && sc == NSC - 4) {
+      // the epilogue's row operands, three chunks ahead (r05: loaded after the loop they were an exposed HBM round
+      // trip, ~13 K cycles); the last head's attention part is done, so its registers are free
+      est = *reinterpret_cast<const float2*>(G.stats + 2 * trow);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        exv[q] = *reinterpret_cast<const f4*>(G.x + tphys * C + 16 * q + 4 * g4);
+        edv[q] = *reinterpret_cast<const f4*>(G.out + tphys * C + 16 * q + 4 * g4);
+      }
+    }
   }
 #undef VV_ABWD_STORE
 #undef VV_ABWD_LOAD
+#undef VV_ABWD_SAVED
   // ---- LN1 backward over the row (lane: token li, channels 16 q + 4 g4 + i) + the residual gradient ----
-  const float2 st = *reinterpret_cast<const float2*>(G.stats + 2 * trow);
+  const float2 st = kEpf ? est : *reinterpret_cast<const float2*>(G.stats + 2 * trow);
   const float mean = st.x, rstd = st.y;
   float o[NQ][4];
   f4 xv[NQ], gv[NQ];
@@ -1482,7 +1578,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   for (int q = 0; q < NQ; ++q) {
     const int n = 16 * q + 4 * g4;
     const f4 sv = *reinterpret_cast<const f4*>(Tqs + n);
-    xv[q] = *reinterpret_cast<const f4*>(G.x + tphys * C + n);
+    xv[q] = kEpf ? exv[q] : *reinterpret_cast<const f4*>(G.x + tphys * C + n);
     gv[q] = *reinterpret_cast<const f4*>(G.n1g + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1499,7 +1595,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
   const float m1 = s1 / (float)C, m2 = s2 / (float)C;
   f4 dv4[NQ];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) dv4[q] = *reinterpret_cast<const f4*>(G.out + tphys * C + 16 * q + 4 * g4);
+  for (int q = 0; q < NQ; ++q) dv4[q] = kEpf ? edv[q] : *reinterpret_cast<const f4*>(G.out + tphys * C + 16 * q + 4 * g4);
   unsigned omx = 0;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -1516,6 +1612,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
     omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
     if (g4 == 0) G.rs[tphys] = sc_of(omx);
   }
+  VV_TR(TRR, 63);
 }
 
 template <int C>
@@ -1532,7 +1629,10 @@ template <int C>
 hipError_t launch_ablk_fwd(const AblkArgs& a, hipStream_t s) {
   constexpr int NW = 4, KS = C / 32, H = C / 32;
   constexpr size_t lds = 2 * ((size_t)NW * KS * 2 * 16 * 32 + 64 * (size_t)C) +
-                         4 * ((size_t)NW * (16 * 36 + 16 * 16) + H * 49 + 8 * C);
+                         4 * ((size_t)NW * (16 * kAblkHBS + 16 * 16) + ((H * 49 + 3) & ~3) + 8 * C);
+  // three dim-96 workgroups per CU: gfx950 allocates LDS in granules, and 3 x 53,836 B measured 2 per CU
+  // (tools/tower_trace.py, r05) while 3 x 53,504 B (k_mlp<96>) gives 3; 53,760 B is the largest size both fit
+  static_assert(C != 96 || lds <= 53760, "three dim-96 workgroups per CU");
   if (hipError_t e = set_lds_limit((const void*)k_ablk_fwd<C>, lds)) return e;
   hipLaunchKernelGGL(k_ablk_fwd<C>, dim3(a.M / (16 * NW) * a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
@@ -1605,5 +1705,13 @@ hipError_t ablk_bwd(const AblkArgs& a, hipStream_t s) {
   return e;
 }
 hipError_t mlp_bwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, false); }
+
+#ifdef VV_TRACE
+// tools/tower_trace.py: point the tower kernels' clock records at buf (8 regions x 2048 workgroups x 64 u64; null: off)
+extern "C" __attribute__((visibility("default"))) int vv_debug_tower_trace(void* buf) {
+  unsigned long long* p = static_cast<unsigned long long*>(buf);
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(vv_trace_buf), &p, sizeof(p));
+}
+#endif
 
 }  // namespace vv
