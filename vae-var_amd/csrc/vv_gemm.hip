@@ -2428,7 +2428,7 @@ bool tuning_value_ok(const char* key, int v) {
   return v == 0 || v == 1;  // every other knob is a switch
 }
 
-bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 34 || h3_tile(t); }
+bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 25 || t == 26 || t == 34 || h3_tile(t); }
 
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
@@ -2436,6 +2436,8 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 2: return launch_tile<64, 64, 32, 2, 2>(a, s);
     case 4: return launch_tile<32, 64, 32, 1, 2>(a, s);
     case 24: return launch_bs<64, 64, 2, 2>(a, s);
+    case 25: return launch_bs<128, 64, 2, 2>(a, s);      // bf16x6, 128 x 64 (r05 short-K experiments)
+    case 26: return launch_bs<64, 64, 2, 2, 3>(a, s);    // bf16x6, 64 x 64, three k-tile buffers
     case 34: return launch_bs2(a, s);
     case 36: return launch_h3<128>(a, s);
     case 44: return launch_h3<256>(a, s);
@@ -2600,7 +2602,7 @@ static int pick_tile(const GemmArgs& a) {
 // tile edge of each variant (for the tail split)
 static void variant_tile(int t, int& bm, int& bn, int& bk) {
   bk = 32;
-  bm = t == 44 || t == 47 || t == 48 || t == 49 ? 256 : t == 0 || t >= 34 ? 128 : t == 4 ? 32 : 64;
+  bm = t == 44 || t == 47 || t == 48 || t == 49 ? 256 : t == 0 || t == 25 || t >= 34 ? 128 : t == 4 ? 32 : 64;
   bn = t == 49 ? 144 : t == 0 || t >= 34 ? 128 : 64;
 }
 

@@ -56,6 +56,36 @@ __device__ unsigned long long* vv_trace_buf;
   } while (0)
 #endif
 
+// __shfl_xor(v, O) without the LDS crossbar (r05): ds_bpermute_b32 (what __shfl_xor compiles to here) costs an LDS
+// round trip per step; these are VALU lane permutes with the same result bit for bit. O = 1, 2: DPP quad_perm; 4, 8:
+// two DPP steps (row_half_mirror is l ^ 7 within 8 lanes, row_mirror l ^ 15 within 16); 16, 32: gfx950's
+// v_permlane16/32_swap, whose two outputs hold lane l's value and its partner's (the partner picked by the lane's row).
+template <int O>
+__device__ __forceinline__ int xshfl_i(int v) {
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor offset");
+  if constexpr (O == 1) {
+    return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (O == 2) {
+    return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (O == 4) {
+    const int t = __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror: l ^ 7
+    return __builtin_amdgcn_mov_dpp(t, 0x1B, 0xF, 0xF, false);           // quad_perm [3,2,1,0]: l ^ 3
+  } else if constexpr (O == 8) {
+    const int t = __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);  // row_mirror: l ^ 15
+    return __builtin_amdgcn_mov_dpp(t, 0x141, 0xF, 0xF, false);          // row_half_mirror: l ^ 7
+  } else if constexpr (O == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)(((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
+  }
+}
+template <int O>
+__device__ __forceinline__ float xshfl(float v) { return __int_as_float(xshfl_i<O>(__float_as_int(v))); }
+template <int O>
+__device__ __forceinline__ int xshfl(int v) { return xshfl_i<O>(v); }
+
 __device__ __forceinline__ float gelu_t(float x) { return gelu_fast(x); }  // vv_gelu.h
 __device__ __forceinline__ float dgelu_t(float x) { return dgelu_fast(x); }
 // fp16x3 row scale 2^(141 - E) of a row whose largest |value| has bit pattern mx, and its inverse 2^(E - 141)
@@ -202,8 +232,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
       float s = 0.f;
 #pragma unroll
       for (int v = 0; v < CQ / 4; ++v) s += (yv[v][0] + yv[v][1]) + (yv[v][2] + yv[v][3]);
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
+      s += xshfl<1>(s);
+      s += xshfl<2>(s);
       const float mean = s / (float)C;
       float q = 0.f;
 #pragma unroll
@@ -213,8 +243,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
           const float d = yv[v][e] - mean;
           q += d * d;
         }
-      q += __shfl_xor(q, 1);
-      q += __shfl_xor(q, 2);
+      q += xshfl<1>(q);
+      q += xshfl<2>(q);
       const float rstd = 1.0f / sqrtf(q / (float)C + a.eps);
 #pragma unroll
       for (int v = 0; v < CQ / 4; ++v)
@@ -227,8 +257,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
     for (int v = 0; v < CQ / 4; ++v)
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = amax(mx, yv[v][e]);
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    mx = max(mx, (unsigned)xshfl<1>((int)mx));
+    mx = max(mx, (unsigned)xshfl<2>((int)mx));
     const float sy = sc_of(mx);
     iy_own = inv_of(mx);
     typedef _Float16 h4t __attribute__((ext_vector_type(4)));
@@ -339,8 +369,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
 #pragma unroll
       for (int i = 0; i < 4; ++i) mx = amax(mx, u[j][i]);
     }
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 16));
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 32));
+    mx = max(mx, (unsigned)xshfl<16>((int)mx));
+    mx = max(mx, (unsigned)xshfl<32>((int)mx));
     const float su = sc_of(mx), iu = inv_of(mx);
     // GEMM2^T: rows = output channels 16 q + 4 g4 + i, columns = tokens; u's planes are the B fragments
     f4 tmp[NQ];
@@ -424,10 +454,10 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
         s2 += gd * ((xv[q][i] - mean) * rstd);
       }
     }
-    s1 += __shfl_xor(s1, 16);
-    s1 += __shfl_xor(s1, 32);
-    s2 += __shfl_xor(s2, 16);
-    s2 += __shfl_xor(s2, 32);
+    s1 += xshfl<16>(s1);
+    s1 += xshfl<32>(s1);
+    s2 += xshfl<16>(s2);
+    s2 += xshfl<32>(s2);
     const float m1 = s1 / (float)C, m2 = s2 / (float)C;
     unsigned omx = 0;
     f4 dv[NQ];
@@ -445,8 +475,8 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
       *reinterpret_cast<f4*>(G.out + trow * C + 16 * q + 4 * g4) = v;
     }
     if (G.rs) {
-      omx = max(omx, (unsigned)__shfl_xor((int)omx, 16));
-      omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
+      omx = max(omx, (unsigned)xshfl<16>((int)omx));
+      omx = max(omx, (unsigned)xshfl<32>((int)omx));
       if (g4 == 0) G.rs[trow] = sc_of(omx);
     }
   }
@@ -557,8 +587,8 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
       float s = 0.f;
 #pragma unroll
       for (int v = 0; v < CQ / 4; ++v) s += (yv[v][0] + yv[v][1]) + (yv[v][2] + yv[v][3]);
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
+      s += xshfl<1>(s);
+      s += xshfl<2>(s);
       const float mean = s / (float)C;
       float q = 0.f;
 #pragma unroll
@@ -568,8 +598,8 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
           const float d = yv[v][e] - mean;
           q += d * d;
         }
-      q += __shfl_xor(q, 1);
-      q += __shfl_xor(q, 2);
+      q += xshfl<1>(q);
+      q += xshfl<2>(q);
       const float rstd = 1.0f / sqrtf(q / (float)C + a.eps);
 #pragma unroll
       for (int v = 0; v < CQ / 4; ++v)
@@ -582,8 +612,8 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
     for (int v = 0; v < CQ / 4; ++v)
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = amax(mx, yv[v][e]);
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    mx = max(mx, (unsigned)xshfl<1>((int)mx));
+    mx = max(mx, (unsigned)xshfl<2>((int)mx));
     const float sy = sc_of(mx), iy = inv_of(mx);
     if (qd == 0) {
       // the u bound of this token: f (K max|W1| max|y| + max|b1|), max|y| < 2^15 iy; x2 margin as epilogue_rows
@@ -837,10 +867,10 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
         s1 += gd;
         s2 += gd * ((xv[v][e] - mean) * rstd);
       }
-    s1 += __shfl_xor(s1, 1);
-    s1 += __shfl_xor(s1, 2);
-    s2 += __shfl_xor(s2, 1);
-    s2 += __shfl_xor(s2, 2);
+    s1 += xshfl<1>(s1);
+    s1 += xshfl<2>(s1);
+    s2 += xshfl<1>(s2);
+    s2 += xshfl<2>(s2);
     const float m1 = s1 / (float)C, m2 = s2 / (float)C;
     unsigned omx = 0;  // out may alias dy: each thread rewrites only the row slice it has read
 #pragma unroll
@@ -854,8 +884,8 @@ __global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
       reinterpret_cast<f4*>(G.out + trow * C + qd * CQ)[v] = r;
     }
     if (G.rs) {
-      omx = max(omx, (unsigned)__shfl_xor((int)omx, 1));
-      omx = max(omx, (unsigned)__shfl_xor((int)omx, 2));
+      omx = max(omx, (unsigned)xshfl<1>((int)omx));
+      omx = max(omx, (unsigned)xshfl<2>((int)omx));
       if (qd == 0) G.rs[trow] = sc_of(omx);
     }
   }
@@ -1004,8 +1034,8 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
     float sm = 0.f;
 #pragma unroll
     for (int v = 0; v < CQ / 4; ++v) sm += (yv[v][0] + yv[v][1]) + (yv[v][2] + yv[v][3]);
-    sm += __shfl_xor(sm, 1);
-    sm += __shfl_xor(sm, 2);
+    sm += xshfl<1>(sm);
+    sm += xshfl<2>(sm);
     const float mean = sm / (float)C;
     float q = 0.f;
 #pragma unroll
@@ -1015,8 +1045,8 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
         const float d = yv[v][e] - mean;
         q += d * d;
       }
-    q += __shfl_xor(q, 1);
-    q += __shfl_xor(q, 2);
+    q += xshfl<1>(q);
+    q += xshfl<2>(q);
     const float rstd = 1.0f / sqrtf(q / (float)C + a.eps);
     unsigned mx = 0;
 #pragma unroll
@@ -1027,8 +1057,8 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
         mx = amax(mx, yv[v][e]);
       }
     if (qd == 0) *reinterpret_cast<float2*>(G.stats + 2 * (size_t)(r0 + tt)) = make_float2(mean, rstd);
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    mx = max(mx, (unsigned)xshfl<1>((int)mx));
+    mx = max(mx, (unsigned)xshfl<2>((int)mx));
     const float sy = sc_of(mx);
     iy_own = inv_of(mx);
     typedef _Float16 h4t __attribute__((ext_vector_type(4)));
@@ -1127,8 +1157,8 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) mx = amax(mx, val[j][i]);
-        mx = max(mx, (unsigned)__shfl_xor((int)mx, 16));
-        mx = max(mx, (unsigned)__shfl_xor((int)mx, 32));
+        mx = max(mx, (unsigned)xshfl<16>((int)mx));
+        mx = max(mx, (unsigned)xshfl<32>((int)mx));
         const float ss = sc_of(mx);
         h8v fh, fl8;
 #pragma unroll
@@ -1164,12 +1194,10 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
           if (masked_row) b += -100.0f;
           float x = sv4[i] * a.scale + b;
           float mx = x;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+          mx = fmaxf(mx, xshfl<1>(mx)); mx = fmaxf(mx, xshfl<2>(mx)); mx = fmaxf(mx, xshfl<4>(mx)); mx = fmaxf(mx, xshfl<8>(mx));
           x = expf(x - mx);
           float sum = x;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o);
+          sum += xshfl<1>(sum); sum += xshfl<2>(sum); sum += xshfl<4>(sum); sum += xshfl<8>(sum);
           const float pv = x * (1.0f / sum);
           G.P[(((size_t)win * a.heads + h) * 16 + 4 * g4 + i) * 16 + li] = pv;
           pb[(4 * g4 + i) * PBS + li] = pv;
@@ -1195,8 +1223,8 @@ __global__ __launch_bounds__(256, C == 96 ? 3 : 1) void k_ablk_fwd(AblkArgs a) {
         unsigned omx = 0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) omx = amax(omx, o[e]);
-        omx = max(omx, (unsigned)__shfl_xor((int)omx, 16));
-        omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
+        omx = max(omx, (unsigned)xshfl<16>((int)omx));
+        omx = max(omx, (unsigned)xshfl<32>((int)omx));
         const float so = sc_of(omx);
         io = inv_of(omx);
 #pragma unroll
@@ -1352,8 +1380,8 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
     for (int v = 0; v < CQ / 4; ++v)
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = amax(mx, yv[v][e]);
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 1));
-    mx = max(mx, (unsigned)__shfl_xor((int)mx, 2));
+    mx = max(mx, (unsigned)xshfl<1>((int)mx));
+    mx = max(mx, (unsigned)xshfl<2>((int)mx));
     const float sy = sc_of(mx);
     id_own = inv_of(mx);
     typedef _Float16 h4t __attribute__((ext_vector_type(4)));
@@ -1463,10 +1491,10 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
           mo = amax(mo, dov[j][i]);
           mv = amax(mv, vv[j][i]);
         }
-      mo = max(mo, (unsigned)__shfl_xor((int)mo, 16));
-      mo = max(mo, (unsigned)__shfl_xor((int)mo, 32));
-      mv = max(mv, (unsigned)__shfl_xor((int)mv, 16));
-      mv = max(mv, (unsigned)__shfl_xor((int)mv, 32));
+      mo = max(mo, (unsigned)xshfl<16>((int)mo));
+      mo = max(mo, (unsigned)xshfl<32>((int)mo));
+      mv = max(mv, (unsigned)xshfl<16>((int)mv));
+      mv = max(mv, (unsigned)xshfl<32>((int)mv));
       const float so = sc_of(mo), svs = sc_of(mv);
       h8v oh, ol, vh, vl;
 #pragma unroll
@@ -1486,8 +1514,7 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
       for (int i = 0; i < 4; ++i) {
         const float d = dp[i] * (__shfl(io_, 4 * g4 + i) * iv_);
         float rsum = pv[i] * d;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) rsum += __shfl_xor(rsum, o);
+        rsum += xshfl<1>(rsum); rsum += xshfl<2>(rsum); rsum += xshfl<4>(rsum); rsum += xshfl<8>(rsum);
         sb[(4 * g4 + i) * SS + li] = pv[i] * (d - rsum);
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores are done
@@ -1523,8 +1550,8 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
         unsigned m = 0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) m = amax(m, src[e]);
-        m = max(m, (unsigned)__shfl_xor((int)m, 16));
-        m = max(m, (unsigned)__shfl_xor((int)m, 32));
+        m = max(m, (unsigned)xshfl<16>((int)m));
+        m = max(m, (unsigned)xshfl<32>((int)m));
         const float sf = sc_of(m);
         fi[p3] = inv_of(m);
 #pragma unroll
@@ -1588,10 +1615,10 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
       s2 += gd * ((xv[q][i] - mean) * rstd);
     }
   }
-  s1 += __shfl_xor(s1, 16);
-  s1 += __shfl_xor(s1, 32);
-  s2 += __shfl_xor(s2, 16);
-  s2 += __shfl_xor(s2, 32);
+  s1 += xshfl<16>(s1);
+  s1 += xshfl<32>(s1);
+  s2 += xshfl<16>(s2);
+  s2 += xshfl<32>(s2);
   const float m1 = s1 / (float)C, m2 = s2 / (float)C;
   f4 dv4[NQ];
 #pragma unroll
@@ -1608,8 +1635,8 @@ __global__ __launch_bounds__(256, C == 96 ? 2 : 1) void k_ablk_bwd(AblkArgs a) {
     *reinterpret_cast<f4*>(G.out + tphys * C + 16 * q + 4 * g4) = v;
   }
   if (G.rs) {
-    omx = max(omx, (unsigned)__shfl_xor((int)omx, 16));
-    omx = max(omx, (unsigned)__shfl_xor((int)omx, 32));
+    omx = max(omx, (unsigned)xshfl<16>((int)omx));
+    omx = max(omx, (unsigned)xshfl<32>((int)omx));
     if (g4 == 0) G.rs[tphys] = sc_of(omx);
   }
   VV_TR(TRR, 63);
