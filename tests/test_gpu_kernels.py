@@ -62,8 +62,9 @@ def test_gemm_split_accuracy(ctx, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(2048, 4608, 1152), (2048, 1152, 4608), (300, 200, 96), (4096, 384, 1152),
                                    (2048, 3456, 1152)])
 def test_gemm_pipelined_registered(ctx, M, N, K):
-    """Pipelined 128x128 split kernels (tile 34 bf16x6, 36 fp16x3) and the 64x64 bf16x6 kernel (24) on a registered weight (pre-split planes),
-    incl. ragged edges and the split-K tail: same fp32-level error bound as the other variants."""
+    """Pipelined 128x128 split kernels (tile 34 bf16x6, 36 fp16x3) and the bf16x6 kernels of 64x64 (24), 128x64 (25) and
+    64x64 with three k-tile buffers (26) on a registered weight (pre-split planes), incl. ragged edges and the split-K
+    tail: same fp32-level error bound as the other variants."""
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
     A = torch.randn(M, K, generator=g)
     B = torch.randn(N, K, generator=g) * 0.03
@@ -71,7 +72,7 @@ def test_gemm_pipelined_registered(ctx, M, N, K):
     scale = A.double().abs() @ B.double().abs().t()
     Bd = B.cuda()
     ctx.gemm_register_weight(Bd)
-    for t in (36, 34, 24):
+    for t in (36, 34, 24, 25, 26):
         C = ctx.gemm(A.cuda(), Bd, tile=t).cpu().double()
         es = float(((C - ref).abs() / scale).max())
         print(f"registered gemm {M}x{N}x{K} t{t}: {es:.2e}")
@@ -225,17 +226,17 @@ def test_reduce_batch_matches_single_calls(ctx):
 
 
 def test_gemm_rejects_non_library_tiles(ctx):
-    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 34, 36, 44, 46, 47, 48, 49): any other hint, e.g. the
-    r01 timing experiments 37-39, returns VV_E_ARG instead of running something."""
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 25, 26, 34, 36, 44, 46, 47, 48, 49): any other hint,
+    e.g. the r01 timing experiments 37-39, returns VV_E_ARG instead of running something."""
     from vaevar._lib import VVError
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 25, 26, 35, 37, 38, 39, 40, 41, 42, 45, 50, 1000):
+    for t in (1, 3, 21, 27, 35, 37, 38, 39, 40, 41, 42, 45, 50, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
-    for t in (0, 2, 4, 24, 34, 36, 44, 46, 47, 48, 49):
+    for t in (0, 2, 4, 24, 25, 26, 34, 36, 44, 46, 47, 48, 49):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
 

@@ -4,6 +4,7 @@
 //   PatchEmbed conv + absolute_pos_embed, ConvTranspose2d with the quirk-Q2 channel reorder
 //   misfit J_o and its adjoint, vector primitives of L-BFGS / Adam
 #include "vv_kernels.h"
+#include "vv_lanes.h"
 #include "vv_gelu.h"
 
 #include <algorithm>
@@ -71,16 +72,8 @@ void prof_read(double* ms, double* flops, double* bytes, int* n) {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return lane_sum<64>(v); }
+__device__ __forceinline__ double wave_sum_d(double v) { return lane_sum<64>(v); }
 
 // ============================================================================
 // LayerNorm  (nn.LayerNorm: biased variance, y = (x-mean)/sqrt(var+eps)*g + b)
@@ -89,18 +82,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // one write of y. Gathers (window / merge / expand) keep float4 granularity (segment widths are multiples of 4).
 constexpr int LN_NVMAX = 8;
 
+// (r05: vv_lanes.h's lane permutes, the same exchange order as the __shfl_xor loops they replace)
 template <int L>
-__device__ __forceinline__ float sub_sum(float v) {
-#pragma unroll
-  for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+__device__ __forceinline__ float sub_sum(float v) { return lane_sum<L>(v); }
 template <int L>
-__device__ __forceinline__ unsigned sub_max(unsigned v) {
-#pragma unroll
-  for (int o = L / 2; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
-  return v;
-}
+__device__ __forceinline__ unsigned sub_max(unsigned v) { return lane_max<L>(v); }
 // the fp16x3 GEMM row scale of a row whose largest |value| has bit pattern mx (k_rowscale's formula, bit-identical)
 __device__ __forceinline__ float row_scale_of(unsigned mx) { return __uint_as_float((268u - max(mx >> 23, 15u)) << 23); }
 __device__ __forceinline__ unsigned absmax4(unsigned m, const f4& o) {
@@ -912,8 +898,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mf(AttnArgs a) {
     const float vr = a.vrs[(size_t)win * WN_ + li];  // 2^e_j: max|A_j| < 2^15 / vr
     const float tw = *a.vbw, tbb = *(a.vbb ? a.vbb : a.vbw);
     float ia = __uint_as_float((254u << 23) - __float_as_uint(vr));
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) ia = fmaxf(ia, __shfl_xor(ia, o));
+    ia = lane_max<16>(ia);
     const unsigned mx = __float_as_uint(2.0f * ((float)C * tw * (32768.0f * ia) + (a.vbb ? tbb : 0.0f)));
     so = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
     if (h == 0 && tid < WN_) a.ors[(size_t)win * WN_ + tid] = so;
@@ -927,12 +912,10 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mf(AttnArgs a) {
     float s = ((pp[0] + pp[WN_ * 17]) + (pp[2 * WN_ * 17] + pp[3 * WN_ * 17])) * a.scale +
               attn_bias_mask(a, tb, win, 0, i, j);
     float mx = s;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    mx = lane_max16_up(mx);
     const float e = expf(s - mx);
     float sum = e;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o);
+    sum = lane_sum16_up(sum);
     const float pv = e * (1.0f / sum);
     p[i * kAmfP + j] = pv;
     G.P[((size_t)win * a.heads + h) * WN_ * WN_ + tid] = pv;
@@ -1002,8 +985,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mf(AttnArgs a) {
     const float* pp = part + i * 17 + j;
     const float dp = (pp[0] + pp[WN_ * 17]) + (pp[2 * WN_ * 17] + pp[3 * WN_ * 17]);
     float rd = pij * dp;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) rd += __shfl_xor(rd, o);
+    rd = lane_sum16_up(rd);
     ds[i * kAmfP + j] = pij * (dp - rd);
   }
   __syncthreads();
@@ -1096,16 +1078,16 @@ __global__ __launch_bounds__(256) void k_attn_fwd_w32(AttnArgs a) {
     sv[r] = st[r] * a.scale + b;
     mx = fmaxf(mx, sv[r]);
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 16));
-  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  mx = fmaxf(mx, xshfl<16>(mx));
+  mx = fmaxf(mx, xshfl<32>(mx));
   float sum = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     sv[r] = expf(sv[r] - mx);
     sum += sv[r];
   }
-  sum += __shfl_xor(sum, 16);
-  sum += __shfl_xor(sum, 32);
+  sum += xshfl<16>(sum);
+  sum += xshfl<32>(sum);
   const float inv = 1.0f / sum;
   f4 pv;
 #pragma unroll
@@ -1152,8 +1134,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_w32(AttnArgs a) {
   float rd = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) rd += pr[r] * dpt[r];
-  rd += __shfl_xor(rd, 16);
-  rd += __shfl_xor(rd, 32);
+  rd += xshfl<16>(rd);
+  rd += xshfl<32>(rd);
   f4 ds;  // dS[li][4g + r]
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -1580,8 +1562,7 @@ hipError_t patch_unembed_bwd(const PatchArgs& a, hipStream_t s) {
 // ============================================================================
 template <typename T>
 __device__ __forceinline__ T block_sum(T v, T* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v = lane_sum<64>(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) red[w] = v;
   __syncthreads();
@@ -1823,8 +1804,7 @@ __global__ __launch_bounds__(384) void k_misfit_grid(MisfitArgs a) {
     *reinterpret_cast<f4*>(colsum + j) = f4{s0, s1, s2, s3};
   }
   // J partial of the band
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  acc = lane_sum<64>(acc);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) red[w] = acc;
   __syncthreads();
@@ -2204,8 +2184,7 @@ __global__ __launch_bounds__(256) void k_absmax(const float* a, int64_t n, float
   __shared__ float red[4];
   float m = 0.f;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, fabsf(a[i]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  m = lane_max<64>(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) partial[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
@@ -2221,8 +2200,7 @@ __global__ __launch_bounds__(256) void k_final_max(const float* partial, int n, 
   __shared__ float red[4];
   float m = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, partial[i]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  m = lane_max<64>(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) out[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
@@ -2233,8 +2211,7 @@ __global__ __launch_bounds__(256) void k_final_max_d(const float* partial, int n
   __shared__ float red[4];
   float m = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, partial[i]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  m = lane_max<64>(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) out[0] = (double)fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));

@@ -19,6 +19,7 @@
 #include <cmath>
 
 #include "vv_gelu.h"
+#include "vv_lanes.h"
 #include "vv_kernels.h"
 
 namespace vv {
@@ -55,36 +56,6 @@ __device__ unsigned long long* vv_trace_buf;
   do {                      \
   } while (0)
 #endif
-
-// __shfl_xor(v, O) without the LDS crossbar (r05): ds_bpermute_b32 (what __shfl_xor compiles to here) costs an LDS
-// round trip per step; these are VALU lane permutes with the same result bit for bit. O = 1, 2: DPP quad_perm; 4, 8:
-// two DPP steps (row_half_mirror is l ^ 7 within 8 lanes, row_mirror l ^ 15 within 16); 16, 32: gfx950's
-// v_permlane16/32_swap, whose two outputs hold lane l's value and its partner's (the partner picked by the lane's row).
-template <int O>
-__device__ __forceinline__ int xshfl_i(int v) {
-  static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor offset");
-  if constexpr (O == 1) {
-    return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  } else if constexpr (O == 2) {
-    return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  } else if constexpr (O == 4) {
-    const int t = __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror: l ^ 7
-    return __builtin_amdgcn_mov_dpp(t, 0x1B, 0xF, 0xF, false);           // quad_perm [3,2,1,0]: l ^ 3
-  } else if constexpr (O == 8) {
-    const int t = __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);  // row_mirror: l ^ 15
-    return __builtin_amdgcn_mov_dpp(t, 0x141, 0xF, 0xF, false);          // row_half_mirror: l ^ 7
-  } else if constexpr (O == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-    return (int)(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
-  } else {
-    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
-    return (int)(((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
-  }
-}
-template <int O>
-__device__ __forceinline__ float xshfl(float v) { return __int_as_float(xshfl_i<O>(__float_as_int(v))); }
-template <int O>
-__device__ __forceinline__ int xshfl(int v) { return xshfl_i<O>(v); }
 
 __device__ __forceinline__ float gelu_t(float x) { return gelu_fast(x); }  // vv_gelu.h
 __device__ __forceinline__ float dgelu_t(float x) { return dgelu_fast(x); }
