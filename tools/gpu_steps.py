@@ -12,12 +12,12 @@ steps (one shell word each; arguments after ':' are split on whitespace):
   smoke                   __graft_entry__.smoke()
   bench[:ARGS]            python bench.py ARGS > NN_bench.json
   ab:REF.so:N[:ARGS]      N interleaved pairs of bench.py ARGS with VAEVAR_LIB=REF.so ("ref") and the tree's build ("new")
-  env:K=V[,K=V]:ARGS      bench.py ARGS with extra environment (e.g. env:VAEVAR_GRID_FUSED=0:--config 5)
+  env:K=V[+K=V]:ARGS      bench.py ARGS with extra environment (e.g. env:VAEVAR_GRID_FUSED=0:--config 5)
   rocprof[:ARGS]          rocprofv3 --kernel-trace --stats of bench.py ARGS; keeps kernel_stats.csv (+ the trace with
                           ARGS containing --trace, as kernel_trace.csv)
   pmc:COUNTER[:ARGS]      rocprofv3 --pmc COUNTER of bench.py ARGS (one counter group per pass); keeps counter_collection.csv
   py:SCRIPT[:ARGS]        python SCRIPT ARGS (tools/quick_time.py, tools/h5_check.py, ...)
-  pyenv:K=V[,K=V]:SCRIPT[:ARGS]  the same with extra environment (e.g. VAEVAR_LIB=vae-var_amd/vaevar/ab/x.so)
+  pyenv:K=V[+K=V]:SCRIPT[:ARGS]  the same with extra environment (e.g. VAEVAR_LIB=vae-var_amd/vaevar/ab/x.so)
   ktrace:SCRIPT[:ARGS]    rocprofv3 --kernel-trace of python SCRIPT ARGS, summarised per (kernel, grid) by tools/kstats.py
                           into NN_ktrace.txt (the trace itself is not kept)
   kseq:MARKER:SCRIPT[:ARGS]  the same, listed launch by launch after the second-to-last MARKER kernel
@@ -67,7 +67,7 @@ def main():
             rc = run([py, "bench.py"] + rest.split(), base + ".json", lim)
         elif kind == "env":
             kv, _, args = rest.partition(":")
-            env = dict(x.split("=", 1) for x in kv.split(",") if x)
+            env = dict(x.split("=", 1) for x in kv.split("+") if x)
             rc = run([py, "bench.py"] + args.split(), base + ".json", lim, env)
         elif kind == "ab":
             ref, _, r2 = rest.partition(":")
@@ -117,7 +117,7 @@ def main():
         elif kind == "pyenv":
             kv, _, r2 = rest.partition(":")
             script, _, args = r2.partition(":")
-            env = dict(x.split("=", 1) for x in kv.split(",") if x)
+            env = dict(x.split("=", 1) for x in kv.split("+") if x)
             rc = run([py, "-u", script] + args.split(), base + ".log", lim, env)
         else:
             sys.exit(f"unknown step {st!r}")

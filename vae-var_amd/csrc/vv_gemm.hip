@@ -12,6 +12,7 @@
 // one barrier per k-tile.
 #include "vv_gelu.h"
 #include "vv_kernels.h"
+#include "vv_lanes.h"
 
 #include <algorithm>
 #include <cmath>
@@ -1139,7 +1140,7 @@ __global__ __launch_bounds__(256) void k_rowscale(GemmArgs args, float* __restri
                        max(__float_as_uint(fabsf(v[2])), __float_as_uint(fabsf(v[3])))));
     }
   }
-  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  mx = lane_max<64>(mx);
   if (lane == 0) out[(size_t)blockIdx.z * args.M + r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
 }
 
@@ -1165,7 +1166,7 @@ __global__ __launch_bounds__(256) void k_rowscale_n(GemmArgs args, float* __rest
   for (int i = 0; i < NV; ++i)
     mx = max(mx, max(max(__float_as_uint(fabsf(v[i][0])), __float_as_uint(fabsf(v[i][1]))),
                      max(__float_as_uint(fabsf(v[i][2])), __float_as_uint(fabsf(v[i][3])))));
-  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  mx = lane_max<64>(mx);
   if (lane == 0) out[(size_t)blockIdx.z * args.M + r] = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
 }
 
@@ -1592,7 +1593,7 @@ __global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restri
   for (int i = 0; i < NV; ++i)
     mx = max(mx, max(max(__float_as_uint(fabsf(v[i][0])), __float_as_uint(fabsf(v[i][1]))),
                      max(__float_as_uint(fabsf(v[i][2])), __float_as_uint(fabsf(v[i][3])))));
-  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  mx = lane_max<64>(mx);
   const float s = __uint_as_float((268u - max(mx >> 23, 15u)) << 23);
   const size_t zr = (size_t)blockIdx.z * args.M + r;
   if (lane == 0) rs[zr] = s;
@@ -2514,7 +2515,7 @@ __global__ __launch_bounds__(256) void k_split16_rows(const float* __restrict__ 
   const float* x = src + (size_t)r * K;
   unsigned mx = 0;
   for (int k = tid; k < K; k += 256) mx = max(mx, __float_as_uint(fabsf(x[k])));
-  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  mx = lane_max<64>(mx);
   if ((tid & 63) == 0) red[tid >> 6] = mx;
   __syncthreads();
   mx = max(max(red[0], red[1]), max(red[2], red[3]));
@@ -2557,7 +2558,7 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, siz
   unsigned mx = 0;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
     mx = max(mx, __float_as_uint(fabsf(x[i])));
-  for (int o = 32; o; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  mx = lane_max<64>(mx);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
   if (threadIdx.x == 0) atomicMax(out, max(max(red[0], red[1]), max(red[2], red[3])));  // |x| bits order as floats
