@@ -738,7 +738,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
       compute(0);
       __syncthreads();
     }
-  } else {
+  } else if constexpr (NBUF == 2) {
     sstore(0, s0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
@@ -746,6 +746,27 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_bs(GemmArgs args) {
       if (kt + 1 < nk) gload((kb + kt + 1) * BK, s0);
       compute(cur);
       if (kt + 1 < nk) sstore(cur ^ 1, s0);
+      __syncthreads();
+    }
+  } else {
+    // NBUF 3 (r05, tile 26): the same two LDS buffers, but two register stages, so a k-tile's global loads are
+    // issued two k-tiles before its LDS store (short-K launches: one k-tile's MFMAs, 12 per wave, do not cover a
+    // load's latency). Unrolled by two so that the stages keep fixed registers.
+    Stg s1;
+    if (nk > 1) gload((kb + 1) * BK, s1);
+    sstore(0, s0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      // s1 holds k-tile kt + 1, s0 is free
+      if (kt + 2 < nk) gload((kb + kt + 2) * BK, s0);
+      compute(0);
+      if (kt + 1 < nk) sstore(1, s1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      // s0 holds k-tile kt + 2, s1 is free
+      if (kt + 3 < nk) gload((kb + kt + 3) * BK, s1);
+      compute(1);
+      if (kt + 2 < nk) sstore(0, s0);
       __syncthreads();
     }
   }
@@ -780,7 +801,7 @@ template <int BM, int BN, int WM, int WN, int NBUF = 2>
 static hipError_t launch_bs(const GemmArgs& a, hipStream_t s) {
   constexpr int BK = 32;
   if (a.K % BK || a.ksplit % BK) return hipErrorInvalidValue;
-  const size_t lds = NBUF * 3 * (BM + BN) * BK * sizeof(unsigned short);
+  const size_t lds = (NBUF < 2 ? NBUF : 2) * 3 * (BM + BN) * BK * sizeof(unsigned short);
   const int T = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
   dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
@@ -2438,7 +2459,7 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 4: return launch_tile<32, 64, 32, 1, 2>(a, s);
     case 24: return launch_bs<64, 64, 2, 2>(a, s);
     case 25: return launch_bs<128, 64, 2, 2>(a, s);      // bf16x6, 128 x 64 (r05 short-K experiments)
-    case 26: return launch_bs<64, 64, 2, 2, 3>(a, s);    // bf16x6, 64 x 64, three k-tile buffers
+    case 26: return launch_bs<64, 64, 2, 2, 3>(a, s);    // bf16x6, 64 x 64, loads two k-tiles ahead
     case 34: return launch_bs2(a, s);
     case 36: return launch_h3<128>(a, s);
     case 44: return launch_h3<256>(a, s);
