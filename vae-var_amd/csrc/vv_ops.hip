@@ -292,14 +292,24 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
 // LayerNorm exactly k_ln_fwd's, so the results are bit-identical to the two launches they replace.
 // 8 rows (waves) per workgroup: GEMM rows 8i .. 8i + 7 are fragment rows r = 0..3 of two lane quarters, so each
 // 128-B line of a partial (rows r and r + 4 of one 16-column block) is consumed inside one workgroup
+constexpr int kFixupLnMaxN = 1280;  // gemm_ln's N limit
 template <int NV, int S>
 __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   // wave = GEMM row gr (ginv) or LN row j: with a gather, walking GEMM rows keeps each 128-B line of a partial
   // (two GEMM rows of one wave quarter) inside one workgroup
   const int w = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
-  if (w >= args.M) return;
   const GemmGroup G = args.g[0];
   const int N = args.N, f4n = N >> 2;
+  // the row-invariant vectors (bias, gamma, beta) once per workgroup into LDS (r05: 15 of a wave's 35 global loads
+  // re-read them per row; the kernel is bound by vector-memory issue, r04 PMC)
+  __shared__ __attribute__((aligned(16))) float lv[3][kFixupLnMaxN];
+  for (int i = threadIdx.x; i < 3 * f4n; i += 512) {
+    const int q = i / f4n, c4 = 4 * (i - q * f4n);
+    const float* src = q == 0 ? G.bias : q == 1 ? l.gamma : l.beta;
+    *reinterpret_cast<f4*>(&lv[q][c4]) = src ? *reinterpret_cast<const f4*>(src + c4) : f4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  if (w >= args.M) return;
   const int j = l.ginv ? l.ginv[w] : w;
   const int gr = l.ginv ? w : l.gmap ? l.gmap[j] : j;
   const int xo = args.crow ? args.crow[gr] : gr;
@@ -323,10 +333,13 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
     for (int c = 0; c < S; ++c)
       pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
     rv[v] = *reinterpret_cast<const f4*>(G.R + (size_t)rrow * args.ldr + c4);
-    const f4 t = *reinterpret_cast<const f4*>(G.bias ? G.bias + c4 : G.R + c4);
-    bv[v] = G.bias ? t : f4{0.f, 0.f, 0.f, 0.f};
-    gv[v] = *reinterpret_cast<const f4*>(l.gamma + c4);
-    bb[v] = *reinterpret_cast<const f4*>(l.beta + c4);
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c4 = 4 * (ok[v] ? sl + v * 64 : f4n - 1);
+    bv[v] = *reinterpret_cast<const f4*>(&lv[0][c4]);
+    gv[v] = *reinterpret_cast<const f4*>(&lv[1][c4]);
+    bb[v] = *reinterpret_cast<const f4*>(&lv[2][c4]);
   }
   // the fixup: chunk partials in chunk order, then + bias, then residual + (k_gemm_fixup_sub16 + epilogue)
   f4 xv[NV];
@@ -385,8 +398,12 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
 template <int NV, int S>
 __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs l) {
   const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
-  if (j >= args.M) return;
   const int N = args.N, f4n = N >> 2, C = N;
+  __shared__ __attribute__((aligned(16))) float lg[kFixupLnMaxN];  // gamma once per workgroup (as k_fixup_ln)
+  for (int i = threadIdx.x; i < f4n; i += 512)
+    *reinterpret_cast<f4*>(&lg[4 * i]) = *reinterpret_cast<const f4*>(l.gamma + 4 * i);
+  __syncthreads();
+  if (j >= args.M) return;
   const int gr = j;
   const int pr = l.lmap ? l.lmap[j] : j;
   const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
@@ -409,9 +426,10 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
     for (int c = 0; c < S; ++c)
       pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
     xv[v] = *reinterpret_cast<const f4*>(l.x + (size_t)pr * N + c4);
-    gv[v] = *reinterpret_cast<const f4*>(l.gamma + c4);
     rv[v] = *reinterpret_cast<const f4*>(res + (size_t)pr * N + c4);
   }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) gv[v] = *reinterpret_cast<const f4*>(&lg[4 * (ok[v] ? sl + v * 64 : f4n - 1)]);
   f4 dv[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
