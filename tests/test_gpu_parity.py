@@ -772,6 +772,8 @@ def test_fixup_ln_bitwise(full_dec):
     res = []
     ln_launches, fused = [], []
     default = full_dec.ctx.get_tuning("fixup_ln")
+    sk_default = full_dec.ctx.get_tuning("h4_streamk_mink")
+    full_dec.ctx.set_tuning("h4_streamk_mink", 0)  # bit-identity holds for the S-chunk split (stream-K: next test)
     try:
         for v in (0, 1):
             full_dec.ctx.set_tuning("fixup_ln", v)
@@ -787,6 +789,7 @@ def test_fixup_ln_bitwise(full_dec):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning("fixup_ln", default)
+        full_dec.ctx.set_tuning("h4_streamk_mink", sk_default)
     # the fused path really ran (gemm_ln falls back to separate launches when it returns hipErrorNotSupported):
     # the LG-stage LayerNorms after split-K GEMMs (proj -> LN2, fc2 -> next LN1, and their backward) leave the
     # LayerNorm class
@@ -797,3 +800,44 @@ def test_fixup_ln_bitwise(full_dec):
     print(f"fixup_ln 1 vs 0: out max diff {(o1 - o0).abs().max().item():.1e}, grad {(d1 - d0).abs().max().item():.1e}, "
           f"J {jb1 + jo1 - jb0 - jo0:.1e}, dJ/dz {(g1 - g0).abs().max().item():.1e}")
     assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1) and jb0 == jb1 and jo0 == jo1
+
+
+def test_streamk_fixup_ln(full_dec):
+    """Stream-K (tuning h4_streamk_mink): the split-K tile-48 GEMMs whose fixup is fused into a LayerNorm (fc2 ->
+    LN1, fc2^T / qkv^T -> LN backward; K >= 3456) run over every CU with each workgroup's unit range cut into one or
+    two tile segments, and the fused fixup sums a tile's 3-5 segment partials in k order. Against the S-chunk split:
+    the same arithmetic per product, another summation split, so fp32-level agreement (decoder output, input
+    gradient, J, dJ/dz); two stream-K runs are bit-identical (a fixed partition, partials summed in a fixed order);
+    the stream-K consumer really ran (launch counter)."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field, uniform_sym
+
+    z = torch.from_numpy(0.5 * smooth_field(431, (1, 32, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(432, (1, 69, 128, 256), 1.0)).cuda()
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    zc = torch.from_numpy(0.3 * smooth_field(433, (1, 32, 128, 256))).cuda()
+    ctx = full_dec.ctx
+    default = ctx.get_tuning("h4_streamk_mink")
+    res, launches = [], []
+    try:
+        for v in (0, 3456, 3456):
+            ctx.set_tuning("h4_streamk_mink", v)
+            c0 = ctx.counter("streamk")
+            out = full_dec.forward_raw(z).clone()
+            dz = torch.empty_like(z)
+            full_dec.backward_raw(cot, dz)
+            launches.append(ctx.counter("streamk") - c0)
+            g = torch.empty_like(zc)
+            jb, jo = prob.closure(zc, g)
+            res.append((out, dz, jb, jo, g))
+    finally:
+        ctx.set_tuning("h4_streamk_mink", default)
+    (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1), (o2, d2, jb2, jo2, g2) = res
+    rel = lambda a, b: float((a - b).abs().max() / b.abs().max())
+    print(f"stream-K launches per forward + backward {launches}; vs S-chunk split: out {rel(o1, o0):.1e}, "
+          f"grad {rel(d1, d0):.1e}, J {abs(jb1 + jo1 - jb0 - jo0) / abs(jb0 + jo0):.1e}, dJ/dz {rel(g1, g0):.1e}")
+    assert launches[0] == 0 and launches[1] >= 24 and launches[2] == launches[1], launches
+    assert torch.equal(o1, o2) and torch.equal(d1, d2) and torch.equal(g1, g2) and jb1 == jb2 and jo1 == jo2
+    assert rel(o1, o0) < 1e-5 and rel(d1, d0) < 1e-4 and rel(g1, g0) < 1e-4
+    assert abs(jb1 + jo1 - jb0 - jo0) <= 1e-6 * abs(jb0 + jo0)

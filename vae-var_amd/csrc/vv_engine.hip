@@ -2470,7 +2470,7 @@ int vv_set_closure_graph(vv_ctx* ctx, int enable) {
 
 int vv_get_counter(const char* name, long long* value) {
   if (!name || !value) return fail(VV_E_ARG, "null argument");
-  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup", "gather_scales"};
+  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup", "gather_scales", "streamk"};
   for (int c = 0; c < vv::CNT_N; ++c)
     if (!strcmp(name, names[c])) {
       *value = vv::launch_count(c);

@@ -1638,7 +1638,7 @@ __global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restri
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 
-template <int EPI>
+template <int EPI, bool SK = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* __restrict__ ascale,
                                                     const unsigned short* __restrict__ apl) {
   constexpr int BM = 256, BN = 128, BK = 32, NT = 512, WN = 2, WM = 4, TM = 4, TN = 4;
@@ -1651,8 +1651,17 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   const int M = args.M, N = args.N, K = args.K;
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
   const int nkt = K / BK;
-  int tile, kb = 0, ke = nkt, part = -1;
-  if (args.tsplit <= 1) {
+  int tile = 0, kb = 0, ke = nkt, part = -1;
+  // stream-K (args.sk): the units [u0, u1) of logical workgroup skw, one or two tile segments
+  long long sku0 = 0, sku1 = 0;
+  int nseg = 1, skw = 0;
+  if constexpr (SK) {
+    skw = xcd_remap(blockIdx.x, gridDim.x);
+    const long long U = (long long)(ntm * ntn) * nkt;
+    sku0 = (long long)skw * U / gridDim.x;
+    sku1 = (long long)(skw + 1) * U / gridDim.x;
+    nseg = (int)((sku1 - 1) / nkt - sku0 / nkt) + 1;
+  } else if (args.tsplit <= 1) {
     tile = xcd_remap(blockIdx.x, ntm * ntn);
   } else if ((int)blockIdx.x < args.tdp) {
     tile = xcd_remap(blockIdx.x, args.tdp);
@@ -1663,6 +1672,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
     tile = args.tdp + tl;
     kb = (c * nkt) / S;
     ke = ((c + 1) * nkt) / S;
+  }
+  for (int seg = 0; seg < (SK ? nseg : 1); ++seg) {
+  if constexpr (SK) {
+    const long long ts = sku0 / nkt + seg, tk0 = ts * nkt;
+    tile = (int)ts;
+    kb = (int)(max(sku0, tk0) - tk0);
+    ke = (int)(min(sku1, tk0 + nkt) - tk0);
+    part = skw + tile;
+    if (seg > 0) __syncthreads();  // every wave's reads of the previous segment's LDS ring are done
   }
   int mb, nb;
   tile_mn(tile, ntm, ntn, mb, nb, args.gm);
@@ -1862,12 +1880,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
       for (int b = 0; b < TN; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) w[(size_t)((a * TN + b) * 4 + r) * NT + tid] = acc[a][b][r];
+    if constexpr (SK) continue;
     return;
   }
   if (m0 + BM <= M && n0 + BN <= N)
     epilogue<BM, BN, WM, WN, EPI, 16, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
   else
     epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
+  }  // segments
 }
 
 // Row-wise epilogue of a full tile staged in LDS (tile 49): a wave's 32 x BN fp32 results, written to LDS from the
@@ -2248,7 +2268,8 @@ static hipError_t launch_h3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   return hipGetLastError();
 }
 
-constexpr size_t kWsFloats = (size_t)1 << 23;      // 32 MB: split-K partials (e.g. 3 x 144 tiles of 128x128)
+constexpr size_t kWsFloats = (size_t)1 << 24;      // 64 MB: split-K partials (3 x 144 tiles of 128x128; stream-K's
+                                                   // P + T tile-48 slots of 128 KB)
 constexpr size_t kScaleFloats = (size_t)1 << 19;   // then the A row scales of GEMM_SPLIT16 (groups x M)
 
 // requires fp16 planes for every group's B (registered weights) and a workspace for the A row scales; the
@@ -2269,6 +2290,14 @@ static bool h4_ready(const GemmArgs& a) {
 template <int EPI>
 static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc,
                               const unsigned short* planes) {
+  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {  // gemm_ln's stream-K (its fixups take STORE / RESID)
+    if (a.sk) {
+      if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI, true>, lds)) return e;
+      hipLaunchKernelGGL((k_gemm_h4<EPI, true>), grid, dim3(512), lds, s, a, sc, planes);
+      return hipGetLastError();
+    }
+  }
+  if (a.sk) return hipErrorInvalidValue;
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_h4<EPI>), grid, dim3(512), lds, s, a, sc, planes);
   if (tail && !a.nofix) {  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
@@ -2352,7 +2381,7 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
   const size_t lds = 3 * (2 * (256 + 128) * 32) * sizeof(unsigned short);
   const int T = ((a.N + 127) / 128) * ((a.M + 255) / 256);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
-  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  dim3 grid(a.sk ? device_cus() : tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
   switch (a.epi) {
     case EPI_STORE: return launch_h4_k<EPI_STORE>(b, s, grid, lds, tail, sc, planes);
     case EPI_GELU:
@@ -2434,12 +2463,13 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "fixup_ln_rows") return &t.fixup_ln_rows;
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
   if (k == "grid_fused") return &t.grid_fused;
+  if (k == "h4_streamk_mink") return &t.h4_streamk_mink;
   if (k == "mlp_w") return &t.mlp_w;
   return nullptr;
 }
 bool tuning_value_ok(const char* key, int v) {
   const std::string k(key ? key : "");
-  if (k == "h3_mink" || k == "fc_h3_mink") return v >= 0;
+  if (k == "h3_mink" || k == "fc_h3_mink" || k == "h4_streamk_mink") return v >= 0;
   if (k == "small_split_minkt" || k == "tail_minkt" || k == "h4_split_minkt") return v >= 1;
   if (k == "mlp_hc") return v == 0 || v == 2 || v == 32 || v == 64;  // vv_tower.hip mlp_run
   if (k == "h5_var") return v >= 0 && v <= 5;
@@ -2676,6 +2706,8 @@ static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
   const int num_cu = device_cus();
   a.tdp = 0;
   a.tsplit = 1;
+  a.sk = 0;
+  a.skp = 0;
   a.ws = ws;
   a.ascale_phys = 0;
   const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
@@ -2765,6 +2797,17 @@ hipError_t gemm_ln(const GemmArgs& a_in, const GemmLnArgs& l, hipStream_t s, flo
   if (hipError_t e = gemm_prepare(a, -1, ws, t)) return e;
   if (t != 48 || a.tsplit < 2 || a.tsplit > 4 || a.tdp != 0) return hipErrorNotSupported;
   a.nofix = 1;
+  {
+    const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+    const long T = tiles_of(a, 256, 128), P = device_cus();
+    const long nkt = a.K / 32, L = nkt * T / P;  // units per workgroup (at least)
+    // at most 6 segments per tile (the consumer's kSkMaxSeg): ceil(nkt / L) + 1 <= 6
+    if (TU.h4_streamk_mink > 0 && a.K >= TU.h4_streamk_mink && T < P && (size_t)(P + T) * 256 * 128 <= kWsFloats &&
+        L >= 1 && nkt <= 5 * L) {
+      a.sk = 1;
+      a.skp = (int)P;
+    }
+  }
   const int ph = prof_begin(s);
   hipError_t e = launch_variant(t, a, s);
   if (e == hipSuccess) e = fixup_ln_launch(a, l, s);

@@ -52,6 +52,8 @@ struct Tuning {
   int mlp_w = 0;                // the fused MLP as k_mlpw (hidden layer split over the waves, per-wave LDS-DMA weight
                                 // rings, one u scale per token): bit 0 at dim 96, bit 1 at dim 192 (0: k_mlp). r05: correct
                                 // but not faster (dim 192: 64.7 / 72.5 vs 66.7 / 67.4 us; profiles/r05/knob_ab_*), off
+  int h4_streamk_mink = 0;      // > 0: gemm_ln's tile-48 split GEMMs with K >= this run stream-K over every CU (GemmArgs.sk)
+                                // instead of S chunks of each tile on T x S workgroups (0: off)
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
                                 // adjoint k_misfit_net_bwd (0: k_misfit_fwd / k_misfit_bwd_gather / k_flow_input(_adj));
                                 // 1: 3 rows of a band in flight per pass (more waves per SIMD), 2: 6 rows (r05: misfit
@@ -131,6 +133,12 @@ struct GemmArgs {
   const float* obb;
   const float* escale;  // set by the tile-48 launch: A's row scales in GEMM row order (what the kernel used)
   int nofix;            // set by gemm_ln: the split-K partials are summed by the consumer (no fixup launch)
+  // set by gemm_ln (tile 48, Tuning.h4_streamk_mink): stream-K. gridDim.x workgroups share the T x K/32 (tile,
+  // k-tile) units evenly; logical workgroup w (xcd_remap of blockIdx.x) owns units [w U / P, (w + 1) U / P), i.e. one
+  // or two tile segments, and writes each segment's partial to slot w + t of ws; tile t's partials are the slots
+  // w + t for w = w_first(t) .. w_last(t), summed in that (k) order by the consumer (k_fixup_ln / k_fixup_ln_bwd)
+  int sk;
+  int skp;  // stream-K: the GEMM's workgroup count P (what the consumer needs to find a tile's slots)
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   int h3_mink;         // > 0: this GEMM's own smallest K for the fp16x3 kernels (the forecast: Tuning.fc_h3_mink)
   GemmGroup g[kMaxGroups];
@@ -473,7 +481,8 @@ bool prof_enabled();
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 // host-side launch counters of the fused-path alternatives (vv_get_counter): tests assert that a fused path really
 // ran, since every fused launcher falls back to the unfused launches with equal results when it does not apply
-enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_N = 4 };
+enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_STREAMK = 4,
+                     CNT_N = 5 };
 void count_launch(int c);
 long long launch_count(int c);
 

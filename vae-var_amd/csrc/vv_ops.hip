@@ -293,7 +293,18 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
 // 8 rows (waves) per workgroup: GEMM rows 8i .. 8i + 7 are fragment rows r = 0..3 of two lane quarters, so each
 // 128-B line of a partial (rows r and r + 4 of one 16-column block) is consumed inside one workgroup
 constexpr int kFixupLnMaxN = 1280;  // gemm_ln's N limit
-template <int NV, int S>
+constexpr int kSkMaxSeg = 6;        // stream-K segments per tile at most (gemm_ln enables it only where that holds)
+// stream-K (GemmArgs.sk): tile t's partial slots are w + t for the logical workgroups w = w0 .. w0 + n - 1 whose
+// unit ranges [w U / P, (w + 1) U / P) meet the tile's units [t nkt, (t + 1) nkt) (k_gemm_h4's partition)
+__device__ __forceinline__ void sk_slots(const GemmArgs& a, int t, int& w0, int& n) {
+  const long long nkt = a.K / 32, P = a.skp;
+  const long long U = (long long)((a.M + 255) >> 8) * ((a.N + 127) >> 7) * nkt;
+  auto wof = [&](long long u) { return (int)(((u + 1) * P + U - 1) / U - 1); };  // the workgroup holding unit u
+  w0 = wof((long long)t * nkt);
+  n = wof((long long)(t + 1) * nkt - 1) - w0 + 1;
+}
+
+template <int NV, int S, bool SK = false>
 __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   // wave = GEMM row gr (ginv) or LN row j: with a gather, walking GEMM rows keeps each 128-B line of a partial
   // (two GEMM rows of one wave quarter) inside one workgroup
@@ -321,6 +332,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   const int rrow = args.rmod > 0 ? xo % args.rmod : xo;
   f4 pv[S][NV], rv[NV], bv[NV], gv[NV], bb[NV];
   bool ok[NV];
+  int sw0[NV], nsk[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int jv = sl + v * 64;
@@ -329,9 +341,17 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
     const int nb = c4 >> 7, cc = c4 & 127, wn = cc >> 6, b = (cc >> 4) & 3, rin = cc & 15;
     const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
     const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + hh * 16 + rin);
+    if (SK) {  // S = the most segments a tile can have; this tile's nsk of them, slots sw0 + c + tl
+      sk_slots(args, tl, sw0[v], nsk[v]);
 #pragma unroll
-    for (int c = 0; c < S; ++c)
-      pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+      for (int c = 0; c < S; ++c)
+        pv[c][v] = c < nsk[v] ? *reinterpret_cast<const f4*>(args.ws + (size_t)(sw0[v] + c + tl) * (16 * 4 * 512) + off)
+                              : f4{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+      for (int c = 0; c < S; ++c)
+        pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+    }
     rv[v] = *reinterpret_cast<const f4*>(G.R + (size_t)rrow * args.ldr + c4);
   }
 #pragma unroll
@@ -347,7 +367,8 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   for (int v = 0; v < NV; ++v) {
     f4 acc = pv[0][v];
 #pragma unroll
-    for (int c = 1; c < S; ++c) acc += pv[c][v];
+    for (int c = 1; c < S; ++c)
+      if (!SK || c < nsk[v]) acc += pv[c][v];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float t = acc[e] + bv[v][e];
@@ -395,7 +416,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
 
 // the backward form: dy = the fixup of a STORE GEMM without bias (chunk-order sum + 0, k_gemm_fixup_sub16's
 // value), then k_ln_bwd<64, NV> on the row (x, res, y and the planes at row lmap[j], stats at j)
-template <int NV, int S>
+template <int NV, int S, bool SK = false>
 __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs l) {
   const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
   const int N = args.N, f4n = N >> 2, C = N;
@@ -414,6 +435,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
   const float* res = l.res ? l.res : l.x;  // dummy source when there is no residual (never added)
   f4 pv[S][NV], xv[NV], gv[NV], rv[NV];
   bool ok[NV];
+  int sw0[NV], nsk[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int jv = sl + v * 64;
@@ -422,9 +444,17 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
     const int nb = c4 >> 7, cc = c4 & 127, wn = cc >> 6, b = (cc >> 4) & 3, rin = cc & 15;
     const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
     const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + hh * 16 + rin);
+    if (SK) {
+      sk_slots(args, tl, sw0[v], nsk[v]);
 #pragma unroll
-    for (int c = 0; c < S; ++c)
-      pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+      for (int c = 0; c < S; ++c)
+        pv[c][v] = c < nsk[v] ? *reinterpret_cast<const f4*>(args.ws + (size_t)(sw0[v] + c + tl) * (16 * 4 * 512) + off)
+                              : f4{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+      for (int c = 0; c < S; ++c)
+        pv[c][v] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+    }
     xv[v] = *reinterpret_cast<const f4*>(l.x + (size_t)pr * N + c4);
     rv[v] = *reinterpret_cast<const f4*>(res + (size_t)pr * N + c4);
   }
@@ -435,7 +465,8 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
   for (int v = 0; v < NV; ++v) {
     f4 acc = pv[0][v];
 #pragma unroll
-    for (int c = 1; c < S; ++c) acc += pv[c][v];
+    for (int c = 1; c < S; ++c)
+      if (!SK || c < nsk[v]) acc += pv[c][v];
 #pragma unroll
     for (int e = 0; e < 4; ++e) dv[v][e] = acc[e] + 0.0f;  // the STORE epilogue's v = acc + bias (none)
   }
@@ -482,6 +513,12 @@ hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s
   if (nv > 5 || a.N % 4) return hipErrorInvalidValue;
   const dim3 grid((a.M + 7) / 8);
   count_launch(CNT_FIXUP_LN);
+  if (a.sk) {  // stream-K partials: at most kSkMaxSeg per tile
+    count_launch(CNT_STREAMK);
+    if (l.bwd) hipLaunchKernelGGL((k_fixup_ln_bwd<5, kSkMaxSeg, true>), grid, dim3(512), 0, s, a, l);
+    else hipLaunchKernelGGL((k_fixup_ln<5, kSkMaxSeg, true>), grid, dim3(512), 0, s, a, l);
+    return hipGetLastError();
+  }
   if (l.bwd) {
     switch (a.tsplit) {
       case 2: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 2>), grid, dim3(512), 0, s, a, l); break;
