@@ -223,6 +223,18 @@ def test_reduce_batch_matches_single_calls(ctx):
         ctx.reduce_batch([(3, a, None)])
     with pytest.raises(VVError):
         ctx.reduce_batch([(1, a, None)] * 9)
+    # r05: all requests in one launch (k_reduce_multi) -- ragged and tiny lengths, the full 8 requests, extras only,
+    # and vv_reduce_enqueue's device results, each equal to the one-call-each values
+    for m in (1_000_003, 5):
+        x, y = a[:m], c[:m]
+        reqs = [(0, x, y), (1, x, None), (2, y, None), (0, y, y), (1, y, None), (2, x, None), (0, x, x), (0, y, x)]
+        want = [ctx.dot(x, y), ctx.abssum(x), ctx.absmax(y), ctx.dot(y, y), ctx.abssum(y), ctx.absmax(x),
+                ctx.dot(x, x), ctx.dot(y, x)]
+        assert ctx.reduce_batch(reqs) == want
+        dev = torch.full((8,), float("nan"), dtype=torch.float64, device="cuda")
+        ctx.reduce_enqueue(reqs, dev)
+        assert dev.cpu().tolist() == want
+    assert ctx.reduce_batch([], extra=extra) == [1.25, -3.5e7]
 
 
 def test_gemm_rejects_non_library_tiles(ctx):

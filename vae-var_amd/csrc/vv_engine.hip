@@ -336,7 +336,8 @@ struct vv_ctx {
   double* dout = nullptr;  // device scalar
   float* doutf = nullptr;
   double* redb = nullptr;   // vv_reduce_batch: kMaxBatch reduction scratch areas
-  double* doutb = nullptr;  // ... and its device results (kMaxBatch + kMaxExtra doubles)
+  double* hredb = nullptr;      // vv_reduce_batch's results: coherent host-mapped doubles (kMaxBatch + kMaxExtra)
+  double* hredb_dev = nullptr;  // ... the device view the final kernel writes through
   float* twoloop = nullptr;  // L-BFGS two-loop scalars: al[kMaxHistory]
   char* metric_ws = nullptr;  // vv_metrics partial sums + latitude weights
   size_t metric_cap = 0;
@@ -363,6 +364,7 @@ namespace {
 
 constexpr int kRedBlocks = 1024;
 constexpr int kMaxBatch = 8, kMaxExtra = 16;  // vv_reduce_batch
+static_assert(kMaxBatch <= vv::ReduceReqs::kMax, "vv_reduce_batch requests exceed the multi-reduction kernel");
 constexpr int kMaxHistory = 256;  // L-BFGS history pairs accepted by vv_lbfgs_two_loop
 
 int set_dev(vv_ctx* ctx) {
@@ -1854,7 +1856,9 @@ int vv_ctx_create(int device, vv_ctx** out) {
   VV_HIP(hipMalloc(&c->dout, 4 * sizeof(double)));
   VV_HIP(hipMalloc(&c->doutf, 4 * sizeof(float)));
   VV_HIP(hipMalloc(&c->redb, (size_t)kMaxBatch * kRedBlocks * sizeof(double)));
-  VV_HIP(hipMalloc(&c->doutb, (size_t)(kMaxBatch + kMaxExtra) * sizeof(double)));
+  VV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hredb), (size_t)(kMaxBatch + kMaxExtra) * sizeof(double),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  VV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hredb_dev), c->hredb, 0));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
   *out = c;
   return 0;
@@ -1882,7 +1886,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   (void)hipFree(ctx->dout);
   (void)hipFree(ctx->doutf);
   (void)hipFree(ctx->redb);
-  (void)hipFree(ctx->doutb);
+  if (ctx->hredb) (void)hipHostFree(ctx->hredb);
   (void)hipFree(ctx->gemm_ws);
   if (ctx->apl) (void)hipFree(ctx->apl);
   if (ctx->gattn_ws) (void)hipFree(ctx->gattn_ws);
@@ -2315,32 +2319,17 @@ int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* 
   int r = set_dev(ctx);
   if (r) return r;
   hipStream_t st = (hipStream_t)stream;
-  // the same kernels, grids and partial layouts as vv_dot / vv_abssum / vv_absmax: identical values
+  // the same grids, element partitions and partial layouts as vv_dot / vv_abssum / vv_absmax (identical values), all
+  // requests in one launch and their finals + the extras in a second, written straight into the host-mapped results
+  vv::ReduceReqs rq{};
   for (int i = 0; i < count; ++i) {
-    double* part = ctx->redb + (size_t)i * kRedBlocks;
-    if (ops[i] == 0)
-      VV_HIP(vv::vec_dot(a[i], b[i], n, part, kRedBlocks, ctx->doutb + i, st));
-    else if (ops[i] == 1)
-      VV_HIP(vv::vec_abssum(a[i], n, part, kRedBlocks, ctx->doutb + i, st));
-    else
-      VV_HIP(vv::vec_absmax(a[i], n, reinterpret_cast<float*>(part), kRedBlocks,
-                            reinterpret_cast<float*>(ctx->doutb + i), st));
+    rq.op[i] = ops[i];
+    rq.a[i] = a[i];
+    rq.b[i] = ops[i] == 0 ? b[i] : nullptr;
   }
-  if (n_extra)
-    VV_HIP(hipMemcpyAsync(ctx->doutb + count, dev_extra, n_extra * sizeof(double), hipMemcpyDeviceToDevice, st));
-  double h[kMaxBatch + kMaxExtra];
-  VV_HIP(hipMemcpyAsync(h, ctx->doutb, (count + n_extra) * sizeof(double), hipMemcpyDeviceToHost, st));
+  VV_HIP(vv::reduce_multi(rq, count, n, ctx->redb, kRedBlocks, ctx->hredb_dev, dev_extra, n_extra, st));
   VV_HIP(hipStreamSynchronize(st));
-  for (int i = 0; i < count; ++i) {
-    if (ops[i] == 2) {
-      float f;
-      memcpy(&f, &h[i], sizeof(float));
-      out[i] = f;
-    } else {
-      out[i] = h[i];
-    }
-  }
-  for (int i = 0; i < n_extra; ++i) out[count + i] = h[count + i];
+  for (int i = 0; i < count + n_extra; ++i) out[i] = ctx->hredb[i];  // absmax widened from float: exact
   return 0;
 }
 int vv_reduce_enqueue(vv_ctx* ctx, int count, const int* ops, const float* const* a, const float* const* b, int64_t n,
@@ -2354,15 +2343,13 @@ int vv_reduce_enqueue(vv_ctx* ctx, int count, const int* ops, const float* const
   if (r) return r;
   hipStream_t st = (hipStream_t)stream;
   // vv_reduce_batch's kernels and partial layouts (the same values), results left in dev_out (doubles), no sync
+  vv::ReduceReqs rq{};
   for (int i = 0; i < count; ++i) {
-    double* part = ctx->redb + (size_t)i * kRedBlocks;
-    if (ops[i] == 0)
-      VV_HIP(vv::vec_dot(a[i], b[i], n, part, kRedBlocks, dev_out + i, st));
-    else if (ops[i] == 1)
-      VV_HIP(vv::vec_abssum(a[i], n, part, kRedBlocks, dev_out + i, st));
-    else
-      VV_HIP(vv::vec_absmax_d(a[i], n, reinterpret_cast<float*>(part), kRedBlocks, dev_out + i, st));
+    rq.op[i] = ops[i];
+    rq.a[i] = a[i];
+    rq.b[i] = ops[i] == 0 ? b[i] : nullptr;
   }
+  VV_HIP(vv::reduce_multi(rq, count, n, ctx->redb, kRedBlocks, dev_out, nullptr, 0, st));
   return 0;
 }
 int vv_axpy(vv_ctx* ctx, float* y, const float* x, float alpha, int64_t n, void* stream) {

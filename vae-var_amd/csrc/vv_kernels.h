@@ -460,6 +460,17 @@ hipError_t vec_scale(float* y, float alpha, int64_t n, hipStream_t s);
 hipError_t vec_absmax(const float* x, int64_t n, float* partial, int nblk, float* out, hipStream_t s);
 hipError_t vec_absmax_d(const float* x, int64_t n, float* partial, int nblk, double* out, hipStream_t s);
 hipError_t vec_abssum(const float* x, int64_t n, double* partial, int nblk, double* out, hipStream_t s);
+// count reductions over equal-length vectors in two launches, request i: op 0 dot(a, b), 1 abssum(a), 2 absmax(a)
+// (the values of vec_dot / vec_abssum / vec_absmax_d with the same nblk); out[i] (device- or host-mapped doubles),
+// then the n_extra device doubles of `extra` copied to out[count...]. partial: count * nblk doubles.
+struct ReduceReqs {
+  static constexpr int kMax = 8;
+  const float* a[kMax];
+  const float* b[kMax];
+  int op[kMax];
+};
+hipError_t reduce_multi(const ReduceReqs& r, int count, int64_t n, double* partial, int nblk, double* out,
+                        const double* extra, int n_extra, hipStream_t s);
 // q (= -g on entry) -> L-BFGS direction d (two-loop recursion, device scalars); al: >= m device floats;
 // partial: 2 * nblk doubles
 hipError_t lbfgs_two_loop(float* q, const float* const* S, const float* const* Y, const float* ro, int m, float H_diag,

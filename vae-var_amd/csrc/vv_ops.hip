@@ -2272,6 +2272,75 @@ __global__ __launch_bounds__(256) void k_final_max_d(const float* partial, int n
   if (threadIdx.x == 0) out[0] = (double)fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// vv_reduce_batch / vv_reduce_enqueue in two launches: blockIdx.y = request i runs k_dot / k_abssum / k_absmax's
+// loop over the same grid-stride element partition (gridDim.x = their nblk) with the same block reduction, into
+// request i's partial area; k_final_multi's block i then finishes it as k_final_d / k_final_max_d, and one more
+// block copies the caller's device extras beside the results. Identical values to the per-request kernels, 2
+// launches instead of 2 per request (+ a copy).
+__global__ __launch_bounds__(256) void k_reduce_multi(ReduceReqs r, int64_t n, double* partial) {
+  __shared__ double red[4];
+  __shared__ float redf[4];
+  const int i = blockIdx.y;
+  const int op = r.op[i];
+  const float* a = r.a[i];
+  double* part = partial + (size_t)i * gridDim.x;
+  const int64_t k0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  if (op == 2) {
+    float m = 0.f;
+    for (int64_t k = k0; k < n; k += stride) m = fmaxf(m, fabsf(a[k]));
+    m = lane_max<64>(m);
+    if ((threadIdx.x & 63) == 0) redf[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      reinterpret_cast<float*>(part)[blockIdx.x] = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    return;
+  }
+  double acc = 0.0;
+  if (op == 0) {
+    const float* b = r.b[i];
+#pragma unroll 4
+    for (int64_t k = k0; k < n; k += stride) acc += (double)a[k] * (double)b[k];
+  } else {
+    for (int64_t k = k0; k < n; k += stride) acc += fabs((double)a[k]);
+  }
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(256) void k_final_multi(ReduceReqs r, int count, int nblk, const double* partial,
+                                                     double* out, const double* extra, int n_extra) {
+  __shared__ double red[4];
+  __shared__ float redf[4];
+  const int i = blockIdx.x;
+  if (i == count) {  // the extras block
+    for (int j = threadIdx.x; j < n_extra; j += 256) out[count + j] = extra[j];
+    return;
+  }
+  const double* part = partial + (size_t)i * nblk;
+  if (r.op[i] == 2) {
+    const float* pf = reinterpret_cast<const float*>(part);
+    float m = 0.f;
+    for (int j = threadIdx.x; j < nblk; j += 256) m = fmaxf(m, pf[j]);
+    m = lane_max<64>(m);
+    if ((threadIdx.x & 63) == 0) redf[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) out[i] = (double)fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    return;
+  }
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < nblk; j += 256) acc += part[j];
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) out[i] = t;
+}
+hipError_t reduce_multi(const ReduceReqs& r, int count, int64_t n, double* partial, int nblk, double* out,
+                        const double* extra, int n_extra, hipStream_t s) {
+  if (count < 0 || count > ReduceReqs::kMax || n_extra < 0 || (n_extra && !extra)) return hipErrorInvalidValue;
+  if (count) hipLaunchKernelGGL(k_reduce_multi, dim3(nblk, count), dim3(256), 0, s, r, n, partial);
+  const int blocks = count + (n_extra ? 1 : 0);
+  if (blocks)
+    hipLaunchKernelGGL(k_final_multi, dim3(blocks), dim3(256), 0, s, r, count, nblk, partial, out, extra, n_extra);
+  return hipGetLastError();
+}
+
 hipError_t vec_absmax_d(const float* x, int64_t n, float* partial, int nblk, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_absmax, dim3(nblk), dim3(256), 0, s, x, n, partial);
   hipLaunchKernelGGL(k_final_max_d, dim3(1), dim3(256), 0, s, partial, nblk, out);

@@ -28,8 +28,11 @@ def _ptr(t: torch.Tensor):
 
 
 def _stream(stream=None):
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return ctypes.c_void_p(s.cuda_stream)
+    # the current stream's raw handle without building a torch.cuda.Stream object (a third of a vector op's host
+    # cost on the L-BFGS mirror's launch-bound stretches)
+    if stream is not None:
+        return ctypes.c_void_p(stream.cuda_stream)
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
 
 
 class Context:
