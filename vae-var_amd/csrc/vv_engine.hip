@@ -1842,14 +1842,9 @@ int vv_lgunet_param_info(const vv_lgunet_config* cfg, int index, char* name, int
   return 0;
 }
 
-int vv_ctx_create(int device, vv_ctx** out) {
-  if (!out) return fail(VV_E_ARG, "null out");
-  int n = 0;
-  VV_HIP(hipGetDeviceCount(&n));
-  if (device < 0 || device >= n) return fail(VV_E_ARG, "device %d of %d", device, n);
-  auto* c = new vv_ctx();
-  c->device = device;
-  VV_HIP(hipSetDevice(device));
+// the context's fixed device buffers; on failure the caller destroys the partly built context (nothing leaks)
+static int ctx_alloc(vv_ctx* c) {
+  VV_HIP(hipSetDevice(c->device));
   VV_HIP(hipMalloc(&c->red, 2 * kRedBlocks * sizeof(double)));  // two halves: lbfgs_two_loop alternates
   VV_HIP(hipMalloc(&c->redf, kRedBlocks * sizeof(float)));
   VV_HIP(hipMalloc(&c->twoloop, kMaxHistory * sizeof(float)));
@@ -1860,6 +1855,20 @@ int vv_ctx_create(int device, vv_ctx** out) {
                        hipHostMallocMapped | hipHostMallocCoherent));
   VV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hredb_dev), c->hredb, 0));
   VV_HIP(hipMalloc(&c->gemm_ws, vv::gemm_ws_floats() * sizeof(float)));
+  return 0;
+}
+
+int vv_ctx_create(int device, vv_ctx** out) {
+  if (!out) return fail(VV_E_ARG, "null out");
+  int n = 0;
+  VV_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(VV_E_ARG, "device %d of %d", device, n);
+  auto* c = new vv_ctx();
+  c->device = device;
+  if (const int r = ctx_alloc(c)) {
+    (void)vv_ctx_destroy(c);
+    return r;
+  }
   *out = c;
   return 0;
 }
