@@ -253,7 +253,7 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
    (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
    launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
-   inverse window map, 1), "h4_streamk_mink" (> 0: the split-K tile-48 GEMMs whose fixup is fused into a LayerNorm run stream-K over every CU when K >= this, 0: off), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
+   inverse window map, 1), "h4_streamk_mink" (> 0: the split-K tile-48 GEMMs whose fixup is fused into a LayerNorm run stream-K over every CU when K >= this, 0: off), "fixup_stage" (the fused fixup + LayerNorm reads a workgroup's split-K partials as whole 128-B lines into LDS, 1, or per row, 0), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
    the misfit reads each state field once per evaluation and its adjoint runs on the network grid, k_misfit_grid /
    k_misfit_net_bwd, 3 rows of a band in flight per pass; 2 = the same with 6 rows; read by vv_bind_problem, 1), "mlp_w" (the fused Swin-tower MLP with its hidden layer split over
    the four waves of a 64-token workgroup, per-wave LDS-DMA weight rings and one u scale per token, k_mlpw: bit 0 at

@@ -672,14 +672,17 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
 
 
-@pytest.mark.parametrize("knob,ref,on", [("h5_var", 5, 4), ("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1)])
+@pytest.mark.parametrize("knob,ref,on", [("h5_var", 5, 4), ("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1),
+                                          ("fixup_stage", 0, 1)])
 def test_bitwise_knobs(full_dec, knob, ref, on):
     """h5_var: tile 49's full tiles go through the row-wise LDS epilogue (4: accumulators -> LDS -> float4 rows: the
     GELU / gelu' plane writers with their pre-activation stores and reads, bias) instead of the per-fragment one
     (5, same main loop). h4_gather: tile 48 reads a gathered A's producer row scales through the row map itself
     instead of a k_gather_scales pass (the counter shows the pass is gone). fixup_ln_rows: the fused fixup + LN1
-    after fc2 walks GEMM rows through the inverse window map (each row's arithmetic unchanged). The same per-element arithmetic either
-    way, so the config-2 decoder output, its input gradient and the closure are bit-identical."""
+    after fc2 walks GEMM rows through the inverse window map (each row's arithmetic unchanged). fixup_stage: the fused
+    fixup + LayerNorm sums its workgroup's split-K partials through LDS (same chunk-order sum per element). The same
+    per-element arithmetic either way, so the config-2 decoder output, its input gradient and the closure are
+    bit-identical."""
     from vaevar.engine import DAProblem
     from vaevar.problem import make_problem
     from vaevar.synth import smooth_field, uniform_sym

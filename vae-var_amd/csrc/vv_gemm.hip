@@ -2464,6 +2464,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
   if (k == "grid_fused") return &t.grid_fused;
   if (k == "h4_streamk_mink") return &t.h4_streamk_mink;
+  if (k == "fixup_stage") return &t.fixup_stage;
   if (k == "mlp_w") return &t.mlp_w;
   return nullptr;
 }

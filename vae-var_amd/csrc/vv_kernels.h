@@ -54,6 +54,8 @@ struct Tuning {
                                 // but not faster (dim 192: 64.7 / 72.5 vs 66.7 / 67.4 us; profiles/r05/knob_ab_*), off
   int h4_streamk_mink = 0;      // > 0: gemm_ln's tile-48 split GEMMs with K >= this run stream-K over every CU (GemmArgs.sk)
                                 // instead of S chunks of each tile on T x S workgroups (0: off)
+  int fixup_stage = 1;          // the fused fixup + LayerNorm sums a workgroup's 8 rows of split-K partials with whole
+                                // 128-B line reads into LDS first (0: each row's loads straight from the partials)
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
                                 // adjoint k_misfit_net_bwd (0: k_misfit_fwd / k_misfit_bwd_gather / k_flow_input(_adj));
                                 // 1: 3 rows of a band in flight per pass (more waves per SIMD), 2: 6 rows (r05: misfit

@@ -304,7 +304,42 @@ __device__ __forceinline__ void sk_slots(const GemmArgs& a, int t, int& w0, int&
   n = wof((long long)(t + 1) * nkt - 1) - w0 + 1;
 }
 
-template <int NV, int S, bool SK = false>
+// the chunk-order sums of the S-chunk partials of the 8 GEMM rows gr0 .. gr0 + 7 (gr0 % 8 == 0: one 8-row block of a
+// 256-row tile, i.e. fixed a, wm and the fragment-row pair hh = 2 hk, 2 hk + 1), read a whole 128-B line per 8 threads
+// (the per-row loads take half lines: rows r and r + 4 share each line) into stg[row][ntn 128] (r05 late). The sum of
+// every element is the per-row loads' (p0 + p1 + ... in chunk order): identical values.
+template <int S>
+__device__ __forceinline__ void fixup_stage(const GemmArgs& args, int gr0, float* stg) {
+  constexpr int PMAX = 5;  // pieces per thread: ntn 32 lines x 8 / 512 <= 5 for N <= 1280
+  const int ntm = (args.M + 255) >> 8, ntn = (args.N + 127) >> 7, LS = ntn * 128, nl = ntn * 256;
+  const int mb = gr0 >> 8, rr0 = gr0 & 255, wm = rr0 >> 6, a = (rr0 >> 4) & 3, hk = (rr0 >> 3) & 1;
+  const int GM = args.gm > 0 ? args.gm : 8;
+  const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
+  f4 pv[PMAX][S];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) {
+    const int e = min((int)threadIdx.x + 512 * p, nl - 1);
+    const int q = e & 7, L = e >> 3, wn = L & 1, r = (L >> 1) & 3, b = (L >> 3) & 3, nb = L >> 5;
+    const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
+    const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + (2 * hk + (q >> 2)) * 16 +
+                                                                     (q & 3) * 4);
+#pragma unroll
+    for (int c = 0; c < S; ++c) pv[p][c] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (16 * 4 * 512) + off);
+  }
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) {
+    const int e = threadIdx.x + 512 * p;
+    if (e < nl) {
+      const int q = e & 7, L = e >> 3, wn = L & 1, r = (L >> 1) & 3, b = (L >> 3) & 3, nb = L >> 5;
+      f4 acc = pv[p][0];
+#pragma unroll
+      for (int c = 1; c < S; ++c) acc += pv[p][c];
+      *reinterpret_cast<f4*>(stg + ((q >> 2) * 4 + r) * LS + nb * 128 + wn * 64 + b * 16 + (q & 3) * 4) = acc;
+    }
+  }
+}
+
+template <int NV, int S, bool SK = false, bool STG = false>
 __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   // wave = GEMM row gr (ginv) or LN row j: with a gather, walking GEMM rows keeps each 128-B line of a partial
   // (two GEMM rows of one wave quarter) inside one workgroup
@@ -314,23 +349,27 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   // the row-invariant vectors (bias, gamma, beta) once per workgroup into LDS (r05: 15 of a wave's 35 global loads
   // re-read them per row; the kernel is bound by vector-memory issue, r04 PMC)
   __shared__ __attribute__((aligned(16))) float lv[3][kFixupLnMaxN];
+  extern __shared__ __attribute__((aligned(16))) float stg[];  // STG: the workgroup's 8 rows of chunk sums
   for (int i = threadIdx.x; i < 3 * f4n; i += 512) {
     const int q = i / f4n, c4 = 4 * (i - q * f4n);
     const float* src = q == 0 ? G.bias : q == 1 ? l.gamma : l.beta;
     *reinterpret_cast<f4*>(&lv[q][c4]) = src ? *reinterpret_cast<const f4*>(src + c4) : f4{0.f, 0.f, 0.f, 0.f};
   }
-  __syncthreads();
-  if (w >= args.M) return;
-  const int j = l.ginv ? l.ginv[w] : w;
-  const int gr = l.ginv ? w : l.gmap ? l.gmap[j] : j;
+  // (STG: the row's own loads are issued after the staging: issued before it they measured slower, r05ae)
+  const int wl = min(w, args.M - 1);  // rows past M (the last workgroup) read row M - 1 and store nothing
+  const int j = l.ginv ? l.ginv[wl] : wl;
+  const int gr = l.ginv ? wl : l.gmap ? l.gmap[j] : j;
   const int xo = args.crow ? args.crow[gr] : gr;
   const int lo = l.lo_x ? xo : j;
+  const int rrow = args.rmod > 0 ? xo % args.rmod : xo;
+  f4 pv[S][NV], rv[NV], bv[NV], gv[NV], bb[NV];
+  if constexpr (STG) fixup_stage<S>(args, blockIdx.x * 8, stg);  // GEMM row = w (host: ginv set or no gmap)
+  __syncthreads();
+  if (w >= args.M) return;
   const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
   const int mb = gr >> 8, rr = gr & 255, wm = rr >> 6, a = (rr >> 4) & 3, hh = (rr >> 2) & 3, r = rr & 3;
   const int GM = args.gm > 0 ? args.gm : 8;  // tile_mn's grouped order (gemm_nt always sets gm)
   const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
-  const int rrow = args.rmod > 0 ? xo % args.rmod : xo;
-  f4 pv[S][NV], rv[NV], bv[NV], gv[NV], bb[NV];
   bool ok[NV];
   int sw0[NV], nsk[NV];
 #pragma unroll
@@ -347,6 +386,8 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
       for (int c = 0; c < S; ++c)
         pv[c][v] = c < nsk[v] ? *reinterpret_cast<const f4*>(args.ws + (size_t)(sw0[v] + c + tl) * (16 * 4 * 512) + off)
                               : f4{0.f, 0.f, 0.f, 0.f};
+    } else if (STG) {  // the chunk sum, staged in LDS (pv[0] holds it, the sum below adds nothing more)
+      pv[0][v] = *reinterpret_cast<const f4*>(stg + (threadIdx.x >> 6) * (((N + 127) >> 7) * 128) + c4);
     } else {
 #pragma unroll
       for (int c = 0; c < S; ++c)
@@ -367,7 +408,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   for (int v = 0; v < NV; ++v) {
     f4 acc = pv[0][v];
 #pragma unroll
-    for (int c = 1; c < S; ++c)
+    for (int c = 1; c < (STG ? 1 : S); ++c)
       if (!SK || c < nsk[v]) acc += pv[c][v];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -416,24 +457,27 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
 
 // the backward form: dy = the fixup of a STORE GEMM without bias (chunk-order sum + 0, k_gemm_fixup_sub16's
 // value), then k_ln_bwd<64, NV> on the row (x, res, y and the planes at row lmap[j], stats at j)
-template <int NV, int S, bool SK = false>
+template <int NV, int S, bool SK = false, bool STG = false>
 __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs l) {
   const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
   const int N = args.N, f4n = N >> 2, C = N;
   __shared__ __attribute__((aligned(16))) float lg[kFixupLnMaxN];  // gamma once per workgroup (as k_fixup_ln)
+  extern __shared__ __attribute__((aligned(16))) float stg[];        // STG: the 8 rows' chunk sums
   for (int i = threadIdx.x; i < f4n; i += 512)
     *reinterpret_cast<f4*>(&lg[4 * i]) = *reinterpret_cast<const f4*>(l.gamma + 4 * i);
+  const int jl = min(j, args.M - 1);  // rows past M read row M - 1 and store nothing
+  const int pr = l.lmap ? l.lmap[jl] : jl;
+  const float* res = l.res ? l.res : l.x;  // dummy source when there is no residual (never added)
+  f4 pv[S][NV], xv[NV], gv[NV], rv[NV];
+  if constexpr (STG) fixup_stage<S>(args, blockIdx.x * 8, stg);  // GEMM row = j
   __syncthreads();
   if (j >= args.M) return;
   const int gr = j;
-  const int pr = l.lmap ? l.lmap[j] : j;
   const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
   const int mb = gr >> 8, rr = gr & 255, wm = rr >> 6, a = (rr >> 4) & 3, hh = (rr >> 2) & 3, r = rr & 3;
   const int GM = args.gm > 0 ? args.gm : 8;
   const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
   const float mean = l.stats[2 * j], rstd = l.stats[2 * j + 1];
-  const float* res = l.res ? l.res : l.x;  // dummy source when there is no residual (never added)
-  f4 pv[S][NV], xv[NV], gv[NV], rv[NV];
   bool ok[NV];
   int sw0[NV], nsk[NV];
 #pragma unroll
@@ -450,6 +494,8 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
       for (int c = 0; c < S; ++c)
         pv[c][v] = c < nsk[v] ? *reinterpret_cast<const f4*>(args.ws + (size_t)(sw0[v] + c + tl) * (16 * 4 * 512) + off)
                               : f4{0.f, 0.f, 0.f, 0.f};
+    } else if (STG) {
+      pv[0][v] = *reinterpret_cast<const f4*>(stg + (threadIdx.x >> 6) * (((N + 127) >> 7) * 128) + c4);
     } else {
 #pragma unroll
       for (int c = 0; c < S; ++c)
@@ -465,7 +511,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
   for (int v = 0; v < NV; ++v) {
     f4 acc = pv[0][v];
 #pragma unroll
-    for (int c = 1; c < S; ++c)
+    for (int c = 1; c < (STG ? 1 : S); ++c)
       if (!SK || c < nsk[v]) acc += pv[c][v];
 #pragma unroll
     for (int e = 0; e < 4; ++e) dv[v][e] = acc[e] + 0.0f;  // the STORE epilogue's v = acc + bias (none)
@@ -519,21 +565,34 @@ hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s
     else hipLaunchKernelGGL((k_fixup_ln<5, kSkMaxSeg, true>), grid, dim3(512), 0, s, a, l);
     return hipGetLastError();
   }
+  // staged chunk sums (whole-line partial reads, fixup_stage) where the workgroup's 8 waves are 8 consecutive GEMM
+  // rows: always in the backward, in the forward when the rows are walked in GEMM order (ginv) or not gathered
+  const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+  const bool stg = TU.fixup_stage && (l.bwd || l.ginv || !l.gmap);
+  const size_t sl = stg ? (size_t)8 * ((a.N + 127) / 128) * 128 * sizeof(float) : 0;
+#define VV_FIXUP_LN(K, S)                                                  \
+  do {                                                                     \
+    if (stg)                                                               \
+      hipLaunchKernelGGL((K<5, S, false, true>), grid, dim3(512), sl, s, a, l); \
+    else                                                                   \
+      hipLaunchKernelGGL((K<5, S, false, false>), grid, dim3(512), 0, s, a, l); \
+  } while (0)
   if (l.bwd) {
     switch (a.tsplit) {
-      case 2: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 2>), grid, dim3(512), 0, s, a, l); break;
-      case 3: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 3>), grid, dim3(512), 0, s, a, l); break;
-      case 4: hipLaunchKernelGGL((k_fixup_ln_bwd<5, 4>), grid, dim3(512), 0, s, a, l); break;
+      case 2: VV_FIXUP_LN(k_fixup_ln_bwd, 2); break;
+      case 3: VV_FIXUP_LN(k_fixup_ln_bwd, 3); break;
+      case 4: VV_FIXUP_LN(k_fixup_ln_bwd, 4); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (a.tsplit) {
-    case 2: hipLaunchKernelGGL((k_fixup_ln<5, 2>), grid, dim3(512), 0, s, a, l); break;
-    case 3: hipLaunchKernelGGL((k_fixup_ln<5, 3>), grid, dim3(512), 0, s, a, l); break;
-    case 4: hipLaunchKernelGGL((k_fixup_ln<5, 4>), grid, dim3(512), 0, s, a, l); break;
+    case 2: VV_FIXUP_LN(k_fixup_ln, 2); break;
+    case 3: VV_FIXUP_LN(k_fixup_ln, 3); break;
+    case 4: VV_FIXUP_LN(k_fixup_ln, 4); break;
     default: return hipErrorInvalidValue;
   }
+#undef VV_FIXUP_LN
   return hipGetLastError();
 }
 

@@ -45,7 +45,7 @@ class Context:
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
                    "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt",
                    "win_mfma", "fc_h3_mink", "fuse_mlp", "fuse_attn", "attn_mfma", "gelu_planes", "attn_planes", "fixup_ln", "h5", "h5_var", "fc_conv_mf",
-                   "mlp_hc", "h4_gather", "fixup_ln_rows", "grid_fused", "mlp_w", "h4_streamk_mink")
+                   "mlp_hc", "h4_gather", "fixup_ln_rows", "grid_fused", "mlp_w", "h4_streamk_mink", "fixup_stage")
 
     def __init__(self, device: int = 0):
         self.device = device
