@@ -225,7 +225,7 @@ def sc4dvar_line(dev_index: int):
 def gemm_rocprof(key="gemm16_avg_us_per_call"):
     """Average rocprofv3 --kernel-trace --stats duration per fp16x3 GEMM call (main kernel + row scales + split-K
     fixup, tools/rocprof_gemm_summary.py) from the latest committed profile of `bench.py` itself."""
-    for rnd in ("r05",):  # the profile of this round's default command (config 3); older rounds profiled config 2
+    for rnd in ("r06", "r05"):  # the latest profile of the default command (config 3); r01-r04 profiled config 2
         path = os.path.join(ROOT, "profiles", rnd, "gemm_rocprof_summary.json")
         try:
             with open(path) as f:
@@ -238,7 +238,7 @@ def gemm_rocprof(key="gemm16_avg_us_per_call"):
 def gemm_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes of `bench.py` (FETCH_SIZE x2 +
     WRITE_SIZE with the gfx950 corrections, tools/pmc_traffic.py); PMC counters cannot be read live."""
-    for rnd in ("r05",):
+    for rnd in ("r06", "r05"):
         path = os.path.join(ROOT, "profiles", rnd, "gemm_traffic.json")
         try:
             with open(path) as f:
@@ -248,6 +248,37 @@ def gemm_traffic(kernel):
         except (OSError, KeyError, ValueError, TypeError):
             continue
     return None, None
+
+
+PMC_CLASSES = {"fp16x3": ("k_gemm_h4", "k_gemm_h5"), "tower": ("k_mlp", "k_ablk"), "bf16x6": ("k_gemm_bs",)}
+
+
+def pmc_mfma():
+    """MFMA busy fraction and held clock per kernel class from the committed rocprofv3 --pmc passes
+    (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE, SQ_INSTS_MFMA, SQ_BUSY_CYCLES, one pass each, over
+    config-3 closures), weighted by each kernel's share of the class's time; PMC counters cannot be read live."""
+    for rnd in ("r06",):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_mfma.json")
+        try:
+            with open(path) as f:
+                ks = json.load(f)["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        out = {}
+        for cls, pre in PMC_CLASSES.items():
+            rows = [r for k, r in ks.items() if k.split("<")[0].split("::")[-1].startswith(pre) and "mfma_busy" in r]
+            w = [r["duration_us_median"] * r["dispatches_per_pass"] for r in rows]
+            if not rows or sum(w) <= 0:
+                continue
+            avg = lambda key: sum(r.get(key, 0.0) * x for r, x in zip(rows, w)) / sum(w)
+            out[cls] = {"mfma_busy": avg("mfma_busy"), "mfma_busy_active_cus": avg("mfma_busy_active_cus"),
+                        "held_clock_ghz": avg("held_clock_ghz"), "kernels": len(rows)}
+        if out:
+            out["source"] = (f"profiles/{rnd}/pmc_mfma.json (tools/pmc_mfma.py: one rocprofv3 --pmc pass per counter + "
+                             "--kernel-trace over config-3 closures; busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 "
+                             "x 1024 SIMDs), clock = GRBM_GUI_ACTIVE / 8 / duration; time-weighted over the class)")
+            return out
+    return None
 
 
 def grid_roofline(prof):
@@ -365,10 +396,43 @@ class SelftestAnalyses:
         return self.analysis
 
 
+def thread_cpu():
+    """{tid: (thread name, CPU seconds)} of this process's threads (/proc/self/task/*/stat utime + stime)."""
+    tick = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+    out = {}
+    try:
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                with open(f"/proc/self/task/{tid}/stat") as f:
+                    s = f.read()
+            except OSError:
+                continue
+            name = s[s.index("(") + 1:s.rindex(")")]
+            fl = s[s.rindex(")") + 2:].split()
+            out[tid] = (name, (int(fl[11]) + int(fl[12])) / tick)
+    except OSError:
+        pass
+    return out
+
+
+def thread_cpu_delta(before, after, seconds):
+    """Per-thread CPU over an interval, as fractions of one CPU, the busiest first (threads named by their comm and
+    whether they are the main thread)."""
+    main = str(os.getpid())
+    rows = []
+    for tid, (name, cs) in after.items():
+        d = cs - before.get(tid, (name, 0.0))[1]
+        if d > 0:
+            rows.append({"thread": name + (" (main)" if tid == main else ""), "cpu_frac": round(d / max(seconds, 1e-9), 3)})
+    rows.sort(key=lambda r: -r["cpu_frac"])
+    return rows[:8]
+
+
 def timed_analyses(w, ensemble, steps, dev):
     """Barrier + sync, `steps` analyses (each gathered to rank 0 at N > 1), sync + barrier; max time over ranks."""
     ensemble.barrier()
     w.sync()
+    th0 = thread_cpu()
     t0 = time.perf_counter()
     c0 = time.process_time()
     d0 = w.discarded()
@@ -383,10 +447,11 @@ def timed_analyses(w, ensemble, steps, dev):
     ensemble.barrier()
     el = time.perf_counter() - t0
     cpu = time.process_time() - c0  # host CPU seconds of this rank (all its threads) over the timed region
+    threads = thread_cpu_delta(th0, thread_cpu(), el)
     disc = w.discarded() - d0
     return (ensemble.reduce_scalar(el, "max", dev), ensemble.reduce_scalar(iters, "sum", dev),
             ensemble.reduce_scalar(evals, "sum", dev), shapes,
-            (ensemble.reduce_scalar(cpu, "max", dev), ensemble.reduce_scalar(cpu, "sum", dev)),
+            (ensemble.reduce_scalar(cpu, "max", dev), ensemble.reduce_scalar(cpu, "sum", dev), threads),
             ensemble.reduce_scalar(disc, "sum", dev))
 
 
@@ -551,7 +616,9 @@ def main():
         # one node, 8 x cpu_frac_max_rank CPUs against the box's CPU quota
         "host_cpu": {"cpu_s_max_rank": host_cpu[0], "cpu_s_all_ranks": host_cpu[1],
                      "cpu_frac_max_rank": host_cpu[0] / max(t_max, 1e-12),
-                     "cpus_busy_all_ranks": host_cpu[1] / max(t_max, 1e-12)},
+                     "cpus_busy_all_ranks": host_cpu[1] / max(t_max, 1e-12),
+                     "threads_rank0": host_cpu[2],
+                     "host_wait": (w.ctx.get_tuning("host_wait") if not args.selftest else None)},
         "timed_region": f"barrier + sync, {args.steps} step(s) of {args.batch} analyses per rank (z = 0, Nit = {cfg['nit']} outer lbfgs.step "
                         "calls, the analysis decode, at N > 1 the RCCL gather of every analysis to rank 0), sync + "
                         "barrier; max over ranks. The per-outer-pass logging evaluation cal_loss and WRMSE/Bias "
@@ -621,6 +688,16 @@ def main():
                 out["roofline"]["rocprof"] = {"avg_call_us": us, "achieved": dom["flops"] / n / (us * 1e-6) / 1e12,
                                               "frac": dom["flops"] / n / (us * 1e-6) / 1e12 / peak,
                                               "source": f"{src} (rocprofv3 --kernel-trace --stats of bench.py)"}
+            pm = pmc_mfma()
+            if pm:
+                if "fp16x3" in pm:
+                    out["roofline"]["mfma_busy"] = pm["fp16x3"]["mfma_busy"]
+                    out["roofline"]["mfma_busy_active_cus"] = pm["fp16x3"]["mfma_busy_active_cus"]
+                    out["roofline"]["held_clock_ghz"] = pm["fp16x3"]["held_clock_ghz"]
+                    # the fp16 MFMA peak at the clock the chip holds under these kernels (2.5 PF is quoted at 2.4 GHz)
+                    out["roofline"]["peak_at_held_clock"] = peak * pm["fp16x3"]["held_clock_ghz"] / 2.4
+                    out["roofline"]["frac_of_held_clock_peak"] = ach / out["roofline"]["peak_at_held_clock"]
+                out["roofline"]["pmc"] = pm
             # the other GEMM class (bf16x6, short-K Swin-tower linears) against its own peak
             g6a = g6["flops"] / max(g6["ms"] * 1e-3, 1e-12) / 1e12
             out["roofline"]["bf16x6_class"] = {"achieved": g6a, "peak": PEAK_SPLIT_TFLOPS,

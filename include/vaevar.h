@@ -81,6 +81,10 @@ int vv_ctx_destroy(vv_ctx* ctx);
 /* a network instance: `batch` images per forward, `n_slots` independent saved-activation sets
    (one per forecast step of the 4D-Var window) */
 int vv_model_create(vv_ctx* ctx, const vv_lgunet_config* cfg, int batch, int n_slots, int* model_id);
+/* free a network instance (its weights, planes, saved activations and workspace; `del model` in the reference): the
+   id becomes invalid; a problem bound to it (vv_bind_problem / vv_sc4dvar_bind) is unbound and the context's closure
+   graphs are dropped. Synchronises the device. */
+int vv_model_destroy(vv_ctx* ctx, int model_id);
 /* ptrs[i] points to parameter i in vv_lgunet_param_info order (host or device memory, fp32) */
 int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n);
 /* out: (batch, sum(outchans), H, W); only channels < out_limit are written (0 = all) */
@@ -115,8 +119,7 @@ int vv_set_closure_graph(vv_ctx* ctx, int enable);
 int vv_get_closure_graph(vv_ctx* ctx, int kind, long long* info);
 /* process-wide host-side launch counters (monotonic; eager launches only, a graph replay does not count):
    "rowsplit" (k_rowsplit passes building a GEMM's fp16x3 A planes), "fixup_ln" (split-K fixups fused into a
-   LayerNorm), "splitk_fixup" (stand-alone tile-48 split-K fixups), "gather_scales" (k_gather_scales passes of tile 48),
-   "streamk" (fused fixup + LayerNorm launches consuming stream-K partials, tuning key "h4_streamk_mink").
+   LayerNorm), "splitk_fixup" (stand-alone tile-48 split-K fixups), "gather_scales" (k_gather_scales passes of tile 48).
    Tests use them to show a fused path ran. */
 int vv_get_counter(const char* name, long long* value);
 /* analysis states xa (B,C,Hs,Ws) */
@@ -238,7 +241,7 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    "win_attn" (LGUnet_all_1 LDS window attention, 1), "win_mfma" (that kernel on the exact-f32 MFMA, 1),
    "fc_h3_mink" (smallest K of the forecast network's fp16x3 GEMMs, 192), "fuse_mlp" (the fused Swin-tower
    LN2 + fc1 + GELU + fc2 + residual sub-block and its backward: bit 0 at dim 96, bit 1 at dim 192, 3), "fuse_attn" (the fused Swin-tower
-   LN1 + qkv + window attention + proj + residual sub-block: bits 0 / 1 forward / backward at dim 96, bits 2 / 3 at dim 192, 3), "attn_mfma" (the window attention of
+   LN1 + qkv + window attention + proj + residual sub-block at dim 96: bits 0 / 1 forward / backward, 3), "attn_mfma" (the window attention of
    the LG stage, head dim 192, and of the unfused tower stages, head dim 32, on the exact-f32 MFMA, 1), "gelu_planes" (the LG-stage GELU / gelu' GEMM
    epilogues write the fp16x3 planes of the K = 4C GEMM after them, 1), "attn_planes" (the LG-stage attention
    forward writes the planes of a tile-48 proj GEMM, 1), "fixup_ln" (that GEMM's split-K fixup fused into the LN2
@@ -247,19 +250,18 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    LGUnet_all_1 global window on the flash MFMA kernel, vv_attention_global, 1), "gattn_qf" (its 16-query blocks per
    wave: 1 = eight waves, two per SIMD; 2 = four waves of 32 queries, 1), "h4_small" (tile 48 with whole-chip split-K
    also for 64..143 256-row tiles, 1), "h4_split_minkt" (k-tiles per chunk of that split, 12), "h5" (tile 49, 256x144, where its
-   tiles fill whole rounds of the chip and tile 48's leave a split-K tail: the N = 4608 GEMMs at 2048 rows, 1), "h5_var"
-   (tile 49's schedule variant, experiments), "fc_conv_mf" (LGUnet_all_1's PatchEmbed / ConvTranspose2d as direct
+   tiles fill whole rounds of the chip and tile 48's leave a split-K tail: the N = 4608 GEMMs at 2048 rows, 1), "fc_conv_mf" (LGUnet_all_1's PatchEmbed / ConvTranspose2d as direct
    exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1), "mlp_hc" (the fused dim-192 MLP: 32 or 64 hidden units
    per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
    (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
    launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
-   inverse window map, 1), "h4_streamk_mink" (> 0: the split-K tile-48 GEMMs whose fixup is fused into a LayerNorm run stream-K over every CU when K >= this, 0: off), "fixup_stage" (the fused fixup + LayerNorm reads a workgroup's split-K partials as whole 128-B lines into LDS, 1, or per row, 0), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
+   inverse window map, 1), "fixup_stage" (the fused fixup + LayerNorm reads a workgroup's split-K partials as whole 128-B lines into LDS, 1, or per row, 0), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
    the misfit reads each state field once per evaluation and its adjoint runs on the network grid, k_misfit_grid /
-   k_misfit_net_bwd, 3 rows of a band in flight per pass; 2 = the same with 6 rows; read by vv_bind_problem, 1), "mlp_w" (the fused Swin-tower MLP with its hidden layer split over
-   the four waves of a 64-token workgroup, per-wave LDS-DMA weight rings and one u scale per token, k_mlpw: bit 0 at
-   dim 96, bit 1 at dim 192, 0: correct, measured no faster than k_mlp). Results stay fp32-level for every value; a change drops the
+   k_misfit_net_bwd, 3 rows of a band in flight per pass; 2 = the same with 6 rows; read by vv_bind_problem, 1), "host_wait" (how
+   vv_reduce_batch waits for the stream: 0 hipStreamSynchronize, which keeps a host CPU busy; 1 sleeps, then polls
+   hipStreamQuery). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key, or a value the dispatch does not accept (switches 0 / 1; "mlp_hc"
-   0, 2, 32, 64; "h5_var" 0..5; "gattn_qf" 1, 2; "grid_fused" 0..2; "fuse_mlp" and "mlp_w" 0..3; "fuse_attn" 0..15; the k-tile floors >= 1; the
+   0, 2, 32, 64; "gattn_qf" 1, 2; "grid_fused" 0..2; "fuse_mlp" and "fuse_attn" 0..3; the k-tile floors >= 1; the
    minimum K >= 0): VV_E_ARG, and the knob keeps its value. */
 int vv_set_tuning(vv_ctx* ctx, const char* key, int value);
 int vv_get_tuning(vv_ctx* ctx, const char* key, int* value);

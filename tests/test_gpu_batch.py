@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import check, check_bitwise
+
 pytestmark = pytest.mark.gpu
 
 
@@ -52,9 +54,9 @@ def test_tiny_batch2_closure_bitwise(T):
         p1 = DAProblem(dec1, probs[b], flow=flow1)
         g1 = torch.empty(1, 4, 32, 64, device="cuda")
         jb1, jo1 = p1.closure(z[b:b + 1].contiguous(), g1)
-        assert jb1 == jb2[b] and jo1 == jo2[b], (b, jb1, jb2[b], jo1, jo2[b])
-        assert torch.equal(g1[0], g2[b])
-        assert torch.equal(p1.trajectory(), x2[b])
+        check_bitwise(f"B=2 vs B=1 T={T} analysis {b} J", (jb1, jo1), (jb2[b], jo2[b]))
+        check_bitwise(f"B=2 vs B=1 T={T} analysis {b} dJ/dz", g1[0], g2[b])
+        check_bitwise(f"B=2 vs B=1 T={T} analysis {b} x_t", p1.trajectory(), x2[b])
 
 
 def test_tiny_batch2_lbfgs_bitwise():
@@ -69,7 +71,7 @@ def test_tiny_batch2_lbfgs_bitwise():
     for b in range(2):
         r1 = one_step_da(DAProblem(dec1, probs[b], flow=flow1), nit=2, log_terms=False)
         assert r1["n_iter"] == res["n_iter"][b] and r1["n_eval"] == res["n_eval"][b]
-        assert torch.equal(r1["xa"], res["xa"][b])
+        check_bitwise(f"batched L-BFGS analysis {b} xa", r1["xa"], res["xa"][b])
     assert res["batched_evals"] == max(res["n_eval"])
 
 
@@ -98,4 +100,7 @@ def test_full_batch2_closure_vs_single():
         e = (abs(jb1 - jb2[b]) / jb1, abs(jo1 - jo2[b]) / jo1, rel(g2[b].cpu(), g1[0].cpu()),
              rel(xa2[b], p1.analysis(z[b:b + 1].contiguous()).cpu()))
         print(f"full B=2 vs B=1, analysis {b}: J_b {e[0]:.1e} J_o {e[1]:.1e} grad {e[2]:.1e} xa {e[3]:.1e}")
-        assert e[0] < 1e-12 and e[1] < 1e-6 and e[2] < 1e-5 and e[3] < 1e-6
+        check(f"full B=2 vs B=1 analysis {b} J_b", e[0], 1e-12)
+        check(f"full B=2 vs B=1 analysis {b} J_o", e[1], 1e-6)
+        check(f"full B=2 vs B=1 analysis {b} dJ/dz", e[2], 1e-5)
+        check(f"full B=2 vs B=1 analysis {b} xa", e[3], 1e-6)

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLD
+from conftest import GOLD, check, check_bitwise
 
 pytestmark = pytest.mark.gpu
 
@@ -90,11 +90,14 @@ def test_cycle_vs_oracle_and_resume(tmp_path):
         ew = float(np.abs(cyc.metrics_list["ana_wrmse"][k] - w).max() / np.abs(w).max())
         eb = float(np.abs(cyc.metrics_list["ana_bias"][k] - b).max() / np.abs(w).max())
         print(f"cycle {k}: xa increment rel {e:.1e}, ana WRMSE rel {ew:.1e}, bias rel {eb:.1e}")
-        assert e < 1e-3 and ew < 1e-3 and eb < 1e-3
+        check(f"cycle {k} xa increment", e, 1e-3)
+        check(f"cycle {k} ana WRMSE", ew, 1e-3)
+        check(f"cycle {k} ana bias", eb, 1e-3)
 
     # resume: a new driver over the same directory continues from the checkpoint (get_current_states)
     cyc2 = CyclicVAE4DVar(dec, fc, obs, T0, end + dt.timedelta(hours=6), Nit=1, name="tiny", out_dir=str(tmp_path))
-    assert cyc2.current_time == end and torch.equal(cyc2.xb, cyc.xb)
+    assert cyc2.current_time == end
+    check_bitwise("cycle resume xb", cyc2.xb, cyc.xb)
     assert len(cyc2.metrics_list["ana_wrmse"]) == 3
     cyc2.run_assimilation()
     assert len(cyc2.metrics_list["ana_wrmse"]) == 4
@@ -115,7 +118,8 @@ def test_metrics_kernel_g9(tag, Hs, Ws, seed):
     ew = float(np.abs(w.cpu().numpy() - g["wrmse_" + tag]).max() / np.abs(g["wrmse_" + tag]).max())
     eb = float(np.abs(b.cpu().numpy() - g["bias_" + tag]).max() / np.abs(g["bias_" + tag]).max())
     print(f"G9 {Hs}x{Ws}: WRMSE rel {ew:.1e}, Bias rel {eb:.1e}")
-    assert ew < 1e-5 and eb < 1e-5
+    check(f"G9 {Hs}x{Ws} WRMSE", ew, 1e-5)
+    check(f"G9 {Hs}x{Ws} Bias", eb, 1e-5)
 
 
 def test_cycle_real_obs_matches_manual_composition(tmp_path):
@@ -160,8 +164,8 @@ def test_cycle_real_obs_matches_manual_composition(tmp_path):
         prob = DAProblem(dec, {"xb": xb, "yo": yo, "H": Hd, "R": Rd, "mean": cyc.mean, "std": cyc.std,
                                "std_tr": cyc.std_tr}, obs_interp=oi.interp)
         xa = one_step_da(prob, nit=1)["xa"]
-        assert torch.equal(xa, xas[k]), k
+        check_bitwise(f"real-obs cycle {k} xa vs hand composition", xa, xas[k])
         xb = integrate(fc, xa, cyc.mean_d, cyc.std_d, 1)
-    assert torch.equal(xb, cyc.xb)
+    check_bitwise("real-obs cycle xb vs hand composition", xb, cyc.xb)
     w = np.asarray(cyc.metrics_list["ana_wrmse"])
     assert w.shape == (2, 69) and np.isfinite(w).all()

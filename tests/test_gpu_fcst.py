@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLD
+from conftest import GOLD, check
 
 pytestmark = pytest.mark.gpu
 
@@ -36,7 +36,7 @@ def test_fcst_tiny_g7():
     out = _model(cfg).forward_raw(x)
     e = rel(out.cpu(), g["out"])
     print(f"G7 tiny LGUnet_all_1: out rel {e:.2e}")
-    assert e < 1e-5
+    check("G7 out", e, 1e-5)
 
 
 def test_fcst_025deg_g11():
@@ -57,7 +57,9 @@ def test_fcst_025deg_g11():
     e_ss = abs((o * o).sum() - float(g["out_sumsq"])) / float(g["out_sumsq"])
     e_as = abs(np.abs(o).sum() - float(g["out_abssum"])) / float(g["out_abssum"])
     print(f"G11 LGUnet_all_1 0.25deg: sampled out rel {e:.2e}, sumsq rel {e_ss:.1e}, abssum rel {e_as:.1e}")
-    assert e < 1e-4 and e_ss < 1e-5 and e_as < 1e-5
+    check("G11 sampled out", e, 1e-4)
+    check("G11 sumsq", e_ss, 1e-5)
+    check("G11 abssum", e_as, 1e-5)
 
 
 @pytest.mark.parametrize("name", ["MID_FCST", "BIG_FCST"])
@@ -77,7 +79,7 @@ def test_fcst_mid_vs_oracle(name):
         ref = lgunet1_forward(synth_params(cfg), cfg, torch.from_numpy(x))
     e = rel(out.cpu(), ref)
     print(f"{name} LGUnet_all_1 {cfg['img_size']}: out rel {e:.2e}")
-    assert e < 1e-4
+    check(f"{name} out vs oracle", e, 1e-4)
 
 
 def test_fcst_window_attention_mfma_vs_valu():
@@ -99,7 +101,8 @@ def test_fcst_window_attention_mfma_vs_valu():
         m.ctx.set_tuning("win_mfma", 1)
     e = rel(b.cpu(), a.cpu())
     print(f"window attention MFMA vs VALU: forecast rel {e:.2e}")
-    assert torch.isfinite(b).all() and e < 1e-5
+    assert torch.isfinite(b).all()
+    check("forecast window attention MFMA vs VALU", e, 1e-5)
 
 
 def test_fcst_backward_refused():
@@ -141,7 +144,7 @@ def test_integrate_forecast(grid):
     ref = y.reshape(Cs, Hs, Ws) * std.view(-1, 1, 1) + mean.view(-1, 1, 1)
     e = rel(out.cpu(), ref)
     print(f"integrate {grid}: rel {e:.2e}")
-    assert e < 1e-5
+    check(f"integrate {grid}", e, 1e-5)
 
 
 def _attn_ref_fp64(qkv, heads):
@@ -188,7 +191,8 @@ def test_attention_global_vs_fp64(N, C, heads, logit):
         o32 = torch.softmax(q[:, sl] @ k[:, sl].t(), dim=1) @ v[:, sl]
         e32 = max(e32, float((o32.double() - ref[:, sl]).abs().max() / ref.abs().max()))
     print(f"global attention N {N} C {C} heads {heads}: rel {e:.2e} (torch fp32: {e32:.2e})")
-    assert torch.isfinite(out).all() and e < max(1e-5, 2 * e32), (e, e32)
+    assert torch.isfinite(out).all()
+    check(f"global attention N {N} C {C} vs fp64 (bound max(1e-5, 2x torch fp32))", e, max(1e-5, 2 * e32))
 
 
 def test_attention_global_rejects():

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLD
+from conftest import GOLD, check, check_bitwise, note
 
 pytestmark = pytest.mark.gpu
 
@@ -38,17 +38,19 @@ def test_obs_augment_kernel(full_dec):
     xa = obs_augment(full_dec.ctx, interp.cuda(), x.cuda()).cpu()
     ref = x_aug_ref(x, interp)
     assert xa.shape == (2, 204, 33, 47)
-    assert rel(xa, ref) < 1e-6
-    assert torch.equal(xa[:, :4], x[:, :4])
+    check("x_aug 13->40 vs F.linear", rel(xa, ref), 1e-6)
+    check_bitwise("x_aug surface channels pass through", xa[:, :4], x[:, :4])
     # a coarser operator (n_out = 7) through the same kernel
     i7, _ = obs_interp_ref(13, 7)
-    assert rel(obs_augment(full_dec.ctx, i7.cuda(), x.cuda()).cpu(), x_aug_ref(x, i7)) < 1e-6
+    check("x_aug 13->7 vs F.linear", rel(obs_augment(full_dec.ctx, i7.cuda(), x.cuda()).cpu(), x_aug_ref(x, i7)), 1e-6)
 
 
-@pytest.mark.parametrize("T", [1, 2])
-def test_real_obs_closure(full_dec, T):
+@pytest.mark.parametrize("T,Hs,Ws", [(1, 128, 256), (2, 128, 256), (2, 150, 300)])
+def test_real_obs_closure(full_dec, T, Hs, Ws):
     """One closure (J + dJ/dz) with the real-observation operator at 128x256 (T=2 adds the flow stand-in, so the
-    operator's gradient also travels through the adjoint of integrate) vs the oracle on CPU."""
+    operator's gradient also travels through the adjoint of integrate) vs the oracle on CPU. 150x300, T=2: an
+    interpolated state grid that binds with the one-pass grid misfit (grid_fused) and then gets the operator, which
+    moves the closure to the per-element kernels and the flow-input adjoint's full-grid carry."""
     from oracle.da_ref import oracle_problem
     from oracle.lgunet_ref import synth_params
     from vaevar import config as C
@@ -56,7 +58,7 @@ def test_real_obs_closure(full_dec, T):
     from vaevar.problem import make_real_problem
     from vaevar.synth import smooth_field
 
-    p = make_real_problem(Hs=128, Ws=256, T=T, seed=20250623, obs_frac=0.05)
+    p = make_real_problem(Hs=Hs, Ws=Ws, T=T, seed=20250623, obs_frac=0.05)
     flow = LGUnet(C.FLOW, 1, 1).load_synthetic() if T > 1 else None
     prob = DAProblem(full_dec, p, flow=flow)
     z = torch.from_numpy(0.3 * smooth_field(406, (1, 32, 128, 256)))
@@ -70,8 +72,9 @@ def test_real_obs_closure(full_dec, T):
     (rb + rob).backward()
     e_j = abs(jo - float(rob)) / abs(float(rob))
     e_g = rel(g.cpu(), zr.grad)
-    print(f"real-obs closure T={T}: J_o {jo:.6e} (oracle {float(rob):.6e}, rel {e_j:.2e}), grad rel {e_g:.2e}")
-    assert e_j < 1e-4 and e_g < 1e-4
+    print(f"real-obs closure T={T} {Hs}x{Ws}: J_o {jo:.6e} (oracle {float(rob):.6e}, rel {e_j:.2e}), grad rel {e_g:.2e}")
+    check(f"real-obs closure T={T} {Hs}x{Ws} J_o", e_j, 1e-4)
+    check(f"real-obs closure T={T} {Hs}x{Ws} dJ/dz", e_g, 1e-4)
     # the identity operator still rejects observation-space fields
     with pytest.raises(ValueError):
         DAProblem(full_dec, dict(p, interp=None), flow=flow)
@@ -97,13 +100,16 @@ def one_step_vs_golden(prob, prob_np, g, tag):
         return eJ, e_xa, e_dx
 
     eJ, e_xa, e_dx = run()
-    assert e_xa < 1e-3 and e_dx < 1e-2 and eJ < 2e-2
+    tag = tag.split()[0]
+    check(f"{tag} free xa rel-L2", e_xa, 1e-3)
+    check(f"{tag} free |xa-xb|^2", e_dx, 1e-2)
+    check(f"{tag} free J per pass (max)", eJ, 2e-2 if "ls_t" in g.files else 1e-3)
     if "ls_t" in g.files:
         steps = [(float(t), int(n)) for t, n in zip(g["ls_t"], g["ls_evals"])]
         rJ, r_xa, r_dx = run(steps)
-        assert rJ < 1e-3 and r_xa < 1e-3 and r_dx < 1e-2
-    else:
-        assert eJ < 1e-3
+        check(f"{tag} replay J per pass (max)", rJ, 1e-3)
+        check(f"{tag} replay xa rel-L2", r_xa, 1e-3)
+        check(f"{tag} replay |xa-xb|^2", r_dx, 1e-2)
 
 
 def test_one_step_da_real_obs_g8(full_dec):

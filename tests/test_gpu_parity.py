@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLD, ROOT
+from conftest import GOLD, ROOT, check, check_bitwise, note
 
 pytestmark = pytest.mark.gpu
 
@@ -41,7 +41,8 @@ def test_tiny_decoder_g1(tiny):
     tiny.backward_raw(torch.from_numpy(g["cot"]).cuda(), dz)
     e_out, e_g = rel(out.cpu(), g["out"]), rel(dz.cpu(), g["grad"])
     print(f"G1 tiny decoder: out rel {e_out:.2e}  grad rel {e_g:.2e}")
-    assert e_out < 1e-5 and e_g < 1e-5
+    check("G1 out", e_out, 1e-5)
+    check("G1 grad", e_g, 1e-5)
 
 
 def test_tiny_autograd_fn(tiny):
@@ -49,7 +50,7 @@ def test_tiny_autograd_fn(tiny):
     z = torch.from_numpy(g["z"]).cuda().requires_grad_(True)
     out = tiny(z)
     (out * torch.from_numpy(g["cot"]).cuda()).sum().backward()
-    assert rel(z.grad.cpu(), g["grad"]) < 1e-5
+    check("G1 autograd grad", rel(z.grad.cpu(), g["grad"]), 1e-5)
 
 
 def test_batch2_matches_batch1():
@@ -62,10 +63,10 @@ def test_batch2_matches_batch1():
     z = torch.from_numpy(g["z"]).cuda()
     z2 = torch.cat([z, 0.5 * z], 0).contiguous()
     out = n2.forward_raw(z2)
-    assert rel(out[0:1].cpu(), g["out"]) < 1e-5
+    check("B=2 image 0 vs G1", rel(out[0:1].cpu(), g["out"]), 1e-5)
     n1 = LGUnet(C.TINY, 1, 1).load_synthetic()
     o1 = n1.forward_raw((0.5 * z).contiguous())
-    assert rel(out[1:2].cpu(), o1.cpu()) < 1e-6
+    check("B=2 image 1 vs B=1", rel(out[1:2].cpu(), o1.cpu()), 1e-6)
 
 
 @pytest.fixture(scope="module")
@@ -92,7 +93,10 @@ def test_full_decoder_g3(full_dec):
     e_ss = abs((o * o).sum() - g["out_sumsq"]) / g["out_sumsq"]
     e_gs = abs((gr * gr).sum() - g["grad_sumsq"]) / g["grad_sumsq"]
     print(f"G3 full decoder: out rel {e_o:.2e} (sumsq {e_ss:.1e})  grad rel {e_g:.2e} (sumsq {e_gs:.1e})")
-    assert e_o < 1e-4 and e_g < 1e-4 and e_ss < 1e-4 and e_gs < 1e-4
+    check("G3 out", e_o, 1e-4)
+    check("G3 grad", e_g, 1e-4)
+    check("G3 out sumsq", e_ss, 1e-4)
+    check("G3 grad sumsq", e_gs, 1e-4)
 
 
 def test_full_closure_g3(full_dec):
@@ -110,7 +114,9 @@ def test_full_closure_g3(full_dec):
     e_o = abs(jo - g["J_o"]) / g["J_o"]
     e_g = rel(gr[g["idx_grad"]], g["cgrad_sample"])
     print(f"G3 closure: J_b rel {e_b:.2e} J_o rel {e_o:.2e} grad rel {e_g:.2e}")
-    assert e_b < 1e-5 and e_o < 1e-4 and e_g < 1e-4
+    check("G3 closure J_b", e_b, 1e-5)
+    check("G3 closure J_o", e_o, 1e-4)
+    check("G3 closure dJ/dz", e_g, 1e-4)
 
 
 def test_full_closure_g3_exact_f32(full_dec):
@@ -135,7 +141,9 @@ def test_full_closure_g3_exact_f32(full_dec):
     e_o = abs(jo - g["J_o"]) / g["J_o"]
     e_g = rel(gr[g["idx_grad"]], g["cgrad_sample"])
     print(f"G3 closure (exact f32 GEMM): J_b rel {e_b:.2e} J_o rel {e_o:.2e} grad rel {e_g:.2e}")
-    assert e_b < 1e-5 and e_o < 1e-4 and e_g < 1e-4
+    check("G3 closure f32 J_b", e_b, 1e-5)
+    check("G3 closure f32 J_o", e_o, 1e-4)
+    check("G3 closure f32 dJ/dz", e_g, 1e-4)
 
 
 def _tiny_problem(T):
@@ -157,7 +165,9 @@ def test_tiny_4dvar_closure_g5b():
     jb, jo = prob.closure(z, grad)
     e = (abs(jb - g["J_b"]) / g["J_b"], abs(jo - g["J_o"]) / g["J_o"], rel(grad.cpu(), g["grad"]))
     print(f"G5b tiny 4D-Var T=2: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    assert e[0] < 1e-5 and e[1] < 1e-5 and e[2] < 1e-5
+    check("G5b J_b", e[0], 1e-5)
+    check("G5b J_o", e[1], 1e-5)
+    check("G5b grad", e[2], 1e-5)
 
 
 def test_tiny_lbfgs_trajectory_g5():
@@ -172,9 +182,9 @@ def test_tiny_lbfgs_trajectory_g5():
     J = np.array([a + b for a, b in res["J"]])
     Jr = g["J"].sum(1)
     print("G5 J per outer pass", J, "reference", Jr, "evals", res["n_eval"], g["n_eval"])
-    assert abs(J[-1] - Jr[-1]) / Jr[-1] < 1e-3
+    check("G5 final J", abs(J[-1] - Jr[-1]) / Jr[-1], 1e-3)
     xa = res["xa"].cpu().numpy()
-    assert np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]) < 1e-3
+    check("G5 xa rel-L2", np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]), 1e-3)
 
 
 def test_lbfgs_batched_scalars_bitwise():
@@ -189,8 +199,9 @@ def test_lbfgs_batched_scalars_bitwise():
     r0 = one_step_da(prob, nit=2, batch_scalars=False)
     r1 = one_step_da(prob, nit=2, batch_scalars=True)
     assert r0["n_eval"] == r1["n_eval"] and r0["n_iter"] == r1["n_iter"]
-    assert r0["J"] == r1["J"]
-    assert torch.equal(r0["z"], r1["z"]) and torch.equal(r0["xa"], r1["xa"])
+    check_bitwise("batched scalars J per pass", r0["J"], r1["J"])
+    check_bitwise("batched scalars z", r0["z"], r1["z"])
+    check_bitwise("batched scalars xa", r0["xa"], r1["xa"])
 
 
 def test_torch_lbfgs_dropin():
@@ -214,7 +225,7 @@ def test_torch_lbfgs_dropin():
         lb.step(closure)
     jb, jo = prob.closure(z.detach(), None)
     Jr = g["J"].sum(1)[-1]
-    assert abs(jb + jo - Jr) / Jr < 1e-3
+    check("torch.optim.LBFGS drop-in final J vs G5", abs(jb + jo - Jr) / Jr, 1e-3)
 
 
 def test_oracle_on_box_tiny_adam():
@@ -242,7 +253,7 @@ def test_oracle_on_box_tiny_adam():
     xa = res["xa"].cpu().numpy()
     e = np.linalg.norm(xa - xa_ref) / np.linalg.norm(xa_ref)
     print(f"config 1 (Adam x20): xa rel-L2 {e:.2e}")
-    assert e < 1e-4
+    check("config 1 Adam xa rel-L2", e, 1e-4)
 
 
 @pytest.mark.parametrize("Hs,Ws,T", [(45, 90, 2), (45, 92, 2), (47, 100, 3)])
@@ -280,7 +291,10 @@ def test_interpolated_grid_4dvar(Hs, Ws, T):
         xr = ro.trajectory(z)
     e_t = max(rel(prob.trajectory()[t].cpu(), xr[t]) for t in range(T))
     print(f"interpolated grid {Hs}x{Ws} T={T}: J_o rel {e_j:.2e} grad rel {e_g:.2e} xa rel {e_x:.2e} x_t rel {e_t:.2e}")
-    assert e_j < 1e-5 and e_g < 1e-5 and e_x < 1e-6 and e_t < 1e-5
+    check("interp J_o", e_j, 1e-5)
+    check("interp dJ/dz", e_g, 1e-5)
+    check("interp xa", e_x, 1e-6)
+    check("interp x_t", e_t, 1e-5)
 
 
 def test_config5_grid_fused_vs_unfused():
@@ -304,15 +318,20 @@ def test_config5_grid_fused_vs_unfused():
         g = torch.empty(1, 32, 128, 256, device="cuda")
         jb, jo = prob.closure(z, g)
         jb2, jo2 = prob.closure(z, None)
-        out[gf] = (jo, g.cpu(), jo2, prob.trajectory().cpu())
+        out[gf] = (jo, g.cpu(), jo2, prob.trajectory().cpu(), jb)
         del prob
     dec.ctx.set_tuning("grid_fused", 1)
     e_j = abs(out[1][0] - out[0][0]) / abs(out[0][0])
+    e_b = abs(out[1][4] - out[0][4]) / abs(out[0][4])  # J_b: the same sum over z, partials grouped by nblk
     e_g = rel(out[1][1], out[0][1])
     e_t = rel(out[1][3], out[0][3])
-    print(f"config-5 grid fused vs unfused: J_o {e_j:.2e} grad {e_g:.2e} J-only J_o {out[1][2]:.6e} vs "
+    print(f"config-5 grid fused vs unfused: J_o {e_j:.2e} J_b {e_b:.2e} grad {e_g:.2e} J-only J_o {out[1][2]:.6e} vs "
           f"{out[0][2]:.6e}, x_t {e_t:.2e}")
-    assert e_j < 1e-6 and e_g < 1e-5 and out[1][2] == out[1][0] and e_t == 0.0
+    check("grid fused vs unfused J_o", e_j, 1e-6)
+    check("grid fused vs unfused J_b", e_b, 1e-6)
+    check("grid fused vs unfused dJ/dz", e_g, 1e-5)
+    check_bitwise("grid fused J-only J_o vs J+grad J_o", out[1][2], out[1][0])
+    check("grid fused vs unfused x_t", e_t, 0.0, "==")
 
 
 def test_config5_grid_closure():
@@ -340,7 +359,8 @@ def test_config5_grid_closure():
     e_j = abs(jo - float(rob)) / abs(float(rob))
     e_g = rel(g.cpu(), zr.grad)
     print(f"config-5 grid closure: J_o rel {e_j:.2e} grad rel {e_g:.2e}")
-    assert e_j < 1e-4 and e_g < 1e-4
+    check("config-5 grid closure J_o", e_j, 1e-4)
+    check("config-5 grid closure dJ/dz", e_g, 1e-4)
 
 
 def test_one_step_da_config5_g6():
@@ -360,6 +380,28 @@ def test_one_step_da_config5_g6():
     flow = LGUnet(C.FLOW, 1, 1).load_synthetic()
     prob_np = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250620)
     one_step_vs_golden(DAProblem(dec, prob_np, flow=flow), prob_np, g, "G6 config 5 one_step_DA")
+
+def traj_checks(tag, mode, e_pass, e_x, e_dx, sens, free_default=None):
+    """The bounds of a full-budget trajectory test (SURVEY §8 c6 with the reference's own summation-order drift,
+    oracle/g10_sensitivity.py): replay — J per pass at max(1e-3, 2x the reference's replay drift), xa rel-L2 1e-3,
+    |xa-xb|^2 1e-2; free-running — the final J at max(1e-3, 2x its free-running drift) and xa at 1e-2 (the per-pass J
+    of a free run may sit on another line-search branch, so it is recorded, not bounded). Every achieved error is
+    recorded next to its bound (tests/conftest.py check / note)."""
+    for i, v in enumerate(e_pass):
+        note(f"{tag} {mode} J rel, pass {i}", v)
+    if mode == "replay":
+        drift = float(sens["replay_rel"].max()) if sens is not None else 0.0
+        bound = max(1e-3, 2 * drift)
+        print(f"{tag} replay J bound {bound:.1e} (reference vs itself under another summation order: {drift:.1e})")
+        check(f"{tag} replay J per pass (max)", e_pass.max(), bound)
+        check(f"{tag} replay xa rel-L2", e_x, 1e-3)
+        check(f"{tag} replay |xa-xb|^2", e_dx, 1e-2)
+    else:
+        bound = max(1e-3, 2 * float(sens["free_rel"][-1])) if sens is not None else free_default
+        check(f"{tag} free final J", e_pass[-1], bound)
+        check(f"{tag} free xa rel-L2", e_x, 1e-2)
+        note(f"{tag} free |xa-xb|^2", e_dx)
+
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
 def test_config5_trajectory_g15(full_dec, mode):
@@ -395,12 +437,7 @@ def test_config5_trajectory_g15(full_dec, mode):
     print(f"G15 config 5 ({mode}): J per pass rel {['%.1e' % v for v in e_pass]}; xa rel-L2 {e_x:.1e}; "
           f"|xa-xb|^2 rel {e_dx:.1e}; iters {res['n_iter']}, evals {res['n_eval']} (reference line searches "
           f"{len(g['ls_t'])}, evals {int(g['ls_evals'].sum()) + 0})")
-    if mode == "replay":
-        bound = max(1e-3, 2 * float(sens["replay_rel"].max())) if sens is not None else 1e-3
-        assert e_pass.max() < bound and e_x < 1e-3 and e_dx < 1e-2
-    else:
-        bound = max(1e-3, 2 * float(sens["free_rel"][-1])) if sens is not None else 2e-2
-        assert e_pass[-1] < bound and e_x < 1e-2
+    traj_checks("G15", mode, e_pass, e_x, e_dx, sens, free_default=2e-2)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -432,15 +469,7 @@ def test_config2_trajectory_g10(full_dec, mode):
     print(f"G10 config 2 ({mode}): J per pass rel {['%.1e' % v for v in e_pass]}; xa rel-L2 {e_x:.1e}; "
           f"|xa-xb|^2 rel {e_dx:.1e}; iters {res['n_iter']} (ref {int(g['n_iter'])}), evals {res['n_eval']} "
           f"(ref {int(g['n_eval'])})")
-    sens = gold("g10_sensitivity.npz")
-    if mode == "replay":
-        bound = max(1e-3, 2 * float(sens["replay_rel"].max()))
-        print(f"replay J bound {bound:.1e} (reference vs itself under another summation order: "
-              f"{float(sens['replay_rel'].max()):.1e})")
-        assert e_pass.max() < bound and e_x < 1e-3 and e_dx < 1e-2
-    else:
-        bound = max(1e-3, 2 * float(sens["free_rel"][-1]))
-        assert e_pass[-1] < bound and e_x < 1e-2
+    traj_checks("G10", mode, e_pass, e_x, e_dx, gold("g10_sensitivity.npz"))
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -477,13 +506,7 @@ def test_config3_trajectory_g13(full_dec, mode):
           f"(ref {int(g['n_eval'])})")
     sp = os.path.join(GOLD, "g13_sensitivity.npz")
     sens = np.load(sp) if os.path.exists(sp) else gold("g10_sensitivity.npz")
-    if mode == "replay":
-        bound = max(1e-3, 2 * float(sens["replay_rel"].max()))
-        print(f"replay J bound {bound:.1e} ({os.path.basename(sp) if os.path.exists(sp) else 'G10 sensitivity'})")
-        assert e_pass.max() < bound and e_x < 1e-3 and e_dx < 1e-2
-    else:
-        bound = max(1e-3, 2 * float(sens["free_rel"][-1]))
-        assert e_pass[-1] < bound and e_x < 1e-2
+    traj_checks("G13", mode, e_pass, e_x, e_dx, sens)
 
 
 def test_closure_graph_replay_bitwise():
@@ -512,8 +535,9 @@ def test_closure_graph_replay_bitwise():
     st = out["graph"][3]
     assert st["enabled"] and st["instantiated"] and not st["eager_only"] and st["launches"] >= out["graph"][2] - 2
     assert out["eager"][3]["launches"] == 0
-    assert out["graph"][0] == out["eager"][0] and out["graph"][2] == out["eager"][2]
-    assert torch.equal(out["graph"][1], out["eager"][1])
+    assert out["graph"][2] == out["eager"][2]
+    check_bitwise("graph vs eager J per pass", out["graph"][0], out["eager"][0])
+    check_bitwise("graph vs eager xa", out["graph"][1], out["eager"][1])
 
 
 def test_device_two_loop_bitwise(tiny):
@@ -536,7 +560,7 @@ def test_device_two_loop_bitwise(tiny):
             opt.step(closure)
         zs.append((z.clone(), opt.state["func_evals"]))
     assert zs[0][1] == zs[1][1]
-    assert torch.equal(zs[0][0], zs[1][0])
+    check_bitwise("device vs host two-loop z", zs[0][0], zs[1][0])
 
 
 def test_closure_edge_cases(tiny):
@@ -553,15 +577,16 @@ def test_closure_edge_cases(tiny):
     g = torch.empty_like(z)
     empty = dict(p, H=np.zeros_like(p["H"]))
     jb, jo = DAProblem(tiny, empty, flow=flow).closure(z, g)
-    assert jo == 0.0 and torch.equal(g, z)
-    assert abs(jb - 0.5 * float((z.double() ** 2).sum())) <= 1e-12 * jb
+    check("no observations: J_o", jo, 0.0, "==")
+    check_bitwise("no observations: dJ/dz vs z", g, z)
+    check("no observations: J_b vs sum(z^2)/2", abs(jb - 0.5 * float((z.double() ** 2).sum())) / jb, 1e-12, "<=")
     g1, g2 = torch.empty_like(z), torch.empty_like(z)
     _, jo1 = DAProblem(tiny, p, flow=flow, obs_coeff=1.0).closure(z, g1)
     _, jo2 = DAProblem(tiny, p, flow=flow, obs_coeff=2.0).closure(z, g2)
-    assert jo1 == jo2  # J_o is returned without the coefficient
+    check_bitwise("obs_coeff: J_o returned without the coefficient", jo1, jo2)
     e = rel((g2 - z).cpu(), (2 * (g1 - z)).cpu())
     print(f"obs_coeff linearity: grad rel {e:.1e}")
-    assert e < 1e-6
+    check("obs_coeff linearity of the observation gradient", e, 1e-6)
 
 
 def test_ln_planes_bitwise(full_dec):
@@ -590,8 +615,8 @@ def test_ln_planes_bitwise(full_dec):
     finally:
         prob.ctx.set_tuning("ln_planes", 1)
     print(f"LN planes on/off: J {out[0][:2]} vs {out[1][:2]}; k_rowsplit passes per decoder forward {rowsplits}")
-    assert out[0][:4] == out[1][:4]
-    assert torch.equal(out[0][4], out[1][4])
+    check_bitwise("LN planes on/off J pairs", out[0][:4], out[1][:4])
+    check_bitwise("LN planes on/off dJ/dz", out[0][4], out[1][4])
     assert rowsplits[0] + 24 <= rowsplits[1], rowsplits  # qkv + fc1 of the 12 LG blocks read LN planes
 
 
@@ -621,24 +646,22 @@ def test_ln_row_scales_bitwise(tmp_path):
         outs.append(np.load(f))
     print(f"LN row scales vs k_rowscale: J {outs[0][:2]} vs {outs[1][:2]}, grad max diff "
           f"{np.abs(outs[0][2:] - outs[1][2:]).max():.1e}")
-    assert np.array_equal(outs[0], outs[1])
+    check_bitwise("LN row scales vs k_rowscale J + dJ/dz", outs[0], outs[1])
 
 
 @pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_mlp", 3), ("fuse_attn", 1), ("fuse_attn", 3),
-                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2),
-                                     ("fuse_attn", 12), ("mlp_w", 2), ("mlp_w", 1), ("mlp_w", 3)])
+                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2)])
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
-    at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient; 1 at dim 96, 3 also at dim 192) and fuse_attn (LN1 + qkv +
-    window attention + proj + residual: 1 the forward, 3 also its input gradient, 12 both at dim 192 only); attn_mfma (the window attention of
-    the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and backward on the exact-f32 MFMA instead of
-    the VALU kernels: fp32 products either way, only the summation order differs); mlp_hc 64 (the dim-192 fused MLP
-    in 64-unit hidden chunks, or 2: its hidden layer split over two waves per 16 tokens -- the hidden operand's
-    per-(token, chunk) scales and the order of the chunk sums change); mlp_w (r05: the fused MLP as k_mlpw, the hidden
-    layer split over the waves with one bound-derived u scale per token, against r04's k_mlp; 2 at dim 192, 1 at
-    dim 96, 3 both; the mlp_hc cases run with mlp_w 0, the kernel they select). The dim-96 tower blocks change arithmetic (fp16x3 with per-chunk /
-    per-head scales instead of bf16x6), so forward output and input gradient agree to rounding (rel <= 2e-6 of
-    max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient bound is 1e-4)."""
+    at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient; 1 at dim 96, 3 also at dim 192) and
+    fuse_attn (LN1 + qkv + window attention + proj + residual at dim 96: 1 the forward, 3 also its input gradient);
+    attn_mfma (the window attention of the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and
+    backward on the exact-f32 MFMA instead of the VALU kernels: fp32 products either way, only the summation order
+    differs); mlp_hc 64 (the dim-192 fused MLP in 64-unit hidden chunks, or 2: its hidden layer split over two waves per
+    16 tokens -- the hidden operand's per-(token, chunk) scales and the order of the chunk sums change). The dim-96 tower
+    blocks change arithmetic (fp16x3 with per-chunk / per-head scales instead of bf16x6), so forward output and input
+    gradient agree to rounding (rel <= 2e-6 of max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient
+    bound is 1e-4)."""
     from vaevar.engine import DAProblem
     from vaevar.problem import make_problem
     from vaevar.synth import smooth_field, uniform_sym
@@ -649,9 +672,6 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     zc = torch.from_numpy(0.3 * smooth_field(403, (1, 32, 128, 256))).cuda()
     res = []
     default = full_dec.ctx.get_tuning(knob)
-    w_default = full_dec.ctx.get_tuning("mlp_w")
-    if knob == "mlp_hc":
-        full_dec.ctx.set_tuning("mlp_w", 0)
     try:
         for v in (0, on):
             full_dec.ctx.set_tuning(knob, v)
@@ -663,21 +683,20 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning(knob, default)
-        full_dec.ctx.set_tuning("mlp_w", w_default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     e_o, e_d, e_g = rel(o1.cpu(), o0.cpu()), rel(d1.cpu(), d0.cpu()), rel(g1.cpu(), g0.cpu())
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
     print(f"{knob} {on} vs 0: out rel {e_o:.2e} grad rel {e_d:.2e} closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
     assert not torch.equal(o0, o1), "the fused kernel did not run"
-    assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
+    check(f"{knob}={on} vs 0 out", e_o, 2e-6)
+    check(f"{knob}={on} vs 0 input grad", e_d, 2e-6)
+    check(f"{knob}={on} vs 0 dJ/dz", e_g, 1e-5)
+    check(f"{knob}={on} vs 0 closure J", e_j, 1e-7)
 
 
-@pytest.mark.parametrize("knob,ref,on", [("h5_var", 5, 4), ("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1),
-                                          ("fixup_stage", 0, 1)])
+@pytest.mark.parametrize("knob,ref,on", [("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1), ("fixup_stage", 0, 1)])
 def test_bitwise_knobs(full_dec, knob, ref, on):
-    """h5_var: tile 49's full tiles go through the row-wise LDS epilogue (4: accumulators -> LDS -> float4 rows: the
-    GELU / gelu' plane writers with their pre-activation stores and reads, bias) instead of the per-fragment one
-    (5, same main loop). h4_gather: tile 48 reads a gathered A's producer row scales through the row map itself
+    """h4_gather: tile 48 reads a gathered A's producer row scales through the row map itself
     instead of a k_gather_scales pass (the counter shows the pass is gone). fixup_ln_rows: the fused fixup + LN1
     after fc2 walks GEMM rows through the inverse window map (each row's arithmetic unchanged). fixup_stage: the fused
     fixup + LayerNorm sums its workgroup's split-K partials through LDS (same chunk-order sum per element). The same
@@ -710,8 +729,10 @@ def test_bitwise_knobs(full_dec, knob, ref, on):
         full_dec.ctx.set_tuning(knob, default)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     print(f"{knob}: k_gather_scales passes {gathers[0]} -> {gathers[1]}")
-    assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1)
-    assert (jb0, jo0) == (jb1, jo1)
+    check_bitwise(f"{knob} out", o0, o1)
+    check_bitwise(f"{knob} input grad", d0, d1)
+    check_bitwise(f"{knob} dJ/dz", g0, g1)
+    check_bitwise(f"{knob} J", (jb0, jo0), (jb1, jo1))
     if knob == "h4_gather":
         assert gathers[0] > 0 and gathers[1] == 0
 
@@ -757,7 +778,10 @@ def test_gelu_planes_vs_rowsplit(full_dec, knob, extra):
     e_j = abs((jb1 + jo1) - (jb0 + jo0)) / (jb0 + jo0)
     print(f"{knob} 1 vs 0 {extra}: out rel {e_o:.2e} (bitwise {torch.equal(o0, o1)}) grad rel {e_d:.2e} "
           f"closure J rel {e_j:.1e} dJ/dz rel {e_g:.2e}")
-    assert e_o < 2e-6 and e_d < 2e-6 and e_g < 1e-5 and e_j < 1e-7
+    check(f"{knob} 1 vs 0 out", e_o, 2e-6)
+    check(f"{knob} 1 vs 0 input grad", e_d, 2e-6)
+    check(f"{knob} 1 vs 0 dJ/dz", e_g, 1e-5)
+    check(f"{knob} 1 vs 0 closure J", e_j, 1e-7)
 
 
 def test_fixup_ln_bitwise(full_dec):
@@ -775,8 +799,6 @@ def test_fixup_ln_bitwise(full_dec):
     res = []
     ln_launches, fused = [], []
     default = full_dec.ctx.get_tuning("fixup_ln")
-    sk_default = full_dec.ctx.get_tuning("h4_streamk_mink")
-    full_dec.ctx.set_tuning("h4_streamk_mink", 0)  # bit-identity holds for the S-chunk split (stream-K: next test)
     try:
         for v in (0, 1):
             full_dec.ctx.set_tuning("fixup_ln", v)
@@ -792,7 +814,6 @@ def test_fixup_ln_bitwise(full_dec):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning("fixup_ln", default)
-        full_dec.ctx.set_tuning("h4_streamk_mink", sk_default)
     # the fused path really ran (gemm_ln falls back to separate launches when it returns hipErrorNotSupported):
     # the LG-stage LayerNorms after split-K GEMMs (proj -> LN2, fc2 -> next LN1, and their backward) leave the
     # LayerNorm class
@@ -802,45 +823,7 @@ def test_fixup_ln_bitwise(full_dec):
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     print(f"fixup_ln 1 vs 0: out max diff {(o1 - o0).abs().max().item():.1e}, grad {(d1 - d0).abs().max().item():.1e}, "
           f"J {jb1 + jo1 - jb0 - jo0:.1e}, dJ/dz {(g1 - g0).abs().max().item():.1e}")
-    assert torch.equal(o0, o1) and torch.equal(d0, d1) and torch.equal(g0, g1) and jb0 == jb1 and jo0 == jo1
-
-
-def test_streamk_fixup_ln(full_dec):
-    """Stream-K (tuning h4_streamk_mink): the split-K tile-48 GEMMs whose fixup is fused into a LayerNorm (fc2 ->
-    LN1, fc2^T / qkv^T -> LN backward; K >= 3456) run over every CU with each workgroup's unit range cut into one or
-    two tile segments, and the fused fixup sums a tile's 3-5 segment partials in k order. Against the S-chunk split:
-    the same arithmetic per product, another summation split, so fp32-level agreement (decoder output, input
-    gradient, J, dJ/dz); two stream-K runs are bit-identical (a fixed partition, partials summed in a fixed order);
-    the stream-K consumer really ran (launch counter)."""
-    from vaevar.engine import DAProblem
-    from vaevar.problem import make_problem
-    from vaevar.synth import smooth_field, uniform_sym
-
-    z = torch.from_numpy(0.5 * smooth_field(431, (1, 32, 128, 256))).cuda()
-    cot = torch.from_numpy(uniform_sym(432, (1, 69, 128, 256), 1.0)).cuda()
-    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
-    zc = torch.from_numpy(0.3 * smooth_field(433, (1, 32, 128, 256))).cuda()
-    ctx = full_dec.ctx
-    default = ctx.get_tuning("h4_streamk_mink")
-    res, launches = [], []
-    try:
-        for v in (0, 3456, 3456):
-            ctx.set_tuning("h4_streamk_mink", v)
-            c0 = ctx.counter("streamk")
-            out = full_dec.forward_raw(z).clone()
-            dz = torch.empty_like(z)
-            full_dec.backward_raw(cot, dz)
-            launches.append(ctx.counter("streamk") - c0)
-            g = torch.empty_like(zc)
-            jb, jo = prob.closure(zc, g)
-            res.append((out, dz, jb, jo, g))
-    finally:
-        ctx.set_tuning("h4_streamk_mink", default)
-    (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1), (o2, d2, jb2, jo2, g2) = res
-    rel = lambda a, b: float((a - b).abs().max() / b.abs().max())
-    print(f"stream-K launches per forward + backward {launches}; vs S-chunk split: out {rel(o1, o0):.1e}, "
-          f"grad {rel(d1, d0):.1e}, J {abs(jb1 + jo1 - jb0 - jo0) / abs(jb0 + jo0):.1e}, dJ/dz {rel(g1, g0):.1e}")
-    assert launches[0] == 0 and launches[1] >= 24 and launches[2] == launches[1], launches
-    assert torch.equal(o1, o2) and torch.equal(d1, d2) and torch.equal(g1, g2) and jb1 == jb2 and jo1 == jo2
-    assert rel(o1, o0) < 1e-5 and rel(d1, d0) < 1e-4 and rel(g1, g0) < 1e-4
-    assert abs(jb1 + jo1 - jb0 - jo0) <= 1e-6 * abs(jb0 + jo0)
+    check_bitwise("fixup_ln out", o0, o1)
+    check_bitwise("fixup_ln input grad", d0, d1)
+    check_bitwise("fixup_ln dJ/dz", g0, g1)
+    check_bitwise("fixup_ln J", (jb0, jo0), (jb1, jo1))

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLD
+from conftest import GOLD, check
 
 pytestmark = pytest.mark.gpu
 BQ = os.path.join(GOLD, "bq_info_lr.npz")
@@ -65,7 +65,8 @@ def test_sc4dvar_transform(grid):
     ulp = torch.from_numpy(np.spacing(np.abs(xr.numpy()).astype(np.float32)).astype(np.float64))
     e = float(((inc - inc_r).abs() - ulp).clamp_min(0).max() / inc_r.abs().max())
     print(f"sc4dvar transform {grid}: state rel {e_state:.2e}, increment rel (beyond 1 ulp) {e:.2e}")
-    assert e_state < 1e-6 and e < 1e-4
+    check(f"sc4dvar transform {grid} state", e_state, 1e-6)
+    check(f"sc4dvar transform {grid} increment beyond 1 ulp", e, 1e-4)
 
 
 @pytest.mark.parametrize("case", ["t1", "t1_interp", "real"])
@@ -80,10 +81,12 @@ def test_sc4dvar_closure(case):
     (rb + ro).backward()
     e = (abs(jb - float(rb)) / float(rb), abs(jo - float(ro)) / float(ro), rel(g.cpu(), wr.grad))
     print(f"sc4dvar closure {case}: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    assert e[0] < 1e-5 and e[1] < 1e-5 and e[2] < 1e-4
+    check(f"sc4dvar closure {case} J_b", e[0], 1e-5)
+    check(f"sc4dvar closure {case} J_o", e[1], 1e-5)
+    check(f"sc4dvar closure {case} dJ/dw", e[2], 1e-4)
     # the observation part of the gradient alone (w subtracted) carries the transform adjoint
     e2 = rel(g.cpu().double() - w.double(), wr.grad - wr.detach())
-    assert e2 < 1e-4, e2
+    check(f"sc4dvar closure {case} observation part of dJ/dw", e2, 1e-4)
 
 
 def test_sc4dvar_closure_t2_detached_flow():
@@ -102,7 +105,9 @@ def test_sc4dvar_closure_t2_detached_flow():
     (rb + ro).backward()
     e = (abs(jb - float(rb)) / float(rb), abs(jo - float(ro)) / float(ro), rel(g.cpu(), wr.grad))
     print(f"sc4dvar closure T=2: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    assert e[0] < 1e-5 and e[1] < 1e-4 and e[2] < 1e-4
+    check("sc4dvar closure T=2 J_b", e[0], 1e-5)
+    check("sc4dvar closure T=2 J_o", e[1], 1e-4)
+    check("sc4dvar closure T=2 dJ/dw", e[2], 1e-4)
 
 
 class _Recorder:
@@ -161,11 +166,11 @@ def test_one_step_sc4dvar_lbfgs(mode):
     e_x = float((inc - inc_r).norm() / inc_r.norm())  # rel-L2: the fp32 state's ulp averages out
     print(f"sc4dvar Nit=1 {mode}: J {g0:.6e} -> {g1:.6e} (oracle {j0:.6e} -> {j1:.6e}), evals {res['n_eval']} "
           f"(oracle line searches {rec.steps}), increment rel-L2 {e_x:.2e}")
-    assert abs(g0 - j0) / j0 < 1e-5
+    check(f"sc4dvar Nit=1 {mode} J at w = 0", abs(g0 - j0) / j0, 1e-5)
     assert g1 < g0
     if mode == "replay":
-        assert abs(g1 - j1) / j1 < 1e-3
-        assert e_x < 1e-2
+        check("sc4dvar Nit=1 replay J after the pass", abs(g1 - j1) / j1, 1e-3)
+        check("sc4dvar Nit=1 replay increment rel-L2", e_x, 1e-2)
 
 
 @pytest.fixture(scope="module")
@@ -195,7 +200,8 @@ def test_sc4dvar_transform_g14(g14, wk):
     e_x = rel(x[idx], g[f"f32_{wk}_x"])
     print(f"G14 transform {wk}: increment vs float64 reference rel {e_inc:.2e} (beyond 1 ulp), state vs float32 "
           f"reference rel {e_x:.2e}")
-    assert e_inc < 1e-4 and e_x < 1e-6
+    check(f"G14 transform {wk} increment beyond 1 ulp", e_inc, 1e-4)
+    check(f"G14 transform {wk} state vs float32 run", e_x, 1e-6)
 
 
 def test_sc4dvar_closure_g14(g14):
@@ -212,7 +218,10 @@ def test_sc4dvar_closure_g14(g14):
     e_s = abs(float((gs * gs).sum()) - float(g["f64_grad_sumsq"])) / float(g["f64_grad_sumsq"])
     print(f"G14 closure: J vs float64 reference {e_j64:.2e}, vs float32 reference {e_j32:.2e}; dJ/dw rel {e_g:.2e}, "
           f"|dJ/dw|^2 rel {e_s:.2e}")
-    assert e_j64 < 1e-5 and e_j32 < 1e-5 and e_g < 1e-4 and e_s < 1e-4
+    check("G14 closure J vs float64 run", e_j64, 1e-5)
+    check("G14 closure J vs float32 run", e_j32, 1e-5)
+    check("G14 closure dJ/dw", e_g, 1e-4)
+    check("G14 closure |dJ/dw|^2", e_s, 1e-4)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -236,8 +245,10 @@ def test_one_step_sc4dvar_g14(g14, mode):
     j0 = sum(res["J"][0])
     print(f"G14 one_step sc4dvar ({mode}): J {j0:.6e} -> {jf:.6e} (reference {float(g['lbfgs_J'][0]):.6e} -> {jr:.6e}), "
           f"J rel {e_j:.2e}, increment rel-L2 {e_x:.2e}, evals {res['n_eval']} (reference {len(g['lbfgs_J'])})")
-    assert abs(j0 - float(g["lbfgs_J"][0])) / float(g["lbfgs_J"][0]) < 1e-5
+    check(f"G14 Nit=2 {mode} J at w = 0", abs(j0 - float(g["lbfgs_J"][0])) / float(g["lbfgs_J"][0]), 1e-5)
     if mode == "replay":
-        assert e_j < 1e-3 and e_x < 1e-2
+        check("G14 Nit=2 replay J", e_j, 1e-3)
+        check("G14 Nit=2 replay increment rel-L2", e_x, 1e-2)
     else:
-        assert e_j < 1e-2 and e_x < 5e-2
+        check("G14 Nit=2 free J", e_j, 1e-2)
+        check("G14 Nit=2 free increment rel-L2", e_x, 5e-2)

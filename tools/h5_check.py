@@ -37,15 +37,13 @@ for (M, N, K) in [(2048, 4608, 1152), (2048, 4608, 4608), (777, 300, 96), (2100,
           f"rel err vs fp64 {err:.1e}", flush=True)
 
 ctx = Context(0)
-VARS = [int(v) for v in os.environ.get("H5_VARS", "0").split(",")]
 for (M, N, K) in [(2048, 4608, 1152), (4096, 4608, 1152)]:
     A, B = mats(M, N, K, 11)
     ctx.gemm_register_weight(B)
     keep.append(B)
     out = {}
-    for t in [48] + [100 + v for v in VARS]:
-        ctx.set_tuning("h5_var", max(t - 100, 0))
-        t, key = (49 if t >= 100 else t), t
+    for t in (48, 49):
+        key = t
         for _ in range(3):
             ctx.gemm(A, B, tile=t)
         torch.cuda.synchronize()
@@ -57,7 +55,7 @@ for (M, N, K) in [(2048, 4608, 1152), (4096, 4608, 1152)]:
         torch.cuda.synchronize()
         out[key] = e0.elapsed_time(e1) * 1e3 / reps
     fl = 2.0 * M * N * K
-    print(f"{M}x{N}x{K}: " + ", ".join(f"{'tile 48' if k == 48 else 'tile 49 var %d' % (k - 100)} {v:.1f} us "
+    print(f"{M}x{N}x{K}: " + ", ".join(f"{'tile %d' % k} {v:.1f} us "
                                       f"({fl / v / 1e6:.0f} TF)" for k, v in out.items()), flush=True)
     # the k_rowsplit pass alone (A planes), for the main-kernel time
 

@@ -8,9 +8,13 @@
 // ([N][K], forward operand) plus a transposed copy ([K][N], backward operand).
 #include <hip/hip_runtime.h>
 
+#include <sys/prctl.h>
+#include <time.h>
+
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -96,7 +100,8 @@ int parse_cfg(const vv_lgunet_config* c, Cfg& o) {
   // one image row per wave, at most kPatchCmax token channels and kPatchKmax = 4 x 28 taps per token: refused here
   // with a message instead of a failing first closure
   if (o.W0 % 16) return fail(VV_E_ARG, "img_size[1] / 2 = %d must be a multiple of 16 (patch kernels)", o.W0);
-  if (o.C0 > 128) return fail(VV_E_ARG, "enc_dim %d > 128 (patch kernels)", o.C0);
+  if (o.C0 > 128 || o.C0 % 16)
+    return fail(VV_E_ARG, "enc_dim %d must be a multiple of 16 and <= 128 (patch kernels)", o.C0);
   for (int g = 0; g < o.G; ++g)
     if (c->inchans[g] < 1 || c->inchans[g] > 28 || c->outchans[g] < 1 || c->outchans[g] > 28)
       return fail(VV_E_ARG, "group %d: inchans %d / outchans %d outside 1..28 (patch kernels)", g, c->inchans[g],
@@ -358,7 +363,56 @@ struct vv_ctx {
   } graphs[2];
   hipStream_t cap_stream = nullptr;
   bool use_graphs = true;  // vv_set_closure_graph / VAEVAR_GRAPH
+  double long_wait_us[2] = {0.0, 0.0};  // host_wait: the last two waits of kind 1 longer than 1 ms (host_sync)
 };
+
+namespace {
+// The host's wait for the stream (the L-BFGS mirror's scalar round trips, vv_reduce_batch). Tuning.host_wait 0:
+// hipStreamSynchronize, whose wait keeps a host CPU busy (ROCm's Yield schedule, the default, is a sched_yield loop;
+// BlockingSync is a synonym for it: hip_runtime_api.h hipSetDeviceFlags). 1: poll hipStreamQuery at 20-us sleeps;
+// for a wait of kind `cls` 1 (the caller expects a queued closure ahead: vv_reduce_batch with device extras, which
+// carry its J), first sleep through 0.8 x the shorter of that kind's last two waits if both exceeded 1 ms. A wait
+// that the sleep overshot clears that history. Returns what hipStreamSynchronize would: hipSuccess once the
+// stream's work is done, or its error.
+hipError_t host_sync(vv_ctx* ctx, hipStream_t st, int cls = 0) {
+  if (!ctx->tune.host_wait) return hipStreamSynchronize(st);
+  static thread_local bool slack = false;
+  if (!slack) {
+    prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1-us timer slack for this thread's short sleeps (default 50 us)
+    slack = true;
+  }
+  auto nap = [](double us) {
+    timespec ts{(time_t)(us * 1e-6), (long)(std::fmod(us, 1e6) * 1e3)};
+    nanosleep(&ts, nullptr);
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  auto elapsed_us = [&] {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  };
+  hipError_t e = hipStreamQuery(st);
+  if (e != hipErrorNotReady) return e;
+  double* hist = ctx->long_wait_us;
+  const double lw = std::min(hist[0], hist[1]);
+  const bool slept = cls == 1 && lw > 1000.0;
+  if (slept) nap(0.8 * lw);
+  bool first = true, over = false;
+  while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    first = false;
+    nap(20.0);
+  }
+  over = slept && first;  // done by the end of the long sleep: it may have overshot
+  if (cls == 1) {
+    const double us = elapsed_us();
+    if (over) {
+      hist[0] = hist[1] = 0.0;
+    } else if (us > 1000.0) {
+      hist[0] = hist[1];
+      hist[1] = us;
+    }
+  }
+  return e;
+}
+}  // namespace
 
 namespace {
 
@@ -629,7 +683,6 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
   ma.ngroups = S.G;
   ma.eps = 1e-5f;
   ma.hc = T.mlp_hc;
-  ma.w = T.mlp_w;
   for (int g = 0; g < S.G; ++g) {
     const auto& w = S.w[b][g];
     vv::MlpGroup& G = ma.g[g];
@@ -641,15 +694,12 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
       G.beta = w.n2b;
       vv::fp16_planes_of(w.fc1W, C, &G.w1h, &G.w1s);
       vv::fp16_planes_of(w.fc2W, 4 * C, &G.w2h, &G.w2s);
-      G.wmax = w.fc1Wmax;
-      G.bmax = w.fc1bmax;
       G.b1 = w.fc1b;
       G.b2 = w.fc2b;
       G.out = sv.x[b + 1] + g * MC;
     } else {
       vv::fp16_planes_of(w.fc2WT, C, &G.w1h, &G.w1s);
       vv::fp16_planes_of(w.fc1WT, 4 * C, &G.w2h, &G.w2s);
-      G.wmax = w.fc2Wmax;
       G.dy = gx + g * MC;
       G.out = gx + g * MC;
       G.rs = sc.rs + (size_t)g * M;
@@ -663,8 +713,8 @@ bool mlp_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, boo
 bool ablk_args(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, int shift, const int* idx,
                vv::AblkArgs& aa, float* gx = nullptr) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  // fuse_attn: bit 0 the forward, bit 1 the backward at dim 96; bits 2, 3 the same at dim 192
-  if (!(T.fuse_attn & ((gx ? 2 : 1) << (S.C == 192 ? 2 : 0))) || sc.math != vv::GEMM_SPLIT16 ||
+  // fuse_attn: bit 0 the forward, bit 1 the backward (dim 96)
+  if (!(T.fuse_attn & (gx ? 2 : 1)) || sc.math != vv::GEMM_SPLIT16 ||
       !vv::ablk_supported(S.C, S.heads, ws, S.M))
     return false;
   memset(&aa, 0, sizeof(aa));
@@ -1878,6 +1928,7 @@ int vv_ctx_destroy(vv_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();
   for (auto& m : ctx->models) {
+    if (!m) continue;  // vv_model_destroy'ed
     for (int* p : m->maps_owned) (void)hipFree(p);
     if (m->warena) vv::unregister_split_arena(reinterpret_cast<const float*>(m->warena->base));
   }
@@ -1980,6 +2031,21 @@ int vv_load_weights(vv_ctx* ctx, int model_id, const void* const* ptrs, int n) {
   return 0;
 }
 
+int vv_model_destroy(vv_ctx* ctx, int model_id) {
+  Model* m = get_model(ctx, model_id);
+  if (!m) return fail(VV_E_ARG, "bad model id %d", model_id);
+  int r = set_dev(ctx);
+  if (r) return r;
+  VV_HIP(hipDeviceSynchronize());  // no launch in flight reads its memory
+  drop_graphs(ctx);
+  if (ctx->prob.bound && (ctx->prob.dec == model_id || ctx->prob.flow == model_id)) ctx->prob = Problem();
+  if (ctx->sc4 && ctx->sc4->flow == model_id) ctx->sc4.reset();
+  for (int* p : m->maps_owned) (void)hipFree(p);
+  if (m->warena) vv::unregister_split_arena(reinterpret_cast<const float*>(m->warena->base));
+  ctx->models[model_id].reset();
+  return 0;
+}
+
 int vv_model_workspace_bytes(vv_ctx* ctx, int model_id, int64_t* bytes) {
   Model* m = get_model(ctx, model_id);
   if (!m || !bytes) return fail(VV_E_ARG, "bad model");
@@ -2063,7 +2129,9 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     bool aligned = true;
     for (const void* p : {(const void*)xb, (const void*)yo, (const void*)Hmask, (const void*)R})
       aligned = aligned && !(reinterpret_cast<uintptr_t>(p) & 15);
-    P.grid_fused = P.interp && ctx->tune.grid_fused && Hs >= P.Hl && Ws >= P.Wl && Ws % 4 == 0 && Ws <= 16384 && aligned;
+    // misfit_grid_fwd's preconditions (vv_ops.hip), so a bound grid_fused problem never fails a closure there
+    P.grid_fused = P.interp && ctx->tune.grid_fused && Hs >= P.Hl && Ws >= P.Wl && Ws % 4 == 0 && Ws <= 16384 &&
+                   P.Wl <= 768 && aligned;
     if (P.grid_fused) P.nblk = C * P.Hl;  // one J partial per (channel, network row) workgroup of k_misfit_grid
     P.grid_mr = ctx->tune.grid_fused == 2 ? 6 : 3;
   }
@@ -2083,7 +2151,9 @@ int vv_bind_problem(vv_ctx* ctx, int dec_model_id, int flow_model_id, int T, int
     P.FO = pl.f(B * fcout * HWl * std::max(T - 1, 1) + 1);
     P.GFO = pl.f(B * fcout * HWl + 1);
     P.GFI = pl.f(B * CHWl);
-    P.carry = pl.f(P.grid_fused ? 1 : B * CHW);
+    // the per-element backward's flow-input adjoint (T > 1). Kept even when grid_fused is chosen: a later
+    // vv_set_obs_operator switches the closure to the per-element path (closure_impl: gf needs nout == 0)
+    P.carry = pl.f(T > 1 ? B * CHW : 1);
     P.GON = P.grid_fused ? pl.f(B * CHWl * T) : nullptr;
     P.zn = B * D->cfg.Cin * D->cfg.Himg * D->cfg.Wimg;
     P.Z = pl.f(P.zn);
@@ -2337,7 +2407,7 @@ int vv_reduce_batch(vv_ctx* ctx, int count, const int* ops, const float* const* 
     rq.b[i] = ops[i] == 0 ? b[i] : nullptr;
   }
   VV_HIP(vv::reduce_multi(rq, count, n, ctx->redb, kRedBlocks, ctx->hredb_dev, dev_extra, n_extra, st));
-  VV_HIP(hipStreamSynchronize(st));
+  VV_HIP(host_sync(ctx, st, n_extra > 0 ? 1 : 0));
   for (int i = 0; i < count + n_extra; ++i) out[i] = ctx->hredb[i];  // absmax widened from float: exact
   return 0;
 }
@@ -2466,7 +2536,7 @@ int vv_set_closure_graph(vv_ctx* ctx, int enable) {
 
 int vv_get_counter(const char* name, long long* value) {
   if (!name || !value) return fail(VV_E_ARG, "null argument");
-  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup", "gather_scales", "streamk"};
+  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup", "gather_scales"};
   for (int c = 0; c < vv::CNT_N; ++c)
     if (!strcmp(name, names[c])) {
       *value = vv::launch_count(c);

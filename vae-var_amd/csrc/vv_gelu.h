@@ -10,7 +10,6 @@
 // relative to |x|). In float32 (Horner fma chain, v_exp_f32): GELU within 8.7e-8 |x|, Phi and GELU' within 8.2e-8
 // absolute of float64 over [-9, 9] -- the rounding of the result itself; the libm erff path costs ~40 VALU
 // instructions per element with its two divergent ranges, this one 15 (GELU) / 19 (GELU').
-// Built with VV_GELU_ERFF: the erff forms (A/B builds only).
 // Infinities: GELU(+inf) = +inf (x - x h would be inf - inf), GELU(-inf) ~ 0 and GELU'(+-inf) = 1 / ~0
 // (x phi(x) would be inf * 0): the x that multiplies h and phi is clamped to +-30 by one v_med3_f32. For |x| <= 30
 // that is x itself; beyond it x h < 2^-25 x for x > 0, and the true x h and x phi(x) are below 1.4e-7 for x < -30.
@@ -55,14 +54,6 @@ __device__ __forceinline__ void gelu_h4(const float (&x)[4], float (&h)[4]) {
   for (int i = 0; i < 4; ++i) h[i] = __builtin_amdgcn_exp2f(fmaf(u[i], s[i], -1.0f));
 }
 
-#ifdef VV_GELU_ERFF
-__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float dgelu_fast(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
-#else
 __device__ __forceinline__ float gelu_clamp(float x) { return __builtin_amdgcn_fmed3f(x, -30.0f, 30.0f); }
 __device__ __forceinline__ float gelu_fast(float x) {
   const float h = gelu_h(x);
@@ -77,18 +68,7 @@ __device__ __forceinline__ float dgelu_fast(float x) {
   const float pdf = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170f, -1.3257480647361593f));
   return fmaf(gelu_clamp(x), pdf, cdf);
 }
-#endif
 
-#ifdef VV_GELU_ERFF
-__device__ __forceinline__ void gelu4(const float (&x)[4], float (&y)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = gelu_fast(x[i]);
-}
-__device__ __forceinline__ void dgelu4(const float (&x)[4], float (&y)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = dgelu_fast(x[i]);
-}
-#else
 __device__ __forceinline__ void gelu4(const float (&x)[4], float (&y)[4]) {
   float h[4];
   gelu_h4(x, h);
@@ -108,6 +88,5 @@ __device__ __forceinline__ void dgelu4(const float (&x)[4], float (&y)[4]) {
     y[i] = fmaf(gelu_clamp(x[i]), pdf, cdf);
   }
 }
-#endif
 
 }  // namespace vv

@@ -1638,7 +1638,7 @@ __global__ __launch_bounds__(256) void k_rowsplit(GemmArgs args, float* __restri
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 
-template <int EPI, bool SK = false>
+template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* __restrict__ ascale,
                                                     const unsigned short* __restrict__ apl) {
   constexpr int BM = 256, BN = 128, BK = 32, NT = 512, WN = 2, WM = 4, TM = 4, TN = 4;
@@ -1652,16 +1652,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
   const int nkt = K / BK;
   int tile = 0, kb = 0, ke = nkt, part = -1;
-  // stream-K (args.sk): the units [u0, u1) of logical workgroup skw, one or two tile segments
-  long long sku0 = 0, sku1 = 0;
-  int nseg = 1, skw = 0;
-  if constexpr (SK) {
-    skw = xcd_remap(blockIdx.x, gridDim.x);
-    const long long U = (long long)(ntm * ntn) * nkt;
-    sku0 = (long long)skw * U / gridDim.x;
-    sku1 = (long long)(skw + 1) * U / gridDim.x;
-    nseg = (int)((sku1 - 1) / nkt - sku0 / nkt) + 1;
-  } else if (args.tsplit <= 1) {
+  if (args.tsplit <= 1) {
     tile = xcd_remap(blockIdx.x, ntm * ntn);
   } else if ((int)blockIdx.x < args.tdp) {
     tile = xcd_remap(blockIdx.x, args.tdp);
@@ -1673,34 +1664,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
     kb = (c * nkt) / S;
     ke = ((c + 1) * nkt) / S;
   }
-  for (int seg = 0; seg < (SK ? nseg : 1); ++seg) {
-  if constexpr (SK) {
-    const long long ts = sku0 / nkt + seg, tk0 = ts * nkt;
-    tile = (int)ts;
-    kb = (int)(max(sku0, tk0) - tk0);
-    ke = (int)(min(sku1, tk0 + nkt) - tk0);
-    part = skw + tile;
-    if (seg > 0) __syncthreads();  // every wave's reads of the previous segment's LDS ring are done
-  }
   int mb, nb;
   tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
   const float* rs = ascale + (size_t)blockIdx.z * M;
   // this lane's 16 A row scales (gathered through arow from the producer's physical-row scales when agather: no
-  // k_gather_scales launch), loaded after the k loop
+  // k_gather_scales launch), loaded after the k loop (before it: +2 % kernel time, profiles/r04/ab_r04s)
   float rsv[4][4];
-#ifdef VV_H4_EARLY_SCALES  // A/B builds only: loaded before the k loop (+2 % kernel time, profiles/r04/ab_r04s)
-  {
-    const int wm_ = (threadIdx.x >> 6) / 2, hh_ = (threadIdx.x & 63) >> 4;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = min(m0 + wm_ * 64 + a * 16 + 4 * hh_ + r, M - 1);
-        rsv[a][r] = rs[args.agather ? args.arow[row] : row];
-      }
-  }
-#endif
 
   // Planes are chunk-interleaved in memory (per row and 32-deep k-tile: h 64 B | l 64 B, one 128-B line) and in
   // LDS ([row][128 B], A rows then B rows). One DMA instruction fills 8 rows: lane i writes LDS bytes 16 i, row
@@ -1849,7 +1819,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
   // drain the DMAs still in flight before the workgroup can exit (their LDS must not be reassigned under them)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-#ifndef VV_H4_EARLY_SCALES
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -1857,7 +1826,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
       const int row = min(m0 + wm * TM * 16 + a * 16 + 4 * hh + r, M - 1);
       rsv[a][r] = rs[args.agather ? args.arow[row] : row];
     }
-#endif
   // undo the scales: rows of A (2^-e_a), rows of B = columns of C (2^-e_b); 16x16 tile: row 4 hh + r, col rin
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
@@ -1880,14 +1848,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h4(GemmArgs args, const float* 
       for (int b = 0; b < TN; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) w[(size_t)((a * TN + b) * 4 + r) * NT + tid] = acc[a][b][r];
-    if constexpr (SK) continue;
     return;
   }
   if (m0 + BM <= M && n0 + BN <= N)
     epilogue<BM, BN, WM, WN, EPI, 16, true>(args, G, acc, m0, n0, wm, wn, rin, hh);
   else
     epilogue<BM, BN, WM, WN, EPI, 16, false>(args, G, acc, m0, n0, wm, wn, rin, hh);
-  }  // segments
 }
 
 // Row-wise epilogue of a full tile staged in LDS (tile 49): a wave's 32 x BN fp32 results, written to LDS from the
@@ -1984,19 +1950,17 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGr
 //
 // LDS stage = [A 256 rows | B 144 rows] x 128 B (h 32 | l 32 halfs per row and k-tile) = 51,200 B; 3 stages.
 // DMA pieces (1 KiB = 8 rows each): A 32 (4 per wave), B 18 (2 per wave, a third for waves 0 and 1).
-// Per k-tile t (frags of t: A in registers, B column blocks 0, 1 in registers):
-//   b = 0..6: fragment reads of B column block b + 2 (distance-two prefetch, 3-slot ring), the 6 MFMAs of block b;
-//             the 4 A pieces of k-tile t + 2 spread over them
-//   wait for my k-tile t + 1 pieces (vmcnt(4): only the 4 younger A pieces of t + 2 may stay in flight) and for my
-//   B block 8 reads, then s_barrier: everyone's t + 1 pieces landed, everyone's reads of buffer t % 3 retired
-//   b = 7, 8: MFMAs of blocks 7, 8 beside the reads of k-tile t + 1's A fragments and B blocks 0, 1, and the B
-//             pieces of k-tile t + 2
+// Per k-tile t (frags of t: A in registers, B column blocks in groups of three, two groups ahead of use):
+//   group 0 (blocks 0..2): the reads of group 1 go out after block 0's MFMAs, the first A pieces of k-tile t + 2
+//   beside them; group 1 (blocks 3..5): the reads of group 2 after block 3, the last A piece; block 6, then wait for
+//   my k-tile t + 1 pieces (vmcnt(4): only the 4 younger A pieces of t + 2 may stay in flight) and my reads, and
+//   s_barrier: everyone's t + 1 pieces landed, everyone's reads of buffer t % 3 retired; blocks 7, 8 beside the reads
+//   of k-tile t + 1's A fragments and group 0, and the B pieces of k-tile t + 2.
+// The compiler waits lgkmcnt(0) before the first MFMA of each group (it does not count in-order LDS reads across these
+// loops), so the reads outstanding at those waits are two groups old (r04 schedule measurements: DESIGN §3e).
 // Buffer (t + 2) % 3 = (t - 1) % 3 was last read before the barrier of k-tile t - 1, so the DMA of t + 2 may start
 // anywhere in k-tile t.
-// VAR (schedule experiments, Tuning.h5_var): 0 reads of block b + 2 before block b's MFMAs; 1 after them; 2 no
-// scheduling barriers inside the block loop (the compiler interleaves reads and MFMAs); 3 as 1, the A pieces two
-// blocks later
-template <int EPI, int VAR = 0>
+template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* __restrict__ ascale,
                                                     const unsigned short* __restrict__ apl) {
   constexpr int BM = 256, BN = 144, BK = 32, WM = 8, WN = 1, TM = 2, TN = 9;
@@ -2084,8 +2048,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
     for (int a = 0; a < TM; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a][0], fb[0], acc[a][b], 0, 0, 0);
   };
 
-  h8v fb[3][2];  // B column block b of the current k-tile in slot b % 3 (9 % 3 == 0: the mapping runs on across k-tiles)
-  // VAR 4: B blocks read in groups of three, two groups ahead of use (6 slots: g0 / g2 of k-tile t and g1 of k-tile
+  // B blocks read in groups of three, two groups ahead of use (6 slots: g0 / g2 of k-tile t and g1 of k-tile
   // t + 1 in one half, the others in the other half); the reads of group g + 1 go out after the first MFMA block of
   // group g, so the compiler's lgkmcnt waits before each group only find old reads outstanding
   h8v gb[2][3][2];
@@ -2132,45 +2095,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
     mfma_b(fa, gb[h][2], 8);
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto step = [&](int t, const h8v (&fa)[TM][2], h8v (&na)[TM][2]) {
-    const int cb = t % 3, nbuf = (t + 1) % 3, sb = (t + 2) % 3, sk = min(t + 2, nk - 1);
-#pragma unroll
-    for (int b = 0; b < 7; ++b) {
-      if constexpr (VAR == 0 || VAR == 2) {
-        read_b(cb, b + 2, fb[(b + 2) % 3]);
-        if (b < 4) apiece(sk, sb, b);
-        if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
-        mfma_b(fa, fb[b % 3], b);
-        if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
-      } else {
-        if (b == 0) read_b(cb, 2, fb[2]);
-        if (VAR == 1 ? b < 4 : (b >= 2 && b < 6)) apiece(sk, sb, VAR == 1 ? b : b - 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_b(fa, fb[b % 3], b);
-        __builtin_amdgcn_sched_barrier(0);
-        if (b < 6) read_b(cb, b + 3, fb[(b + 3) % 3]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // block 7 beside the next k-tile's A fragments, block 8 beside its B blocks 0, 1 (slots 0, 1: blocks 7, 8 sit in
-    // slots 1, 2 -- block 7 is consumed before slot 1 is refilled)
-    read_a(nbuf, na);
-    bpieces(sk, sb);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_b(fa, fb[7 % 3], 7);
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(nbuf, 0, fb[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_b(fa, fb[8 % 3], 8);
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(nbuf, 1, fb[1]);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
   // prologue: k-tiles 0 and 1 in flight, wait for 0, its A fragments and B blocks 0, 1
   h8v fa0[TM][2], fa1[TM][2];
 #pragma unroll
@@ -2187,29 +2111,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   read_a(0, fa0);
-  if constexpr (VAR == 4 || VAR == 5) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) read_b(0, i, gb[0][i]);
-  } else {
-    read_b(0, 0, fb[0]);
-    read_b(0, 1, fb[1]);
-  }
+  for (int i = 0; i < 3; ++i) read_b(0, i, gb[0][i]);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int t = 0;
-  if constexpr (VAR == 4 || VAR == 5) {
-    for (; t + 1 < nk; t += 2) {
-      step4(t, fa0, fa1, 0);
-      step4(t + 1, fa1, fa0, 1);
-    }
-    if (t < nk) step4(t, fa0, fa1, 0);
-  } else {
-    for (; t + 1 < nk; t += 2) {
-      step(t, fa0, fa1);
-      step(t + 1, fa1, fa0);
-    }
-    if (t < nk) step(t, fa0, fa1);
+  for (; t + 1 < nk; t += 2) {
+    step4(t, fa0, fa1, 0);
+    step4(t + 1, fa1, fa0, 1);
   }
+  if (t < nk) step4(t, fa0, fa1, 0);
   // drain the DMAs still in flight before the workgroup can exit (their LDS must not be reassigned under them)
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
@@ -2227,7 +2138,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
         acc[a][b][r] *= ia * sbv;
       }
   }
-  if (VAR != 5 && EPI != EPI_RESID && !args.crow && m0 + BM <= M && n0 + BN <= N && (args.ldc & 3) == 0 &&
+  if (EPI != EPI_RESID && !args.crow && m0 + BM <= M && n0 + BN <= N && (args.ldc & 3) == 0 &&
       (args.ldaux & 3) == 0) {
     // full tile: through LDS to a row-wise epilogue (every wave's fragment reads retired first; each wave then
     // writes and reads back only its own 32 rows)
@@ -2268,8 +2179,7 @@ static hipError_t launch_h3_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   return hipGetLastError();
 }
 
-constexpr size_t kWsFloats = (size_t)1 << 24;      // 64 MB: split-K partials (3 x 144 tiles of 128x128; stream-K's
-                                                   // P + T tile-48 slots of 128 KB)
+constexpr size_t kWsFloats = (size_t)1 << 24;      // 64 MB: split-K partials (3 x 144 tiles of 128x128)
 constexpr size_t kScaleFloats = (size_t)1 << 19;   // then the A row scales of GEMM_SPLIT16 (groups x M)
 
 // requires fp16 planes for every group's B (registered weights) and a workspace for the A row scales; the
@@ -2290,14 +2200,6 @@ static bool h4_ready(const GemmArgs& a) {
 template <int EPI>
 static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, int tail, const float* sc,
                               const unsigned short* planes) {
-  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {  // gemm_ln's stream-K (its fixups take STORE / RESID)
-    if (a.sk) {
-      if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI, true>, lds)) return e;
-      hipLaunchKernelGGL((k_gemm_h4<EPI, true>), grid, dim3(512), lds, s, a, sc, planes);
-      return hipGetLastError();
-    }
-  }
-  if (a.sk) return hipErrorInvalidValue;
   if (hipError_t e = set_lds_limit((const void*)k_gemm_h4<EPI>, lds)) return e;
   hipLaunchKernelGGL((k_gemm_h4<EPI>), grid, dim3(512), lds, s, a, sc, planes);
   if (tail && !a.nofix) {  // y: the 4 fragment rows of each wave (4x the workgroups of a per-tile fixup)
@@ -2307,25 +2209,12 @@ static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   return hipGetLastError();
 }
 
-template <int EPI, int VAR>
-static hipError_t launch_h5_v(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, const float* sc,
-                              const unsigned short* planes) {
-  if (hipError_t e = set_lds_limit((const void*)k_gemm_h5<EPI, VAR>, lds)) return e;
-  hipLaunchKernelGGL((k_gemm_h5<EPI, VAR>), grid, dim3(512), lds, s, a, sc, planes);
-  return hipGetLastError();
-}
 template <int EPI>
 static hipError_t launch_h5_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, const float* sc,
                               const unsigned short* planes) {
-  const Tuning& T = a.tune ? *a.tune : kDefaultTuning;
-  switch (T.h5_var) {
-    case 1: return launch_h5_v<EPI, 1>(a, s, grid, lds, sc, planes);
-    case 2: return launch_h5_v<EPI, 2>(a, s, grid, lds, sc, planes);
-    case 3: return launch_h5_v<EPI, 3>(a, s, grid, lds, sc, planes);
-    case 4: return launch_h5_v<EPI, 4>(a, s, grid, lds, sc, planes);
-    case 5: return launch_h5_v<EPI, 5>(a, s, grid, lds, sc, planes);
-    default: return launch_h5_v<EPI, 0>(a, s, grid, lds, sc, planes);
-  }
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_h5<EPI>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_h5<EPI>), grid, dim3(512), lds, s, a, sc, planes);
+  return hipGetLastError();
 }
 
 // tiles 48 and 49 (t49: 256 x 144 tiles, data-parallel only)
@@ -2381,7 +2270,7 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
   const size_t lds = 3 * (2 * (256 + 128) * 32) * sizeof(unsigned short);
   const int T = ((a.N + 127) / 128) * ((a.M + 255) / 256);
   const int tail = a.tsplit > 1 ? T - a.tdp : 0;
-  dim3 grid(a.sk ? device_cus() : tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
+  dim3 grid(tail ? a.tdp + tail * a.tsplit : T, 1, a.ngroups);
   switch (a.epi) {
     case EPI_STORE: return launch_h4_k<EPI_STORE>(b, s, grid, lds, tail, sc, planes);
     case EPI_GELU:
@@ -2458,26 +2347,23 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h4_small") return &t.h4_small;
   if (k == "h4_split_minkt") return &t.h4_split_minkt;
   if (k == "h5") return &t.h5;
-  if (k == "h5_var") return &t.h5_var;
   if (k == "h4_gather") return &t.h4_gather;
   if (k == "fixup_ln_rows") return &t.fixup_ln_rows;
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
   if (k == "grid_fused") return &t.grid_fused;
-  if (k == "h4_streamk_mink") return &t.h4_streamk_mink;
   if (k == "fixup_stage") return &t.fixup_stage;
-  if (k == "mlp_w") return &t.mlp_w;
+  if (k == "host_wait") return &t.host_wait;
   return nullptr;
 }
 bool tuning_value_ok(const char* key, int v) {
   const std::string k(key ? key : "");
-  if (k == "h3_mink" || k == "fc_h3_mink" || k == "h4_streamk_mink") return v >= 0;
+  if (k == "h3_mink" || k == "fc_h3_mink") return v >= 0;
   if (k == "small_split_minkt" || k == "tail_minkt" || k == "h4_split_minkt") return v >= 1;
   if (k == "mlp_hc") return v == 0 || v == 2 || v == 32 || v == 64;  // vv_tower.hip mlp_run
-  if (k == "h5_var") return v >= 0 && v <= 5;
   if (k == "gattn_qf") return v == 1 || v == 2;
   if (k == "grid_fused") return v >= 0 && v <= 2;
-  if (k == "fuse_mlp" || k == "mlp_w") return v >= 0 && v <= 3;
-  if (k == "fuse_attn") return v >= 0 && v <= 15;
+  if (k == "fuse_mlp") return v >= 0 && v <= 3;
+  if (k == "fuse_attn") return v >= 0 && v <= 3;
   return v == 0 || v == 1;  // every other knob is a switch
 }
 
@@ -2707,8 +2593,6 @@ static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
   const int num_cu = device_cus();
   a.tdp = 0;
   a.tsplit = 1;
-  a.sk = 0;
-  a.skp = 0;
   a.ws = ws;
   a.ascale_phys = 0;
   const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
@@ -2798,17 +2682,6 @@ hipError_t gemm_ln(const GemmArgs& a_in, const GemmLnArgs& l, hipStream_t s, flo
   if (hipError_t e = gemm_prepare(a, -1, ws, t)) return e;
   if (t != 48 || a.tsplit < 2 || a.tsplit > 4 || a.tdp != 0) return hipErrorNotSupported;
   a.nofix = 1;
-  {
-    const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
-    const long T = tiles_of(a, 256, 128), P = device_cus();
-    const long nkt = a.K / 32, L = nkt * T / P;  // units per workgroup (at least)
-    // at most 6 segments per tile (the consumer's kSkMaxSeg): ceil(nkt / L) + 1 <= 6
-    if (TU.h4_streamk_mink > 0 && a.K >= TU.h4_streamk_mink && T < P && (size_t)(P + T) * 256 * 128 <= kWsFloats &&
-        L >= 1 && nkt <= 5 * L) {
-      a.sk = 1;
-      a.skp = (int)P;
-    }
-  }
   const int ph = prof_begin(s);
   hipError_t e = launch_variant(t, a, s);
   if (e == hipSuccess) e = fixup_ln_launch(a, l, s);

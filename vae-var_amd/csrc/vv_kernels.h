@@ -30,8 +30,6 @@ struct Tuning {
   int h4_split_minkt = 12;      // k-tiles per chunk at least, for that split of tile 48
   int h5 = 1;                   // tile 49 (256 x 144, k_gemm_h5) where its tiles fill whole rounds and tile 48's do not
   int fc_conv_mf = 1;           // LGUnet_all_1 PatchEmbed / ConvTranspose2d as direct MFMA kernels (0: im2col / col2im + GEMM)
-  int h5_var = 4;               // tile 49 schedule variant (4: B blocks read in groups of three, two groups ahead, full
-                                // tiles through the row-wise LDS epilogue; 5: the same with the per-fragment epilogue)
   int gattn = 1;                // LGUnet_all_1 global window: the flash MFMA kernel (0: split GEMMs / streaming kernel)
   int gattn_qf = 1;             // its 16-query blocks per wave (1: 8 waves, two per SIMD; 2: 4 waves of 32 queries)
   int win_attn = 1;             // LGUnet_all_1: the LDS window-attention kernel for small windows (0: streaming)
@@ -46,14 +44,8 @@ struct Tuning {
   int h4_gather = 1;            // tile 48 reads gathered producer row scales through arow itself (0: k_gather_scales)
   int mlp_hc = 2;               // the fused dim-192 MLP: hidden units per chunk (32 or 64: fewer chunk steps, 151 KB LDS),
                                 // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
-  int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) where ablk_supported: bit 0
-                                // the forward, bit 1 the backward at dim 96, bits 2 / 3 at dim 192 (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box,
-                                // profiles/r04/ab_r04j)
-  int mlp_w = 0;                // the fused MLP as k_mlpw (hidden layer split over the waves, per-wave LDS-DMA weight
-                                // rings, one u scale per token): bit 0 at dim 96, bit 1 at dim 192 (0: k_mlp). r05: correct
-                                // but not faster (dim 192: 64.7 / 72.5 vs 66.7 / 67.4 us; profiles/r05/knob_ab_*), off
-  int h4_streamk_mink = 0;      // > 0: gemm_ln's tile-48 split GEMMs with K >= this run stream-K over every CU (GemmArgs.sk)
-                                // instead of S chunks of each tile on T x S workgroups (0: off)
+  int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) at dim 96: bit 0 the forward,
+                                // bit 1 the backward (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box, profiles/r04/ab_r04j)
   int fixup_stage = 1;          // the fused fixup + LayerNorm sums a workgroup's 8 rows of split-K partials with whole
                                 // 128-B line reads into LDS first (0: each row's loads straight from the partials)
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
@@ -61,6 +53,8 @@ struct Tuning {
                                 // 1: 3 rows of a band in flight per pass (more waves per SIMD), 2: 6 rows (r05: misfit
                                 // class 0.404 vs 0.480 ms / eval at 721x1440, profiles/r05/knob_ab_grid_mr_r05g.jsonl);
                                 // read by vv_bind_problem
+  int host_wait = 0;            // the host's wait in vv_reduce_batch (vv_engine.hip host_sync): 0 hipStreamSynchronize
+                                // (a busy CPU), 1 sleep + hipStreamQuery polls
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
@@ -135,12 +129,6 @@ struct GemmArgs {
   const float* obb;
   const float* escale;  // set by the tile-48 launch: A's row scales in GEMM row order (what the kernel used)
   int nofix;            // set by gemm_ln: the split-K partials are summed by the consumer (no fixup launch)
-  // set by gemm_ln (tile 48, Tuning.h4_streamk_mink): stream-K. gridDim.x workgroups share the T x K/32 (tile,
-  // k-tile) units evenly; logical workgroup w (xcd_remap of blockIdx.x) owns units [w U / P, (w + 1) U / P), i.e. one
-  // or two tile segments, and writes each segment's partial to slot w + t of ws; tile t's partials are the slots
-  // w + t for w = w_first(t) .. w_last(t), summed in that (k) order by the consumer (k_fixup_ln / k_fixup_ln_bwd)
-  int sk;
-  int skp;  // stream-K: the GEMM's workgroup count P (what the consumer needs to find a tile's slots)
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   int h3_mink;         // > 0: this GEMM's own smallest K for the fp16x3 kernels (the forecast: Tuning.fc_h3_mink)
   GemmGroup g[kMaxGroups];
@@ -494,8 +482,7 @@ bool prof_enabled();
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 // host-side launch counters of the fused-path alternatives (vv_get_counter): tests assert that a fused path really
 // ran, since every fused launcher falls back to the unfused launches with equal results when it does not apply
-enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_STREAMK = 4,
-                     CNT_N = 5 };
+enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_N = 4 };
 void count_launch(int c);
 long long launch_count(int c);
 
@@ -520,13 +507,10 @@ struct MlpGroup {
   const float* dy;                   // bwd: dx2 [M][C]
   float* out;                        // fwd x2, bwd dx1 [M][C]
   float* rs;                         // bwd, optional: fp16x3 row scales of dx1 (k_rowscale's formula)
-  const float* wmax;                 // k_mlpw: device scalar max |w1h's weight| (fc1.weight fwd, fc2.weight bwd)
-  const float* bmax;                 //   and max |fc1.bias| (fwd; null bwd): the bound of the u scale
 };
 struct MlpArgs {
   int M, C, ngroups;
   int hc;  // C = 192: hidden units per chunk (32 or 64; 0 = 32), or 2 (32, hidden layer split over two waves)
-  int w;   // k_mlpw (hidden layer split over the 4 waves of a 64-token workgroup): bit 0 at dim 96, bit 1 at dim 192
   float eps;
   MlpGroup g[kMaxGroups];
 };

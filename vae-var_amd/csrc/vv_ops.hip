@@ -293,17 +293,6 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnArgs a) {
 // 8 rows (waves) per workgroup: GEMM rows 8i .. 8i + 7 are fragment rows r = 0..3 of two lane quarters, so each
 // 128-B line of a partial (rows r and r + 4 of one 16-column block) is consumed inside one workgroup
 constexpr int kFixupLnMaxN = 1280;  // gemm_ln's N limit
-constexpr int kSkMaxSeg = 6;        // stream-K segments per tile at most (gemm_ln enables it only where that holds)
-// stream-K (GemmArgs.sk): tile t's partial slots are w + t for the logical workgroups w = w0 .. w0 + n - 1 whose
-// unit ranges [w U / P, (w + 1) U / P) meet the tile's units [t nkt, (t + 1) nkt) (k_gemm_h4's partition)
-__device__ __forceinline__ void sk_slots(const GemmArgs& a, int t, int& w0, int& n) {
-  const long long nkt = a.K / 32, P = a.skp;
-  const long long U = (long long)((a.M + 255) >> 8) * ((a.N + 127) >> 7) * nkt;
-  auto wof = [&](long long u) { return (int)(((u + 1) * P + U - 1) / U - 1); };  // the workgroup holding unit u
-  w0 = wof((long long)t * nkt);
-  n = wof((long long)(t + 1) * nkt - 1) - w0 + 1;
-}
-
 // the chunk-order sums of the S-chunk partials of the 8 GEMM rows gr0 .. gr0 + 7 (gr0 % 8 == 0: one 8-row block of a
 // 256-row tile, i.e. fixed a, wm and the fragment-row pair hh = 2 hk, 2 hk + 1), read a whole 128-B line per 8 threads
 // (the per-row loads take half lines: rows r and r + 4 share each line) into stg[row][ntn 128] (r05 late). The sum of
@@ -339,7 +328,7 @@ __device__ __forceinline__ void fixup_stage(const GemmArgs& args, int gr0, float
   }
 }
 
-template <int NV, int S, bool SK = false, bool STG = false>
+template <int NV, int S, bool STG = false>
 __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   // wave = GEMM row gr (ginv) or LN row j: with a gather, walking GEMM rows keeps each 128-B line of a partial
   // (two GEMM rows of one wave quarter) inside one workgroup
@@ -371,7 +360,6 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   const int GM = args.gm > 0 ? args.gm : 8;  // tile_mn's grouped order (gemm_nt always sets gm)
   const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
   bool ok[NV];
-  int sw0[NV], nsk[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int jv = sl + v * 64;
@@ -380,13 +368,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
     const int nb = c4 >> 7, cc = c4 & 127, wn = cc >> 6, b = (cc >> 4) & 3, rin = cc & 15;
     const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
     const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + hh * 16 + rin);
-    if (SK) {  // S = the most segments a tile can have; this tile's nsk of them, slots sw0 + c + tl
-      sk_slots(args, tl, sw0[v], nsk[v]);
-#pragma unroll
-      for (int c = 0; c < S; ++c)
-        pv[c][v] = c < nsk[v] ? *reinterpret_cast<const f4*>(args.ws + (size_t)(sw0[v] + c + tl) * (16 * 4 * 512) + off)
-                              : f4{0.f, 0.f, 0.f, 0.f};
-    } else if (STG) {  // the chunk sum, staged in LDS (pv[0] holds it, the sum below adds nothing more)
+    if (STG) {  // the chunk sum, staged in LDS (pv[0] holds it, the sum below adds nothing more)
       pv[0][v] = *reinterpret_cast<const f4*>(stg + (threadIdx.x >> 6) * (((N + 127) >> 7) * 128) + c4);
     } else {
 #pragma unroll
@@ -408,8 +390,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   for (int v = 0; v < NV; ++v) {
     f4 acc = pv[0][v];
 #pragma unroll
-    for (int c = 1; c < (STG ? 1 : S); ++c)
-      if (!SK || c < nsk[v]) acc += pv[c][v];
+    for (int c = 1; c < (STG ? 1 : S); ++c) acc += pv[c][v];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float t = acc[e] + bv[v][e];
@@ -457,7 +438,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
 
 // the backward form: dy = the fixup of a STORE GEMM without bias (chunk-order sum + 0, k_gemm_fixup_sub16's
 // value), then k_ln_bwd<64, NV> on the row (x, res, y and the planes at row lmap[j], stats at j)
-template <int NV, int S, bool SK = false, bool STG = false>
+template <int NV, int S, bool STG = false>
 __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs l) {
   const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
   const int N = args.N, f4n = N >> 2, C = N;
@@ -479,7 +460,6 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
   const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
   const float mean = l.stats[2 * j], rstd = l.stats[2 * j + 1];
   bool ok[NV];
-  int sw0[NV], nsk[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int jv = sl + v * 64;
@@ -488,13 +468,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
     const int nb = c4 >> 7, cc = c4 & 127, wn = cc >> 6, b = (cc >> 4) & 3, rin = cc & 15;
     const int tl = g0 * GM * ntn + nb * gmm + (mb - m0) - args.tdp;
     const size_t off = (size_t)((a * 4 + b) * 4 + r) * 512 + (size_t)((wm * 2 + wn) * 64 + hh * 16 + rin);
-    if (SK) {
-      sk_slots(args, tl, sw0[v], nsk[v]);
-#pragma unroll
-      for (int c = 0; c < S; ++c)
-        pv[c][v] = c < nsk[v] ? *reinterpret_cast<const f4*>(args.ws + (size_t)(sw0[v] + c + tl) * (16 * 4 * 512) + off)
-                              : f4{0.f, 0.f, 0.f, 0.f};
-    } else if (STG) {
+    if (STG) {
       pv[0][v] = *reinterpret_cast<const f4*>(stg + (threadIdx.x >> 6) * (((N + 127) >> 7) * 128) + c4);
     } else {
 #pragma unroll
@@ -511,8 +485,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
   for (int v = 0; v < NV; ++v) {
     f4 acc = pv[0][v];
 #pragma unroll
-    for (int c = 1; c < (STG ? 1 : S); ++c)
-      if (!SK || c < nsk[v]) acc += pv[c][v];
+    for (int c = 1; c < (STG ? 1 : S); ++c) acc += pv[c][v];
 #pragma unroll
     for (int e = 0; e < 4; ++e) dv[v][e] = acc[e] + 0.0f;  // the STORE epilogue's v = acc + bias (none)
   }
@@ -559,12 +532,6 @@ hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s
   if (nv > 5 || a.N % 4) return hipErrorInvalidValue;
   const dim3 grid((a.M + 7) / 8);
   count_launch(CNT_FIXUP_LN);
-  if (a.sk) {  // stream-K partials: at most kSkMaxSeg per tile
-    count_launch(CNT_STREAMK);
-    if (l.bwd) hipLaunchKernelGGL((k_fixup_ln_bwd<5, kSkMaxSeg, true>), grid, dim3(512), 0, s, a, l);
-    else hipLaunchKernelGGL((k_fixup_ln<5, kSkMaxSeg, true>), grid, dim3(512), 0, s, a, l);
-    return hipGetLastError();
-  }
   // staged chunk sums (whole-line partial reads, fixup_stage) where the workgroup's 8 waves are 8 consecutive GEMM
   // rows: always in the backward, in the forward when the rows are walked in GEMM order (ginv) or not gathered
   const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
@@ -573,9 +540,9 @@ hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s
 #define VV_FIXUP_LN(K, S)                                                  \
   do {                                                                     \
     if (stg)                                                               \
-      hipLaunchKernelGGL((K<5, S, false, true>), grid, dim3(512), sl, s, a, l); \
+      hipLaunchKernelGGL((K<5, S, true>), grid, dim3(512), sl, s, a, l);   \
     else                                                                   \
-      hipLaunchKernelGGL((K<5, S, false, false>), grid, dim3(512), 0, s, a, l); \
+      hipLaunchKernelGGL((K<5, S, false>), grid, dim3(512), 0, s, a, l);   \
   } while (0)
   if (l.bwd) {
     switch (a.tsplit) {
@@ -1892,13 +1859,14 @@ __global__ __launch_bounds__(384) void k_misfit_grid(MisfitArgs a) {
         float v[4], g[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          // k_misfit_fwd's arithmetic, element for element
+          // x as k_misfit_fwd forms it (bit-identical x_t); the misfit multiplies by one reciprocal of R where
+          // k_misfit_fwd divides twice, so J_o and the gradient agree with the per-element path at fp32 level only
           float t = base[u];
           if (XB) t = t + xv[k][u];
           if (a.offset) t = t + off;
           v[u] = t;
           const float d = t - yv[k][u];
-          const float ri = 1.0f / rv[k][u];  // one division per element (k_misfit_fwd: two)
+          const float ri = 1.0f / rv[k][u];
           acc += (double)((hv[k][u] * (d * d)) * ri);
           g[u] = a.coeff * ((hv[k][u] * d) * ri);
         }
@@ -2059,15 +2027,15 @@ hipError_t misfit_fwd(const MisfitArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t misfit_grid_fwd(const MisfitArgs& a, hipStream_t s) {
+  // Wl <= 768: two network columns per thread in the final reduction (vv_bind_problem checks the same)
   if (!a.mi || !a.mj || !a.ri0 || !a.rj0 || !a.Hm || !a.yo || !a.R || (a.Ws & 3) || a.nblk != a.C * a.Hl ||
-      a.Ws > 16384 || (a.flow_in && (!a.rowinv || !a.colinv)))
+      a.Ws > 16384 || a.Wl > 2 * 384 || (a.flow_in && (!a.rowinv || !a.colinv)))
     return hipErrorInvalidValue;
   for (const void* p : {(const void*)a.xb, (const void*)a.yo, (const void*)a.Hm, (const void*)a.R,
                         (const void*)a.x_out, (const void*)a.mj, (const void*)a.colinv})
     if (reinterpret_cast<uintptr_t>(p) & 15) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
   const size_t n = (size_t)a.C * a.Hs * a.Ws;
-  if (a.Wl > 2 * 384) return hipErrorInvalidValue;  // two network columns per thread in the final reduction
   // mr: rows of the band whose loads are in flight together (6: the whole 721 -> 128 band, 152 VGPRs, 3 waves per
   // SIMD; 3: two passes per band, 5 waves per SIMD)
   const dim3 g(a.C * a.Hl), b(384);
@@ -2092,11 +2060,11 @@ hipError_t misfit_net_bwd(const MisfitNetBwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t misfit_bwd(const MisfitBwdArgs& a, hipStream_t s) {
+  if (!a.ri0 && (a.Hs != a.Hl || a.Ws != a.Wl)) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
   if (a.ri0) {
     hipLaunchKernelGGL(k_misfit_bwd_gather, dim3(1024), dim3(256), 0, s, a);
   } else {
-    if (a.Hs != a.Hl || a.Ws != a.Wl) return hipErrorInvalidValue;
     bool v4 = (a.Hs * a.Ws) % 4 == 0;
     for (const void* p : {(const void*)a.g_obs, (const void*)a.Hm, (const void*)a.x, (const void*)a.yo, (const void*)a.R,
                           (const void*)a.g_carry, (const void*)a.g_net})

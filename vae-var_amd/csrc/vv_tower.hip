@@ -78,10 +78,9 @@ __device__ __forceinline__ void tower_wg(int nb, int ng, int& blk, int& grp) {
 // groups of a 16x16x32 fragment read (rows lane & 15, chunk lane >> 4) hit 16 distinct 16-B slots
 __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
 __device__ __forceinline__ int frag(int r, int q) { return r * 32 + ((q ^ hsw(r >> 2)) << 3); }
-#ifndef VV_MLP_BLOCK_PAD
-#define VV_MLP_BLOCK_PAD 32  // halves (64 B); 0 = the unpadded r03 layout (A/B builds)
-#endif
-constexpr int kMlpBlockPad = VV_MLP_BLOCK_PAD;
+// weight-chunk plane blocks padded by 32 halves (64 B): unpadded, the chunk staging stores hit one bank group six ways
+// (dim 192: 68.7 / 68.9 -> 67.6 / 67.7 us, profiles/r04/ab_r04ab)
+constexpr int kMlpBlockPad = 32;
 // k_ablk_fwd's per-wave v buffer row stride (floats): 32, not 36, so that three dim-96 workgroups fit a CU's LDS (the v
 // rows are read as broadcasts, 4 addresses per instruction; only the 6 row stores per wave take a 4-way conflict)
 constexpr int kAblkHBS = 32;
@@ -259,11 +258,7 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
 
   // two chunks per loop trip for the dim-192 forward (the hidden-split backward spills at 2; dim 96 runs faster
   // without: profiles/r04/ab_r04p)
-#ifdef VV_MLP_UNR
-  constexpr int UNR = VV_MLP_UNR;  // A/B builds only
-#else
   constexpr int UNR = (C == 96 || (NH == 2 && !FWD)) ? 1 : 2;  // dim 96: 50.0 / 54.0 vs 53.2 / 55.3 us unrolled
-#endif
 #pragma unroll UNR
   for (int c = 0; c < NC; ++c) {
     // bwd: this chunk's pre-activations, in flight before the next chunk's weight loads (vmcnt is in order)
@@ -455,421 +450,6 @@ __global__ __launch_bounds__(64 * NW * NH, C == 96 ? 3 : 1) void k_mlp(MlpArgs a
 }
 
 #undef VV_MLP_LOAD
-
-// ---------------------------------------------------------------------------------------------------------
-// k_mlpw (r05): the same sub-block with the hidden layer split over the waves instead of the tokens.
-// One workgroup of 4 waves (one per SIMD) per 64 tokens; wave w owns hidden units [w C, w C + C) for ALL 64 tokens:
-//  - every weight fragment is read from LDS by exactly one wave and feeds 4 token groups x 3 products (k_mlp: every
-//    wave of a half read that half's whole chunk, 4x the fragment reads per MFMA), and reaches LDS by the wave's own
-//    LDS-DMA ring (R 1-KB slots) in MFMA fragment order: no VGPR staging, no ds_write, no barrier per chunk -- a wave
-//    waits only for its own DMAs (counted vmcnt: one DMA is issued per fragment consumed, dummies past the end, so
-//    at least R - g DMAs follow the g fragments a step needs);
-//  - the u operand of fc2 has ONE power-of-two scale per token for all chunks, from a bound instead of a maximum,
-//    |u| <= f (C max|W1| max|y_t| + max|b1|) (f = 1 GELU, 1.25 GELU'), as the plane-writing GEMM epilogues do
-//    (a looser scale only moves the planes' exponent), so fc2 accumulates straight into acc2;
-//  - GEMM1's A rows are loaded in the permuted hidden order 8 (r >> 2) + 4 j + (r & 3), so the 8 values a lane
-//    holds after GELU are 8 consecutive hidden units: fc2's natural B fragment (no permuted weight copy);
-//  - the four waves' fc2 partial sums meet in LDS in a fixed order, (w0 + w2) + (w1 + w3).
-// Row phases (LN2 / dx2 in, residual / LN2-backward out) as k_mlp, 4 lanes per token.
-template <int C, bool FWD>
-__global__ __launch_bounds__(256, 1) void k_mlpw(MlpArgs a) {
-  constexpr int TG = 4, NT = 256, NC = C / 32, KS1 = C / 32, NQ = C / 16, CQ = C / 4;
-  constexpr int F1 = KS1 * 4, F2 = NQ * 2, FC = F1 + F2, FT = NC * FC, R = 24;
-  constexpr int YB = TG * KS1 * 2 * 512;  // halves of the Y planes (fragment order, 1-KB blocks)
-  constexpr int RB = R * 512;             // halves of one wave's ring
-  constexpr int LS = C + 4;               // fp32 row stride of the reduction buffers (rows 4 banks apart)
-  static_assert(FT >= R && 2 * 64 * LS * 2 <= YB + 4 * RB, "ring / reduction buffers");
-  extern __shared__ __attribute__((aligned(16))) u16 lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g4 = lane >> 4;
-  int blk, grp;
-  tower_wg(a.M / 64, a.ngroups, blk, grp);
-  const MlpGroup G = a.g[grp];
-  u16* Y = lds;
-  u16* ring = lds + YB + wave * RB;
-  float* T1s = reinterpret_cast<float*>(lds + YB + 4 * RB);
-  float* T1b = T1s + 4 * C;
-  float* T2s = T1b + 4 * C;
-  float* T2b = T2s + C;
-  float* Tiy = T2b + C;   // [64] 2^-e of token t's Y row
-  float* Tsu = Tiy + 64;  // [64] scale of token t's u values
-  const int t0 = blk * 64;
-  const int hb = wave * C;  // this wave's hidden units [hb, hb + C)
-
-  // fragment F (0..FT-1) of this wave's stream: chunk c = F / FC, then W1 (ks, j, p) and W2 (q, p); lane (row li,
-  // k-chunk g4) sources 16 B; lands in slot F % R at byte 16 lane
-  auto issue = [&](int F) {
-    const int Fe = min(F, FT - 1), c = Fe / FC, f = Fe - c * FC;
-    const u16* src;
-    if (f < F1) {
-      const int ks = f >> 2, j = (f >> 1) & 1, p = f & 1;
-      const int hid = hb + 32 * c + 8 * (li >> 2) + 4 * j + (li & 3);
-      src = G.w1h + (size_t)hid * 2 * C + ks * 64 + p * 32 + g4 * 8;
-    } else {
-      const int q = (f - F1) >> 1, p = (f - F1) & 1;
-      src = G.w2h + (size_t)(16 * q + li) * 2 * (4 * C) + ((hb >> 5) + c) * 64 + p * 32 + g4 * 8;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(ring + (F % R) * 512), 16, 0, 0);
-  };
-  for (int F = 0; F < R; ++F) issue(F);
-
-  {  // tables: W1 row scales / fc1 bias [4C], W2 row scales / fc2 bias [C]
-    constexpr int N1 = (4 * C + NT - 1) / NT, N2 = (C + NT - 1) / NT;
-    float a1[N1], c1[N1], a2[N2], c2[N2];
-#pragma unroll
-    for (int i = 0; i < N1; ++i) {
-      const int r = min(tid + i * NT, 4 * C - 1);
-      a1[i] = G.w1s[(size_t)r * (C / 32)];
-      c1[i] = FWD ? G.b1[r] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < N2; ++i) {
-      const int r = min(tid + i * NT, C - 1);
-      a2[i] = G.w2s[(size_t)r * (4 * C / 32)];
-      c2[i] = FWD ? G.b2[r] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < N1; ++i)
-      if (tid + i * NT < 4 * C) {
-        T1s[tid + i * NT] = a1[i];
-        T1b[tid + i * NT] = c1[i];
-      }
-#pragma unroll
-    for (int i = 0; i < N2; ++i)
-      if (tid + i * NT < C) {
-        T2s[tid + i * NT] = a2[i];
-        T2b[tid + i * NT] = c2[i];
-      }
-  }
-
-  // ---- row phase: Y = LN2(x1) (fwd) or dx2 (bwd) of token tt, scaled and split into fragment-order planes ----
-  const int tt = tid >> 2, qd = tid & 3;
-  {
-    const f4* src = reinterpret_cast<const f4*>((FWD ? G.x : G.dy) + (size_t)(t0 + tt) * C + qd * CQ);
-    f4 yv[CQ / 4];
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) yv[v] = src[v];
-    if (FWD) {
-      f4 gv[CQ / 4], bv[CQ / 4];
-#pragma unroll
-      for (int v = 0; v < CQ / 4; ++v) {
-        gv[v] = reinterpret_cast<const f4*>(G.gamma + qd * CQ)[v];
-        bv[v] = reinterpret_cast<const f4*>(G.beta + qd * CQ)[v];
-      }
-      float s = 0.f;
-#pragma unroll
-      for (int v = 0; v < CQ / 4; ++v) s += (yv[v][0] + yv[v][1]) + (yv[v][2] + yv[v][3]);
-      s += xshfl<1>(s);
-      s += xshfl<2>(s);
-      const float mean = s / (float)C;
-      float q = 0.f;
-#pragma unroll
-      for (int v = 0; v < CQ / 4; ++v)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float d = yv[v][e] - mean;
-          q += d * d;
-        }
-      q += xshfl<1>(q);
-      q += xshfl<2>(q);
-      const float rstd = 1.0f / sqrtf(q / (float)C + a.eps);
-#pragma unroll
-      for (int v = 0; v < CQ / 4; ++v)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) yv[v][e] = (yv[v][e] - mean) * rstd * gv[v][e] + bv[v][e];
-      if (qd == 0) *reinterpret_cast<float2*>(G.stats + 2 * (size_t)(t0 + tt)) = make_float2(mean, rstd);
-    }
-    unsigned mx = 0;
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mx = amax(mx, yv[v][e]);
-    mx = max(mx, (unsigned)xshfl<1>((int)mx));
-    mx = max(mx, (unsigned)xshfl<2>((int)mx));
-    const float sy = sc_of(mx), iy = inv_of(mx);
-    if (qd == 0) {
-      // the u bound of this token: f (K max|W1| max|y| + max|b1|), max|y| < 2^15 iy; x2 margin as epilogue_rows
-      constexpr float f = FWD ? 1.0f : 1.25f;
-      const float bmx = G.bmax ? *G.bmax : 0.0f;
-      const float ub = f * ((float)C * *G.wmax * (32768.0f * iy) + bmx);
-      Tiy[tt] = iy;
-      Tsu[tt] = sc_of(__float_as_uint(2.0f * ub));
-    }
-    typedef _Float16 h4t __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) {
-      const int k = qd * CQ + 4 * v, ks = k >> 5, kk = k & 31;
-      h4t hv, lv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = yv[v][e] * sy;
-        hv[e] = (_Float16)x;
-        lv[e] = (_Float16)(x - (float)hv[e]);
-      }
-      u16* blk = Y + ((tt >> 4) * KS1 + ks) * 2 * 512 + ((tt & 15) + 16 * (kk >> 3)) * 8 + (kk & 7);
-      *reinterpret_cast<h4t*>(blk) = hv;
-      *reinterpret_cast<h4t*>(blk + 512) = lv;
-    }
-  }
-  __syncthreads();  // Y planes and tables written
-
-  float iyl[TG], sul[TG];
-#pragma unroll
-  for (int tg = 0; tg < TG; ++tg) {
-    iyl[tg] = Tiy[16 * tg + li];
-    sul[tg] = Tsu[16 * tg + li];
-  }
-  f4 acc2[NQ][TG];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int tg = 0; tg < TG; ++tg) acc2[q][tg] = f4{0.f, 0.f, 0.f, 0.f};
-
-  int F = 0;  // next fragment to consume (this wave's stream)
-  for (int c = 0; c < NC; ++c) {
-    const int hc = hb + 32 * c + 8 * g4;  // the 8 hidden units of this lane's u values
-    f4 ex[2][TG];
-    if (!FWD) {  // the pre-activations of this chunk, in flight under GEMM1
-#pragma unroll
-      for (int tg = 0; tg < TG; ++tg)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          ex[j][tg] = *reinterpret_cast<const f4*>(G.h1 + (size_t)(t0 + 16 * tg + li) * (4 * C) + hc + 4 * j);
-    }
-    // GEMM1^T: rows = hidden units (permuted), columns = tokens
-    f4 acc1[2][TG];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int tg = 0; tg < TG; ++tg) acc1[j][tg] = f4{0.f, 0.f, 0.f, 0.f};
-    // the fragments of step ks + 1 are read under step ks's MFMAs (one exposed LDS latency per GEMM, not per step);
-    // a step's slots are refilled once its fragments are in registers
-    h8v w[2][2], y[TG][2];
-    auto rd1 = [&](int ks, int f0, h8v (&wv)[2][2], h8v (&yv)[TG][2]) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-          wv[j][p] = *reinterpret_cast<const h8v*>(ring + ((f0 + 2 * j + p) % R) * 512 + lane * 8);
-#pragma unroll
-      for (int tg = 0; tg < TG; ++tg)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-          yv[tg][p] = *reinterpret_cast<const h8v*>(Y + ((tg * KS1 + ks) * 2 + p) * 512 + lane * 8);
-    };
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 4) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    rd1(0, F, w, y);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int ks = 0; ks < KS1; ++ks) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) issue(F + R + k);
-      F += 4;
-      h8v wn[2][2], yn[TG][2];
-      if (ks + 1 < KS1) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 4) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        rd1(ks + 1, F, wn, yn);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int pr = 0; pr < 3; ++pr)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int tg = 0; tg < TG; ++tg)
-            acc1[j][tg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[j][pr == 0 ? 1 : 0], y[tg][pr == 1 ? 1 : 0],
-                                                                 acc1[j][tg], 0, 0, 0);
-      if (ks + 1 < KS1) {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int p = 0; p < 2; ++p) w[j][p] = wn[j][p];
-#pragma unroll
-        for (int tg = 0; tg < TG; ++tg)
-#pragma unroll
-          for (int p = 0; p < 2; ++p) y[tg][p] = yn[tg][p];
-      }
-    }
-    // epilogue 1: lane (token li of group tg, g4) holds hidden hc + 4 j + i in acc1[j][tg][i]
-    const f4 s1a = *reinterpret_cast<const f4*>(T1s + hc), s1b = *reinterpret_cast<const f4*>(T1s + hc + 4);
-    const f4 b1a = *reinterpret_cast<const f4*>(T1b + hc), b1b = *reinterpret_cast<const f4*>(T1b + hc + 4);
-    const float s1v[8] = {s1a[0], s1a[1], s1a[2], s1a[3], s1b[0], s1b[1], s1b[2], s1b[3]};
-    const float b1v[8] = {b1a[0], b1a[1], b1a[2], b1a[3], b1b[0], b1b[1], b1b[2], b1b[3]};
-    h8v ub[TG][2];
-#pragma unroll
-    for (int tg = 0; tg < TG; ++tg) {
-      float u[8];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float vv[4], uu[4];
-        if (FWD) {
-          f4 v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = acc1[j][tg][i] * (iyl[tg] * s1v[4 * j + i]) + b1v[4 * j + i];
-          *reinterpret_cast<f4*>(G.h1 + (size_t)(t0 + 16 * tg + li) * (4 * C) + hc + 4 * j) = v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) vv[i] = v[i];
-          gelu4(vv, uu);
-        } else {
-          float xv[4], dg[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) xv[i] = ex[j][tg][i];
-          dgelu4(xv, dg);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) uu[i] = acc1[j][tg][i] * (iyl[tg] * s1v[4 * j + i]) * dg[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) u[4 * j + i] = uu[i];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = u[e] * sul[tg];
-        ub[tg][0][e] = (_Float16)x;
-        ub[tg][1][e] = (_Float16)(x - (float)ub[tg][0][e]);
-      }
-    }
-    // GEMM2^T: rows = output channels 16 q + 4 g4 + i, columns = tokens; acc2 += W2 . u
-    h8v w2c[2];
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) w2c[p] = *reinterpret_cast<const h8v*>(ring + ((F + p) % R) * 512 + lane * 8);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      issue(F + R);
-      issue(F + R + 1);
-      F += 2;
-      h8v w2n[2];
-      if (q + 1 < NQ) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) w2n[p] = *reinterpret_cast<const h8v*>(ring + ((F + p) % R) * 512 + lane * 8);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int pr = 0; pr < 3; ++pr)
-#pragma unroll
-        for (int tg = 0; tg < TG; ++tg)
-          acc2[q][tg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2c[pr == 0 ? 1 : 0], ub[tg][pr == 1 ? 1 : 0],
-                                                               acc2[q][tg], 0, 0, 0);
-      if (q + 1 < NQ) {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        w2c[0] = w2n[0];
-        w2c[1] = w2n[1];
-      }
-    }
-  }
-
-  // ---- the four waves' partial sums: red[0] = w0 + w2, red[1] = w1 + w3 (rows = tokens, stride LS) ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs past the end: the rings are reused below
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(lds) + (wave & 1) * 64 * LS;
-  if (wave < 2) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int tg = 0; tg < TG; ++tg)
-        *reinterpret_cast<f4*>(red + (16 * tg + li) * LS + 16 * q + 4 * g4) = acc2[q][tg];
-  }
-  __syncthreads();
-  if (wave >= 2) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int tg = 0; tg < TG; ++tg) {
-        f4* p = reinterpret_cast<f4*>(red + (16 * tg + li) * LS + 16 * q + 4 * g4);
-        *p = *p + acc2[q][tg];
-      }
-  }
-  __syncthreads();
-
-  // ---- epilogue 2, row layout (token tt, channels qd CQ ..): o = (red0 + red1) / su_t * s2[n] ----
-  const float* r0 = reinterpret_cast<const float*>(lds) + tt * LS + qd * CQ;
-  const float* r1 = r0 + 64 * LS;
-  const float iu = __uint_as_float((254u << 23) - __float_as_uint(Tsu[tt]));
-  const size_t trow = (size_t)(t0 + tt);
-  f4 o[CQ / 4];
-#pragma unroll
-  for (int v = 0; v < CQ / 4; ++v) {
-    const f4 a0 = reinterpret_cast<const f4*>(r0)[v], a1 = reinterpret_cast<const f4*>(r1)[v];
-    const f4 sv = reinterpret_cast<const f4*>(T2s + qd * CQ)[v];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[v][e] = ((a0[e] + a1[e]) * iu) * sv[e];
-  }
-  if (FWD) {
-    f4 xv[CQ / 4];
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) xv[v] = reinterpret_cast<const f4*>(G.x + trow * C + qd * CQ)[v];
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) {
-      const f4 bv = reinterpret_cast<const f4*>(T2b + qd * CQ)[v];
-      f4 r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) r[e] = xv[v][e] + (o[v][e] + bv[e]);
-      reinterpret_cast<f4*>(G.out + trow * C + qd * CQ)[v] = r;
-    }
-  } else {
-    // LayerNorm backward over the row (4 lanes per token): dx = rstd (g dy - mean(g dy) - xhat mean(g dy xhat)) + dx2
-    const float2 st = *reinterpret_cast<const float2*>(G.stats + 2 * trow);
-    const float mean = st.x, rstd = st.y;
-    f4 xv[CQ / 4], gv[CQ / 4], dv[CQ / 4];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) {
-      xv[v] = reinterpret_cast<const f4*>(G.x + trow * C + qd * CQ)[v];
-      gv[v] = reinterpret_cast<const f4*>(G.gamma + qd * CQ)[v];
-      dv[v] = reinterpret_cast<const f4*>(G.dy + trow * C + qd * CQ)[v];
-    }
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float gd = gv[v][e] * o[v][e];
-        s1 += gd;
-        s2 += gd * ((xv[v][e] - mean) * rstd);
-      }
-    s1 += xshfl<1>(s1);
-    s1 += xshfl<2>(s1);
-    s2 += xshfl<1>(s2);
-    s2 += xshfl<2>(s2);
-    const float m1 = s1 / (float)C, m2 = s2 / (float)C;
-    unsigned omx = 0;  // out may alias dy: each thread rewrites only the row slice it has read
-#pragma unroll
-    for (int v = 0; v < CQ / 4; ++v) {
-      f4 r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        r[e] = rstd * (gv[v][e] * o[v][e] - m1 - ((xv[v][e] - mean) * rstd) * m2) + dv[v][e];
-        omx = amax(omx, r[e]);
-      }
-      reinterpret_cast<f4*>(G.out + trow * C + qd * CQ)[v] = r;
-    }
-    if (G.rs) {
-      omx = max(omx, (unsigned)xshfl<1>((int)omx));
-      omx = max(omx, (unsigned)xshfl<2>((int)omx));
-      if (qd == 0) G.rs[trow] = sc_of(omx);
-    }
-  }
-}
-
-template <int C, bool FWD>
-hipError_t launch_mlpw(const MlpArgs& a, hipStream_t s) {
-  constexpr size_t lds = 2 * ((size_t)4 * (C / 32) * 2 * 512 + 4 * 24 * 512) + 4 * (8 * C + 2 * C + 128);
-  static_assert(lds <= 163840, "LDS");
-  if (hipError_t e = set_lds_limit((const void*)k_mlpw<C, FWD>, lds)) return e;
-  hipLaunchKernelGGL((k_mlpw<C, FWD>), dim3(a.M / 64 * a.ngroups), dim3(256), lds, s, a);
-  return hipGetLastError();
-}
 
 template <int C, int NW, int HC, bool FWD, int NH = 1>
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t s) {
@@ -1649,13 +1229,9 @@ static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
       return hipErrorInvalidValue;
     if (fwd ? (!G.beta || !G.b1 || !G.b2) : !G.dy) return hipErrorInvalidValue;
   }
-  if ((a.w & (a.C == 96 ? 1 : 2)) && !a.g[0].wmax) return hipErrorInvalidValue;
   const int ph = prof_begin(s);
   const hipError_t e =
-      (a.w & (a.C == 96 ? 1 : 2))
-          ? (a.C == 96 ? (fwd ? launch_mlpw<96, true>(a, s) : launch_mlpw<96, false>(a, s))
-                       : (fwd ? launch_mlpw<192, true>(a, s) : launch_mlpw<192, false>(a, s)))
-      : a.C == 96  ? (fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s))
+      a.C == 96    ? (fwd ? launch_mlp<96, 4, 32, true>(a, s) : launch_mlp<96, 4, 32, false>(a, s))
       : a.hc == 64 ? (fwd ? launch_mlp<192, 4, 64, true>(a, s) : launch_mlp<192, 4, 64, false>(a, s))
       : a.hc == 2  ? (fwd ? launch_mlp<192, 4, 32, true, 2>(a, s) : launch_mlp<192, 4, 32, false, 2>(a, s))
                    : (fwd ? launch_mlp<192, 4, 32, true>(a, s) : launch_mlp<192, 4, 32, false>(a, s));
@@ -1667,7 +1243,9 @@ static hipError_t mlp_run(const MlpArgs& a, hipStream_t s, bool fwd) {
 hipError_t mlp_fwd(const MlpArgs& a, hipStream_t s) { return mlp_run(a, s, true); }
 
 bool ablk_supported(int C, int heads, int ws, int M) {
-  return ((C == 96 && heads == 3) || (C == 192 && heads == 6)) && ws == 4 && M > 0 && M % 64 == 0;
+  // dim 96 only: the dim-192 form (2048-token towers, 192 workgroups of one wave per SIMD) measured slower than the
+  // unfused launches (r04: closure 8.62-8.65 vs 8.51-8.54 ms; r05: +0.4-0.9 %) and was removed in r06
+  return C == 96 && heads == 3 && ws == 4 && M > 0 && M % 64 == 0;
 }
 
 hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s) {
@@ -1680,7 +1258,7 @@ hipError_t ablk_fwd(const AblkArgs& a, hipStream_t s) {
       return hipErrorInvalidValue;
   }
   const int ph = prof_begin(s);
-  const hipError_t e = a.C == 96 ? launch_ablk_fwd<96>(a, s) : launch_ablk_fwd<192>(a, s);
+  const hipError_t e = launch_ablk_fwd<96>(a, s);
   // qkv + proj GEMMs (2 M 4C C) and the window attention (4 M 16 C); bytes: x in, qkv + P + stats + x1 out
   prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 64.0 * a.M * a.C),
            (double)a.ngroups * a.M * 4.0 * (a.C + 3 * a.C + 16 * a.heads + 2 + a.C));
@@ -1696,7 +1274,7 @@ hipError_t ablk_bwd(const AblkArgs& a, hipStream_t s) {
       return hipErrorInvalidValue;
   }
   const int ph = prof_begin(s);
-  const hipError_t e = a.C == 96 ? launch_ablk_bwd<96>(a, s) : launch_ablk_bwd<192>(a, s);
+  const hipError_t e = launch_ablk_bwd<96>(a, s);
   // proj^T and qkv^T GEMMs (2 M 4C C), the attention backward (8 M 16 C); bytes: gx in / out, qkv, P, x
   prof_end(ph, s, PC_TOWER, a.ngroups * (8.0 * a.M * a.C * a.C + 128.0 * a.M * a.C),
            (double)a.ngroups * a.M * 4.0 * (2 * a.C + 3 * a.C + 16 * a.heads + 2 + a.C));

@@ -74,6 +74,7 @@ _SIGS = {
     "vv_ctx_create": (c_int, [c_int, P(c_void_p)]),
     "vv_ctx_destroy": (c_int, [c_void_p]),
     "vv_model_create": (c_int, [c_void_p, P(VVConfig), c_int, c_int, P(c_int)]),
+    "vv_model_destroy": (c_int, [c_void_p, c_int]),
     "vv_load_weights": (c_int, [c_void_p, c_int, P(c_void_p), c_int]),
     "vv_model_forward": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "vv_model_backward": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),

@@ -44,8 +44,8 @@ class Context:
     # environment as VAEVAR_<KEY> (e.g. VAEVAR_H3_MINK=384); the library itself reads no environment.
     TUNING_KEYS = ("h3_mink", "h3_big", "h3_mf16", "small_split", "small_split_minkt", "tail_minkt", "ln_scales",
                    "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt",
-                   "win_mfma", "fc_h3_mink", "fuse_mlp", "fuse_attn", "attn_mfma", "gelu_planes", "attn_planes", "fixup_ln", "h5", "h5_var", "fc_conv_mf",
-                   "mlp_hc", "h4_gather", "fixup_ln_rows", "grid_fused", "mlp_w", "h4_streamk_mink", "fixup_stage")
+                   "win_mfma", "fc_h3_mink", "fuse_mlp", "fuse_attn", "attn_mfma", "gelu_planes", "attn_planes", "fixup_ln", "h5", "fc_conv_mf",
+                   "mlp_hc", "h4_gather", "fixup_ln_rows", "grid_fused", "fixup_stage", "host_wait")
 
     def __init__(self, device: int = 0):
         self.device = device
@@ -208,7 +208,7 @@ class Context:
     @staticmethod
     def counter(name: str) -> int:
         """vv_get_counter: process-wide eager launch count of a fused-path alternative ("rowsplit", "fixup_ln",
-        "splitk_fixup", "gather_scales", "streamk")."""
+        "splitk_fixup", "gather_scales")."""
         v = ctypes.c_longlong()
         check(lib.vv_get_counter(name.encode(), ctypes.byref(v)), "get_counter")
         return v.value
@@ -299,6 +299,17 @@ class LGUnet:
         self.in_ch = int(sum(cfg["inchans_list"]))
         self.out_ch = int(sum(cfg["outchans_list"]))
         self.H, self.W = cfg["img_size"]
+
+    def __del__(self):
+        # vv_model_destroy: the network's device memory goes with the object (a DAProblem keeps its networks alive;
+        # the bound problem of a destroyed network is unbound by the library). Skipped at interpreter shutdown.
+        mid = getattr(self, "id", None)
+        if mid is not None and lib is not None and getattr(self.ctx, "h", None):
+            try:
+                lib.vv_model_destroy(self.ctx.h, mid)
+            except Exception:
+                pass
+        self.id = None
 
     def workspace_bytes(self) -> int:
         b = ctypes.c_int64()
