@@ -152,7 +152,7 @@ def test_launch_counters_abi():
     from vaevar import _lib
     from vaevar.engine import Context
 
-    for name in ("rowsplit", "fixup_ln", "splitk_fixup", "gather_scales"):
+    for name in ("rowsplit", "fixup_ln", "splitk_fixup", "gather_scales", "h5_split"):
         assert Context.counter(name) >= 0
     with pytest.raises(_lib.VVError, match="unknown counter"):
         Context.counter("nope")

@@ -827,3 +827,47 @@ def test_fixup_ln_bitwise(full_dec):
     check_bitwise("fixup_ln input grad", d0, d1)
     check_bitwise("fixup_ln dJ/dz", g0, g1)
     check_bitwise("fixup_ln J", (jb0, jo0), (jb1, jo1))
+
+
+def test_h5_split_fixup_ln(full_dec):
+    """h5_split (r06): the split-K GEMMs whose fixup is fused into a LayerNorm (proj -> LN2, fc2 -> LN1, qkv^T / fc1^T
+    -> the LN backward; N = 1152 at 2048 rows) on tile 49 with every 256 x 144 tile split four ways (64 x 4 = 256
+    workgroups) instead of tile 48's 72 x 3 = 216; the fused fixup stages tile 49's partials (fixup_stage49). The same
+    products per element, another k-chunking of the sum: fp32-level agreement with the tile-48 split (decoder output,
+    input gradient, closure J and dJ/dz); two runs bit-identical (a fixed partition, partials summed in chunk order);
+    the tile-49 consumer really ran (launch counter)."""
+    from vaevar.engine import DAProblem
+    from vaevar.problem import make_problem
+    from vaevar.synth import smooth_field, uniform_sym
+
+    z = torch.from_numpy(0.5 * smooth_field(431, (1, 32, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(432, (1, 69, 128, 256), 1.0)).cuda()
+    prob = DAProblem(full_dec, make_problem(nch=69, Hs=128, Ws=256, T=1, seed=20250620))
+    zc = torch.from_numpy(0.3 * smooth_field(433, (1, 32, 128, 256))).cuda()
+    ctx = full_dec.ctx
+    default = ctx.get_tuning("h5_split")
+    res, launches = [], []
+    try:
+        for v in (0, 1, 1):
+            ctx.set_tuning("h5_split", v)
+            c0 = ctx.counter("h5_split")
+            out = full_dec.forward_raw(z).clone()
+            dz = torch.empty_like(z)
+            full_dec.backward_raw(cot, dz)
+            launches.append(ctx.counter("h5_split") - c0)
+            g = torch.empty_like(zc)
+            jb, jo = prob.closure(zc, g)
+            res.append((out, dz, jb, jo, g))
+    finally:
+        ctx.set_tuning("h5_split", default)
+    (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1), (o2, d2, jb2, jo2, g2) = res
+    print(f"tile-49 split fixups per forward + backward {launches}")
+    assert launches[0] == 0 and launches[1] >= 24 and launches[2] == launches[1], launches
+    check_bitwise("h5_split run 1 vs 2 out", o1, o2)
+    check_bitwise("h5_split run 1 vs 2 input grad", d1, d2)
+    check_bitwise("h5_split run 1 vs 2 dJ/dz", g1, g2)
+    check_bitwise("h5_split run 1 vs 2 J", (jb1, jo1), (jb2, jo2))
+    check("h5_split vs tile-48 split out", rel(o1.cpu(), o0.cpu()), 1e-5)
+    check("h5_split vs tile-48 split input grad", rel(d1.cpu(), d0.cpu()), 1e-4)
+    check("h5_split vs tile-48 split dJ/dz", rel(g1.cpu(), g0.cpu()), 1e-4)
+    check("h5_split vs tile-48 split closure J", abs(jb1 + jo1 - jb0 - jo0) / abs(jb0 + jo0), 1e-6, "<=")

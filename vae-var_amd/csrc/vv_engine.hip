@@ -2496,6 +2496,7 @@ int vv_set_gemm_math(vv_ctx* ctx, int math) {
   if (math != ctx->math) drop_graphs(ctx);
   ctx->math = math;
   for (auto& m : ctx->models) {
+    if (!m) continue;  // vv_model_destroy'ed
     m->sc.math = math;
     if (m->fm) vvf::set_math(m->fm, math);
   }
@@ -2536,7 +2537,7 @@ int vv_set_closure_graph(vv_ctx* ctx, int enable) {
 
 int vv_get_counter(const char* name, long long* value) {
   if (!name || !value) return fail(VV_E_ARG, "null argument");
-  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup", "gather_scales"};
+  static const char* names[vv::CNT_N] = {"rowsplit", "fixup_ln", "splitk_fixup", "gather_scales", "h5_split"};
   for (int c = 0; c < vv::CNT_N; ++c)
     if (!strcmp(name, names[c])) {
       *value = vv::launch_count(c);

@@ -1973,8 +1973,18 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
   const GemmGroup G = args.g[blockIdx.z];
   const int M = args.M, N = args.N, K = args.K;
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int nk = K / BK;
-  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  // data-parallel, or (r06, gemm_ln) every tile split S = args.tsplit ways along K: chunk-major and XCD-contiguous as
+  // tile 48's split (an XCD's workgroups stream the same k-slice of A and B), partials to ws for the fused fixup
+  int tile, kb = 0, part = -1, nk = K / BK;
+  if (args.tsplit <= 1) {
+    tile = xcd_remap(blockIdx.x, ntm * ntn);
+  } else {
+    const int S = args.tsplit, tt = ntm * ntn, L = xcd_remap(blockIdx.x, tt * S), c = L / tt;
+    tile = L - c * tt;
+    part = tile * S + c;
+    kb = (c * nk) / S;
+    nk = ((c + 1) * nk) / S - kb;
+  }
   int mb, nb;
   tile_mn(tile, ntm, ntn, mb, nb, args.gm);
   const int m0 = mb * BM, n0 = nb * BN;
@@ -2053,7 +2063,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
   // group g, so the compiler's lgkmcnt waits before each group only find old reads outstanding
   h8v gb[2][3][2];
   auto step4 = [&](int t, const h8v (&fa)[TM][2], h8v (&na)[TM][2], int h) {  // h: half holding groups 0 and 2
-    const int cb = t % 3, nbuf = (t + 1) % 3, sb = (t + 2) % 3, sk = min(t + 2, nk - 1);
+    const int cb = t % 3, nbuf = (t + 1) % 3, sb = (t + 2) % 3, sk = kb + min(t + 2, nk - 1);
     // group 0: blocks 0..2 in half h
     mfma_b(fa, gb[h][0], 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -2098,11 +2108,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
   // prologue: k-tiles 0 and 1 in flight, wait for 0, its A fragments and B blocks 0, 1
   h8v fa0[TM][2], fa1[TM][2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) apiece(0, 0, j);
-  bpieces(0, 0);
+  for (int j = 0; j < 4; ++j) apiece(kb, 0, j);
+  bpieces(kb, 0);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) apiece(min(1, nk - 1), 1, j);
-  bpieces(min(1, nk - 1), 1);
+  for (int j = 0; j < 4; ++j) apiece(kb + min(1, nk - 1), 1, j);
+  bpieces(kb + min(1, nk - 1), 1);
   if (b3)
     asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
   else
@@ -2137,6 +2147,18 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
         const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));  // 2^-e_a
         acc[a][b][r] *= ia * sbv;
       }
+  }
+  if (part >= 0) {
+    // the chunk's partial in fragment order: element (row 32 wave + 16 a + 4 hh + r, column 16 b + rin) at
+    // ((a * TN + b) * 4 + r) * 512 + 64 wave + lane (fixup_stage49 reads it back)
+    float* w = args.ws + ((size_t)blockIdx.z * gridDim.x + part) * (size_t)(TM * TN * 4 * 512);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[(size_t)((a * TN + b) * 4 + r) * 512 + tid] = acc[a][b][r];
+    return;
   }
   if (EPI != EPI_RESID && !args.crow && m0 + BM <= M && n0 + BN <= N && (args.ldc & 3) == 0 &&
       (args.ldaux & 3) == 0) {
@@ -2220,7 +2242,8 @@ static hipError_t launch_h5_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
 // tiles 48 and 49 (t49: 256 x 144 tiles, data-parallel only)
 static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) {
   if (a.K % 32 || a.ksplit % 32 || !h3_ready(a) || !h4_ready(a)) return hipErrorInvalidValue;
-  if (t49 && (a.tsplit > 1 || a.nofix)) return hipErrorInvalidValue;
+  // tile 49 splits only for gemm_ln (every tile, the fused fixup + LayerNorm sums the partials)
+  if (t49 && ((a.tsplit > 1) != (a.nofix != 0) || a.tdp)) return hipErrorInvalidValue;
   float* sc = a.ws + kWsFloats;
   const unsigned short* planes = a.apl;
   bool agather = false;
@@ -2254,7 +2277,7 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
   b.agather = agather ? 1 : 0;
   if (t49) {
     const size_t lds = 3 * (2 * (256 + 144) * 32) * sizeof(unsigned short);
-    const dim3 grid(((a.N + 143) / 144) * ((a.M + 255) / 256), 1, a.ngroups);
+    const dim3 grid(((a.N + 143) / 144) * ((a.M + 255) / 256) * std::max(a.tsplit, 1), 1, a.ngroups);
     switch (a.epi) {
       case EPI_STORE: return launch_h5_k<EPI_STORE>(b, s, grid, lds, sc, planes);
       case EPI_GELU:
@@ -2352,6 +2375,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "fc_conv_mf") return &t.fc_conv_mf;
   if (k == "grid_fused") return &t.grid_fused;
   if (k == "fixup_stage") return &t.fixup_stage;
+  if (k == "h5_split") return &t.h5_split;
   if (k == "host_wait") return &t.host_wait;
   return nullptr;
 }
@@ -2659,6 +2683,7 @@ static hipError_t gemm_prepare(GemmArgs& a, int tile_hint, float* ws, int& t) {
 hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws) {
   GemmArgs a = a_in;
   a.nofix = 0;
+  a.t49 = 0;
   int t = -1;
   if (hipError_t e = gemm_prepare(a, tile_hint, ws, t)) return e;
   const int ph = prof_begin(s);
@@ -2682,6 +2707,23 @@ hipError_t gemm_ln(const GemmArgs& a_in, const GemmLnArgs& l, hipStream_t s, flo
   if (hipError_t e = gemm_prepare(a, -1, ws, t)) return e;
   if (t != 48 || a.tsplit < 2 || a.tsplit > 4 || a.tdp != 0) return hipErrorNotSupported;
   a.nofix = 1;
+  a.t49 = 0;
+  {
+    // r06 (h5_split): tile 49 with every tile split S = P / T ways where that fills the chip exactly (N = 1152 at
+    // 2048 rows: 64 tiles x 4 = 256 workgroups; tile 48: 72 x 3 = 216); its partials are staged by the consumer
+    // (fixup_stage49), so only where the fused fixup stages (fixup_ln_launch's stg condition)
+    const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+    const long P = device_cus(), T49 = tiles_of(a, 256, 144);
+    const bool stg = TU.fixup_stage && (l.bwd || l.ginv || !l.gmap);
+    if (TU.h5_split && stg && a.N % 144 == 0 && a.N % 128 == 0 && T49 > 0 && P % T49 == 0 && P / T49 >= 2 &&
+        P / T49 <= 4 && (size_t)P * 256 * 144 <= kWsFloats && a.K / 32 >= P / T49) {
+      t = 49;
+      a.t49 = 1;
+      a.tsplit = (int)(P / T49);
+      const int ntm = (a.M + 255) / 256, ntn = (a.N + 143) / 144;
+      a.gm = std::max(1, std::min(ntm, (int)std::lround(std::sqrt((double)ntm * ntn / 8.0 * 144 / 256))));
+    }
+  }
   const int ph = prof_begin(s);
   hipError_t e = launch_variant(t, a, s);
   if (e == hipSuccess) e = fixup_ln_launch(a, l, s);

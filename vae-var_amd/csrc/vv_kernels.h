@@ -46,6 +46,8 @@ struct Tuning {
                                 // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
   int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) at dim 96: bit 0 the forward,
                                 // bit 1 the backward (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box, profiles/r04/ab_r04j)
+  int h5_split = 0;             // gemm_ln: tile 49 with every tile split P / T ways (64 tiles x 4 = 256 workgroups for the
+                                // N = 1152 GEMMs at 2048 rows) instead of tile 48's 72 tiles x 3 = 216 (r06, A/B knob)
   int fixup_stage = 1;          // the fused fixup + LayerNorm sums a workgroup's 8 rows of split-K partials with whole
                                 // 128-B line reads into LDS first (0: each row's loads straight from the partials)
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
@@ -129,6 +131,7 @@ struct GemmArgs {
   const float* obb;
   const float* escale;  // set by the tile-48 launch: A's row scales in GEMM row order (what the kernel used)
   int nofix;            // set by gemm_ln: the split-K partials are summed by the consumer (no fixup launch)
+  int t49;              // set by gemm_ln: the partials are tile 49's (256 x 144 tiles, fragment order of k_gemm_h5)
   const Tuning* tune;  // host-side dispatch knobs of the owning context (null: kDefaultTuning); never read on the device
   int h3_mink;         // > 0: this GEMM's own smallest K for the fp16x3 kernels (the forecast: Tuning.fc_h3_mink)
   GemmGroup g[kMaxGroups];
@@ -482,7 +485,7 @@ bool prof_enabled();
 void prof_read(double* ms, double* flops, double* bytes, int* n);
 // host-side launch counters of the fused-path alternatives (vv_get_counter): tests assert that a fused path really
 // ran, since every fused launcher falls back to the unfused launches with equal results when it does not apply
-enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_N = 4 };
+enum Counter : int { CNT_ROWSPLIT = 0, CNT_FIXUP_LN = 1, CNT_SPLITK_FIXUP = 2, CNT_GATHER_SCALES = 3, CNT_H5_SPLIT = 4, CNT_N = 5 };
 void count_launch(int c);
 long long launch_count(int c);
 

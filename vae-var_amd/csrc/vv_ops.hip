@@ -328,7 +328,41 @@ __device__ __forceinline__ void fixup_stage(const GemmArgs& args, int gr0, float
   }
 }
 
-template <int NV, int S, bool STG = false>
+// The same for tile 49's partials (r06, Tuning.h5_split: 256 x 144 tiles, every tile split S ways; k_gemm_h5 writes
+// element (row 32 w + 16 a + 4 hh + r, column 16 b + rin) of a tile at ((a * 9 + b) * 4 + r) * 512 + 64 w + 16 hh + rin).
+// The 8 rows gr0 .. gr0 + 7 are one wave w, one a and the fragment-row pair hh = 2 hk, 2 hk + 1: for each (tile column
+// nb, b, r) one 128-B line holds rows 4 (hh & 1) + r of 16 columns. Chunk-order sums, as fixup_stage.
+template <int S>
+__device__ __forceinline__ void fixup_stage49(const GemmArgs& args, int gr0, float* stg) {
+  constexpr int PMAX = 5;  // pieces per thread: ntn 8 x 36 lines x 8 / 512 = 4.5 for N = 1152
+  const int ntm = (args.M + 255) >> 8, ntn = args.N / 144, LS = ((args.N + 127) >> 7) * 128, nl = ntn * 36 * 8;
+  const int mb = gr0 >> 8, rr0 = gr0 & 255, w = rr0 >> 5, a = (rr0 >> 4) & 1, hk = (rr0 >> 3) & 1;
+  const int GM = args.gm > 0 ? args.gm : 8;
+  const int g0 = mb / GM, m0 = g0 * GM, gmm = min(GM, ntm - m0);
+  f4 pv[PMAX][S];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) {
+    const int e = min((int)threadIdx.x + 512 * p, nl - 1);
+    const int q = e & 7, L = e >> 3, r = L & 3, b = (L >> 2) % 9, nb = (L >> 2) / 9;
+    const int tl = g0 * GM * ntn + nb * gmm + (mb - m0);
+    const size_t off = (size_t)((a * 9 + b) * 4 + r) * 512 + (size_t)(w * 64 + (2 * hk + (q >> 2)) * 16 + (q & 3) * 4);
+#pragma unroll
+    for (int c = 0; c < S; ++c) pv[p][c] = *reinterpret_cast<const f4*>(args.ws + (size_t)(tl * S + c) * (18 * 4 * 512) + off);
+  }
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) {
+    const int e = threadIdx.x + 512 * p;
+    if (e < nl) {
+      const int q = e & 7, L = e >> 3, r = L & 3, b = (L >> 2) % 9, nb = (L >> 2) / 9;
+      f4 acc = pv[p][0];
+#pragma unroll
+      for (int c = 1; c < S; ++c) acc += pv[p][c];
+      *reinterpret_cast<f4*>(stg + ((q >> 2) * 4 + r) * LS + nb * 144 + b * 16 + (q & 3) * 4) = acc;
+    }
+  }
+}
+
+template <int NV, int S, bool STG = false, bool T49 = false>
 __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   // wave = GEMM row gr (ginv) or LN row j: with a gather, walking GEMM rows keeps each 128-B line of a partial
   // (two GEMM rows of one wave quarter) inside one workgroup
@@ -352,7 +386,8 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
   const int lo = l.lo_x ? xo : j;
   const int rrow = args.rmod > 0 ? xo % args.rmod : xo;
   f4 pv[S][NV], rv[NV], bv[NV], gv[NV], bb[NV];
-  if constexpr (STG) fixup_stage<S>(args, blockIdx.x * 8, stg);  // GEMM row = w (host: ginv set or no gmap)
+  if constexpr (STG && T49) fixup_stage49<S>(args, blockIdx.x * 8, stg);  // GEMM row = w (host: ginv or no gmap)
+  else if constexpr (STG) fixup_stage<S>(args, blockIdx.x * 8, stg);
   __syncthreads();
   if (w >= args.M) return;
   const int ntm = (args.M + 255) >> 8, ntn = (N + 127) >> 7;
@@ -438,7 +473,7 @@ __global__ __launch_bounds__(512) void k_fixup_ln(GemmArgs args, GemmLnArgs l) {
 
 // the backward form: dy = the fixup of a STORE GEMM without bias (chunk-order sum + 0, k_gemm_fixup_sub16's
 // value), then k_ln_bwd<64, NV> on the row (x, res, y and the planes at row lmap[j], stats at j)
-template <int NV, int S, bool STG = false>
+template <int NV, int S, bool STG = false, bool T49 = false>
 __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs l) {
   const int j = blockIdx.x * 8 + (threadIdx.x >> 6), sl = threadIdx.x & 63;
   const int N = args.N, f4n = N >> 2, C = N;
@@ -450,7 +485,8 @@ __global__ __launch_bounds__(512) void k_fixup_ln_bwd(GemmArgs args, GemmLnArgs 
   const int pr = l.lmap ? l.lmap[jl] : jl;
   const float* res = l.res ? l.res : l.x;  // dummy source when there is no residual (never added)
   f4 pv[S][NV], xv[NV], gv[NV], rv[NV];
-  if constexpr (STG) fixup_stage<S>(args, blockIdx.x * 8, stg);  // GEMM row = j
+  if constexpr (STG && T49) fixup_stage49<S>(args, blockIdx.x * 8, stg);  // GEMM row = j
+  else if constexpr (STG) fixup_stage<S>(args, blockIdx.x * 8, stg);
   __syncthreads();
   if (j >= args.M) return;
   const int gr = j;
@@ -537,12 +573,16 @@ hipError_t fixup_ln_launch(const GemmArgs& a, const GemmLnArgs& l, hipStream_t s
   const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
   const bool stg = TU.fixup_stage && (l.bwd || l.ginv || !l.gmap);
   const size_t sl = stg ? (size_t)8 * ((a.N + 127) / 128) * 128 * sizeof(float) : 0;
-#define VV_FIXUP_LN(K, S)                                                  \
-  do {                                                                     \
-    if (stg)                                                               \
-      hipLaunchKernelGGL((K<5, S, true>), grid, dim3(512), sl, s, a, l);   \
-    else                                                                   \
-      hipLaunchKernelGGL((K<5, S, false>), grid, dim3(512), 0, s, a, l);   \
+  if (a.t49 && !stg) return hipErrorInvalidValue;  // tile 49's partials are read by fixup_stage49 only
+  if (a.t49) count_launch(CNT_H5_SPLIT);
+#define VV_FIXUP_LN(K, S)                                                        \
+  do {                                                                           \
+    if (a.t49)                                                                   \
+      hipLaunchKernelGGL((K<5, S, true, true>), grid, dim3(512), sl, s, a, l);   \
+    else if (stg)                                                                \
+      hipLaunchKernelGGL((K<5, S, true>), grid, dim3(512), sl, s, a, l);         \
+    else                                                                         \
+      hipLaunchKernelGGL((K<5, S, false>), grid, dim3(512), 0, s, a, l);         \
   } while (0)
   if (l.bwd) {
     switch (a.tsplit) {
