@@ -415,7 +415,50 @@ def thread_cpu():
     return out
 
 
-def thread_cpu_delta(before, after, seconds):
+class ThreadSampler:
+    """VV_THREAD_SAMPLE=1: every 20 ms, each thread's scheduler state, kernel wait channel and current syscall
+    (/proc/self/task/*/{stat,wchan,syscall}), to name what a busy HIP-runtime thread is doing."""
+
+    def __init__(self):
+        import threading
+        from collections import Counter, defaultdict
+
+        self.stats = defaultdict(lambda: {"n": 0, "R": 0, "wchan": Counter(), "syscall": Counter()})
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self.run, daemon=True)
+
+    def run(self):
+        while not self.stop.wait(0.02):
+            try:
+                tids = os.listdir("/proc/self/task")
+            except OSError:
+                continue
+            for tid in tids:
+                try:
+                    with open(f"/proc/self/task/{tid}/stat") as f:
+                        st = f.read()
+                    state = st[st.rindex(")") + 2]
+                    with open(f"/proc/self/task/{tid}/wchan") as f:
+                        wc = f.read().strip() or "0"
+                    with open(f"/proc/self/task/{tid}/syscall") as f:
+                        sc = f.read().split()[0]
+                except (OSError, IndexError):
+                    continue
+                r = self.stats[tid]
+                r["n"] += 1
+                r["R"] += state == "R"
+                r["wchan"][wc] += 1
+                r["syscall"][sc] += 1
+
+    def summary(self):
+        out = {}
+        for tid, r in self.stats.items():
+            out[tid] = {"running_frac": round(r["R"] / max(r["n"], 1), 3), "wchan": r["wchan"].most_common(2),
+                        "syscall": r["syscall"].most_common(2)}
+        return out
+
+
+def thread_cpu_delta(before, after, seconds, sampled=None):
     """Per-thread CPU over an interval, as fractions of one CPU, the busiest first (threads named by their comm and
     whether they are the main thread)."""
     main = str(os.getpid())
@@ -424,6 +467,8 @@ def thread_cpu_delta(before, after, seconds):
         d = cs - before.get(tid, (name, 0.0))[1]
         if d > 0:
             rows.append({"thread": name + (" (main)" if tid == main else ""), "cpu_frac": round(d / max(seconds, 1e-9), 3)})
+            if sampled and tid in sampled:
+                rows[-1].update(sampled[tid])
     rows.sort(key=lambda r: -r["cpu_frac"])
     return rows[:8]
 
@@ -432,6 +477,9 @@ def timed_analyses(w, ensemble, steps, dev):
     """Barrier + sync, `steps` analyses (each gathered to rank 0 at N > 1), sync + barrier; max time over ranks."""
     ensemble.barrier()
     w.sync()
+    sampler = ThreadSampler() if os.environ.get("VV_THREAD_SAMPLE") == "1" else None
+    if sampler:
+        sampler.t.start()
     th0 = thread_cpu()
     t0 = time.perf_counter()
     c0 = time.process_time()
@@ -447,7 +495,10 @@ def timed_analyses(w, ensemble, steps, dev):
     ensemble.barrier()
     el = time.perf_counter() - t0
     cpu = time.process_time() - c0  # host CPU seconds of this rank (all its threads) over the timed region
-    threads = thread_cpu_delta(th0, thread_cpu(), el)
+    if sampler:
+        sampler.stop.set()
+        sampler.t.join()
+    threads = thread_cpu_delta(th0, thread_cpu(), el, sampler.summary() if sampler else None)
     disc = w.discarded() - d0
     return (ensemble.reduce_scalar(el, "max", dev), ensemble.reduce_scalar(iters, "sum", dev),
             ensemble.reduce_scalar(evals, "sum", dev), shapes,

@@ -145,8 +145,9 @@ def test_config4_trajectory_g16(mode):
         note(f"G16 {mode} J rel, pass {i}", v)
     if mode == "replay":
         check("G16 replay J per pass (max)", e_pass.max(), max(1e-3, 2 * float(sens["replay_rel"].max())))
-        check("G16 replay xa rel-L2", e_x, 1e-3)
+        check("G16 replay xa rel-L2", e_x, 2e-4)  # r06: 1e-3 -> 2e-4 (achieved 2.7e-5, parity_margins.jsonl)
+        check("G16 replay |xa-xb|^2", e_dx, 2e-3)
     else:
         check("G16 free final J", e_pass[-1], max(1e-3, 2 * float(sens["free_rel"][-1])))
         check("G16 free xa rel-L2", e_x, 1e-2)
-    check(f"G16 {mode} |xa-xb|^2", e_dx, 1e-2)
+        check("G16 free |xa-xb|^2", e_dx, 1e-2)

@@ -107,9 +107,11 @@ def one_step_vs_golden(prob, prob_np, g, tag):
     if "ls_t" in g.files:
         steps = [(float(t), int(n)) for t, n in zip(g["ls_t"], g["ls_evals"])]
         rJ, r_xa, r_dx = run(steps)
+        # J printed to 4 digits by the reference: 1e-3; xa / |xa-xb|^2 tightened in r06 from c6's 1e-3 / 1e-2 to
+        # within ~100x of what the HIP path achieves (G6 / G8 replay xa 1.2e-8, |xa-xb|^2 8e-8: parity_margins.jsonl)
         check(f"{tag} replay J per pass (max)", rJ, 1e-3)
-        check(f"{tag} replay xa rel-L2", r_xa, 1e-3)
-        check(f"{tag} replay |xa-xb|^2", r_dx, 1e-2)
+        check(f"{tag} replay xa rel-L2", r_xa, 1e-6)
+        check(f"{tag} replay |xa-xb|^2", r_dx, 1e-5)
 
 
 def test_one_step_da_real_obs_g8(full_dec):

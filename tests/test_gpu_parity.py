@@ -381,12 +381,14 @@ def test_one_step_da_config5_g6():
     prob_np = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250620)
     one_step_vs_golden(DAProblem(dec, prob_np, flow=flow), prob_np, g, "G6 config 5 one_step_DA")
 
-def traj_checks(tag, mode, e_pass, e_x, e_dx, sens, free_default=None):
+def traj_checks(tag, mode, e_pass, e_x, e_dx, sens, free_default=None, replay_xa=2e-4, replay_dx=2e-3):
     """The bounds of a full-budget trajectory test (SURVEY §8 c6 with the reference's own summation-order drift,
-    oracle/g10_sensitivity.py): replay — J per pass at max(1e-3, 2x the reference's replay drift), xa rel-L2 1e-3,
-    |xa-xb|^2 1e-2; free-running — the final J at max(1e-3, 2x its free-running drift) and xa at 1e-2 (the per-pass J
-    of a free run may sit on another line-search branch, so it is recorded, not bounded). Every achieved error is
-    recorded next to its bound (tests/conftest.py check / note)."""
+    oracle/g10_sensitivity.py): replay — J per pass at max(1e-3, 2x the reference's replay drift); xa rel-L2 and
+    |xa-xb|^2 at replay_xa / replay_dx (r06: tightened from c6's 1e-3 / 1e-2 to within ~10x of what the HIP path
+    achieves, profiles/r06/parity_margins.jsonl: G10 / G13 / G16 replay xa 2.0e-5 / 2.7e-5 / 2.7e-5); free-running —
+    the final J at max(1e-3, 2x its free-running drift) and xa at 1e-2 (a free run may take another line-search
+    branch, where xa still agrees to ~1e-4: DESIGN §2; the per-pass J is recorded, not bounded). Every achieved error
+    is recorded next to its bound (tests/conftest.py check / note)."""
     for i, v in enumerate(e_pass):
         note(f"{tag} {mode} J rel, pass {i}", v)
     if mode == "replay":
@@ -394,8 +396,8 @@ def traj_checks(tag, mode, e_pass, e_x, e_dx, sens, free_default=None):
         bound = max(1e-3, 2 * drift)
         print(f"{tag} replay J bound {bound:.1e} (reference vs itself under another summation order: {drift:.1e})")
         check(f"{tag} replay J per pass (max)", e_pass.max(), bound)
-        check(f"{tag} replay xa rel-L2", e_x, 1e-3)
-        check(f"{tag} replay |xa-xb|^2", e_dx, 1e-2)
+        check(f"{tag} replay xa rel-L2", e_x, replay_xa)
+        check(f"{tag} replay |xa-xb|^2", e_dx, replay_dx)
     else:
         bound = max(1e-3, 2 * float(sens["free_rel"][-1])) if sens is not None else free_default
         check(f"{tag} free final J", e_pass[-1], bound)
@@ -437,7 +439,7 @@ def test_config5_trajectory_g15(full_dec, mode):
     print(f"G15 config 5 ({mode}): J per pass rel {['%.1e' % v for v in e_pass]}; xa rel-L2 {e_x:.1e}; "
           f"|xa-xb|^2 rel {e_dx:.1e}; iters {res['n_iter']}, evals {res['n_eval']} (reference line searches "
           f"{len(g['ls_t'])}, evals {int(g['ls_evals'].sum()) + 0})")
-    traj_checks("G15", mode, e_pass, e_x, e_dx, sens, free_default=2e-2)
+    traj_checks("G15", mode, e_pass, e_x, e_dx, sens, free_default=2e-2, replay_xa=1e-6, replay_dx=1e-5)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -714,6 +716,10 @@ def test_bitwise_knobs(full_dec, knob, ref, on):
 
     res, gathers = [], []
     default = full_dec.ctx.get_tuning(knob)
+    h5s = full_dec.ctx.get_tuning("h5_split")
+    # tile 49's split (h5_split) runs only where the fused fixup stages its partials, which fixup_stage / fixup_ln_rows
+    # switch: the tile-48 split on both sides keeps the comparison bitwise
+    full_dec.ctx.set_tuning("h5_split", 0)
     try:
         for v in (ref, on):
             full_dec.ctx.set_tuning(knob, v)
@@ -727,6 +733,7 @@ def test_bitwise_knobs(full_dec, knob, ref, on):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning(knob, default)
+        full_dec.ctx.set_tuning("h5_split", h5s)
     (o0, d0, jb0, jo0, g0), (o1, d1, jb1, jo1, g1) = res
     print(f"{knob}: k_gather_scales passes {gathers[0]} -> {gathers[1]}")
     check_bitwise(f"{knob} out", o0, o1)
@@ -799,6 +806,8 @@ def test_fixup_ln_bitwise(full_dec):
     res = []
     ln_launches, fused = [], []
     default = full_dec.ctx.get_tuning("fixup_ln")
+    h5s = full_dec.ctx.get_tuning("h5_split")
+    full_dec.ctx.set_tuning("h5_split", 0)  # bit-identity holds for tile 48's S-chunk split (tile 49's: h5_split test)
     try:
         for v in (0, 1):
             full_dec.ctx.set_tuning("fixup_ln", v)
@@ -814,6 +823,7 @@ def test_fixup_ln_bitwise(full_dec):
             res.append((out, dz, jb, jo, g))
     finally:
         full_dec.ctx.set_tuning("fixup_ln", default)
+        full_dec.ctx.set_tuning("h5_split", h5s)
     # the fused path really ran (gemm_ln falls back to separate launches when it returns hipErrorNotSupported):
     # the LG-stage LayerNorms after split-K GEMMs (proj -> LN2, fc2 -> next LN1, and their backward) leave the
     # LayerNorm class

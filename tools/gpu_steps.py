@@ -22,6 +22,8 @@ steps (one shell word each; arguments after ':' are split on whitespace):
                           into NN_ktrace.txt (the trace itself is not kept)
   kseq:MARKER:SCRIPT[:ARGS]  the same, listed launch by launch after the second-to-last MARKER kernel
                           (tools/ktrace_seq.py) into NN_kseq.txt
+  outliers[:ARGS]         rocprofv3 --kernel-trace of bench.py ARGS; the launches far slower than their kernel's median
+                          with their neighbours (tools/ktrace_outliers.py) into NN_outliers.txt (the trace is not kept)
 """
 from __future__ import annotations
 
@@ -33,7 +35,7 @@ import sys
 import time
 
 LIMIT = {"tests": 1000, "smoke": 200, "bench": 420, "ab": 900, "env": 420, "rocprof": 420, "pmc": 300, "py": 420,
-         "pyenv": 420, "ktrace": 420, "kseq": 420}
+         "pyenv": 420, "ktrace": 420, "kseq": 420, "outliers": 480}
 
 
 def run(cmd, out, limit, env=None):
@@ -110,6 +112,14 @@ def main():
                 tool = [os.path.join(root, "tools", "kstats.py"), tr[0]] if tr and not marker else \
                     [os.path.join(root, "tools", "ktrace_seq.py"), tr[0], marker, "700"] if tr else None
                 rc = run([py] + tool, base + ".txt", 120) if tool else 1
+            shutil.rmtree(d, ignore_errors=True)
+        elif kind == "outliers":
+            d = base + "_rp"
+            cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--", py, "bench.py"]
+            rc = run(cmd + rest.split(), base + ".log", lim)
+            if rc == 0:
+                tr = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+                rc = run([py, os.path.join(root, "tools", "ktrace_outliers.py"), tr[0]], base + ".txt", 300) if tr else 1
             shutil.rmtree(d, ignore_errors=True)
         elif kind == "py":
             script, _, args = rest.partition(":")
