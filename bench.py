@@ -261,7 +261,8 @@ def pmc_mfma():
         path = os.path.join(ROOT, "profiles", rnd, "pmc_mfma.json")
         try:
             with open(path) as f:
-                ks = json.load(f)["kernels"]
+                pm = json.load(f)
+            ks = pm["kernels"]
         except (OSError, ValueError, KeyError):
             continue
         out = {}
@@ -272,7 +273,13 @@ def pmc_mfma():
                 continue
             avg = lambda key: sum(r.get(key, 0.0) * x for r, x in zip(rows, w)) / sum(w)
             out[cls] = {"mfma_busy": avg("mfma_busy"), "mfma_busy_active_cus": avg("mfma_busy_active_cus"),
-                        "held_clock_ghz": avg("held_clock_ghz"), "kernels": len(rows)}
+                        "mfma_rate_of_spec": avg("mfma_rate_of_spec"), "grbm_clock_ghz": avg("held_clock_ghz"),
+                        "kernels": len(rows)}
+        lg = pm.get("long_gemm", {})
+        if lg:
+            out["long_gemm"] = {k: {"shape": v.get("shape"), "duration_us": v.get("duration_us_median"),
+                                    "held_clock_ghz": v.get("held_clock_ghz"), "mfma_busy": v.get("mfma_busy")}
+                                for k, v in lg.items()}
         if out:
             out["source"] = (f"profiles/{rnd}/pmc_mfma.json (tools/pmc_mfma.py: one rocprofv3 --pmc pass per counter + "
                              "--kernel-trace over config-3 closures; busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 "
@@ -742,11 +749,17 @@ def main():
             pm = pmc_mfma()
             if pm:
                 if "fp16x3" in pm:
+                    # MFMA-pipe busy cycles over the class's dispatches: of their active cycles (GRBM_GUI_ACTIVE, which
+                    # over-counts dispatches this short, so a lower bound) and of the 2.4 GHz spec rate
                     out["roofline"]["mfma_busy"] = pm["fp16x3"]["mfma_busy"]
                     out["roofline"]["mfma_busy_active_cus"] = pm["fp16x3"]["mfma_busy_active_cus"]
-                    out["roofline"]["held_clock_ghz"] = pm["fp16x3"]["held_clock_ghz"]
-                    # the fp16 MFMA peak at the clock the chip holds under these kernels (2.5 PF is quoted at 2.4 GHz)
-                    out["roofline"]["peak_at_held_clock"] = peak * pm["fp16x3"]["held_clock_ghz"] / 2.4
+                    out["roofline"]["mfma_rate_of_spec"] = pm["fp16x3"]["mfma_rate_of_spec"]
+                lg = pm.get("long_gemm", {}).get("tile48")
+                if lg and lg.get("held_clock_ghz"):
+                    # the clock the chip holds under the tile-48 main loop (a ~2 ms dispatch of the same kernel: the
+                    # GRBM clock is exact there), the fp16 peak at that clock and the class's fraction of it
+                    out["roofline"]["held_clock_ghz"] = lg["held_clock_ghz"]
+                    out["roofline"]["peak_at_held_clock"] = peak * lg["held_clock_ghz"] / 2.4
                     out["roofline"]["frac_of_held_clock_peak"] = ach / out["roofline"]["peak_at_held_clock"]
                 out["roofline"]["pmc"] = pm
             # the other GEMM class (bf16x6, short-K Swin-tower linears) against its own peak

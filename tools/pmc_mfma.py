@@ -8,9 +8,14 @@ is divided by its own duration:
   held_clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration                            (MI355X_MICROARCH.md DVFS item)
   mfma_insts     = SQ_INSTS_MFMA per dispatch; SQ_BUSY_CYCLES per dispatch (SQ busy, summed over the SEs)
 
-The GRBM pass's durations give the clock; the busy fraction uses the GRBM_GUI_ACTIVE of the same kernel (means over its
-dispatches). This script never touches the GPU itself: every pass is a child process (rocprofv3 runs the program after
-`--`). Usage: python tools/pmc_mfma.py OUTDIR  -> OUTDIR/pmc_mfma.json
+  mfma_rate_of_spec = SQ_VALU_MFMA_BUSY_CYCLES / (duration x 2.4 GHz x 1024 SIMDs)   (clock-independent)
+
+GRBM_GUI_ACTIVE / duration reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, DVFS give-back): the
+closure's GEMMs run 15-70 us, so their held_clock_ghz is an upper bound and mfma_busy a lower one. The held clock under
+the fp16x3 main loops is therefore also measured on long dispatches of the same kernels (LONG: tools/gemm_one.py,
+65536 x 4608 x 1152 on tiles 48 / 49, ~2 ms each, random operands). This script never touches the GPU itself: every
+pass is a child process (rocprofv3 runs the program after `--`).
+Usage: python tools/pmc_mfma.py OUTDIR  -> OUTDIR/pmc_mfma.json
 """
 import csv
 import glob
@@ -32,23 +37,22 @@ def short(name):
     return re.sub(r"\(.*", "", n).replace("void ", "")
 
 
-def main():
-    out = os.path.abspath(sys.argv[1])
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    os.makedirs(out, exist_ok=True)
-    env = dict(os.environ, T="2", TMPDIR="/tmp")
+LONG = [("tile48", ["65536", "4608", "1152", "48", "6"]), ("tile49", ["65536", "4608", "1152", "49", "6"])]
+
+
+def passes(out, root, env, prog, tag, regex):
+    """one rocprofv3 --pmc pass per counter (+ --kernel-trace) of `prog`; per (kernel, grid) counter means, durations"""
     per = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> [values]
     dur = defaultdict(list)                          # kernel -> [ns] (all passes)
     durn = defaultdict(list)                         # kernel name alone -> [ns] (fallback if the grid keys differ)
     wgs = {}
     for c in COUNTERS:
-        d = os.path.join(out, "p_" + c)
+        d = os.path.join(out, f"p_{tag}_{c}")
         cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", c, "--kernel-trace", "--kernel-include-regex",
-               KERNELS, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable, "-u",
-               os.path.join(root, "tools", "quick_time.py")]
-        with open(os.path.join(out, f"p_{c}.log"), "w") as f:
+               regex, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable, "-u"] + prog
+        with open(os.path.join(out, f"p_{tag}_{c}.log"), "w") as f:
             rc = subprocess.run(cmd, stdout=f, stderr=subprocess.STDOUT, env=env, cwd=root).returncode
-        print(f"pass {c}: rc {rc}", flush=True)
+        print(f"pass {tag} {c}: rc {rc}", flush=True)
         if rc:
             sys.exit(rc)
         cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -68,6 +72,10 @@ def main():
             dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             durn[short(r["Kernel_Name"])].append(dur[k][-1])
         shutil.rmtree(d, ignore_errors=True)
+    return summarise(per, dur, durn, wgs)
+
+
+def summarise(per, dur, durn, wgs):
     res = {}
     for k, cs in per.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -81,6 +89,7 @@ def main():
             rec["workgroups"] = wgs[k]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
             rec["mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS)
+            rec["mfma_rate_of_spec"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (dmed * 2.4 * SIMDS)
             if k in wgs:
                 rec["mfma_busy_active_cus"] = rec["mfma_busy"] * 256 / min(256, wgs[k])
         if "SQ_INSTS_MFMA" in m:
@@ -88,9 +97,27 @@ def main():
         if "SQ_BUSY_CYCLES" in m:
             rec["sq_busy_cycles"] = m["SQ_BUSY_CYCLES"]
         res[k] = rec
+    return res
+
+
+def main():
+    out = os.path.abspath(sys.argv[1])
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(out, exist_ok=True)
+    env = dict(os.environ, T="2", TMPDIR="/tmp")
+    res = passes(out, root, env, [os.path.join(root, "tools", "quick_time.py")], "closure", KERNELS)
+    long = {}
+    for name, args in LONG:
+        r = passes(out, root, dict(env, PRE="1"), [os.path.join(root, "tools", "gemm_one.py")] + args, name,
+                   r"k_gemm_h4|k_gemm_h5")
+        long[name] = {"shape": "x".join(args[:3]), **max(r.values(), key=lambda x: x["duration_us_median"])}
     with open(os.path.join(out, "pmc_mfma.json"), "w") as f:
         json.dump({"workload": "config-3 closures (tools/quick_time.py, T = 2: decoder + flow stand-in, 69x128x256)",
-                   "counters": COUNTERS, "formulas": __doc__.split("\n\n")[1], "kernels": res}, f, indent=1)
+                   "counters": COUNTERS, "formulas": __doc__.split("\n\n")[1], "kernels": res,
+                   "long_gemm": long}, f, indent=1)
+    for name, r in long.items():
+        print(f"long {name} {r['shape']}: {r['duration_us_median']:.0f} us, clock {r['held_clock_ghz']:.2f} GHz, "
+              f"mfma_busy {r.get('mfma_busy', float('nan')):.3f}", flush=True)
     for k, r in sorted(res.items(), key=lambda x: -x[1]["duration_us_median"]):
         print(f"{k[:60]:60s} {r['duration_us_median']:8.1f} us  clock {r['held_clock_ghz']:.2f} GHz  "
               f"mfma_busy {r.get('mfma_busy', float('nan')):.3f}", flush=True)

@@ -56,8 +56,9 @@ struct Tuning {
                                 // 1: 3 rows of a band in flight per pass (more waves per SIMD), 2: 6 rows (r05: misfit
                                 // class 0.404 vs 0.480 ms / eval at 721x1440, profiles/r05/knob_ab_grid_mr_r05g.jsonl);
                                 // read by vv_bind_problem
-  int host_wait = 0;            // the host's wait in vv_reduce_batch (vv_engine.hip host_sync): 0 hipStreamSynchronize
-                                // (a busy CPU), 1 sleep + hipStreamQuery polls
+  int host_wait = 1;            // the host's wait in vv_reduce_batch (vv_engine.hip host_sync): 0 hipStreamSynchronize
+                                // (a busy CPU), 1 sleep + hipStreamQuery polls (r06: main thread 1.00 -> 0.04 CPU at
+                                // equal throughput, 51.91 / 51.89 vs 51.91 / 52.01 it/s, profiles/r06/host_wait_ab)
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
