@@ -701,12 +701,49 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     check(f"{knob}={on} vs 0 closure J", e_j, 1e-7)
 
 
-@pytest.mark.parametrize("knob,ref,on", [("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1), ("fixup_stage", 0, 1)])
+@pytest.mark.parametrize("B", [1, 2])
+def test_patch_pers_flow_bitwise(B):
+    """The persistent PatchEmbed / ConvTranspose2d kernels (patch_pers 1) against the r05 ones (0) at the flow's
+    shapes, which the decoder's do not reach: 69 -> 138 channels, i.e. the 52-tap PatchEmbed and the 104-tap (112-padded)
+    ConvTranspose2d forward and backward instances, B = 1 and 2, the output limit on and off and the added image of
+    the PatchEmbed backward. Same MFMA sequence per output element: bit-identical."""
+    from vaevar import config as C
+    from vaevar.engine import LGUnet
+    from vaevar.synth import smooth_field, uniform_sym
+
+    m = LGUnet(C.FLOW, B, 1).load_synthetic()
+    x = torch.from_numpy(0.5 * smooth_field(431, (B, 69, 128, 256))).cuda()
+    cot = torch.from_numpy(uniform_sym(432, (B, 138, 128, 256), 1.0)).cuda()
+    add = torch.from_numpy(uniform_sym(433, (B, 69, 128, 256), 1.0)).cuda()
+    default = m.ctx.get_tuning("patch_pers")
+    res = {}
+    try:
+        for v in (0, 1):
+            m.ctx.set_tuning("patch_pers", v)
+            outs = []
+            for lim in (0, 100):
+                # channels >= the limit are not produced (forward_raw's output is uninitialised there)
+                outs.append(m.forward_raw(x, out_limit=lim)[:, :lim or None].clone())
+                dx = torch.empty_like(x)
+                m.backward_raw(cot, dx, out_limit=lim, add=add)
+                outs.append(dx.clone())
+            res[v] = outs
+    finally:
+        m.ctx.set_tuning("patch_pers", default)
+    names = ("out", "input grad", "out (limit 100)", "input grad (limit 100)")
+    for n, a, b in zip(names, res[0], res[1]):
+        check_bitwise(f"patch_pers B={B} {n}", a, b)
+
+
+@pytest.mark.parametrize("knob,ref,on", [("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1), ("fixup_stage", 0, 1),
+                                         ("patch_pers", 0, 1)])
 def test_bitwise_knobs(full_dec, knob, ref, on):
     """h4_gather: tile 48 reads a gathered A's producer row scales through the row map itself
     instead of a k_gather_scales pass (the counter shows the pass is gone). fixup_ln_rows: the fused fixup + LN1
     after fc2 walks GEMM rows through the inverse window map (each row's arithmetic unchanged). fixup_stage: the fused
-    fixup + LayerNorm sums its workgroup's split-K partials through LDS (same chunk-order sum per element). The same
+    fixup + LayerNorm sums its workgroup's split-K partials through LDS (same chunk-order sum per element).
+    patch_pers: the persistent PatchEmbed / ConvTranspose2d kernels (k_p2t_mp / k_t2p_mp) run each output's MFMA
+    sequence in the r05 kernels' k order. The same
     per-element arithmetic either way, so the config-2 decoder output, its input gradient and the closure are
     bit-identical."""
     from vaevar.engine import DAProblem

@@ -1181,6 +1181,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   pa.Ctok = C0;
   pa.img = in;
   pa.ngroups = G;
+  pa.tune = m.sc.tune;
   for (int g = 0, off = 0; g < G; off += c.raw.inchans[g], ++g) {
     pa.g[g].w = w(eg(g) + ".patch_embed.proj.weight");
     pa.g[g].bias = w(eg(g) + ".patch_embed.proj.bias");
@@ -1286,6 +1287,7 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   pu.climit = climit > 0 ? std::min(climit, c.Cout) : c.Cout;
   pu.img_out = out;
   pu.ngroups = G;
+  pu.tune = m.sc.tune;
   int moff = 0, soff = 0;
   for (int g = 0; g < G; ++g) soff += c.raw.outchans[g] / 2;
   for (int g = 0; g < G; ++g) {
@@ -1324,6 +1326,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   pu.climit = climit > 0 ? std::min(climit, c.Cout) : c.Cout;
   pu.img = dout;
   pu.ngroups = G;
+  pu.tune = m.sc.tune;
   int moff = 0, soff = 0;
   for (int g = 0; g < G; ++g) soff += c.raw.outchans[g] / 2;
   for (int g = 0; g < G; ++g) {
@@ -1424,6 +1427,7 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   pa.img_out = din;
   pa.add_img = add;
   pa.ngroups = G;
+  pa.tune = m.sc.tune;
   for (int g = 0, off = 0; g < G; off += c.raw.inchans[g], ++g) {
     pa.g[g].w = w(eg(g) + ".patch_embed.proj.weight");
     pa.g[g].dtok = m.gsk0 + g * M0C0;

@@ -46,7 +46,7 @@ hipError_t set_lds_limit(const void* k, size_t lds) {
 }
 
 // compute units of the current device (cached per device)
-static int device_cus() {
+int device_cus() {
   static std::mutex mu;
   static int cus[64] = {0};
   int dev = 0;
@@ -2377,6 +2377,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "fixup_stage") return &t.fixup_stage;
   if (k == "h5_split") return &t.h5_split;
   if (k == "host_wait") return &t.host_wait;
+  if (k == "patch_pers") return &t.patch_pers;
   return nullptr;
 }
 bool tuning_value_ok(const char* key, int v) {

@@ -59,6 +59,10 @@ struct Tuning {
   int host_wait = 1;            // the host's wait in vv_reduce_batch (vv_engine.hip host_sync): 0 hipStreamSynchronize
                                 // (a busy CPU), 1 sleep + hipStreamQuery polls (r06: main thread 1.00 -> 0.04 CPU at
                                 // equal throughput, 51.91 / 51.89 vs 51.91 / 52.01 it/s, profiles/r06/host_wait_ab)
+  int patch_pers = 1;           // the decoder PatchEmbed / ConvTranspose2d kernels in their persistent form (one workgroup
+                                // of 8 waves per CU share, weights staged once, each wave prefetching its next 16-token
+                                // tile behind the current one's MFMAs; 0: one 64-token workgroup per tile, bit-identical;
+                                // r06: patch class 0.295 -> 0.177 ms / eval, profiles/r06/knob_ab_patch_pers.jsonl)
 };
 extern const Tuning kDefaultTuning;
 // the tuning key names (vv_set_tuning); returns the field or null
@@ -153,6 +157,7 @@ struct GattnArgs {
 // device; locked, so concurrent contexts on several devices are safe). The first value set for a kernel stays: callers
 // whose LDS varies pass their maximum.
 hipError_t set_lds_limit(const void* k, size_t lds);
+int device_cus();  // compute units of the current device (cached)
 // the split-operand fp16x3 kernels that read producer planes (GemmArgs.apre) and write them (opl): tiles 48, 49
 bool gemm_plane_tile(int t);
 bool gattn_supported(int C, int heads);
@@ -318,6 +323,7 @@ struct PatchArgs {
   const float* add_img;      // conv bwd: added to dz (latent regulariser term z), may be null
   int ngroups;
   PatchGroup g[kMaxGroups];
+  const Tuning* tune;        // null: kDefaultTuning (host dispatch only)
 };
 
 hipError_t patch_embed_fwd(const PatchArgs& a, hipStream_t s);

@@ -1598,6 +1598,248 @@ __global__ __launch_bounds__(256) void k_t2p_mf(PatchArgs a) {
   }
 }
 
+// Persistent forms (r06). The r05 kernels above stage the weights per 64-token workgroup (57 KB from L2 for every 64
+// tokens at 112 taps), run their loads, MFMAs and stores in lockstep per workgroup, and chain each accumulator's
+// MFMAs back to back (40-cycle dependent latency against a 32-cycle issue). Here a workgroup of 8 waves per CU share
+// of a group stages its group's weights once; each wave walks its own 16-token tiles (a contiguous range of the
+// group's tiles per workgroup), prefetching the next tile's operands into registers behind the current tile's MFMAs,
+// and interleaves its accumulators (k step outer, output tile inner). Per output element the MFMA sequence -- k in
+// steps of 4, ascending -- is the r05 kernels', so both forms give bit-identical results.
+constexpr int kPmWaves = 8;
+
+// the 16-token tiles [r0, r1) of workgroup j of P over a group's nwt tiles
+__device__ __forceinline__ void pm_range(int nwt, int& r0, int& r1) {
+  r0 = (int)((long long)blockIdx.x * nwt / gridDim.x);
+  r1 = (int)((long long)(blockIdx.x + 1) * nwt / gridDim.x);
+}
+
+template <int MODE, int KPM>
+__global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const PatchGroup& G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
+  // compile-time shapes (zero-padded to KPM taps and kPatchCmax channels): MFMAs under runtime conditions made the
+  // compiler keep every accumulator live across branches (thousands of VGPRs spilled)
+  constexpr int KS = KPM + 4;                                     // weight row stride (floats)
+  constexpr int RS = KS > kPatchCmax + 4 ? KS : kPatchCmax + 4;   // the wave's rows: operands, then the staging
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  float* Wsm = sm;                                    // [kPatchCmax][KS]
+  float* R = sm + kPatchCmax * KS + wave * 16 * RS;  // [16][RS], this wave's only
+  int r0, r1;
+  pm_range(ntok / 16, r0, r1);
+  constexpr int NC = KPM / 4;  // channel rows per lane: lane (pp = lane / 32, col = lane % 32) of the tile's
+                               // 32-pixel-wide, 2-row image strip, one channel per load
+  constexpr int NO = kPatchCmax / 16, NTM = kPatchCmax / 16;
+  const int col = lane & 31, pp = lane >> 5;
+  const size_t plane = (size_t)a.Himg * a.Wimg;
+  float xv[NC];
+  f4 pv[NO];
+  auto load_tile = [&](int wt) {
+    int b, ho, wo;
+    tok_coords(wt * 16, Ho, Wo, b, ho, wo);
+    const float* base = a.img + (size_t)b * a.Cimg * plane + (size_t)(2 * ho + pp) * a.Wimg + 2 * wo + col;
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) {
+      xv[ci] = 0.f;
+      if (ci * 4 < kc) {
+        const int ch = MODE == 0 ? G.cin_off + ci : unembed_ch(G, ci);
+        if (MODE == 0 || ch < a.climit) xv[ci] = base[(size_t)ch * plane];
+      }
+    }
+    if (MODE == 0) {
+      const size_t pbase = (size_t)((wt * 16) % (Ho * Wo)) * C;
+#pragma unroll
+      for (int i = 0; i < NO; ++i)
+        pv[i] = i < C / 16 ? *reinterpret_cast<const f4*>(G.pos + pbase + 4 * (i * 64 + lane)) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  int wt = r0 + wave;
+  if (wt < r1) load_tile(wt);
+  float bv[NTM];
+#pragma unroll
+  for (int n = 0; n < NTM; ++n) bv[n] = MODE == 0 ? G.bias[min(n * 16 + li, C - 1)] : 0.f;
+  {
+    constexpr int NW = kPatchCmax * KPM / 512, NB = NW < 16 ? NW : 16;
+#pragma unroll
+    for (int h = 0; h < NW; h += NB) {
+      float wv[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int i = threadIdx.x + 512 * (h + r), c = i / KPM, j = i - c * KPM;
+        wv[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int i = threadIdx.x + 512 * (h + r), c = i / KPM, j = i - c * KPM;
+        if (h + r < NW) Wsm[c * KS + j] = wv[r];  // NW need not be a multiple of NB (28 at 112 taps)
+      }
+    }
+  }
+  __syncthreads();
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  for (; wt < r1; wt += kPmWaves) {
+    // this tile's operand rows (zeros at the padded taps); the previous tile's staging is read back already
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) R[(col >> 1) * RS + ci * 4 + pp * 2 + (col & 1)] = xv[ci];
+    f4 pc[NO];
+#pragma unroll
+    for (int i = 0; i < NO; ++i) pc[i] = pv[i];
+    if (wt + kPmWaves < r1) load_tile(wt + kPmWaves);  // in flight behind this tile's MFMAs
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    fr4 acc[NTM];
+#pragma unroll
+    for (int n = 0; n < NTM; ++n) acc[n] = fr4{0.f, 0.f, 0.f, 0.f};
+    const float* xr = R + li * RS + 4 * g;
+#pragma unroll
+    for (int s4 = 0; s4 < KPM; s4 += 16) {
+      const f4 xa = *reinterpret_cast<const f4*>(xr + s4);
+      f4 wb[NTM];
+#pragma unroll
+      for (int n = 0; n < NTM; ++n) wb[n] = *reinterpret_cast<const f4*>(Wsm + (n * 16 + li) * KS + 4 * g + s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int n = 0; n < NTM; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], wb[n][e], acc[n], 0, 0, 0);
+    }
+    // (D + bias) over the operand rows (every lane's reads of them are issued: same-wave LDS order), then whole-row
+    // float4 stores of the tile's contiguous [16][C] block (+ pos)
+#pragma unroll
+    for (int n = 0; n < NTM; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) R[(4 * g + r) * RS + n * 16 + li] = MODE == 0 ? acc[n][r] + bv[n] : acc[n][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    float* out = G.tok + (size_t)wt * 16 * C;
+#pragma unroll
+    for (int i = 0; i < NO; ++i) {
+      if (i >= C / 16) break;
+      const int e = 4 * (i * 64 + lane), row = e / C, cc = e - row * C;
+      f4 v = *reinterpret_cast<const f4*>(R + row * RS + cc);
+      if (MODE == 0) v = v + pc[i];
+      *reinterpret_cast<f4*>(out + e) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the next operand rows overlay them
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int MODE, int KPM>
+__global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const PatchGroup& G = a.g[blockIdx.y];
+  const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
+  constexpr int CS = kPatchCmax + 4;
+  float* Wt = sm;  // [KPM][CS]: W[c][j] at Wt[j][c], zero-padded (compile-time MFMA shapes, as k_p2t_mp)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  int r0, r1;
+  pm_range(ntok / 16, r0, r1);
+  constexpr int NMT = KPM / 16, NS = kPatchCmax / 16;
+  f4 y[NS];
+  float2 ex[NMT][2];
+  // lane (token li, g): the token row's float4 at 16 s + 4 g, and what its outputs add (the added image, the bias)
+  auto load_tile = [&](int wt) {
+    const int tok = wt * 16 + li;
+    const float* yr = (MODE == 0 ? G.dtok : G.tok) + (size_t)tok * C + 4 * g;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) y[s] = 16 * s < C ? *reinterpret_cast<const f4*>(yr + 16 * s) : f4{0.f, 0.f, 0.f, 0.f};
+    if (MODE == 0 && a.add_img) {
+      int b, ho, wo;
+      tok_coords(tok, Ho, Wo, b, ho, wo);
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) {
+        const int o = 4 * mt + g;
+        const size_t off = (((size_t)b * a.Cimg + G.cin_off + min(o, kc / 4 - 1)) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          ex[mt][q] = o * 4 < kc ? *reinterpret_cast<const float2*>(a.add_img + off + q * a.Wimg) : make_float2(0.f, 0.f);
+      }
+    }
+  };
+  int wt = r0 + wave;
+  float bz[NMT];  // MODE 1: the bias of output channel 4 mt + g
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    bz[mt] = MODE == 1 ? G.bias[min(4 * mt + g, kc / 4 - 1)] : 0.f;
+    if (MODE == 1 || !a.add_img) ex[mt][0] = ex[mt][1] = make_float2(0.f, 0.f);
+  }
+  if (wt < r1) load_tile(wt);
+  {
+    constexpr int NW = kPatchCmax * KPM / 512, NB = NW < 16 ? NW : 16;
+#pragma unroll
+    for (int h = 0; h < NW; h += NB) {
+      float v[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int i = threadIdx.x + 512 * (h + r), c = i / KPM, j = i - c * KPM;
+        v[r] = (c < C && j < kc) ? G.w[(size_t)c * kc + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int i = threadIdx.x + 512 * (h + r), c = i / KPM, j = i - c * KPM;
+        if (h + r < NW) Wt[j * CS + c] = v[r];  // NW need not be a multiple of NB (28 at 112 taps)
+      }
+    }
+  }
+  __syncthreads();
+  typedef float fr4 __attribute__((ext_vector_type(4)));
+  for (; wt < r1; wt += kPmWaves) {
+    f4 yc[NS];
+    float2 xc[NMT][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) yc[s] = y[s];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt)
+      if (MODE == 0) xc[mt][0] = ex[mt][0], xc[mt][1] = ex[mt][1];
+    if (wt + kPmWaves < r1) load_tile(wt + kPmWaves);  // in flight behind this tile's MFMAs
+    fr4 acc[NMT];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) acc[mt] = fr4{0.f, 0.f, 0.f, 0.f};
+    // W^T fragments one k step ahead (double-buffered): left to itself the scheduler hoisted every step's LDS reads
+    // and spilled
+    const float* wr = Wt + li * CS + 4 * g;
+    f4 wa[2][NMT];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) wa[0][mt] = *reinterpret_cast<const f4*>(wr + mt * 16 * CS);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS)
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt)
+          wa[(s + 1) & 1][mt] = *reinterpret_cast<const f4*>(wr + mt * 16 * CS + 16 * (s + 1));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[s & 1][mt][e], yc[s][e], acc[mt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int b, ho, wo;
+    tok_coords(wt * 16 + li, Ho, Wo, b, ho, wo);
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) {
+      const int o = 4 * mt + g;
+      if (o * 4 >= kc) continue;
+      const int ch = MODE == 0 ? G.cin_off + o : unembed_ch(G, o);
+      if (MODE == 1 && ch >= a.climit) continue;
+      float* dst = a.img_out + (((size_t)b * a.Cimg + ch) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        *reinterpret_cast<float2*>(dst + q * a.Wimg) =
+            MODE == 0 ? make_float2(acc[mt][2 * q] + xc[mt][q].x, acc[mt][2 * q + 1] + xc[mt][q].y)
+                      : make_float2(acc[mt][2 * q] + bz[mt], acc[mt][2 * q + 1] + bz[mt]);
+    }
+  }
+}
+
+// persistent grid: P workgroups per group, `per_cu` resident per CU, at most one per 8 of the group's 16-token tiles
+static int pm_grid(const PatchArgs& a, int per_cu) {
+  const int nwt = a.B * (a.Himg / 2) * (a.Wimg / 2) / 16;
+  return std::max(1, std::min((nwt + kPmWaves - 1) / kPmWaves, device_cus() * per_cu / a.ngroups));
+}
+
 static int max_k(const PatchArgs& a, bool in) {
   int m = 0;
   for (int g = 0; g < a.ngroups; ++g) m = std::max(m, (in ? a.g[g].cin : a.g[g].cout) * 4);
@@ -1607,6 +1849,13 @@ static int max_k(const PatchArgs& a, bool in) {
 template <int MODE, int KPM>
 static hipError_t p2t_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
+  if ((a.tune ? a.tune->patch_pers : kDefaultTuning.patch_pers) > 0) {
+    const size_t lds =
+        ((size_t)kPatchCmax * (KPM + 4) + (size_t)kPmWaves * 16 * std::max(KPM + 4, kPatchCmax + 4)) * sizeof(float);
+    if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM>, lds)) return e;
+    hipLaunchKernelGGL((k_p2t_mp<MODE, KPM>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
+    return hipGetLastError();
+  }
   const int KS = (kc + 15) / 16 * 16 + 4;
   const size_t lds = std::max((size_t)(PT + a.Ctok) * KS, (size_t)PT * (a.Ctok + 4)) * sizeof(float);
   if (lds > 64 * 1024)
@@ -1627,6 +1876,13 @@ template <int MODE, int KPM>
 static hipError_t t2p_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   const size_t lds = (size_t)((kc + 15) / 16 * 16) * ((a.Ctok + 15) / 16 * 16 + 4) * sizeof(float);
+  if ((a.tune ? a.tune->patch_pers : kDefaultTuning.patch_pers) > 0) {
+    const size_t lm = (size_t)KPM * (kPatchCmax + 4) * sizeof(float);
+    if (lm > 64 * 1024)
+      if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM>, lm)) return e;
+    hipLaunchKernelGGL((k_t2p_mp<MODE, KPM>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lm, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((k_t2p_mf<MODE, KPM>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
 }
