@@ -4,7 +4,7 @@ the decoder / flow GEMMs run on B x tokens rows, the misfit per analysis, each a
   tiny networks: no GEMM of the tiny config splits K, so every output element is summed in the same order at
       B = 1 and B = 2 -> the batched closure and the batched L-BFGS trajectories equal B = 1 runs BIT FOR BIT.
   full networks: at B = 1 the chip is filled by splitting K of the 2048-row LG GEMMs; at B > 1 the rows fill it and
-      the split is dropped, so results differ at fp32 rounding level (bounded here at 1e-6 / 1e-5).
+      the split is dropped, so results differ at fp32 rounding level (bounded here at ~5x the measured difference, profiles/r06/parity_margins.jsonl).
 """
 import numpy as np
 import pytest
@@ -100,7 +100,7 @@ def test_full_batch2_closure_vs_single():
         e = (abs(jb1 - jb2[b]) / jb1, abs(jo1 - jo2[b]) / jo1, rel(g2[b].cpu(), g1[0].cpu()),
              rel(xa2[b], p1.analysis(z[b:b + 1].contiguous()).cpu()))
         print(f"full B=2 vs B=1, analysis {b}: J_b {e[0]:.1e} J_o {e[1]:.1e} grad {e[2]:.1e} xa {e[3]:.1e}")
-        check(f"full B=2 vs B=1 analysis {b} J_b", e[0], 1e-12)
-        check(f"full B=2 vs B=1 analysis {b} J_o", e[1], 1e-6)
+        check(f"full B=2 vs B=1 analysis {b} J_b", e[0], 1e-12, "<=")
+        check(f"full B=2 vs B=1 analysis {b} J_o", e[1], 5e-8)
         check(f"full B=2 vs B=1 analysis {b} dJ/dz", e[2], 1e-5)
-        check(f"full B=2 vs B=1 analysis {b} xa", e[3], 1e-6)
+        check(f"full B=2 vs B=1 analysis {b} xa", e[3], 5e-7)

@@ -45,8 +45,8 @@ def test_tiny_t6_closure_g12():
     jb, jo = prob.closure(z, grad)
     e = (abs(jb - g["J_b"]) / g["J_b"], abs(jo - g["J_o"]) / g["J_o"], rel(grad.cpu(), g["grad"]))
     print(f"G12 tiny 4D-Var T=6 closure: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    check("G12 J_b", e[0], 1e-5)
-    check("G12 J_o", e[1], 1e-5)
+    check("G12 J_b", e[0], 5e-8)
+    check("G12 J_o", e[1], 5e-7)
     check("G12 grad", e[2], 1e-5)
     # the trajectory x_t of the five integrate steps is kept per slot
     assert prob.trajectory().shape == (6, 4, 32, 64)
@@ -68,8 +68,8 @@ def test_tiny_t6_lbfgs_g12(mode):
     e_x = float(np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]))
     print(f"G12 T=6 L-BFGS {mode}: J {J.tolist()} vs {Jr.tolist()} (rel {e_j:.1e}), xa rel-L2 {e_x:.1e}, "
           f"evals {res['n_eval']} (ref {int(g['n_eval'])}), iters {res['n_iter']} (ref {int(g['n_iter'])})")
-    check(f"G12 T=6 L-BFGS {mode} J per pass (max)", e_j, 1e-3)
-    check(f"G12 T=6 L-BFGS {mode} xa rel-L2", e_x, 1e-3)
+    check(f"G12 T=6 L-BFGS {mode} J per pass (max)", e_j, 2e-5)
+    check(f"G12 T=6 L-BFGS {mode} xa rel-L2", e_x, 2e-6)
     if mode == "free":
         assert res["n_iter"] == int(g["n_iter"])
 
@@ -103,9 +103,9 @@ def test_full_t6_closure_vs_oracle():
     e_x = [rel(xs[t], xr[t]) for t in range(6)]
     print(f"config-4 T=6 closure: J_o {jo:.6e} (oracle {float(rob):.6e}, rel {e_j:.2e}), grad rel {e_g:.2e}, "
           f"x_t rel {['%.1e' % v for v in e_x]}")
-    check("config-4 T=6 closure J_o", e_j, 1e-4)
-    check("config-4 T=6 closure dJ/dz", e_g, 1e-4)
-    check("config-4 T=6 closure x_t (max over t)", max(e_x), 1e-4)
+    check("config-4 T=6 closure J_o", e_j, 5e-8)
+    check("config-4 T=6 closure dJ/dz", e_g, 2e-5)
+    check("config-4 T=6 closure x_t (max over t)", max(e_x), 1e-6)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -116,7 +116,8 @@ def test_config4_trajectory_g16(mode):
     (oracle/make_golden.py --g16, da_4dvar.py:1183-1208, :1238-1299). Bounds: SURVEY c6's 1e-3 on J, or twice the
     reference's own summation-order drift on this trajectory where that is larger (g16_sensitivity.npz: the same run
     on 4 threads, free-running and replayed along G16's line searches, oracle/g10_sensitivity.py --case g16); xa
-    rel-L2 1e-2 free, 1e-3 replayed."""
+    rel-L2 2e-4 free (r06: ~5x what the HIP path achieves, profiles/r06/parity_margins.jsonl; c6: 1e-2), 2e-4
+    replayed, |xa-xb|^2 1e-3 free / 2e-3 replayed."""
     from vaevar import config as C
     from vaevar.da import one_step_da
     from vaevar.engine import DAProblem, LGUnet
@@ -149,5 +150,5 @@ def test_config4_trajectory_g16(mode):
         check("G16 replay |xa-xb|^2", e_dx, 2e-3)
     else:
         check("G16 free final J", e_pass[-1], max(1e-3, 2 * float(sens["free_rel"][-1])))
-        check("G16 free xa rel-L2", e_x, 1e-2)
-        check("G16 free |xa-xb|^2", e_dx, 1e-2)
+        check("G16 free xa rel-L2", e_x, 2e-4)
+        check("G16 free |xa-xb|^2", e_dx, 1e-3)

@@ -1,7 +1,8 @@
 """The assimilation cycle (run_assimilation da_4dvar.py:1314-1342, checkpoint/resume :683-702,
 device WRMSE/Bias :1256-1291) on the GPU against the oracle's restated cycle (oracle/da_ref.py run_cycles_ref)
 and the G9-pinned metric restatement. Tiny networks (BASELINE config-1 decoder, tiny flow as the forecast
-model) so the CPU oracle runs the same cycles in seconds. Tolerances: SURVEY §8 c6 (after L-BFGS: rel 1e-3)."""
+model) so the CPU oracle runs the same cycles in seconds. Tolerances: ~5x what the HIP path achieves (r06, profiles/r06/parity_margins.jsonl; SURVEY §8 c6 allows rel 1e-3
+after L-BFGS)."""
 import datetime as dt
 import os
 
@@ -90,9 +91,9 @@ def test_cycle_vs_oracle_and_resume(tmp_path):
         ew = float(np.abs(cyc.metrics_list["ana_wrmse"][k] - w).max() / np.abs(w).max())
         eb = float(np.abs(cyc.metrics_list["ana_bias"][k] - b).max() / np.abs(w).max())
         print(f"cycle {k}: xa increment rel {e:.1e}, ana WRMSE rel {ew:.1e}, bias rel {eb:.1e}")
-        check(f"cycle {k} xa increment", e, 1e-3)
-        check(f"cycle {k} ana WRMSE", ew, 1e-3)
-        check(f"cycle {k} ana bias", eb, 1e-3)
+        check(f"cycle {k} xa increment", e, 2e-4)
+        check(f"cycle {k} ana WRMSE", ew, 1e-6)
+        check(f"cycle {k} ana bias", eb, 1e-6)
 
     # resume: a new driver over the same directory continues from the checkpoint (get_current_states)
     cyc2 = CyclicVAE4DVar(dec, fc, obs, T0, end + dt.timedelta(hours=6), Nit=1, name="tiny", out_dir=str(tmp_path))
@@ -118,8 +119,8 @@ def test_metrics_kernel_g9(tag, Hs, Ws, seed):
     ew = float(np.abs(w.cpu().numpy() - g["wrmse_" + tag]).max() / np.abs(g["wrmse_" + tag]).max())
     eb = float(np.abs(b.cpu().numpy() - g["bias_" + tag]).max() / np.abs(g["bias_" + tag]).max())
     print(f"G9 {Hs}x{Ws}: WRMSE rel {ew:.1e}, Bias rel {eb:.1e}")
-    check(f"G9 {Hs}x{Ws} WRMSE", ew, 1e-5)
-    check(f"G9 {Hs}x{Ws} Bias", eb, 1e-5)
+    check(f"G9 {Hs}x{Ws} WRMSE", ew, 5e-7)
+    check(f"G9 {Hs}x{Ws} Bias", eb, 1e-6)
 
 
 def test_cycle_real_obs_matches_manual_composition(tmp_path):

@@ -137,7 +137,7 @@ def test_tuning_knobs_per_context():
     scale = float((A.double().abs() @ B.double().abs().t()).max())
     for c in (c1, c2):
         err = float((c.gemm(A, B).double() - ref).abs().max()) / scale
-        check("routing knobs change only the kernel", err, 2e-6)
+        check("routing knobs change only the kernel", err, 1e-6)
 
 
 @pytest.mark.parametrize("tile", [36, 44, 46, 47, 48])
@@ -347,7 +347,7 @@ def test_resample_nearest_matches_interpolate(ctx, src, dst):
     out.backward(cot.cuda())
     xr = x.clone().requires_grad_(True)
     torch.nn.functional.interpolate(xr, dst).backward(cot)
-    check(f"nearest {src}->{dst} adjoint", float((xd.grad.cpu() - xr.grad).abs().max()) / float(xr.grad.abs().max()), 1e-5, "<=")
+    check(f"nearest {src}->{dst} adjoint", float((xd.grad.cpu() - xr.grad).abs().max()) / float(xr.grad.abs().max()), 1e-12, "<=")
 
 
 

@@ -38,7 +38,7 @@ def test_obs_augment_kernel(full_dec):
     xa = obs_augment(full_dec.ctx, interp.cuda(), x.cuda()).cpu()
     ref = x_aug_ref(x, interp)
     assert xa.shape == (2, 204, 33, 47)
-    check("x_aug 13->40 vs F.linear", rel(xa, ref), 1e-6)
+    check("x_aug 13->40 vs F.linear", rel(xa, ref), 1e-12, "<=")
     check_bitwise("x_aug surface channels pass through", xa[:, :4], x[:, :4])
     # a coarser operator (n_out = 7) through the same kernel
     i7, _ = obs_interp_ref(13, 7)
@@ -73,18 +73,21 @@ def test_real_obs_closure(full_dec, T, Hs, Ws):
     e_j = abs(jo - float(rob)) / abs(float(rob))
     e_g = rel(g.cpu(), zr.grad)
     print(f"real-obs closure T={T} {Hs}x{Ws}: J_o {jo:.6e} (oracle {float(rob):.6e}, rel {e_j:.2e}), grad rel {e_g:.2e}")
-    check(f"real-obs closure T={T} {Hs}x{Ws} J_o", e_j, 1e-4)
-    check(f"real-obs closure T={T} {Hs}x{Ws} dJ/dz", e_g, 1e-4)
+    check(f"real-obs closure T={T} {Hs}x{Ws} J_o", e_j, 5e-7)
+    check(f"real-obs closure T={T} {Hs}x{Ws} dJ/dz", e_g, 5e-5)
     # the identity operator still rejects observation-space fields
     with pytest.raises(ValueError):
         DAProblem(full_dec, dict(p, interp=None), flow=flow)
 
 
-def one_step_vs_golden(prob, prob_np, g, tag):
+def one_step_vs_golden(prob, prob_np, g, tag, b):
     """The vae4dvar step against a genuine-reference golden: free-running, xa and its increment
     must match; the J printed per outer pass must match too unless the strong-Wolfe line search took another branch
     (a rounding-level difference in f or g.d can flip a Wolfe test on these ill-conditioned problems), and the
-    fixed-step replay — the reference's own recorded (t, evals) per line search — must match J and xa to 1e-3."""
+    fixed-step replay — the reference's own recorded (t, evals) per line search — must match J and xa.
+    Bounds `b` (r06): xa / |xa-xb|^2 at ~5-10x what the HIP path achieves (profiles/r06/parity_margins.jsonl); the J
+    per pass stays at 1e-3 replayed (2e-2 free where the line search may branch): the reference prints it to 4
+    significant digits, so a tighter J bound would sit under the golden's own rounding (up to 5e-4)."""
     from vaevar.da import one_step_da
 
     def run(replay=None):
@@ -101,17 +104,15 @@ def one_step_vs_golden(prob, prob_np, g, tag):
 
     eJ, e_xa, e_dx = run()
     tag = tag.split()[0]
-    check(f"{tag} free xa rel-L2", e_xa, 1e-3)
-    check(f"{tag} free |xa-xb|^2", e_dx, 1e-2)
+    check(f"{tag} free xa rel-L2", e_xa, b["free_xa"])
+    check(f"{tag} free |xa-xb|^2", e_dx, b["free_dx"])
     check(f"{tag} free J per pass (max)", eJ, 2e-2 if "ls_t" in g.files else 1e-3)
     if "ls_t" in g.files:
         steps = [(float(t), int(n)) for t, n in zip(g["ls_t"], g["ls_evals"])]
         rJ, r_xa, r_dx = run(steps)
-        # J printed to 4 digits by the reference: 1e-3; xa / |xa-xb|^2 tightened in r06 from c6's 1e-3 / 1e-2 to
-        # within ~100x of what the HIP path achieves (G6 / G8 replay xa 1.2e-8, |xa-xb|^2 8e-8: parity_margins.jsonl)
         check(f"{tag} replay J per pass (max)", rJ, 1e-3)
-        check(f"{tag} replay xa rel-L2", r_xa, 1e-6)
-        check(f"{tag} replay |xa-xb|^2", r_dx, 1e-5)
+        check(f"{tag} replay xa rel-L2", r_xa, b["replay_xa"])
+        check(f"{tag} replay |xa-xb|^2", r_dx, b["replay_dx"])
 
 
 def test_one_step_da_real_obs_g8(full_dec):
@@ -126,4 +127,6 @@ def test_one_step_da_real_obs_g8(full_dec):
     g = np.load(path)
     prob_np = make_real_problem(Hs=721, Ws=1440, T=1, seed=20250622)
     assert np.array_equal(prob_np["interp"], g["interp"])
-    one_step_vs_golden(DAProblem(full_dec, prob_np), prob_np, g, "G8 real-obs one_step_DA")
+    # r06 achieved: free xa 1.0e-4, |xa-xb|^2 2.9e-3; replay xa 1.3e-8, |xa-xb|^2 2.9e-8
+    one_step_vs_golden(DAProblem(full_dec, prob_np), prob_np, g, "G8 real-obs one_step_DA",
+                       dict(free_xa=5e-4, free_dx=1e-2, replay_xa=1e-7, replay_dx=2e-7))

@@ -41,8 +41,8 @@ def test_tiny_decoder_g1(tiny):
     tiny.backward_raw(torch.from_numpy(g["cot"]).cuda(), dz)
     e_out, e_g = rel(out.cpu(), g["out"]), rel(dz.cpu(), g["grad"])
     print(f"G1 tiny decoder: out rel {e_out:.2e}  grad rel {e_g:.2e}")
-    check("G1 out", e_out, 1e-5)
-    check("G1 grad", e_g, 1e-5)
+    check("G1 out", e_out, 5e-6)
+    check("G1 grad", e_g, 5e-6)
 
 
 def test_tiny_autograd_fn(tiny):
@@ -50,7 +50,7 @@ def test_tiny_autograd_fn(tiny):
     z = torch.from_numpy(g["z"]).cuda().requires_grad_(True)
     out = tiny(z)
     (out * torch.from_numpy(g["cot"]).cuda()).sum().backward()
-    check("G1 autograd grad", rel(z.grad.cpu(), g["grad"]), 1e-5)
+    check("G1 autograd grad", rel(z.grad.cpu(), g["grad"]), 5e-6)
 
 
 def test_batch2_matches_batch1():
@@ -63,10 +63,10 @@ def test_batch2_matches_batch1():
     z = torch.from_numpy(g["z"]).cuda()
     z2 = torch.cat([z, 0.5 * z], 0).contiguous()
     out = n2.forward_raw(z2)
-    check("B=2 image 0 vs G1", rel(out[0:1].cpu(), g["out"]), 1e-5)
+    check("B=2 image 0 vs G1", rel(out[0:1].cpu(), g["out"]), 5e-6)
     n1 = LGUnet(C.TINY, 1, 1).load_synthetic()
     o1 = n1.forward_raw((0.5 * z).contiguous())
-    check("B=2 image 1 vs B=1", rel(out[1:2].cpu(), o1.cpu()), 1e-6)
+    check("B=2 image 1 vs B=1", rel(out[1:2].cpu(), o1.cpu()), 1e-12, "<=")
 
 
 @pytest.fixture(scope="module")
@@ -93,10 +93,10 @@ def test_full_decoder_g3(full_dec):
     e_ss = abs((o * o).sum() - g["out_sumsq"]) / g["out_sumsq"]
     e_gs = abs((gr * gr).sum() - g["grad_sumsq"]) / g["grad_sumsq"]
     print(f"G3 full decoder: out rel {e_o:.2e} (sumsq {e_ss:.1e})  grad rel {e_g:.2e} (sumsq {e_gs:.1e})")
-    check("G3 out", e_o, 1e-4)
-    check("G3 grad", e_g, 1e-4)
-    check("G3 out sumsq", e_ss, 1e-4)
-    check("G3 grad sumsq", e_gs, 1e-4)
+    check("G3 out", e_o, 1e-5)
+    check("G3 grad", e_g, 1e-5)
+    check("G3 out sumsq", e_ss, 2e-8)
+    check("G3 grad sumsq", e_gs, 5e-7)
 
 
 def test_full_closure_g3(full_dec):
@@ -114,8 +114,8 @@ def test_full_closure_g3(full_dec):
     e_o = abs(jo - g["J_o"]) / g["J_o"]
     e_g = rel(gr[g["idx_grad"]], g["cgrad_sample"])
     print(f"G3 closure: J_b rel {e_b:.2e} J_o rel {e_o:.2e} grad rel {e_g:.2e}")
-    check("G3 closure J_b", e_b, 1e-5)
-    check("G3 closure J_o", e_o, 1e-4)
+    check("G3 closure J_b", e_b, 2e-7)
+    check("G3 closure J_o", e_o, 2e-7)
     check("G3 closure dJ/dz", e_g, 1e-4)
 
 
@@ -141,9 +141,9 @@ def test_full_closure_g3_exact_f32(full_dec):
     e_o = abs(jo - g["J_o"]) / g["J_o"]
     e_g = rel(gr[g["idx_grad"]], g["cgrad_sample"])
     print(f"G3 closure (exact f32 GEMM): J_b rel {e_b:.2e} J_o rel {e_o:.2e} grad rel {e_g:.2e}")
-    check("G3 closure f32 J_b", e_b, 1e-5)
-    check("G3 closure f32 J_o", e_o, 1e-4)
-    check("G3 closure f32 dJ/dz", e_g, 1e-4)
+    check("G3 closure f32 J_b", e_b, 2e-7)
+    check("G3 closure f32 J_o", e_o, 5e-7)
+    check("G3 closure f32 dJ/dz", e_g, 5e-5)
 
 
 def _tiny_problem(T):
@@ -165,8 +165,8 @@ def test_tiny_4dvar_closure_g5b():
     jb, jo = prob.closure(z, grad)
     e = (abs(jb - g["J_b"]) / g["J_b"], abs(jo - g["J_o"]) / g["J_o"], rel(grad.cpu(), g["grad"]))
     print(f"G5b tiny 4D-Var T=2: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    check("G5b J_b", e[0], 1e-5)
-    check("G5b J_o", e[1], 1e-5)
+    check("G5b J_b", e[0], 5e-7)
+    check("G5b J_o", e[1], 1e-6)
     check("G5b grad", e[2], 1e-5)
 
 
@@ -182,9 +182,9 @@ def test_tiny_lbfgs_trajectory_g5():
     J = np.array([a + b for a, b in res["J"]])
     Jr = g["J"].sum(1)
     print("G5 J per outer pass", J, "reference", Jr, "evals", res["n_eval"], g["n_eval"])
-    check("G5 final J", abs(J[-1] - Jr[-1]) / Jr[-1], 1e-3)
+    check("G5 final J", abs(J[-1] - Jr[-1]) / Jr[-1], 2e-6)
     xa = res["xa"].cpu().numpy()
-    check("G5 xa rel-L2", np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]), 1e-3)
+    check("G5 xa rel-L2", np.linalg.norm(xa - g["xa"]) / np.linalg.norm(g["xa"]), 2e-7)
 
 
 def test_lbfgs_batched_scalars_bitwise():
@@ -225,7 +225,7 @@ def test_torch_lbfgs_dropin():
         lb.step(closure)
     jb, jo = prob.closure(z.detach(), None)
     Jr = g["J"].sum(1)[-1]
-    check("torch.optim.LBFGS drop-in final J vs G5", abs(jb + jo - Jr) / Jr, 1e-3)
+    check("torch.optim.LBFGS drop-in final J vs G5", abs(jb + jo - Jr) / Jr, 5e-6)
 
 
 def test_oracle_on_box_tiny_adam():
@@ -253,7 +253,7 @@ def test_oracle_on_box_tiny_adam():
     xa = res["xa"].cpu().numpy()
     e = np.linalg.norm(xa - xa_ref) / np.linalg.norm(xa_ref)
     print(f"config 1 (Adam x20): xa rel-L2 {e:.2e}")
-    check("config 1 Adam xa rel-L2", e, 1e-4)
+    check("config 1 Adam xa rel-L2", e, 1e-7)
 
 
 @pytest.mark.parametrize("Hs,Ws,T", [(45, 90, 2), (45, 92, 2), (47, 100, 3)])
@@ -291,10 +291,10 @@ def test_interpolated_grid_4dvar(Hs, Ws, T):
         xr = ro.trajectory(z)
     e_t = max(rel(prob.trajectory()[t].cpu(), xr[t]) for t in range(T))
     print(f"interpolated grid {Hs}x{Ws} T={T}: J_o rel {e_j:.2e} grad rel {e_g:.2e} xa rel {e_x:.2e} x_t rel {e_t:.2e}")
-    check("interp J_o", e_j, 1e-5)
+    check("interp J_o", e_j, 1e-6)
     check("interp dJ/dz", e_g, 1e-5)
-    check("interp xa", e_x, 1e-6)
-    check("interp x_t", e_t, 1e-5)
+    check("interp xa", e_x, 5e-7)
+    check("interp x_t", e_t, 1e-6)
 
 
 def test_config5_grid_fused_vs_unfused():
@@ -327,9 +327,9 @@ def test_config5_grid_fused_vs_unfused():
     e_t = rel(out[1][3], out[0][3])
     print(f"config-5 grid fused vs unfused: J_o {e_j:.2e} J_b {e_b:.2e} grad {e_g:.2e} J-only J_o {out[1][2]:.6e} vs "
           f"{out[0][2]:.6e}, x_t {e_t:.2e}")
-    check("grid fused vs unfused J_o", e_j, 1e-6)
-    check("grid fused vs unfused J_b", e_b, 1e-6)
-    check("grid fused vs unfused dJ/dz", e_g, 1e-5)
+    check("grid fused vs unfused J_o", e_j, 1e-8)
+    check("grid fused vs unfused J_b", e_b, 1e-15)
+    check("grid fused vs unfused dJ/dz", e_g, 5e-6)
     check_bitwise("grid fused J-only J_o vs J+grad J_o", out[1][2], out[1][0])
     check("grid fused vs unfused x_t", e_t, 0.0, "==")
 
@@ -359,8 +359,8 @@ def test_config5_grid_closure():
     e_j = abs(jo - float(rob)) / abs(float(rob))
     e_g = rel(g.cpu(), zr.grad)
     print(f"config-5 grid closure: J_o rel {e_j:.2e} grad rel {e_g:.2e}")
-    check("config-5 grid closure J_o", e_j, 1e-4)
-    check("config-5 grid closure dJ/dz", e_g, 1e-4)
+    check("config-5 grid closure J_o", e_j, 5e-7)
+    check("config-5 grid closure dJ/dz", e_g, 2e-5)
 
 
 def test_one_step_da_config5_g6():
@@ -379,29 +379,33 @@ def test_one_step_da_config5_g6():
     dec = LGUnet(C.DECODER, 1, 1).load_synthetic()
     flow = LGUnet(C.FLOW, 1, 1).load_synthetic()
     prob_np = make_problem(nch=69, Hs=721, Ws=1440, T=2, seed=20250620)
-    one_step_vs_golden(DAProblem(dec, prob_np, flow=flow), prob_np, g, "G6 config 5 one_step_DA")
+    # r06 achieved: free xa 3.3e-8, |xa-xb|^2 7.3e-7; replay xa 1.3e-8, |xa-xb|^2 8.8e-8
+    one_step_vs_golden(DAProblem(dec, prob_np, flow=flow), prob_np, g, "G6 config 5 one_step_DA",
+                       dict(free_xa=2e-7, free_dx=5e-6, replay_xa=1e-7, replay_dx=5e-7))
 
-def traj_checks(tag, mode, e_pass, e_x, e_dx, sens, free_default=None, replay_xa=2e-4, replay_dx=2e-3):
+def traj_checks(tag, mode, e_pass, e_x, e_dx, sens, free_default=None, replay_xa=1e-4, replay_dx=2e-3, free_xa=1e-3,
+                j_floor=1e-3):
     """The bounds of a full-budget trajectory test (SURVEY §8 c6 with the reference's own summation-order drift,
-    oracle/g10_sensitivity.py): replay — J per pass at max(1e-3, 2x the reference's replay drift); xa rel-L2 and
-    |xa-xb|^2 at replay_xa / replay_dx (r06: tightened from c6's 1e-3 / 1e-2 to within ~10x of what the HIP path
-    achieves, profiles/r06/parity_margins.jsonl: G10 / G13 / G16 replay xa 2.0e-5 / 2.7e-5 / 2.7e-5); free-running —
-    the final J at max(1e-3, 2x its free-running drift) and xa at 1e-2 (a free run may take another line-search
-    branch, where xa still agrees to ~1e-4: DESIGN §2; the per-pass J is recorded, not bounded). Every achieved error
-    is recorded next to its bound (tests/conftest.py check / note)."""
+    oracle/g10_sensitivity.py): replay — J per pass at max(j_floor, 2x the reference's replay drift); xa rel-L2 and
+    |xa-xb|^2 at replay_xa / replay_dx; free-running — the final J at max(j_floor, 2x its free-running drift) and xa at
+    free_xa (a free run may take another line-search branch; the per-pass J is recorded, not bounded). r06: the xa
+    and |xa-xb|^2 bounds sit at ~5-10x what the HIP path achieves (profiles/r06/parity_margins.jsonl; c6 allowed
+    1e-3 / 1e-2); j_floor is c6's 1e-3 where the reference prints J to 4 digits (its own rounding reaches 5e-4), lower
+    where the golden holds J at full precision. Every achieved error is recorded next to its bound (tests/conftest.py
+    check / note)."""
     for i, v in enumerate(e_pass):
         note(f"{tag} {mode} J rel, pass {i}", v)
     if mode == "replay":
         drift = float(sens["replay_rel"].max()) if sens is not None else 0.0
-        bound = max(1e-3, 2 * drift)
+        bound = max(j_floor, 2 * drift)
         print(f"{tag} replay J bound {bound:.1e} (reference vs itself under another summation order: {drift:.1e})")
         check(f"{tag} replay J per pass (max)", e_pass.max(), bound)
         check(f"{tag} replay xa rel-L2", e_x, replay_xa)
         check(f"{tag} replay |xa-xb|^2", e_dx, replay_dx)
     else:
-        bound = max(1e-3, 2 * float(sens["free_rel"][-1])) if sens is not None else free_default
+        bound = max(j_floor, 2 * float(sens["free_rel"][-1])) if sens is not None else free_default
         check(f"{tag} free final J", e_pass[-1], bound)
-        check(f"{tag} free xa rel-L2", e_x, 1e-2)
+        check(f"{tag} free xa rel-L2", e_x, free_xa)
         note(f"{tag} free |xa-xb|^2", e_dx)
 
 
@@ -411,8 +415,9 @@ def test_config5_trajectory_g15(full_dec, mode):
     reference method cyclic_4dvar.one_step_DA run on CPU (oracle/make_golden.py --g15, da_4dvar.py:1179-1306; the flow
     stand-in in the loss through integrate, :1191-1193). The reference prints J per pass to 4 significant digits.
     Bounds: free-running final J at twice the reference's own summation-order drift on this trajectory
-    (oracle/g10_sensitivity.py --case g15 -> g15_sensitivity.npz, else 2e-2 as G6) and xa at 1e-2; the fixed-step
-    replay of the reference's recorded line searches at max(1e-3, 2x its replay drift) per pass, xa at 1e-3."""
+    (oracle/g10_sensitivity.py --case g15 -> g15_sensitivity.npz, else 2e-2 as G6) and xa at 5e-7; the fixed-step
+    replay of the reference's recorded line searches at max(1e-3, 2x its replay drift) per pass, xa at 2e-7 (r06: xa
+    bounds at ~5x what the HIP path achieves; c6 allowed 1e-2 / 1e-3)."""
     path = os.path.join(GOLD, "g15_config5_trajectory.npz")
     if not os.path.exists(path):
         pytest.skip("G15 fixture not generated (oracle/make_golden.py --g15)")
@@ -439,7 +444,9 @@ def test_config5_trajectory_g15(full_dec, mode):
     print(f"G15 config 5 ({mode}): J per pass rel {['%.1e' % v for v in e_pass]}; xa rel-L2 {e_x:.1e}; "
           f"|xa-xb|^2 rel {e_dx:.1e}; iters {res['n_iter']}, evals {res['n_eval']} (reference line searches "
           f"{len(g['ls_t'])}, evals {int(g['ls_evals'].sum()) + 0})")
-    traj_checks("G15", mode, e_pass, e_x, e_dx, sens, free_default=2e-2, replay_xa=1e-6, replay_dx=1e-5)
+    # r06 achieved: replay J 7.4e-5 (the reference's own replay drift 7.4e-5), xa 3.3e-8, |xa-xb|^2 5.3e-8; free final
+    # J 6.0e-5, xa 8.6e-8
+    traj_checks("G15", mode, e_pass, e_x, e_dx, sens, free_default=2e-2, replay_xa=2e-7, replay_dx=5e-7, free_xa=5e-7)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -471,7 +478,9 @@ def test_config2_trajectory_g10(full_dec, mode):
     print(f"G10 config 2 ({mode}): J per pass rel {['%.1e' % v for v in e_pass]}; xa rel-L2 {e_x:.1e}; "
           f"|xa-xb|^2 rel {e_dx:.1e}; iters {res['n_iter']} (ref {int(g['n_iter'])}), evals {res['n_eval']} "
           f"(ref {int(g['n_eval'])})")
-    traj_checks("G10", mode, e_pass, e_x, e_dx, gold("g10_sensitivity.npz"))
+    # r06 achieved: replay J 1.0e-2 (bound 2x the reference's drift 7.8e-3), xa 2.4e-5, |xa-xb|^2 3.1e-6; free final J
+    # 5.3e-3 (bound 1.8e-2), xa 1.3e-4
+    traj_checks("G10", mode, e_pass, e_x, e_dx, gold("g10_sensitivity.npz"), replay_dx=2e-5)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -483,7 +492,8 @@ def test_config3_trajectory_g13(full_dec, mode):
     Bounds as G10's, from the reference's own summation-order sensitivity on this trajectory
     (oracle/g10_sensitivity.py --case g13 -> tests/golden/g13_sensitivity.npz) when that fixture exists, else G10's
     (the same ill-conditioned R): J per pass at twice the reference's replay drift (>= 1e-3) in replay, the final J at
-    twice its free-running drift; xa at SURVEY §8 c6's 1e-3 (replay) / 1e-2 (free)."""
+    twice its free-running drift; xa at 1e-4 (replay) / 1e-3 (free), ~5x what the HIP path achieves (r06; SURVEY §8
+    c6 allowed 1e-3 / 1e-2)."""
     from vaevar import config as C
     from vaevar.da import one_step_da
     from vaevar.engine import DAProblem, LGUnet
@@ -508,7 +518,9 @@ def test_config3_trajectory_g13(full_dec, mode):
           f"(ref {int(g['n_eval'])})")
     sp = os.path.join(GOLD, "g13_sensitivity.npz")
     sens = np.load(sp) if os.path.exists(sp) else gold("g10_sensitivity.npz")
-    traj_checks("G13", mode, e_pass, e_x, e_dx, sens)
+    # r06 achieved: replay J 5.0e-4 (bound 1.4e-3), xa 2.0e-5, |xa-xb|^2 8.8e-5; free final J 6.7e-3 (bound 1.5e-2),
+    # xa 1.7e-4
+    traj_checks("G13", mode, e_pass, e_x, e_dx, sens, replay_dx=5e-4)
 
 
 def test_closure_graph_replay_bitwise():
@@ -581,14 +593,14 @@ def test_closure_edge_cases(tiny):
     jb, jo = DAProblem(tiny, empty, flow=flow).closure(z, g)
     check("no observations: J_o", jo, 0.0, "==")
     check_bitwise("no observations: dJ/dz vs z", g, z)
-    check("no observations: J_b vs sum(z^2)/2", abs(jb - 0.5 * float((z.double() ** 2).sum())) / jb, 1e-12, "<=")
+    check("no observations: J_b vs sum(z^2)/2", abs(jb - 0.5 * float((z.double() ** 2).sum())) / jb, 1e-15, "<=")
     g1, g2 = torch.empty_like(z), torch.empty_like(z)
     _, jo1 = DAProblem(tiny, p, flow=flow, obs_coeff=1.0).closure(z, g1)
     _, jo2 = DAProblem(tiny, p, flow=flow, obs_coeff=2.0).closure(z, g2)
     check_bitwise("obs_coeff: J_o returned without the coefficient", jo1, jo2)
     e = rel((g2 - z).cpu(), (2 * (g1 - z)).cpu())
     print(f"obs_coeff linearity: grad rel {e:.1e}")
-    check("obs_coeff linearity of the observation gradient", e, 1e-6)
+    check("obs_coeff linearity of the observation gradient", e, 5e-8)
 
 
 def test_ln_planes_bitwise(full_dec):
@@ -920,6 +932,6 @@ def test_h5_split_fixup_ln(full_dec):
     check_bitwise("h5_split run 1 vs 2 dJ/dz", g1, g2)
     check_bitwise("h5_split run 1 vs 2 J", (jb1, jo1), (jb2, jo2))
     check("h5_split vs tile-48 split out", rel(o1.cpu(), o0.cpu()), 1e-5)
-    check("h5_split vs tile-48 split input grad", rel(d1.cpu(), d0.cpu()), 1e-4)
-    check("h5_split vs tile-48 split dJ/dz", rel(g1.cpu(), g0.cpu()), 1e-4)
-    check("h5_split vs tile-48 split closure J", abs(jb1 + jo1 - jb0 - jo0) / abs(jb0 + jo0), 1e-6, "<=")
+    check("h5_split vs tile-48 split input grad", rel(d1.cpu(), d0.cpu()), 1e-5)
+    check("h5_split vs tile-48 split dJ/dz", rel(g1.cpu(), g0.cpu()), 2e-5)
+    check("h5_split vs tile-48 split closure J", abs(jb1 + jo1 - jb0 - jo0) / abs(jb0 + jo0), 5e-7, "<=")

@@ -65,8 +65,8 @@ def test_sc4dvar_transform(grid):
     ulp = torch.from_numpy(np.spacing(np.abs(xr.numpy()).astype(np.float32)).astype(np.float64))
     e = float(((inc - inc_r).abs() - ulp).clamp_min(0).max() / inc_r.abs().max())
     print(f"sc4dvar transform {grid}: state rel {e_state:.2e}, increment rel (beyond 1 ulp) {e:.2e}")
-    check(f"sc4dvar transform {grid} state", e_state, 1e-6)
-    check(f"sc4dvar transform {grid} increment beyond 1 ulp", e, 1e-4)
+    check(f"sc4dvar transform {grid} state", e_state, 2e-7)
+    check(f"sc4dvar transform {grid} increment beyond 1 ulp", e, 2e-6)
 
 
 @pytest.mark.parametrize("case", ["t1", "t1_interp", "real"])
@@ -81,12 +81,12 @@ def test_sc4dvar_closure(case):
     (rb + ro).backward()
     e = (abs(jb - float(rb)) / float(rb), abs(jo - float(ro)) / float(ro), rel(g.cpu(), wr.grad))
     print(f"sc4dvar closure {case}: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    check(f"sc4dvar closure {case} J_b", e[0], 1e-5)
-    check(f"sc4dvar closure {case} J_o", e[1], 1e-5)
-    check(f"sc4dvar closure {case} dJ/dw", e[2], 1e-4)
+    check(f"sc4dvar closure {case} J_b", e[0], 1e-12, "<=")
+    check(f"sc4dvar closure {case} J_o", e[1], 2e-6)
+    check(f"sc4dvar closure {case} dJ/dw", e[2], 5e-5)
     # the observation part of the gradient alone (w subtracted) carries the transform adjoint
     e2 = rel(g.cpu().double() - w.double(), wr.grad - wr.detach())
-    check(f"sc4dvar closure {case} observation part of dJ/dw", e2, 1e-4)
+    check(f"sc4dvar closure {case} observation part of dJ/dw", e2, 5e-5)
 
 
 def test_sc4dvar_closure_t2_detached_flow():
@@ -105,9 +105,9 @@ def test_sc4dvar_closure_t2_detached_flow():
     (rb + ro).backward()
     e = (abs(jb - float(rb)) / float(rb), abs(jo - float(ro)) / float(ro), rel(g.cpu(), wr.grad))
     print(f"sc4dvar closure T=2: J_b {e[0]:.2e} J_o {e[1]:.2e} grad {e[2]:.2e}")
-    check("sc4dvar closure T=2 J_b", e[0], 1e-5)
-    check("sc4dvar closure T=2 J_o", e[1], 1e-4)
-    check("sc4dvar closure T=2 dJ/dw", e[2], 1e-4)
+    check("sc4dvar closure T=2 J_b", e[0], 1e-12, "<=")
+    check("sc4dvar closure T=2 J_o", e[1], 2e-7)
+    check("sc4dvar closure T=2 dJ/dw", e[2], 2e-5)
 
 
 class _Recorder:
@@ -166,10 +166,10 @@ def test_one_step_sc4dvar_lbfgs(mode):
     e_x = float((inc - inc_r).norm() / inc_r.norm())  # rel-L2: the fp32 state's ulp averages out
     print(f"sc4dvar Nit=1 {mode}: J {g0:.6e} -> {g1:.6e} (oracle {j0:.6e} -> {j1:.6e}), evals {res['n_eval']} "
           f"(oracle line searches {rec.steps}), increment rel-L2 {e_x:.2e}")
-    check(f"sc4dvar Nit=1 {mode} J at w = 0", abs(g0 - j0) / j0, 1e-5)
+    check(f"sc4dvar Nit=1 {mode} J at w = 0", abs(g0 - j0) / j0, 1e-8)
     assert g1 < g0
     if mode == "replay":
-        check("sc4dvar Nit=1 replay J after the pass", abs(g1 - j1) / j1, 1e-3)
+        check("sc4dvar Nit=1 replay J after the pass", abs(g1 - j1) / j1, 2e-7)
         check("sc4dvar Nit=1 replay increment rel-L2", e_x, 1e-2)
 
 
@@ -200,8 +200,8 @@ def test_sc4dvar_transform_g14(g14, wk):
     e_x = rel(x[idx], g[f"f32_{wk}_x"])
     print(f"G14 transform {wk}: increment vs float64 reference rel {e_inc:.2e} (beyond 1 ulp), state vs float32 "
           f"reference rel {e_x:.2e}")
-    check(f"G14 transform {wk} increment beyond 1 ulp", e_inc, 1e-4)
-    check(f"G14 transform {wk} state vs float32 run", e_x, 1e-6)
+    check(f"G14 transform {wk} increment beyond 1 ulp", e_inc, 1e-6)
+    check(f"G14 transform {wk} state vs float32 run", e_x, 2e-8)
 
 
 def test_sc4dvar_closure_g14(g14):
@@ -218,10 +218,10 @@ def test_sc4dvar_closure_g14(g14):
     e_s = abs(float((gs * gs).sum()) - float(g["f64_grad_sumsq"])) / float(g["f64_grad_sumsq"])
     print(f"G14 closure: J vs float64 reference {e_j64:.2e}, vs float32 reference {e_j32:.2e}; dJ/dw rel {e_g:.2e}, "
           f"|dJ/dw|^2 rel {e_s:.2e}")
-    check("G14 closure J vs float64 run", e_j64, 1e-5)
-    check("G14 closure J vs float32 run", e_j32, 1e-5)
-    check("G14 closure dJ/dw", e_g, 1e-4)
-    check("G14 closure |dJ/dw|^2", e_s, 1e-4)
+    check("G14 closure J vs float64 run", e_j64, 1e-7)
+    check("G14 closure J vs float32 run", e_j32, 1e-12, "<=")
+    check("G14 closure dJ/dw", e_g, 5e-5)
+    check("G14 closure |dJ/dw|^2", e_s, 2e-6)
 
 
 @pytest.mark.parametrize("mode", ["free", "replay"])
@@ -229,8 +229,9 @@ def test_one_step_sc4dvar_g14(g14, mode):
     """The genuine one_step_DA(..., 'sc4dvar') (Nit = 2 passes of LBFGS(history 10, max_iter 5, strong Wolfe),
     da_4dvar.py:1116-1177; J 1.70e7 -> 7.40e6 in 13 evaluations) against the product mirror over the HIP closure:
     the final J and the analysis increment xhat - xb; replay along the reference's recorded line-search steps at
-    SURVEY c6's 1e-3 (J) / 1e-2 (increment rel-L2, the fp32 state's ulp averages out); free-running at 1e-2 / 5e-2
-    (the strong-Wolfe branches on rounding-level differences, as in test_one_step_sc4dvar_lbfgs)."""
+    SURVEY c6's 1e-3 (J) / 1e-2 (increment rel-L2, the fp32 state's ulp averages out); free-running at 5e-3 / 1e-2
+    (r06: ~5-10x what the HIP path achieves; the strong-Wolfe branches on rounding-level differences, as in
+    test_one_step_sc4dvar_lbfgs)."""
     from vaevar.sc4dvar import one_step_sc4dvar
 
     g, p, ws, prob = g14
@@ -245,10 +246,10 @@ def test_one_step_sc4dvar_g14(g14, mode):
     j0 = sum(res["J"][0])
     print(f"G14 one_step sc4dvar ({mode}): J {j0:.6e} -> {jf:.6e} (reference {float(g['lbfgs_J'][0]):.6e} -> {jr:.6e}), "
           f"J rel {e_j:.2e}, increment rel-L2 {e_x:.2e}, evals {res['n_eval']} (reference {len(g['lbfgs_J'])})")
-    check(f"G14 Nit=2 {mode} J at w = 0", abs(j0 - float(g["lbfgs_J"][0])) / float(g["lbfgs_J"][0]), 1e-5)
+    check(f"G14 Nit=2 {mode} J at w = 0", abs(j0 - float(g["lbfgs_J"][0])) / float(g["lbfgs_J"][0]), 5e-8)
     if mode == "replay":
         check("G14 Nit=2 replay J", e_j, 1e-3)
         check("G14 Nit=2 replay increment rel-L2", e_x, 1e-2)
     else:
-        check("G14 Nit=2 free J", e_j, 1e-2)
-        check("G14 Nit=2 free increment rel-L2", e_x, 5e-2)
+        check("G14 Nit=2 free J", e_j, 5e-3)
+        check("G14 Nit=2 free increment rel-L2", e_x, 1e-2)
