@@ -113,7 +113,7 @@ def test_tuning_knobs_per_context():
     for k in Context.TUNING_KEYS:
         v = c1.get_tuning(k)
         alt = {"mlp_hc": 32 if v != 32 else 64, "gattn_qf": 3 - v,
-               "fuse_mlp": (v + 1) % 4, "fuse_attn": (v + 1) % 4}.get(k, v + 1 if v > 1 or "mink" in k else 1 - v)
+               "fuse_mlp": (v + 1) % 4, "fuse_attn": (v + 1) % 4, "bs_tile": 24 if v != 24 else 27}.get(k, v + 1 if v > 1 or "mink" in k else 1 - v)
         c1.set_tuning(k, alt)
         assert c1.get_tuning(k) == alt
         assert c2.get_tuning(k) == v
@@ -121,7 +121,8 @@ def test_tuning_knobs_per_context():
     with pytest.raises(VVError):
         c1.set_tuning("no_such_knob", 1)
     # values the dispatch does not accept are refused at vv_set_tuning, not inside a later closure
-    for k, bad in (("mlp_hc", 48), ("fuse_attn", 12), ("grid_fused", 3), ("gattn_qf", 0), ("tail_minkt", 0), ("host_wait", 2)):
+    for k, bad in (("mlp_hc", 48), ("fuse_attn", 12), ("grid_fused", 3), ("gattn_qf", 0), ("tail_minkt", 0), ("host_wait", 2),
+                   ("bs_tile", 0)):
         with pytest.raises(VVError):
             c1.set_tuning(k, bad)
         assert c1.get_tuning(k) != bad

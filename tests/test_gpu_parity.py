@@ -748,14 +748,15 @@ def test_patch_pers_flow_bitwise(B):
 
 
 @pytest.mark.parametrize("knob,ref,on", [("h4_gather", 0, 1), ("fixup_ln_rows", 0, 1), ("fixup_stage", 0, 1),
-                                         ("patch_pers", 0, 1)])
+                                         ("patch_pers", 0, 1), ("bs_tile", 24, 27)])
 def test_bitwise_knobs(full_dec, knob, ref, on):
     """h4_gather: tile 48 reads a gathered A's producer row scales through the row map itself
     instead of a k_gather_scales pass (the counter shows the pass is gone). fixup_ln_rows: the fused fixup + LN1
     after fc2 walks GEMM rows through the inverse window map (each row's arithmetic unchanged). fixup_stage: the fused
     fixup + LayerNorm sums its workgroup's split-K partials through LDS (same chunk-order sum per element).
     patch_pers: the persistent PatchEmbed / ConvTranspose2d kernels (k_p2t_mp / k_t2p_mp) run each output's MFMA
-    sequence in the r05 kernels' k order. The same
+    sequence in the r05 kernels' k order. bs_tile: the short-K bf16x6 GEMMs on one LDS buffer (27) instead of two (24),
+    the same k loop per element. The same
     per-element arithmetic either way, so the config-2 decoder output, its input gradient and the closure are
     bit-identical."""
     from vaevar.engine import DAProblem

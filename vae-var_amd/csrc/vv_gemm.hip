@@ -2378,6 +2378,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h5_split") return &t.h5_split;
   if (k == "host_wait") return &t.host_wait;
   if (k == "patch_pers") return &t.patch_pers;
+  if (k == "bs_tile") return &t.bs_tile;
   return nullptr;
 }
 bool tuning_value_ok(const char* key, int v) {
@@ -2389,10 +2390,11 @@ bool tuning_value_ok(const char* key, int v) {
   if (k == "grid_fused") return v >= 0 && v <= 2;
   if (k == "fuse_mlp") return v >= 0 && v <= 3;
   if (k == "fuse_attn") return v >= 0 && v <= 3;
+  if (k == "bs_tile") return v >= 24 && v <= 27;
   return v == 0 || v == 1;  // every other knob is a switch
 }
 
-bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || t == 24 || t == 25 || t == 26 || t == 34 || h3_tile(t); }
+bool valid_tile(int t) { return t == 0 || t == 2 || t == 4 || (t >= 24 && t <= 27) || t == 34 || h3_tile(t); }
 
 static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
   switch (t) {
@@ -2402,6 +2404,7 @@ static hipError_t launch_variant(int t, const GemmArgs& a, hipStream_t s) {
     case 24: return launch_bs<64, 64, 2, 2>(a, s);
     case 25: return launch_bs<128, 64, 2, 2>(a, s);      // bf16x6, 128 x 64 (r05 short-K experiments)
     case 26: return launch_bs<64, 64, 2, 2, 3>(a, s);    // bf16x6, 64 x 64, loads two k-tiles ahead
+    case 27: return launch_bs<64, 64, 2, 2, 1>(a, s);    // bf16x6, 64 x 64, one LDS buffer (24 KB: more workgroups per CU)
     case 34: return launch_bs2(a, s);
     case 36: return launch_h3<128>(a, s);
     case 44: return launch_h3<256>(a, s);
@@ -2552,10 +2555,11 @@ static int pick_tile(const GemmArgs& a) {
       return h3_mf16 && a.K < 3456 ? 47 : 44;
     if (a.math == GEMM_SPLIT16 && a.K >= h3_mink && tiles_of(a, 128, 128) >= 128) return 36;
     // pipelined 128x128 (64x64 per wave, one barrier per k-tile) for the deep-K GEMMs that fill the chip with
-    // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline)
+    // 128x128 tiles (LG stage, K >= 1152); 64x64 tiles otherwise (few tiles, or K too short to pipeline: Tuning.bs_tile,
+    // one LDS buffer since r06)
     const long t128 = tiles_of(a, 128, 128);
     if (a.K >= 768 && (t128 >= 256 || (t128 >= 128 && a.K <= 1536))) return 34;
-    return 24;
+    return T.bs_tile;
   }
   // f32 MFMA: high-occupancy 64x64 tiles beat larger tiles on every decoder shape at M = 2048 / 8192;
   // 32x64 when 64x64 leaves CUs idle

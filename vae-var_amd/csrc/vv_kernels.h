@@ -59,6 +59,10 @@ struct Tuning {
   int host_wait = 1;            // the host's wait in vv_reduce_batch (vv_engine.hip host_sync): 0 hipStreamSynchronize
                                 // (a busy CPU), 1 sleep + hipStreamQuery polls (r06: main thread 1.00 -> 0.04 CPU at
                                 // equal throughput, 51.91 / 51.89 vs 51.91 / 52.01 it/s, profiles/r06/host_wait_ab)
+  int bs_tile = 27;             // the bf16x6 tile of the short-K tower GEMMs: 27 = 64x64 with one LDS buffer (24 KB: four
+                                // workgroups per CU; r06: closure 16.816 / 16.856 -> 16.780 / 16.800 ms, bf16x6 class
+                                // 1.206 -> 1.186 ms / eval, bit-identical, profiles/r06/knob_ab_bs_tile.jsonl); 24 the
+                                // two-buffer form (r05), 25 128x64, 26 loads two k-tiles ahead (both slower)
   int patch_pers = 1;           // the decoder PatchEmbed / ConvTranspose2d kernels in their persistent form (one workgroup
                                 // of 8 waves per CU share, weights staged once, each wave prefetching its next 16-token
                                 // tile behind the current one's MFMAs; 0: one 64-token workgroup per tile, bit-identical;
