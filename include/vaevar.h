@@ -264,7 +264,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    hipStreamQuery), "patch_pers" (the decoder PatchEmbed / ConvTranspose2d kernels in their persistent form, one
    workgroup of 8 waves per CU share with the weights staged once, bit-identical to 0 = one workgroup per 64-token
    tile, 1), "bs_tile" (the bf16x6 tile of the short-K tower GEMMs: 27 = 64x64 with one LDS buffer, 27; 24 = two buffers, 25 =
-   128x64, 26 = two k-tiles ahead: 24..27, bit-identical). Results stay fp32-level for every value; a change drops the
+   128x64, 26 = two k-tiles ahead: 24..27, bit-identical), "fixup_ln_cross" (the fused fixup + LN1 also between
+   consecutive LG stages, 1). Results stay fp32-level for every value; a change drops the
    context's captured closure graphs. Unknown key, or a value the dispatch does not accept (switches 0 / 1; "mlp_hc"
    0, 2, 32, 64; "gattn_qf" 1, 2; "grid_fused" 0..2; "fuse_mlp" and "fuse_attn" 0..3; the k-tile floors >= 1; the
    minimum K >= 0): VV_E_ARG, and the knob keeps its value. */

@@ -669,7 +669,7 @@ def test_ln_row_scales_bitwise(tmp_path):
 
 
 @pytest.mark.parametrize("knob,on", [("fuse_mlp", 1), ("fuse_mlp", 3), ("fuse_attn", 1), ("fuse_attn", 3),
-                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2)])
+                                     ("attn_mfma", 1), ("mlp_hc", 64), ("mlp_hc", 2), ("fixup_ln_cross", 1)])
 def test_fused_tower_vs_unfused(full_dec, knob, on):
     """The fused Swin-tower sub-blocks (vv_tower.hip) against the unfused launches on the config-2 decoder, one knob
     at a time: fuse_mlp (LN2 + fc1 + GELU + fc2 + residual, and its input gradient; 1 at dim 96, 3 also at dim 192) and
@@ -677,7 +677,9 @@ def test_fused_tower_vs_unfused(full_dec, knob, on):
     attn_mfma (the window attention of the LG stage, hd 192, and of the unfused tower stages, hd 32, forward and
     backward on the exact-f32 MFMA instead of the VALU kernels: fp32 products either way, only the summation order
     differs); mlp_hc 64 (the dim-192 fused MLP in 64-unit hidden chunks, or 2: its hidden layer split over two waves per
-    16 tokens -- the hidden operand's per-(token, chunk) scales and the order of the chunk sums change). The dim-96 tower
+    16 tokens -- the hidden operand's per-(token, chunk) scales and the order of the chunk sums change);
+    fixup_ln_cross (the last fc2 of an LG stage on tile 49's split-K with its fixup fused into the next stage's first
+    LN1, instead of tile 48's split + fixup + LayerNorm: another split of K, so rounding-level). The dim-96 tower
     blocks change arithmetic (fp16x3 with per-chunk / per-head scales instead of bf16x6), so forward output and input
     gradient agree to rounding (rel <= 2e-6 of max), the closure J to 1e-7 and dJ/dz to 1e-5 (the G3 closure-gradient
     bound is 1e-4)."""

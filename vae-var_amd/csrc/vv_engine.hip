@@ -783,38 +783,49 @@ hipError_t proj_ln2(const Stage& S, int b, const StageSave& sv, const Scratch& s
   return vv::gemm_ln(p, l, st, sc.ws);
 }
 
-// the LG-stage fc2 GEMM (RESID) of block b with its split-K fixup fused into block b + 1's LN1 (window gather:
-// LN row j reads GEMM row idx[j]) when that LayerNorm only has to write qkv's tile-48 planes
+// the LG-stage fc2 GEMM (RESID) of block b with its split-K fixup fused into the next block's LN1 (window gather:
+// LN row j reads GEMM row idx[j]) when that LayerNorm only has to write qkv's tile-48 planes. The next block is
+// block b + 1, or for the last block block 0 of the next LG stage NS (r06: same rows and width, its input buffer
+// is this stage's output, plan_stage_save), whose stage_fwd then skips that LN1
 hipError_t fc2_ln1(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, const GemmArgs& f2,
-                   hipStream_t st) {
+                   hipStream_t st, const Stage* NS = nullptr, const StageSave* nsv = nullptr) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  if (!T.fixup_ln || S.G != 1 || b + 1 >= S.depth) return hipErrorNotSupported;
-  const int nb = b + 1, shift = (nb % 2 == 0) ? 0 : ws / 2;
+  const bool cross = b + 1 >= S.depth;
+  if (cross && (!NS || !nsv || NS->G != 1 || NS->M != S.M || NS->C != S.C || NS->depth < 1 || nsv->x[0] != sv.x[b + 1]))
+    return hipErrorNotSupported;
+  const Stage& TS = cross ? *NS : S;        // the stage of the next block
+  const StageSave& tsv = cross ? *nsv : sv;
+  if (!T.fixup_ln || S.G != 1) return hipErrorNotSupported;
+  const int nb = cross ? 0 : b + 1, shift = (nb % 2 == 0) ? 0 : ws / 2;
   vv::AblkArgs aa;
-  if (ablk_args(S, nb, sv, sc, ws, shift, S.idx[shift ? 1 : 0], aa)) return hipErrorNotSupported;
-  GemmArgs q = gemm_base(S.M, 3 * S.C, S.C, 1, EPI_STORE, sc);
+  if (ablk_args(TS, nb, tsv, sc, ws, shift, TS.idx[shift ? 1 : 0], aa)) return hipErrorNotSupported;
+  GemmArgs q = gemm_base(TS.M, 3 * TS.C, TS.C, 1, EPI_STORE, sc);
   q.ascale = sc.rs;
-  q.g[0] = {sc.t1, nullptr, S.w[nb][0].qkvW, S.w[nb][0].qkvb, sv.qkv[nb], nullptr, nullptr};
+  q.g[0] = {sc.t1, nullptr, TS.w[nb][0].qkvW, TS.w[nb][0].qkvb, tsv.qkv[nb], nullptr, nullptr};
   if (!ln_feeds_planes(q, sc)) return hipErrorNotSupported;
   vv::GemmLnArgs l;
   memset(&l, 0, sizeof(l));
-  l.gmap = S.idx[shift ? 1 : 0];  // LN1 -> window order
-  l.ginv = T.fixup_ln_rows ? S.idxinv[shift ? 1 : 0] : nullptr;
+  l.gmap = TS.idx[shift ? 1 : 0];  // LN1 -> window order
+  l.ginv = T.fixup_ln_rows ? TS.idxinv[shift ? 1 : 0] : nullptr;
   l.lo_x = 0;
-  l.gamma = S.w[nb][0].n1g;
-  l.beta = S.w[nb][0].n1b;
+  l.gamma = TS.w[nb][0].n1g;
+  l.beta = TS.w[nb][0].n1b;
   l.eps = 1e-5f;
   l.pl = sc.apl;
   l.rs = sc.rs;
-  l.stats = sv.st1[nb];
+  l.stats = tsv.st1[nb];
   return vv::gemm_ln(f2, l, st, sc.ws);
 }
 
-int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st) {
+// NS / nsv: the LG stage that follows (its block 0's LN1 may be fused into this stage's last fc2 fixup: *ln1_next
+// says whether it was); ln1_pre: this stage's block-0 LN1 already ran, fused into the previous stage's last fc2
+int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStream_t st, const Stage* NS = nullptr,
+              const StageSave* nsv = nullptr, bool ln1_pre = false, bool* ln1_next = nullptr) {
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
   const int nwin = M / 16;
-  bool ln1_done = false;  // block b's LN1 already ran, fused into block b - 1's fc2 fixup
+  if (ln1_next) *ln1_next = false;
+  bool ln1_done = ln1_pre;  // block b's LN1 already ran, fused into the fc2 fixup before it
   for (int b = 0; b < S.depth; ++b) {
     const int shift = (b % 2 == 0) ? 0 : ws / 2;
     const int* idx = S.idx[shift ? 1 : 0];
@@ -903,9 +914,11 @@ int stage_fwd(const Stage& S, StageSave& sv, const Scratch& sc, int ws, hipStrea
     gelu_feeds_planes(f1, f2, S.w[b][0].fc1Wmax, S.w[b][0].fc1bmax, sc);
     CK(gemm_nt(f1, st, -1, sc.ws));
     // fc2's split-K fixup fused into the next block's LN1 where that LayerNorm feeds qkv's planes
-    const hipError_t fe = fc2_ln1(S, b, sv, sc, ws, f2, st);
-    if (fe == hipSuccess)
+    const hipError_t fe = fc2_ln1(S, b, sv, sc, ws, f2, st, ln1_next ? NS : nullptr, nsv);
+    if (fe == hipSuccess) {
       ln1_done = true;
+      if (b + 1 == S.depth) *ln1_next = true;
+    }
     else if (fe == hipErrorNotSupported)
       CK(gemm_nt(f2, st, -1, sc.ws));
     else
@@ -936,8 +949,11 @@ hipError_t gemm_ln_bwd(const GemmArgs& g, const LnArgs& ln, const Scratch& sc, h
   return vv::gemm_ln(g, l, st, sc.ws);
 }
 
-// gx: [G][M][C] gradient w.r.t. the stage output, overwritten in place with the input gradient
-int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, float* gx, hipStream_t st) {
+// gx: [G][M][C] gradient w.r.t. the stage output, overwritten in place with the input gradient. Consecutive LG
+// stages (r06, Tuning.fixup_ln_cross): planes_out -- block 0's LN1 backward also writes gx's row scales and fp16x3
+// planes for the last fc2 input-gradient GEMM of the stage below; gx_planes_in -- this stage's gx arrives with them
+int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, float* gx, hipStream_t st,
+              bool gx_planes_in = false, bool planes_out = false) {
   const int G = S.G, M = S.M, C = S.C;
   const size_t MC = (size_t)M * C;
   const int nwin = M / 16;
@@ -961,8 +977,8 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       CK(vv::mlp_bwd(ma, st));  // fc2^T + GELU' + fc1^T + LN2 backward + residual, gx in place (+ its row scales)
     } else {
       GemmArgs f2 = gemm_base(M, 4 * C, C, G, EPI_DGELU, sc);
-      if (b < S.depth - 1) {
-        f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below), with its row scales
+      if (b < S.depth - 1 || gx_planes_in) {
+        f2.ascale = sc.rs;  // gx from the LN1 backward of block b + 1 (below) or of the next stage, with its row scales
         if (f2_pl) f2.apre = sc.apl;
       }
       for (int g = 0; g < G; ++g)
@@ -986,7 +1002,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
     }
     if (p_pl) p.apre = sc.apl;  // planes in physical row order: the kernel gathers them through arow
     vv::AblkArgs ab;
-    if (!(f2_pl && b > 0) && ablk_args(S, b, sv, sc, ws, shift, idx, ab, gx)) {
+    if (!(f2_pl && (b > 0 || planes_out)) && ablk_args(S, b, sv, sc, ws, shift, idx, ab, gx)) {
       CK(vv::ablk_bwd(ab, st));  // proj^T + window-attention backward + qkv^T + LN1 backward + residual, in place
       continue;
     }
@@ -1013,7 +1029,7 @@ int stage_bwd(const Stage& S, const StageSave& sv, const Scratch& sc, int ws, fl
       q.g[g] = {sc.dqkv + g * MC * 3, nullptr, S.w[b][g].qkvWT, nullptr, sc.t1 + g * MC, nullptr, nullptr};
     LnArgs ln1 = ln_base(M, C, G, 1e-5f);
     ln1.map = idx;
-    const bool l1_pl = f2_pl && b > 0;  // planes for the next block's fc2 input-gradient GEMM
+    const bool l1_pl = f2_pl && (b > 0 || planes_out);  // planes for the next fc2 input-gradient GEMM
     for (int g = 0; g < G; ++g)
       ln1.g[g] = {sv.x[b] + g * MC, S.w[b][g].n1g, nullptr, gx + g * MC, sv.st1[b] + (size_t)g * M * 2,
                   sc.t1 + g * MC, gx + g * MC, sc.rs + (size_t)g * M, l1_pl ? sc.apl + (size_t)g * M * 2 * C : nullptr};
@@ -1227,8 +1243,16 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
   CK(gemm_nt(ep, st, -1, m.sc.ws));
   // ---- LG_net layers
-  for (size_t l = 0; l < m.lg.size(); ++l)
-    if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st))) return r;
+  // consecutive LG stages: the last fc2 fixup of one runs the next stage's first LN1 (Tuning.fixup_ln_cross)
+  const bool cross = (m.sc.tune ? *m.sc.tune : vv::kDefaultTuning).fixup_ln_cross;
+  for (size_t l = 0, pre = 0; l < m.lg.size(); ++l) {
+    bool nxt = false;
+    const bool has_next = cross && l + 1 < m.lg.size();
+    if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st, has_next ? &m.lg[l + 1] : nullptr,
+                       has_next ? &sv.lg[l + 1] : nullptr, pre != 0, &nxt)))
+      return r;
+    pre = nxt;
+  }
   const float* lg_out = m.lg.empty() ? lg_in : sv.lg.back().x.back();
   // ---- Dec_net.proj (transformer.py:600)
   GemmArgs dp = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc);
@@ -1384,8 +1408,12 @@ int model_bwd(Model& m, int slot, const float* dout, float* din, const float* ad
   GemmArgs dp = gemm_base(M1, E, G * C1, 1, EPI_STORE, m.sc);
   dp.g[0] = {m.gdp, nullptr, w("dec.proj.weight^T"), nullptr, glg, nullptr, nullptr};
   CK(gemm_nt(dp, st, -1, m.sc.ws));
-  for (int l = (int)m.lg.size() - 1; l >= 0; --l)
-    if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st))) return r;
+  {
+    const bool cross = (m.sc.tune ? *m.sc.tune : vv::kDefaultTuning).fixup_ln_cross;
+    for (int l = (int)m.lg.size() - 1; l >= 0; --l)
+      if ((r = stage_bwd(m.lg[l], sv.lg[l], m.sc, c.ws, glg, st, cross && l + 1 < (int)m.lg.size(), cross && l > 0)))
+        return r;
+  }
   // pos_embed: identity ; Enc_net.proj backward
   GemmArgs ep = gemm_base(M1, G * C1, E, 1, EPI_STORE, m.sc);
   ep.g[0] = {glg, nullptr, w("enc.proj.weight^T"), nullptr, m.gcat, nullptr, nullptr};

@@ -2378,6 +2378,7 @@ int* tuning_field(Tuning& t, const char* key) {
   if (k == "h5_split") return &t.h5_split;
   if (k == "host_wait") return &t.host_wait;
   if (k == "patch_pers") return &t.patch_pers;
+  if (k == "fixup_ln_cross") return &t.fixup_ln_cross;
   if (k == "bs_tile") return &t.bs_tile;
   return nullptr;
 }

@@ -63,6 +63,8 @@ struct Tuning {
                                 // workgroups per CU; r06: closure 16.816 / 16.856 -> 16.780 / 16.800 ms, bf16x6 class
                                 // 1.206 -> 1.186 ms / eval, bit-identical, profiles/r06/knob_ab_bs_tile.jsonl); 24 the
                                 // two-buffer form (r05), 25 128x64, 26 loads two k-tiles ahead (both slower)
+  int fixup_ln_cross = 1;       // the fused fixup + LN1 also across consecutive LG stages (the last fc2 of a stage + the
+                                // next stage's first LN1; 0: tile-48 split + fixup + a separate LayerNorm there)
   int patch_pers = 1;           // the decoder PatchEmbed / ConvTranspose2d kernels in their persistent form (one workgroup
                                 // of 8 waves per CU share, weights staged once, each wave prefetching its next 16-token
                                 // tile behind the current one's MFMAs; 0: one 64-token workgroup per tile, bit-identical;

@@ -46,7 +46,7 @@ class Context:
                    "win_attn", "h4", "ln_planes", "gattn", "gattn_qf", "h4_small", "h4_split_minkt",
                    "win_mfma", "fc_h3_mink", "fuse_mlp", "fuse_attn", "attn_mfma", "gelu_planes", "attn_planes", "fixup_ln", "h5", "fc_conv_mf",
                    "mlp_hc", "h4_gather", "fixup_ln_rows", "grid_fused", "fixup_stage", "host_wait", "h5_split",
-                   "patch_pers", "bs_tile")
+                   "patch_pers", "bs_tile", "fixup_ln_cross")
 
     def __init__(self, device: int = 0):
         self.device = device
