@@ -787,16 +787,15 @@ hipError_t proj_ln2(const Stage& S, int b, const StageSave& sv, const Scratch& s
 // LN row j reads GEMM row idx[j]) when that LayerNorm only has to write qkv's tile-48 planes. The next block is
 // block b + 1, or for the last block block 0 of the next LG stage NS (r06: same rows and width, its input buffer
 // is this stage's output, plan_stage_save), whose stage_fwd then skips that LN1
-hipError_t fc2_ln1(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, const GemmArgs& f2,
-                   hipStream_t st, const Stage* NS = nullptr, const StageSave* nsv = nullptr) {
+// a RESID GEMM `f` (one group, output = block nb's input x) with its split-K fixup fused into block nb's LN1 of stage
+// TS (the LayerNorm then writes only qkv's tile-48 planes, row scales and stats); hipErrorNotSupported where that
+// does not apply
+hipError_t gemm_ln1_into(const GemmArgs& f, const Stage& TS, const StageSave& tsv, int nb, const Scratch& sc, int ws,
+                         hipStream_t st) {
   const vv::Tuning& T = sc.tune ? *sc.tune : vv::kDefaultTuning;
-  const bool cross = b + 1 >= S.depth;
-  if (cross && (!NS || !nsv || NS->G != 1 || NS->M != S.M || NS->C != S.C || NS->depth < 1 || nsv->x[0] != sv.x[b + 1]))
+  if (!T.fixup_ln || TS.G != 1 || f.ngroups != 1 || f.M != TS.M || f.N != TS.C || f.g[0].C != tsv.x[nb])
     return hipErrorNotSupported;
-  const Stage& TS = cross ? *NS : S;        // the stage of the next block
-  const StageSave& tsv = cross ? *nsv : sv;
-  if (!T.fixup_ln || S.G != 1) return hipErrorNotSupported;
-  const int nb = cross ? 0 : b + 1, shift = (nb % 2 == 0) ? 0 : ws / 2;
+  const int shift = (nb % 2 == 0) ? 0 : ws / 2;
   vv::AblkArgs aa;
   if (ablk_args(TS, nb, tsv, sc, ws, shift, TS.idx[shift ? 1 : 0], aa)) return hipErrorNotSupported;
   GemmArgs q = gemm_base(TS.M, 3 * TS.C, TS.C, 1, EPI_STORE, sc);
@@ -814,7 +813,14 @@ hipError_t fc2_ln1(const Stage& S, int b, const StageSave& sv, const Scratch& sc
   l.pl = sc.apl;
   l.rs = sc.rs;
   l.stats = tsv.st1[nb];
-  return vv::gemm_ln(f2, l, st, sc.ws);
+  return vv::gemm_ln(f, l, st, sc.ws);
+}
+
+hipError_t fc2_ln1(const Stage& S, int b, const StageSave& sv, const Scratch& sc, int ws, const GemmArgs& f2,
+                   hipStream_t st, const Stage* NS = nullptr, const StageSave* nsv = nullptr) {
+  if (b + 1 < S.depth) return gemm_ln1_into(f2, S, sv, b + 1, sc, ws, st);
+  if (!NS || !nsv || NS->depth < 1) return hipErrorNotSupported;
+  return gemm_ln1_into(f2, *NS, *nsv, 0, sc, ws, st);
 }
 
 // NS / nsv: the LG stage that follows (its block 0's LN1 may be fused into this stage's last fc2 fixup: *ln1_next
@@ -1241,11 +1247,22 @@ int model_fwd(Model& m, int slot, const float* in, float* out, int climit, hipSt
   ep.rmod = c.H1 * c.W1;
   ep.ldr = E;
   ep.g[0] = {m.cat, nullptr, w("enc.proj.weight"), w("enc.proj.bias"), lg_in, w("net.pos_embed"), nullptr};
-  CK(gemm_nt(ep, st, -1, m.sc.ws));
-  // ---- LG_net layers
-  // consecutive LG stages: the last fc2 fixup of one runs the next stage's first LN1 (Tuning.fixup_ln_cross)
+  // consecutive LG stages: the last fc2 fixup of one runs the next stage's first LN1, and Enc_net.proj's fixup the
+  // first LG stage's (Tuning.fixup_ln_cross)
   const bool cross = (m.sc.tune ? *m.sc.tune : vv::kDefaultTuning).fixup_ln_cross;
-  for (size_t l = 0, pre = 0; l < m.lg.size(); ++l) {
+  size_t pre = 0;
+  {
+    const hipError_t e = cross && !m.lg.empty() ? gemm_ln1_into(ep, m.lg[0], sv.lg[0], 0, m.sc, c.ws, st)
+                                                : hipErrorNotSupported;
+    if (e == hipSuccess)
+      pre = 1;
+    else if (e == hipErrorNotSupported)
+      CK(gemm_nt(ep, st, -1, m.sc.ws));
+    else
+      CK(e);
+  }
+  // ---- LG_net layers
+  for (size_t l = 0; l < m.lg.size(); ++l) {
     bool nxt = false;
     const bool has_next = cross && l + 1 < m.lg.size();
     if ((r = stage_fwd(m.lg[l], sv.lg[l], m.sc, c.ws, st, has_next ? &m.lg[l + 1] : nullptr,
