@@ -5,7 +5,7 @@
 #   held-clock passes (tools/pmc_mfma.py) and the kernel-outlier trace (tools/ktrace_outliers.py).
 # Usage: VV_HEAD=<commit> bash tools/round_r06.sh TAG   -> gpurun_out/TAG/...
 set -e
-TAG=${1:-r06f}
+TAG=${1:-r06q}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
