@@ -241,17 +241,17 @@ def test_reduce_batch_matches_single_calls(ctx):
 
 
 def test_gemm_rejects_non_library_tiles(ctx):
-    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24, 25, 26, 34, 36, 44, 46, 47, 48, 49): any other hint,
+    """vv_gemm accepts only the library's kernels (tile -1, 0, 2, 4, 24..27, 34, 36, 44, 46, 47, 48, 49): any other hint,
     e.g. the r01 timing experiments 37-39, returns VV_E_ARG instead of running something."""
     from vaevar._lib import VVError
 
     A = torch.rand(64, 64, device="cuda")
     B = torch.rand(64, 64, device="cuda")
-    for t in (1, 3, 21, 27, 35, 37, 38, 39, 40, 41, 42, 45, 50, 1000):
+    for t in (1, 3, 21, 28, 35, 37, 38, 39, 40, 41, 42, 45, 50, 1000):
         with pytest.raises(VVError, match="1001"):
             ctx.gemm(A, B, tile=t)
     ref = A.double().cpu() @ B.double().cpu().t()
-    for t in (0, 2, 4, 24, 25, 26, 34, 36, 44, 46, 47, 48, 49):
+    for t in (0, 2, 4, 24, 25, 26, 27, 34, 36, 44, 46, 47, 48, 49):
         C = ctx.gemm(A, B, tile=t).cpu().double()
         assert float((C - ref).abs().max()) < 1e-4
 
