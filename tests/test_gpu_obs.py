@@ -85,7 +85,8 @@ def one_step_vs_golden(prob, prob_np, g, tag, b):
     must match; the J printed per outer pass must match too unless the strong-Wolfe line search took another branch
     (a rounding-level difference in f or g.d can flip a Wolfe test on these ill-conditioned problems), and the
     fixed-step replay — the reference's own recorded (t, evals) per line search — must match J and xa.
-    Bounds `b` (r06): xa / |xa-xb|^2 at ~5-10x what the HIP path achieves (profiles/r06/parity_margins.jsonl); the J
+    Bounds `b` (r06): xa / |xa-xb|^2 at ~10-40x what the HIP path achieves (profiles/r06/parity_margins.jsonl: room for
+    the rounding-level changes a trajectory amplifies); the J
     per pass stays at 1e-3 replayed (2e-2 free where the line search may branch): the reference prints it to 4
     significant digits, so a tighter J bound would sit under the golden's own rounding (up to 5e-4)."""
     from vaevar.da import one_step_da
@@ -129,4 +130,4 @@ def test_one_step_da_real_obs_g8(full_dec):
     assert np.array_equal(prob_np["interp"], g["interp"])
     # r06 achieved: free xa 1.0e-4, |xa-xb|^2 2.9e-3; replay xa 1.3e-8, |xa-xb|^2 2.9e-8
     one_step_vs_golden(DAProblem(full_dec, prob_np), prob_np, g, "G8 real-obs one_step_DA",
-                       dict(free_xa=5e-4, free_dx=1e-2, replay_xa=1e-7, replay_dx=2e-7))
+                       dict(free_xa=2e-3, free_dx=1e-2, replay_xa=5e-7, replay_dx=1e-6))

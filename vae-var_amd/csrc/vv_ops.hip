@@ -1613,12 +1613,16 @@ __device__ __forceinline__ void pm_range(int nwt, int& r0, int& r1) {
   r1 = (int)((long long)(blockIdx.x + 1) * nwt / gridDim.x);
 }
 
-template <int MODE, int KPM>
+// CF: C = kPatchCmax (every production configuration), so the row stores need no runtime bound. Loads are branch-free
+// (clamped address, then a select) and the prefetch is unconditional (the last tile again past the range): a load or
+// store under a branch leaves the compiler unable to count vmcnt, and it then waits for every one of them (stores
+// included) before the next tile's operand rows
+template <int MODE, int KPM, bool CF>
 __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const PatchGroup& G = a.g[blockIdx.y];
+  const PatchGroup G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = CF ? kPatchCmax : a.Ctok;
   // compile-time shapes (zero-padded to KPM taps and kPatchCmax channels): MFMAs under runtime conditions made the
   // compiler keep every accumulator live across branches (thousands of VGPRs spilled)
   constexpr int KS = KPM + 4;                                     // weight row stride (floats)
@@ -1641,21 +1645,22 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
     const float* base = a.img + (size_t)b * a.Cimg * plane + (size_t)(2 * ho + pp) * a.Wimg + 2 * wo + col;
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) {
-      xv[ci] = 0.f;
-      if (ci * 4 < kc) {
-        const int ch = MODE == 0 ? G.cin_off + ci : unembed_ch(G, ci);
-        if (MODE == 0 || ch < a.climit) xv[ci] = base[(size_t)ch * plane];
-      }
+      const int ch = MODE == 0 ? G.cin_off + min(ci, kc / 4 - 1) : unembed_ch(G, min(ci, kc / 4 - 1));
+      const bool ok = ci * 4 < kc && (MODE == 0 || ch < a.climit);
+      const float v = base[(size_t)(ok ? ch : 0) * plane];
+      xv[ci] = ok ? v : 0.f;
     }
     if (MODE == 0) {
       const size_t pbase = (size_t)((wt * 16) % (Ho * Wo)) * C;
 #pragma unroll
-      for (int i = 0; i < NO; ++i)
-        pv[i] = i < C / 16 ? *reinterpret_cast<const f4*>(G.pos + pbase + 4 * (i * 64 + lane)) : f4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NO; ++i) {
+        const f4 v = *reinterpret_cast<const f4*>(G.pos + pbase + 4 * (min(i, C / 16 - 1) * 64 + lane));
+        pv[i] = i < C / 16 ? v : f4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
   int wt = r0 + wave;
-  if (wt < r1) load_tile(wt);
+  load_tile(min(wt, r1 - 1));  // (r1 > r0: the grid has at most one workgroup per 8 tiles)
   float bv[NTM];
 #pragma unroll
   for (int n = 0; n < NTM; ++n) bv[n] = MODE == 0 ? G.bias[min(n * 16 + li, C - 1)] : 0.f;
@@ -1685,7 +1690,7 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
     f4 pc[NO];
 #pragma unroll
     for (int i = 0; i < NO; ++i) pc[i] = pv[i];
-    if (wt + kPmWaves < r1) load_tile(wt + kPmWaves);  // in flight behind this tile's MFMAs
+    load_tile(min(wt + kPmWaves, r1 - 1));  // in flight behind this tile's MFMAs
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     fr4 acc[NTM];
@@ -1714,7 +1719,7 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
     float* out = G.tok + (size_t)wt * 16 * C;
 #pragma unroll
     for (int i = 0; i < NO; ++i) {
-      if (i >= C / 16) break;
+      if (!CF && i >= C / 16) break;
       const int e = 4 * (i * 64 + lane), row = e / C, cc = e - row * C;
       f4 v = *reinterpret_cast<const f4*>(R + row * RS + cc);
       if (MODE == 0) v = v + pc[i];
@@ -1725,12 +1730,13 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
   }
 }
 
-template <int MODE, int KPM>
+// CF, branch-free loads and the unconditional prefetch: as k_p2t_mp
+template <int MODE, int KPM, bool CF>
 __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const PatchGroup& G = a.g[blockIdx.y];
+  const PatchGroup G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = a.Ctok;
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = CF ? kPatchCmax : a.Ctok;
   constexpr int CS = kPatchCmax + 4;
   float* Wt = sm;  // [KPM][CS]: W[c][j] at Wt[j][c], zero-padded (compile-time MFMA shapes, as k_p2t_mp)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
@@ -1744,8 +1750,13 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
     const int tok = wt * 16 + li;
     const float* yr = (MODE == 0 ? G.dtok : G.tok) + (size_t)tok * C + 4 * g;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) y[s] = 16 * s < C ? *reinterpret_cast<const f4*>(yr + 16 * s) : f4{0.f, 0.f, 0.f, 0.f};
-    if (MODE == 0 && a.add_img) {
+    for (int s = 0; s < NS; ++s) {
+      const f4 v = *reinterpret_cast<const f4*>(yr + 16 * (CF ? s : min(s, C / 16 - 1)));
+      y[s] = CF || 16 * s < C ? v : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (MODE == 0) {
+      // the added image, or (none) the output image itself as a dummy source, selected to 0
+      const float* src = a.add_img ? a.add_img : a.img_out;
       int b, ho, wo;
       tok_coords(tok, Ho, Wo, b, ho, wo);
 #pragma unroll
@@ -1753,8 +1764,10 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
         const int o = 4 * mt + g;
         const size_t off = (((size_t)b * a.Cimg + G.cin_off + min(o, kc / 4 - 1)) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
-          ex[mt][q] = o * 4 < kc ? *reinterpret_cast<const float2*>(a.add_img + off + q * a.Wimg) : make_float2(0.f, 0.f);
+        for (int q = 0; q < 2; ++q) {
+          const float2 v = *reinterpret_cast<const float2*>(src + off + q * a.Wimg);
+          ex[mt][q] = o * 4 < kc && a.add_img ? v : make_float2(0.f, 0.f);
+        }
       }
     }
   };
@@ -1763,9 +1776,9 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
 #pragma unroll
   for (int mt = 0; mt < NMT; ++mt) {
     bz[mt] = MODE == 1 ? G.bias[min(4 * mt + g, kc / 4 - 1)] : 0.f;
-    if (MODE == 1 || !a.add_img) ex[mt][0] = ex[mt][1] = make_float2(0.f, 0.f);
+    if (MODE == 1) ex[mt][0] = ex[mt][1] = make_float2(0.f, 0.f);
   }
-  if (wt < r1) load_tile(wt);
+  load_tile(min(wt, r1 - 1));
   {
     constexpr int NW = kPatchCmax * KPM / 512, NB = NW < 16 ? NW : 16;
 #pragma unroll
@@ -1793,7 +1806,7 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt)
       if (MODE == 0) xc[mt][0] = ex[mt][0], xc[mt][1] = ex[mt][1];
-    if (wt + kPmWaves < r1) load_tile(wt + kPmWaves);  // in flight behind this tile's MFMAs
+    load_tile(min(wt + kPmWaves, r1 - 1));  // in flight behind this tile's MFMAs
     fr4 acc[NMT];
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt) acc[mt] = fr4{0.f, 0.f, 0.f, 0.f};
@@ -1852,8 +1865,13 @@ static hipError_t p2t_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   if ((a.tune ? a.tune->patch_pers : kDefaultTuning.patch_pers) > 0) {
     const size_t lds =
         ((size_t)kPatchCmax * (KPM + 4) + (size_t)kPmWaves * 16 * std::max(KPM + 4, kPatchCmax + 4)) * sizeof(float);
-    if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM>, lds)) return e;
-    hipLaunchKernelGGL((k_p2t_mp<MODE, KPM>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
+    if (a.Ctok == kPatchCmax) {
+      if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM, true>, lds)) return e;
+      hipLaunchKernelGGL((k_p2t_mp<MODE, KPM, true>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
+    } else {
+      if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM, false>, lds)) return e;
+      hipLaunchKernelGGL((k_p2t_mp<MODE, KPM, false>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
+    }
     return hipGetLastError();
   }
   const int KS = (kc + 15) / 16 * 16 + 4;
@@ -1879,8 +1897,13 @@ static hipError_t t2p_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   if ((a.tune ? a.tune->patch_pers : kDefaultTuning.patch_pers) > 0) {
     const size_t lm = (size_t)KPM * (kPatchCmax + 4) * sizeof(float);
     if (lm > 64 * 1024)
-      if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM>, lm)) return e;
-    hipLaunchKernelGGL((k_t2p_mp<MODE, KPM>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lm, s, a);
+      if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM, true>, lm)) return e;
+    if (lm > 64 * 1024)
+      if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM, false>, lm)) return e;
+    if (a.Ctok == kPatchCmax)
+      hipLaunchKernelGGL((k_t2p_mp<MODE, KPM, true>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lm, s, a);
+    else
+      hipLaunchKernelGGL((k_t2p_mp<MODE, KPM, false>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lm, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((k_t2p_mf<MODE, KPM>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
