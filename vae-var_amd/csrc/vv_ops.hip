@@ -1613,28 +1613,30 @@ __device__ __forceinline__ void pm_range(int nwt, int& r0, int& r1) {
   r1 = (int)((long long)(blockIdx.x + 1) * nwt / gridDim.x);
 }
 
-// CF: C = kPatchCmax (every production configuration), so the row stores need no runtime bound. Loads are branch-free
-// (clamped address, then a select) and the prefetch is unconditional (the last tile again past the range): a load or
-// store under a branch leaves the compiler unable to count vmcnt, and it then waits for every one of them (stores
-// included) before the next tile's operand rows
-template <int MODE, int KPM, bool CF>
+// CT: the token width at compile time (96 -- the decoder's enc_dim -- and 128 are instantiated; 0 = any width up to
+// kPatchCmax, zero-padded to it, with the row loads and stores under a runtime bound). With CT the MFMA tiles are the
+// width's own (no zero tiles) and the loads are branch-free (clamped address, then a select), the prefetch
+// unconditional (the last tile again past the range): a load or store under a branch leaves the compiler unable to
+// count vmcnt, and it then waits for every one of them, this tile's stores included, before the next tile's rows
+template <int MODE, int KPM, int CT>
 __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const PatchGroup G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = CF ? kPatchCmax : a.Ctok;
-  // compile-time shapes (zero-padded to KPM taps and kPatchCmax channels): MFMAs under runtime conditions made the
-  // compiler keep every accumulator live across branches (thousands of VGPRs spilled)
-  constexpr int KS = KPM + 4;                                     // weight row stride (floats)
-  constexpr int RS = KS > kPatchCmax + 4 ? KS : kPatchCmax + 4;   // the wave's rows: operands, then the staging
+  constexpr int CM = CT ? CT : kPatchCmax;  // channels the MFMA tiles cover
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = CT ? CT : a.Ctok;
+  // compile-time shapes (zero-padded to KPM taps and CM channels): MFMAs under runtime conditions made the compiler
+  // keep every accumulator live across branches (thousands of VGPRs spilled)
+  constexpr int KS = KPM + 4;                       // weight row stride (floats)
+  constexpr int RS = KS > CM + 4 ? KS : CM + 4;     // the wave's rows: operands, then the staging
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-  float* Wsm = sm;                                    // [kPatchCmax][KS]
-  float* R = sm + kPatchCmax * KS + wave * 16 * RS;  // [16][RS], this wave's only
+  float* Wsm = sm;                             // [CM][KS]
+  float* R = sm + CM * KS + wave * 16 * RS;   // [16][RS], this wave's only
   int r0, r1;
   pm_range(ntok / 16, r0, r1);
   constexpr int NC = KPM / 4;  // channel rows per lane: lane (pp = lane / 32, col = lane % 32) of the tile's
                                // 32-pixel-wide, 2-row image strip, one channel per load
-  constexpr int NO = kPatchCmax / 16, NTM = kPatchCmax / 16;
+  constexpr int NO = CM / 16, NTM = CM / 16;
   const int col = lane & 31, pp = lane >> 5;
   const size_t plane = (size_t)a.Himg * a.Wimg;
   float xv[NC];
@@ -1654,8 +1656,8 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
       const size_t pbase = (size_t)((wt * 16) % (Ho * Wo)) * C;
 #pragma unroll
       for (int i = 0; i < NO; ++i) {
-        const f4 v = *reinterpret_cast<const f4*>(G.pos + pbase + 4 * (min(i, C / 16 - 1) * 64 + lane));
-        pv[i] = i < C / 16 ? v : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 v = *reinterpret_cast<const f4*>(G.pos + pbase + 4 * ((CT ? i : min(i, C / 16 - 1)) * 64 + lane));
+        pv[i] = CT || i < C / 16 ? v : f4{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
@@ -1665,7 +1667,7 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
 #pragma unroll
   for (int n = 0; n < NTM; ++n) bv[n] = MODE == 0 ? G.bias[min(n * 16 + li, C - 1)] : 0.f;
   {
-    constexpr int NW = kPatchCmax * KPM / 512, NB = NW < 16 ? NW : 16;
+    constexpr int NW = CM * KPM / 512, NB = NW < 16 ? NW : 16;
 #pragma unroll
     for (int h = 0; h < NW; h += NB) {
       float wv[NB];
@@ -1719,7 +1721,7 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
     float* out = G.tok + (size_t)wt * 16 * C;
 #pragma unroll
     for (int i = 0; i < NO; ++i) {
-      if (!CF && i >= C / 16) break;
+      if (!CT && i >= C / 16) break;
       const int e = 4 * (i * 64 + lane), row = e / C, cc = e - row * C;
       f4 v = *reinterpret_cast<const f4*>(R + row * RS + cc);
       if (MODE == 0) v = v + pc[i];
@@ -1730,19 +1732,20 @@ __global__ __launch_bounds__(512) void k_p2t_mp(PatchArgs a) {
   }
 }
 
-// CF, branch-free loads and the unconditional prefetch: as k_p2t_mp
-template <int MODE, int KPM, bool CF>
+// CT, branch-free loads and the unconditional prefetch: as k_p2t_mp
+template <int MODE, int KPM, int CT>
 __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const PatchGroup G = a.g[blockIdx.y];
   const int Ho = a.Himg / 2, Wo = a.Wimg / 2, ntok = a.B * Ho * Wo;
-  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = CF ? kPatchCmax : a.Ctok;
-  constexpr int CS = kPatchCmax + 4;
+  constexpr int CM = CT ? CT : kPatchCmax;
+  const int kc = MODE == 0 ? G.cin * 4 : G.cout * 4, C = CT ? CT : a.Ctok;
+  constexpr int CS = CM + 4;
   float* Wt = sm;  // [KPM][CS]: W[c][j] at Wt[j][c], zero-padded (compile-time MFMA shapes, as k_p2t_mp)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   int r0, r1;
   pm_range(ntok / 16, r0, r1);
-  constexpr int NMT = KPM / 16, NS = kPatchCmax / 16;
+  constexpr int NMT = KPM / 16, NS = CM / 16;
   f4 y[NS];
   float2 ex[NMT][2];
   // lane (token li, g): the token row's float4 at 16 s + 4 g, and what its outputs add (the added image, the bias)
@@ -1751,12 +1754,13 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
     const float* yr = (MODE == 0 ? G.dtok : G.tok) + (size_t)tok * C + 4 * g;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const f4 v = *reinterpret_cast<const f4*>(yr + 16 * (CF ? s : min(s, C / 16 - 1)));
-      y[s] = CF || 16 * s < C ? v : f4{0.f, 0.f, 0.f, 0.f};
+      if (CT) {
+        y[s] = *reinterpret_cast<const f4*>(yr + 16 * s);
+      } else {
+        y[s] = 16 * s < C ? *reinterpret_cast<const f4*>(yr + 16 * s) : f4{0.f, 0.f, 0.f, 0.f};
+      }
     }
-    if (MODE == 0) {
-      // the added image, or (none) the output image itself as a dummy source, selected to 0
-      const float* src = a.add_img ? a.add_img : a.img_out;
+    if (MODE == 0 && a.add_img) {
       int b, ho, wo;
       tok_coords(tok, Ho, Wo, b, ho, wo);
 #pragma unroll
@@ -1765,8 +1769,8 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
         const size_t off = (((size_t)b * a.Cimg + G.cin_off + min(o, kc / 4 - 1)) * a.Himg + 2 * ho) * a.Wimg + 2 * wo;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const float2 v = *reinterpret_cast<const float2*>(src + off + q * a.Wimg);
-          ex[mt][q] = o * 4 < kc && a.add_img ? v : make_float2(0.f, 0.f);
+          const float2 v = *reinterpret_cast<const float2*>(a.add_img + off + q * a.Wimg);
+          ex[mt][q] = o * 4 < kc ? v : make_float2(0.f, 0.f);
         }
       }
     }
@@ -1776,11 +1780,11 @@ __global__ __launch_bounds__(512) void k_t2p_mp(PatchArgs a) {
 #pragma unroll
   for (int mt = 0; mt < NMT; ++mt) {
     bz[mt] = MODE == 1 ? G.bias[min(4 * mt + g, kc / 4 - 1)] : 0.f;
-    if (MODE == 1) ex[mt][0] = ex[mt][1] = make_float2(0.f, 0.f);
+    if (MODE == 1 || !a.add_img) ex[mt][0] = ex[mt][1] = make_float2(0.f, 0.f);
   }
   load_tile(min(wt, r1 - 1));
   {
-    constexpr int NW = kPatchCmax * KPM / 512, NB = NW < 16 ? NW : 16;
+    constexpr int NW = CM * KPM / 512, NB = NW < 16 ? NW : 16;
 #pragma unroll
     for (int h = 0; h < NW; h += NB) {
       float v[NB];
@@ -1853,6 +1857,24 @@ static int pm_grid(const PatchArgs& a, int per_cu) {
   return std::max(1, std::min((nwt + kPmWaves - 1) / kPmWaves, device_cus() * per_cu / a.ngroups));
 }
 
+template <int MODE, int KPM, int CT>
+static hipError_t p2t_mp_launch(const PatchArgs& a, hipStream_t s) {
+  constexpr int CM = CT ? CT : kPatchCmax;
+  constexpr size_t lds = ((size_t)CM * (KPM + 4) + (size_t)kPmWaves * 16 * std::max(KPM + 4, CM + 4)) * sizeof(float);
+  if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM, CT>, lds)) return e;
+  hipLaunchKernelGGL((k_p2t_mp<MODE, KPM, CT>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
+  return hipGetLastError();
+}
+
+template <int MODE, int KPM, int CT>
+static hipError_t t2p_mp_launch(const PatchArgs& a, hipStream_t s) {
+  constexpr size_t lds = (size_t)KPM * ((CT ? CT : kPatchCmax) + 4) * sizeof(float);
+  if (lds > 64 * 1024)
+    if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM, CT>, lds)) return e;
+  hipLaunchKernelGGL((k_t2p_mp<MODE, KPM, CT>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
+  return hipGetLastError();
+}
+
 static int max_k(const PatchArgs& a, bool in) {
   int m = 0;
   for (int g = 0; g < a.ngroups; ++g) m = std::max(m, (in ? a.g[g].cin : a.g[g].cout) * 4);
@@ -1863,16 +1885,8 @@ template <int MODE, int KPM>
 static hipError_t p2t_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   if ((a.tune ? a.tune->patch_pers : kDefaultTuning.patch_pers) > 0) {
-    const size_t lds =
-        ((size_t)kPatchCmax * (KPM + 4) + (size_t)kPmWaves * 16 * std::max(KPM + 4, kPatchCmax + 4)) * sizeof(float);
-    if (a.Ctok == kPatchCmax) {
-      if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM, true>, lds)) return e;
-      hipLaunchKernelGGL((k_p2t_mp<MODE, KPM, true>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
-    } else {
-      if (hipError_t e = set_lds_limit((const void*)k_p2t_mp<MODE, KPM, false>, lds)) return e;
-      hipLaunchKernelGGL((k_p2t_mp<MODE, KPM, false>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lds, s, a);
-    }
-    return hipGetLastError();
+    return a.Ctok == 96 ? p2t_mp_launch<MODE, KPM, 96>(a, s) : a.Ctok == 128 ? p2t_mp_launch<MODE, KPM, 128>(a, s)
+                                                                           : p2t_mp_launch<MODE, KPM, 0>(a, s);
   }
   const int KS = (kc + 15) / 16 * 16 + 4;
   const size_t lds = std::max((size_t)(PT + a.Ctok) * KS, (size_t)PT * (a.Ctok + 4)) * sizeof(float);
@@ -1895,16 +1909,8 @@ static hipError_t t2p_launch_k(const PatchArgs& a, int kc, hipStream_t s) {
   const int ntok = a.B * (a.Himg / 2) * (a.Wimg / 2);
   const size_t lds = (size_t)((kc + 15) / 16 * 16) * ((a.Ctok + 15) / 16 * 16 + 4) * sizeof(float);
   if ((a.tune ? a.tune->patch_pers : kDefaultTuning.patch_pers) > 0) {
-    const size_t lm = (size_t)KPM * (kPatchCmax + 4) * sizeof(float);
-    if (lm > 64 * 1024)
-      if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM, true>, lm)) return e;
-    if (lm > 64 * 1024)
-      if (hipError_t e = set_lds_limit((const void*)k_t2p_mp<MODE, KPM, false>, lm)) return e;
-    if (a.Ctok == kPatchCmax)
-      hipLaunchKernelGGL((k_t2p_mp<MODE, KPM, true>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lm, s, a);
-    else
-      hipLaunchKernelGGL((k_t2p_mp<MODE, KPM, false>), dim3(pm_grid(a, 1), a.ngroups), dim3(64 * kPmWaves), lm, s, a);
-    return hipGetLastError();
+    return a.Ctok == 96 ? t2p_mp_launch<MODE, KPM, 96>(a, s) : a.Ctok == 128 ? t2p_mp_launch<MODE, KPM, 128>(a, s)
+                                                                           : t2p_mp_launch<MODE, KPM, 0>(a, s);
   }
   hipLaunchKernelGGL((k_t2p_mf<MODE, KPM>), dim3((ntok + PT - 1) / PT, a.ngroups), dim3(256), lds, s, a);
   return hipGetLastError();
