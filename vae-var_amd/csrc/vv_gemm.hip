@@ -462,6 +462,43 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_fixup_sub16(GemmArgs args
     epilogue<16, TN * 16, 1, 1, EPI, 16, false>(args, G, acc, m0, n0, 0, 0, rin, hh);
 }
 
+// Tile 49's split-K fixup for a plain GEMM (r06: gemm_nt's N = 1152 split GEMMs on 64 tiles x 4 chunks = 256
+// workgroups, as gemm_ln's): workgroup (tile, a) sums the S chunk partials of fragment row a of every wave in chunk
+// order (k_gemm_h5 wrote element (row 32 wave + 16 a + 4 hh + r, column 16 b + rin) at ((a 9 + b) 4 + r) 512 + 64 wave
+// + lane of partial tile S + c) and runs the GEMM's epilogue on the 16 x 144 rows of each wave
+template <int EPI>
+__global__ __launch_bounds__(512) void k_gemm_fixup49(GemmArgs args) {
+  constexpr int TN = 9, PS = 2 * TN * 4 * 512;  // floats per partial
+  typedef float accv __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const GemmGroup G = args.g[0];
+  const int M = args.M, N = args.N, ntn = (N + 143) / 144, ntm = (M + 255) / 256, S = args.tsplit;
+  const int tile = blockIdx.x, a = blockIdx.y;
+  int mb, nb;
+  tile_mn(tile, ntm, ntn, mb, nb, args.gm);
+  const float* w = args.ws + (size_t)tile * S * PS + (size_t)(a * TN * 4) * 512 + tid;
+  accv acc[1][TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[0][b][r] = w[(size_t)(b * 4 + r) * 512];
+  for (int c = 1; c < S; ++c) {  // one chunk's loads in flight together, chunks summed in order
+    accv t[TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[b][r] = w[(size_t)c * PS + (size_t)(b * 4 + r) * 512];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[0][b] += t[b];
+  }
+  const int m0 = mb * 256 + wave * 32 + a * 16, n0 = nb * 144;
+  const int rin = lane & 15, hh = lane >> 4;
+  if (m0 + 16 <= M && n0 + 144 <= N)
+    epilogue<16, 144, 1, 1, EPI, 16, true>(args, G, acc, m0, n0, 0, 0, rin, hh);
+  else
+    epilogue<16, 144, 1, 1, EPI, 16, false>(args, G, acc, m0, n0, 0, 0, rin, hh);
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // fp32 GEMM as six bf16 MFMA products (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate on gfx950).
 //
@@ -2692,8 +2729,34 @@ hipError_t gemm_nt(const GemmArgs& a_in, hipStream_t s, int tile_hint, float* ws
   a.t49 = 0;
   int t = -1;
   if (hipError_t e = gemm_prepare(a, tile_hint, ws, t)) return e;
+  // r06 (h5_split): the plain N = 1152 split-K GEMMs (projection input gradients, Dec_net.proj, ...) on tile 49 split
+  // P / T ways as gemm_ln's, their partials summed by k_gemm_fixup49 (tile 48: 72 tiles x 3 = 216 workgroups)
+  bool fix49 = false;
+  {
+    const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
+    const long P = device_cus(), T49 = tiles_of(a, 256, 144);
+    if (tile_hint < 0 && TU.h5_split && t == 48 && a.tsplit > 1 && a.tdp == 0 && a.ngroups == 1 && !a.crow &&
+        !a.opl && (a.epi == EPI_STORE || a.epi == EPI_RESID) && a.N % 144 == 0 && a.N % 128 == 0 && T49 > 0 &&
+        P % T49 == 0 && P / T49 >= 2 && P / T49 <= 4 && (size_t)P * 256 * 144 <= kWsFloats && a.K / 32 >= P / T49) {
+      t = 49;
+      a.tsplit = (int)(P / T49);
+      a.nofix = 1;
+      const int ntm = (a.M + 255) / 256, ntn = (a.N + 143) / 144;
+      a.gm = std::max(1, std::min(ntm, (int)std::lround(std::sqrt((double)ntm * ntn / 8.0 * 144 / 256))));
+      fix49 = true;
+    }
+  }
   const int ph = prof_begin(s);
-  const hipError_t e = launch_variant(t, a, s);
+  hipError_t e = launch_variant(t, a, s);
+  if (e == hipSuccess && fix49) {
+    count_launch(CNT_SPLITK_FIXUP);
+    const dim3 grid(tiles_of(a, 256, 144), 2, 1);
+    if (a.epi == EPI_STORE)
+      hipLaunchKernelGGL((k_gemm_fixup49<EPI_STORE>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_gemm_fixup49<EPI_RESID>), grid, dim3(512), 0, s, a);
+    e = hipGetLastError();
+  }
   // algorithmic: 2MNK flops; bytes = A + B + C (+R/aux) once each
   const double G = a.ngroups;
   double bytes = 4.0 * G * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N);

@@ -48,7 +48,9 @@ struct Tuning {
                                 // bit 1 the backward (r03: neutral; r04: closure 8.56 vs 8.69 ms, same box, profiles/r04/ab_r04j)
   int h5_split = 1;             // gemm_ln: tile 49 with every tile split P / T ways (64 tiles x 4 = 256 workgroups for the
                                 // N = 1152 GEMMs at 2048 rows) instead of tile 48's 72 tiles x 3 = 216 (r06: closure 16.62 ->
-                                // 16.56 ms same process, profiles/r06/knob_ab_h5_split.jsonl)
+                                // 16.56 ms same process, profiles/r06/knob_ab_h5_split.jsonl); later in r06 also gemm_nt's
+                                // plain N = 1152 split GEMMs (k_gemm_fixup49): 16.649 / 16.671 -> 16.585 / 16.594 ms with
+                                // both, profiles/r06/knob_ab_h5_split_r06t.jsonl
   int fixup_stage = 1;          // the fused fixup + LayerNorm sums a workgroup's 8 rows of split-K partials with whole
                                 // 128-B line reads into LDS first (0: each row's loads straight from the partials)
   int grid_fused = 1;           // interpolated state grids (config 5): the one-pass misfit k_misfit_grid + the network-grid
