@@ -2181,7 +2181,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = min(m0 + wave * TM * 16 + a * 16 + 4 * hh + r, M - 1);
-        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[args.agather ? args.arow[row] : row]));
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));  // 2^-e_a
         acc[a][b][r] *= ia * sbv;
       }
   }
@@ -2290,7 +2290,7 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
     const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
     if (!a.arow) {
       sc = const_cast<float*>(a.ascale);
-    } else if (!a.opl && TU.h4_gather) {  // tiles 48 / 49 read ascale[arow[r]] themselves (no plane epilogue here)
+    } else if (!t49 && !a.opl && TU.h4_gather) {  // tile 48 reads ascale[arow[r]] itself (no plane epilogue here)
       sc = const_cast<float*>(a.ascale);
       agather = true;
     } else {
