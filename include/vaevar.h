@@ -256,8 +256,9 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
    (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
    launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
-   inverse window map, 1), "h5_split" (the split-K GEMMs whose fixup is fused into a LayerNorm on tile 49 with every
-   tile split P / T ways, 256 workgroups for N = 1152 at 2048 rows, instead of tile 48's 216), "fixup_stage" (the fused fixup + LayerNorm reads a workgroup's split-K partials as whole 128-B lines into LDS, 1, or per row, 0), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
+   inverse window map, 1), "h5_split" (the N = 1152 split-K GEMMs -- those whose fixup is fused into a LayerNorm and the
+   plain ones, summed by k_gemm_fixup49 -- on tile 49 with every tile split P / T ways, 256 workgroups at 2048 rows,
+   instead of tile 48's 216, 1), "fixup_stage" (the fused fixup + LayerNorm reads a workgroup's split-K partials as whole 128-B lines into LDS, 1, or per row, 0), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:
    the misfit reads each state field once per evaluation and its adjoint runs on the network grid, k_misfit_grid /
    k_misfit_net_bwd, 3 rows of a band in flight per pass; 2 = the same with 6 rows; read by vv_bind_problem, 1), "host_wait" (how
    vv_reduce_batch waits for the stream: 0 hipStreamSynchronize, which keeps a host CPU busy; 1 sleeps, then polls
