@@ -254,8 +254,8 @@ int vv_get_gemm_math(vv_ctx* ctx, int* math);
    tiles fill whole rounds of the chip and tile 48's leave a split-K tail: the N = 4608 GEMMs at 2048 rows, 1), "fc_conv_mf" (LGUnet_all_1's PatchEmbed / ConvTranspose2d as direct
    exact-f32 MFMA kernels instead of im2col / col2im + GEMM, 1), "mlp_hc" (the fused dim-192 MLP: 32 or 64 hidden units
    per chunk step, or 2 = 32-unit chunks with the hidden layer split over two waves per 16 tokens, 2), "h4_gather"
-   (tile 48 reads a gathered A's producer row scales through the row map itself instead of a k_gather_scales
-   launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
+   (tiles 48 and 49 read a gathered A's producer row scales through the row map themselves instead of a
+   k_gather_scales launch, 1), "fixup_ln_rows" (the fused fixup + LN1 after fc2 walks the GEMM's rows in order through the
    inverse window map, 1), "h5_split" (the N = 1152 split-K GEMMs -- those whose fixup is fused into a LayerNorm and the
    plain ones, summed by k_gemm_fixup49 -- on tile 49 with every tile split P / T ways, 256 workgroups at 2048 rows,
    instead of tile 48's 216, 1), "fixup_stage" (the fused fixup + LayerNorm reads a workgroup's split-K partials as whole 128-B lines into LDS, 1, or per row, 0), "grid_fused" (interpolated state grids, Hs >= Hl and Ws >= Wl with synthetic observations:

@@ -1997,7 +1997,9 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& args, const GemmGr
 // loops), so the reads outstanding at those waits are two groups old (r04 schedule measurements: DESIGN §3e).
 // Buffer (t + 2) % 3 = (t - 1) % 3 was last read before the barrier of k-tile t - 1, so the DMA of t + 2 may start
 // anywhere in k-tile t.
-template <int EPI>
+// AG: A's row scales gathered through arow from the producer's physical rows (h4_gather; a compile-time form: as a
+// runtime condition the index changed the code of every tile-49 launch and cost 5 % of the closure, r06)
+template <int EPI, bool AG = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* __restrict__ ascale,
                                                     const unsigned short* __restrict__ apl) {
   constexpr int BM = 256, BN = 144, BK = 32, WM = 8, WN = 1, TM = 2, TN = 9;
@@ -2181,7 +2183,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_h5(GemmArgs args, const float* 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = min(m0 + wave * TM * 16 + a * 16 + 4 * hh + r, M - 1);
-        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[row]));  // 2^-e_a
+        const float ia = __uint_as_float((254u << 23) - __float_as_uint(rs[AG ? args.arow[row] : row]));  // 2^-e_a
         acc[a][b][r] *= ia * sbv;
       }
   }
@@ -2268,11 +2270,11 @@ static hipError_t launch_h4_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_
   return hipGetLastError();
 }
 
-template <int EPI>
+template <int EPI, bool AG = false>
 static hipError_t launch_h5_k(const GemmArgs& a, hipStream_t s, dim3 grid, size_t lds, const float* sc,
                               const unsigned short* planes) {
-  if (hipError_t e = set_lds_limit((const void*)k_gemm_h5<EPI>, lds)) return e;
-  hipLaunchKernelGGL((k_gemm_h5<EPI>), grid, dim3(512), lds, s, a, sc, planes);
+  if (hipError_t e = set_lds_limit((const void*)k_gemm_h5<EPI, AG>, lds)) return e;
+  hipLaunchKernelGGL((k_gemm_h5<EPI, AG>), grid, dim3(512), lds, s, a, sc, planes);
   return hipGetLastError();
 }
 
@@ -2290,7 +2292,8 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
     const Tuning& TU = a.tune ? *a.tune : kDefaultTuning;
     if (!a.arow) {
       sc = const_cast<float*>(a.ascale);
-    } else if (!t49 && !a.opl && TU.h4_gather) {  // tile 48 reads ascale[arow[r]] itself (no plane epilogue here)
+    } else if (!a.opl && TU.h4_gather && (!t49 || a.epi == EPI_STORE || a.epi == EPI_RESID)) {
+      // tiles 48 / 49 read ascale[arow[r]] themselves (no plane epilogue here; tile 49: k_gemm_h5<EPI, true>)
       sc = const_cast<float*>(a.ascale);
       agather = true;
     } else {
@@ -2316,11 +2319,15 @@ static hipError_t launch_h4(const GemmArgs& a, hipStream_t s, bool t49 = false) 
     const size_t lds = 3 * (2 * (256 + 144) * 32) * sizeof(unsigned short);
     const dim3 grid(((a.N + 143) / 144) * ((a.M + 255) / 256) * std::max(a.tsplit, 1), 1, a.ngroups);
     switch (a.epi) {
-      case EPI_STORE: return launch_h5_k<EPI_STORE>(b, s, grid, lds, sc, planes);
+      case EPI_STORE:
+        return agather ? launch_h5_k<EPI_STORE, true>(b, s, grid, lds, sc, planes)
+                       : launch_h5_k<EPI_STORE>(b, s, grid, lds, sc, planes);
       case EPI_GELU:
         return a.opl ? launch_h5_k<EPI_GELU_PL>(b, s, grid, lds, sc, planes)
                      : launch_h5_k<EPI_GELU>(b, s, grid, lds, sc, planes);
-      case EPI_RESID: return launch_h5_k<EPI_RESID>(b, s, grid, lds, sc, planes);
+      case EPI_RESID:
+        return agather ? launch_h5_k<EPI_RESID, true>(b, s, grid, lds, sc, planes)
+                       : launch_h5_k<EPI_RESID>(b, s, grid, lds, sc, planes);
       case EPI_DGELU:
         return a.opl ? launch_h5_k<EPI_DGELU_PL>(b, s, grid, lds, sc, planes)
                      : launch_h5_k<EPI_DGELU>(b, s, grid, lds, sc, planes);
@@ -2429,6 +2436,7 @@ bool tuning_value_ok(const char* key, int v) {
   if (k == "fuse_mlp") return v >= 0 && v <= 3;
   if (k == "fuse_attn") return v >= 0 && v <= 3;
   if (k == "bs_tile") return v >= 24 && v <= 27;
+  if (k == "patch_pers") return v == 0 || v == 1 || v == 2 || v == 4;
   return v == 0 || v == 1;  // every other knob is a switch
 }
 

@@ -41,7 +41,8 @@ struct Tuning {
   int gelu_planes = 1;          // the LG-stage fc1 (GELU) / fc2-input-gradient (gelu') GEMMs write the fp16x3 planes of
                                 // the K = 4C GEMM that follows (bound-derived row scales: no k_rowsplit pass)
   int fixup_ln_rows = 1;        // the fused fixup + LN1 walks GEMM rows in order through the inverse window map
-  int h4_gather = 1;            // tile 48 reads gathered producer row scales through arow itself (0: k_gather_scales)
+  int h4_gather = 1;            // tiles 48 / 49 read gathered producer row scales through arow themselves (tile 49: the
+                                // STORE / RESID epilogues, k_gemm_h5<EPI, true>; 0: k_gather_scales)
   int mlp_hc = 2;               // the fused dim-192 MLP: hidden units per chunk (32 or 64: fewer chunk steps, 151 KB LDS),
                                 // or 2: 32-unit chunks, the hidden layer split over two waves per 16 tokens
   int fuse_attn = 3;            // the fused Swin-tower attention sub-block (vv_tower.hip) at dim 96: bit 0 the forward,
